@@ -1,0 +1,159 @@
+/*
+ * pmx.h — C ABI of the MI355X-native ICP inner loop (the drop-in boundary).
+ *
+ * One pmx_ctx per ICP object (and per GPU rank).  It owns a HIP stream, the
+ * device-resident reference / reading clouds, the k x N match and weight
+ * arrays, and (optionally) an RCCL communicator.  Not thread-safe — exactly
+ * like the reference's ICP object (pointmatcher/PointMatcher.h:652-764 keeps
+ * mutable per-object state).  Plain pointers and sizes only: no torch/HIP
+ * types cross this boundary.
+ *
+ * Each entry point replaces one reference interface (paths relative to the
+ * libpointmatcher repository root):
+ *
+ *   pmx_set_reference   Matcher::init(filteredReference)
+ *                         pointmatcher/PointMatcher.h:481, MatchersImpl.cpp:77-83
+ *                         (+ the centred reference of ICP.cpp:291-302)
+ *   pmx_set_reading     the once-per-compute reading copy + transformations.apply
+ *                         (ICP.cpp:337-347)
+ *   pmx_match           transformations.apply(stepReading, T_iter) fused with
+ *                         Matcher::findClosests (ICP.cpp:381-387,
+ *                         PointMatcher.h:484, MatchersImpl.cpp:85-101)
+ *   pmx_outlier_*       OutlierFilter::compute and the chain product
+ *                         (PointMatcher.h:504-512, OutlierFilter.cpp:63-103,
+ *                          OutlierFiltersImpl.cpp:51-223)
+ *   pmx_p2plane_system  ErrorElements + PointToPlane normal equations
+ *                         (ErrorMinimizer.cpp:58-193, PointToPlane.cpp:171-243)
+ *   pmx_p2point_system  ErrorElements + PointToPoint weighted moments
+ *                         (PointToPoint.cpp:61-81)
+ *   pmx_get_matches /   lazy host mirrors of Matches / OutlierWeights for
+ *   pmx_get_weights       CPU modules and inspectors (PointMatcher.h:371-391)
+ *
+ * The 6x6 / 3x3 solves, the transform update and the convergence checks stay
+ * on the host (PointToPlane.cpp:108-161, ICP.cpp:411-427).
+ *
+ * Errors: every call returns 0 or a negative PMX_E_* code; pmx_last_error()
+ * gives the message.  The host shim maps codes to the reference exception
+ * types (PointMatcher.h:83-100):
+ *   PMX_E_NO_POINTS       -> ConvergenceError("ErrorMnimizer: no point to minimize")
+ *   PMX_E_EMPTY_QUANTILE  -> ConvergenceError("no outlier to filter")
+ *   PMX_E_BAD_PARAM       -> InvalidParameter
+ *   PMX_E_HIP / PMX_E_RCCL / PMX_E_STATE -> std::runtime_error
+ */
+#ifndef PMX_H
+#define PMX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pmx_ctx pmx_ctx;
+
+enum { PMX_F32 = 0, PMX_F64 = 1 };
+
+enum {
+    PMX_OK = 0,
+    PMX_E_NO_POINTS = -1,
+    PMX_E_EMPTY_QUANTILE = -2,
+    PMX_E_BAD_PARAM = -3,
+    PMX_E_HIP = -10,
+    PMX_E_RCCL = -11,
+    PMX_E_STATE = -12,
+    PMX_E_NO_DEVICE = -13
+};
+
+/* per-iteration statistics (ErrorElements, ErrorMinimizer.cpp:133-192;
+ * ICP.cpp:432-436).  Counts are global over all ranks. */
+typedef struct pmx_stats {
+    int64_t kept;               /* ErrorElements columns P: dist != inf && w != 0 */
+    int64_t nonzero_weights;    /* (w != 0).count()                 ErrorMinimizer.cpp:75 */
+    int64_t rejected_matches;   /* nbRejectedMatches                ErrorMinimizer.cpp:191 */
+    int64_t rejected_points;    /* nbRejectedPoints                 ErrorMinimizer.cpp:192 */
+    double sum_w;               /* sum of kept weights (weightedPointUsedRatio * k * N) */
+    double limit;               /* last quantile threshold (diagnostic, T value) */
+    int64_t n_total;            /* k * N over all ranks */
+} pmx_stats;
+
+/* ------------------------------------------------------------ context --- */
+/* device: HIP device ordinal; dtype: PMX_F32 | PMX_F64. */
+int pmx_ctx_create(int device, int dtype, pmx_ctx** out);
+int pmx_ctx_destroy(pmx_ctx* ctx);
+const char* pmx_last_error(const pmx_ctx* ctx);
+/* number of visible HIP devices (0 when no GPU / driver) */
+int pmx_device_count(void);
+/* library build string, e.g. "pmx 0.1 gfx950" */
+const char* pmx_version(void);
+
+/* ---------------------------------------------------------- multi-GPU --- */
+/* RCCL unique id (128 bytes) generated on rank 0 and broadcast by the
+ * launcher; every rank then calls pmx_comm_init.  With a communicator set,
+ * pmx_set_reading takes the rank's shard of the reading cloud and every
+ * reduction (quantile histograms, normal equations) is all-reduced on the
+ * context stream over RCCL/xGMI. */
+int pmx_comm_unique_id(void* out128);
+int pmx_comm_init(pmx_ctx* ctx, const void* uid128, int nranks, int rank);
+
+/* ------------------------------------------------------------ clouds --- */
+/* feat: rows x M column-major (point-major) T array, rows = D + 1 with the
+ * homogeneous row last (D = 2 or 3).  The caller passes the CENTRED
+ * reference (ICP.cpp:299).  normals: D x M (point-major) or NULL.  Copied
+ * to HBM once and kept resident across iterations and ICP calls. */
+int pmx_set_reference(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const void* normals);
+/* reading shard: rows x N.  T0 (rows x rows, row-major T) is applied once on
+ * the device (T_refMean_dataIn, ICP.cpp:345-347). */
+int pmx_set_reading(pmx_ctx* ctx, const void* feat, int rows, int64_t N, const void* T0);
+
+/* ------------------------------------------------------------- match --- */
+/* T_iter: rows x rows row-major T.  knn >= 1 (<= 16 on this path),
+ * maxDist: radius (inclusive, squared in T; +inf = none), epsilon: the
+ * search is exact, so any epsilon >= 0 is satisfied.  visited (may be NULL)
+ * receives the pair evaluations of this call (PointCountTouched).  Results
+ * stay on the device. */
+int pmx_match(pmx_ctx* ctx, const void* T_iter, int knn, double maxDist, double epsilon,
+              uint64_t* visited);
+
+/* ----------------------------------------------------- outlier filters --- */
+/* chain_pos 0 writes the weights, chain_pos > 0 multiplies into them
+ * (OutlierFilter.cpp:90-99).  pmx_outlier_default = empty chain
+ * (w = dist != inf, OutlierFilter.cpp:70-85). */
+int pmx_outlier_default(pmx_ctx* ctx);
+int pmx_outlier_null(pmx_ctx* ctx, int chain_pos);
+int pmx_outlier_maxdist(pmx_ctx* ctx, int chain_pos, double maxDist);
+int pmx_outlier_mindist(pmx_ctx* ctx, int chain_pos, double minDist);
+int pmx_outlier_mediandist(pmx_ctx* ctx, int chain_pos, double factor);
+int pmx_outlier_trimmed(pmx_ctx* ctx, int chain_pos, double ratio);
+int pmx_outlier_vartrimmed(pmx_ctx* ctx, int chain_pos, double minRatio, double maxRatio,
+                           double lambda);
+
+/* ---------------------------------------------------------- minimizers --- */
+/* Point-to-plane normal equations for the step transform of the last
+ * pmx_match: A (n x n row-major, n = 6 in 3D / 3 in 2D, full matrix, not
+ * symmetrised: A = sum w F F^T) and b = -sum w F (d . n), accumulated in
+ * double from T-precision products.  Synchronises the stream.  Returns
+ * PMX_E_EMPTY_QUANTILE if a quantile filter of this iteration had no finite
+ * distance, PMX_E_NO_POINTS if no weight is non-zero. */
+int pmx_p2plane_system(pmx_ctx* ctx, double* A, double* b, pmx_stats* st);
+/* Point-to-point: mean_p, mean_q (D each, T values), m = sum (qc w) pc^T
+ * (D x D row-major, double sums of T products). */
+int pmx_p2point_system(pmx_ctx* ctx, double* mean_p, double* mean_q, double* m, pmx_stats* st);
+
+/* ---------------------------------------------------------- host mirrors --- */
+/* dists: k x N T (point-major), ids: k x N int32 (this rank's shard) */
+int pmx_get_matches(pmx_ctx* ctx, void* dists, int32_t* ids);
+int pmx_get_weights(pmx_ctx* ctx, void* w);
+/* shape of the current match arrays */
+int pmx_get_shape(const pmx_ctx* ctx, int64_t* n_local, int* knn);
+
+/* ------------------------------------------------------------- timing --- */
+/* HIP-event timing of the dominant kernel (the match kernel) on the context
+ * stream: enable, then read the accumulated device time and launch count. */
+int pmx_timing_enable(pmx_ctx* ctx, int on);
+int pmx_timing_read(pmx_ctx* ctx, double* match_ms, int64_t* match_launches, double* other_ms);
+int pmx_sync(pmx_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PMX_H */

@@ -1,0 +1,255 @@
+"""ctypes binding of the C ABI in include/pmx.h (libpointmatcher_amd/lib/libpmx.so).
+
+This is plumbing for Python callers (tests, bench, smoke): every call goes to
+the HIP library.  There is no CPU fallback — if the library or a GPU is
+missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "lib")
+LIBPMX = os.path.join(LIBDIR, "libpmx.so")
+LIBPMX_ICP = os.path.join(LIBDIR, "libpmx_icp.so")
+
+PMX_F32, PMX_F64 = 0, 1
+PMX_OK = 0
+PMX_E_NO_POINTS = -1
+PMX_E_EMPTY_QUANTILE = -2
+PMX_E_BAD_PARAM = -3
+PMX_E_TRANSFORMATION = -4
+PMX_E_HIP = -10
+PMX_E_RCCL = -11
+PMX_E_STATE = -12
+PMX_E_NO_DEVICE = -13
+
+
+class ConvergenceError(RuntimeError):
+    """PointMatcher<T>::ConvergenceError (pointmatcher/PointMatcher.h:83-87)."""
+
+
+class InvalidParameter(RuntimeError):
+    """Parametrizable::InvalidParameter (pointmatcher/Parametrizable.h:101-104)."""
+
+
+class TransformationError(RuntimeError):
+    """TransformationError (pointmatcher/PointMatcher.h:148-151)."""
+
+
+class PmxError(RuntimeError):
+    pass
+
+
+class Stats(C.Structure):
+    _fields_ = [("kept", C.c_int64), ("nonzero_weights", C.c_int64),
+                ("rejected_matches", C.c_int64), ("rejected_points", C.c_int64),
+                ("sum_w", C.c_double), ("limit", C.c_double), ("n_total", C.c_int64)]
+
+    def asdict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+
+EXPORTS = [
+    "pmx_ctx_create", "pmx_ctx_destroy", "pmx_last_error", "pmx_device_count", "pmx_version",
+    "pmx_comm_unique_id", "pmx_comm_init", "pmx_set_reference", "pmx_set_reading", "pmx_match",
+    "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
+    "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed",
+    "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
+    "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
+]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIBPMX):
+            raise PmxError(f"{LIBPMX} not built (run __graft_entry__.build() or make -C libpointmatcher_amd)")
+        l = C.CDLL(LIBPMX, mode=C.RTLD_GLOBAL)
+        l.pmx_last_error.restype = C.c_char_p
+        l.pmx_version.restype = C.c_char_p
+        l.pmx_last_error.argtypes = [C.c_void_p]
+        l.pmx_ctx_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        l.pmx_ctx_destroy.argtypes = [C.c_void_p]
+        l.pmx_comm_unique_id.argtypes = [C.c_void_p]
+        l.pmx_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        l.pmx_set_reference.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
+        l.pmx_set_reading.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
+        l.pmx_match.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double,
+                                C.POINTER(C.c_uint64)]
+        l.pmx_outlier_default.argtypes = [C.c_void_p]
+        l.pmx_outlier_null.argtypes = [C.c_void_p, C.c_int]
+        for f in ("maxdist", "mindist", "mediandist", "trimmed"):
+            getattr(l, "pmx_outlier_" + f).argtypes = [C.c_void_p, C.c_int, C.c_double]
+        l.pmx_outlier_vartrimmed.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_double]
+        l.pmx_p2plane_system.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(Stats)]
+        l.pmx_p2point_system.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.POINTER(Stats)]
+        l.pmx_get_matches.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        l.pmx_get_weights.argtypes = [C.c_void_p, C.c_void_p]
+        l.pmx_get_shape.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
+        l.pmx_timing_enable.argtypes = [C.c_void_p, C.c_int]
+        l.pmx_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                      C.POINTER(C.c_double)]
+        l.pmx_sync.argtypes = [C.c_void_p]
+        _lib = l
+    return _lib
+
+
+def device_count():
+    return lib().pmx_device_count()
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def raise_for(code, msg=""):
+    if code == PMX_OK:
+        return
+    if code in (PMX_E_NO_POINTS, PMX_E_EMPTY_QUANTILE):
+        raise ConvergenceError(msg)
+    if code == PMX_E_BAD_PARAM:
+        raise InvalidParameter(msg)
+    if code == PMX_E_TRANSFORMATION:
+        raise TransformationError(msg)
+    raise PmxError(f"pmx error {code}: {msg}")
+
+
+class Context:
+    """One device context (one ICP object / one rank)."""
+
+    def __init__(self, device=0, dtype=np.float32):
+        self.dtype = np.dtype(dtype)
+        self._l = lib()
+        h = C.c_void_p()
+        rc = self._l.pmx_ctx_create(device, PMX_F64 if self.dtype == np.float64 else PMX_F32, C.byref(h))
+        if rc != PMX_OK:
+            raise PmxError(f"pmx_ctx_create failed ({rc}); visible HIP devices: {device_count()}")
+        self.h = h
+        self.rows = None
+        self.knn = None
+        self.N = 0
+
+    def close(self):
+        if self.h:
+            self._l.pmx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc != PMX_OK:
+            raise_for(rc, self._l.pmx_last_error(self.h).decode())
+
+    def _arr(self, a):
+        return np.ascontiguousarray(a, dtype=self.dtype)
+
+    # --- multi-GPU
+    @staticmethod
+    def unique_id():
+        buf = (C.c_char * 128)()
+        rc = lib().pmx_comm_unique_id(buf)
+        if rc != PMX_OK:
+            raise PmxError(f"pmx_comm_unique_id failed ({rc})")
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = (C.c_char * 128).from_buffer_copy(uid)
+        self._chk(self._l.pmx_comm_init(self.h, buf, nranks, rank))
+
+    # --- clouds
+    def set_reference(self, feat, normals=None):
+        feat = self._arr(feat)
+        nrm = self._arr(normals) if normals is not None else None
+        self.rows = feat.shape[1]
+        self._ref_keep = (feat, nrm)
+        self._chk(self._l.pmx_set_reference(self.h, _ptr(feat), feat.shape[1], feat.shape[0], _ptr(nrm)))
+
+    def set_reading(self, feat, T0=None):
+        feat = self._arr(feat)
+        rows = feat.shape[1]
+        T0 = self._arr(np.eye(rows) if T0 is None else T0)
+        self.N = feat.shape[0]
+        self._chk(self._l.pmx_set_reading(self.h, _ptr(feat), rows, feat.shape[0], _ptr(T0)))
+
+    # --- per-iteration
+    def match(self, T, knn=1, max_dist=np.inf, epsilon=0.0):
+        T = self._arr(T)
+        v = C.c_uint64(0)
+        self._chk(self._l.pmx_match(self.h, _ptr(T), knn, float(max_dist), float(epsilon), C.byref(v)))
+        self.knn = knn
+        return v.value
+
+    def outlier_default(self):
+        self._chk(self._l.pmx_outlier_default(self.h))
+
+    def outlier(self, name, pos=0, **p):
+        l, h = self._l, self.h
+        if name == "NullOutlierFilter":
+            rc = l.pmx_outlier_null(h, pos)
+        elif name == "MaxDistOutlierFilter":
+            rc = l.pmx_outlier_maxdist(h, pos, float(p.get("maxDist", 1.0)))
+        elif name == "MinDistOutlierFilter":
+            rc = l.pmx_outlier_mindist(h, pos, float(p.get("minDist", 1.0)))
+        elif name == "MedianDistOutlierFilter":
+            rc = l.pmx_outlier_mediandist(h, pos, float(p.get("factor", 3.0)))
+        elif name == "TrimmedDistOutlierFilter":
+            rc = l.pmx_outlier_trimmed(h, pos, float(p.get("ratio", 0.85)))
+        elif name == "VarTrimmedDistOutlierFilter":
+            rc = l.pmx_outlier_vartrimmed(h, pos, float(p.get("minRatio", 0.05)),
+                                          float(p.get("maxRatio", 0.99)), float(p.get("lambda", 2.35)))
+        else:
+            raise InvalidParameter(f"unknown outlier filter {name}")
+        self._chk(rc)
+
+    def p2plane_system(self):
+        n = 6 if self.rows == 4 else 3
+        A = np.zeros(n * n)
+        b = np.zeros(n)
+        st = Stats()
+        self._chk(self._l.pmx_p2plane_system(self.h, _ptr(A), _ptr(b), C.byref(st)))
+        return A.reshape(n, n), b, st
+
+    def p2point_system(self):
+        D = self.rows - 1
+        mp = np.zeros(D)
+        mq = np.zeros(D)
+        m = np.zeros(D * D)
+        st = Stats()
+        self._chk(self._l.pmx_p2point_system(self.h, _ptr(mp), _ptr(mq), _ptr(m), C.byref(st)))
+        return mp, mq, m.reshape(D, D), st
+
+    def get_matches(self):
+        d = np.empty((self.N, self.knn), self.dtype)
+        i = np.empty((self.N, self.knn), np.int32)
+        self._chk(self._l.pmx_get_matches(self.h, _ptr(d), _ptr(i)))
+        return d, i
+
+    def get_weights(self):
+        w = np.empty((self.N, self.knn), self.dtype)
+        self._chk(self._l.pmx_get_weights(self.h, _ptr(w)))
+        return w
+
+    # --- timing
+    def timing(self, on=True):
+        self._chk(self._l.pmx_timing_enable(self.h, 1 if on else 0))
+
+    def timing_read(self):
+        ms = C.c_double()
+        n = C.c_int64()
+        o = C.c_double()
+        self._chk(self._l.pmx_timing_read(self.h, C.byref(ms), C.byref(n), C.byref(o)))
+        return ms.value, n.value
+
+    def sync(self):
+        self._chk(self._l.pmx_sync(self.h))

@@ -1,0 +1,726 @@
+// pmx_capi.hip — the C ABI declared in include/pmx.h.
+//
+// Owns the per-ICP-object device state (stream, resident clouds, match /
+// weight arrays, select state, reduction buffers, RCCL communicator) and
+// sequences the kernels of pmx_match.hip / pmx_select.hip / pmx_reduce.hip on
+// one HIP stream.  Host synchronisation happens once per ICP iteration, in
+// pmx_p2plane_system / pmx_p2point_system, when the ~400-byte system is
+// copied back for the host solve (PointToPlane.cpp:108-161).
+#include "pmx_internal.h"
+
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/pmx.h"
+
+using namespace pmx;
+
+struct pmx_ctx {
+    int device = 0;
+    int dtype = PMX_F32;
+    int cu_count = 256;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // reference (Matcher::init)
+    int rows = 0, dim = 0;
+    int64_t M = 0, M_pad = 0;
+    void* d_ref = nullptr;
+    void* d_nrm = nullptr;
+    bool has_normals = false;
+
+    // reading shard
+    int64_t N = 0, N_total = 0, N_max = 0;
+    void* d_rd = nullptr;
+
+    // matches / weights
+    int knn = 0;
+    int64_t match_cap = 0;  // elements
+    void* d_dists = nullptr;
+    int32_t* d_ids = nullptr;
+    void* d_w = nullptr;
+    int64_t part_cap = 0;
+    void* d_part_d = nullptr;
+    int32_t* d_part_i = nullptr;
+    double Tstep[16] = {0};  // step transform (embedded 4x4, T values)
+    bool have_match = false;
+
+    // quantile select: SelectState followed by the per-iteration error word
+    SelectState* d_sel = nullptr;
+    int* d_iter_err = nullptr;
+    uint32_t* d_hist = nullptr;
+    double* d_ratio = nullptr;
+
+    // VarTrimmed scratch + cached pow table
+    void* d_vt = nullptr;
+    size_t vt_bytes = 0;
+    void* d_deno = nullptr;
+    size_t deno_bytes = 0;
+    int deno_pts = -1, deno_min = -1, deno_max = -1;
+    double deno_lambda = NAN;
+    void* d_gather = nullptr;  // multi-rank all-gathered distances
+    size_t gather_bytes = 0;
+
+    // reductions
+    double* d_partials = nullptr;
+    double* d_result = nullptr;  // [0..63] system, [64..127] second pass
+    void* d_means = nullptr;
+    double* h_result = nullptr;  // pinned
+
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+
+    // timing of the match kernel
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    double match_ms = 0.0;
+    int64_t match_launches = 0;
+};
+
+namespace {
+
+int fail(pmx_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(ctx, PMX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define NCCLCHK(ctx, expr)                                                                     \
+    do {                                                                                       \
+        ncclResult_t r_ = (expr);                                                              \
+        if (r_ != ncclSuccess)                                                                 \
+            return fail(ctx, PMX_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+size_t tsize(const pmx_ctx* c) { return c->dtype == PMX_F64 ? 8 : 4; }
+
+int ensure(pmx_ctx* c, void** p, size_t* cap, size_t bytes) {
+    if (*cap >= bytes && *p) return PMX_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIPCHK(c, hipMalloc(p, bytes > 0 ? bytes : 16));
+    *cap = bytes;
+    return PMX_OK;
+}
+
+// embed a rows x rows host transform (row-major T) into a 4x4 (see pmx_internal.h)
+template <typename T>
+Mat4<T> embed(const T* src, int rows) {
+    Mat4<T> m{};
+    if (rows == 4) {
+        for (int i = 0; i < 16; ++i) m.m[i] = src[i];
+    } else {
+        const T a[16] = {src[0], src[1], 0, src[2], src[3], src[4], 0, src[5],
+                         0,      0,      1, 0,      src[6], src[7], 0, src[8]};
+        for (int i = 0; i < 16; ++i) m.m[i] = a[i];
+    }
+    return m;
+}
+
+template <typename T>
+Mat4<T> step_mat(const pmx_ctx* c) {
+    Mat4<T> m{};
+    for (int i = 0; i < 16; ++i) m.m[i] = (T)c->Tstep[i];
+    return m;
+}
+
+template <typename T>
+int ncclType() {
+    return sizeof(T) == 8 ? (int)ncclFloat64 : (int)ncclFloat32;
+}
+
+int allreduce_f64(pmx_ctx* c, double* buf, size_t n) {
+    if (!c->comm || c->nranks == 1) return PMX_OK;
+    NCCLCHK(c, ncclAllReduce(buf, buf, n, ncclFloat64, ncclSum, c->comm, c->stream));
+    return PMX_OK;
+}
+
+void resolve_events(pmx_ctx* c) {
+    for (auto& pr : c->ev_pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+            c->match_ms += ms;
+            c->match_launches += 1;
+        }
+        c->ev_pool.push_back(pr.first);
+        c->ev_pool.push_back(pr.second);
+    }
+    c->ev_pending.clear();
+}
+
+hipEvent_t get_event(pmx_ctx* c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// ------------------------------------------------------------------ clouds --
+template <typename T>
+int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals) {
+    if (rows != 3 && rows != 4) return fail(c, PMX_E_BAD_PARAM, "reference must have 3 (2-D) or 4 (3-D) rows");
+    if (M <= 0) return fail(c, PMX_E_BAD_PARAM, "empty reference");
+    if (M > (int64_t)0x7fffffff - kTile) return fail(c, PMX_E_BAD_PARAM, "reference larger than int32 ids");
+    const int D = rows - 1;
+    const int64_t M_pad = ((M + kTile - 1) / kTile) * kTile;
+    std::vector<P4<T>> h((size_t)M_pad);
+    const T inf = std::numeric_limits<T>::infinity();
+    for (int64_t j = 0; j < M; ++j) {
+        const T* p = feat + j * rows;
+        h[j] = (D == 3) ? P4<T>{p[0], p[1], p[2], p[3]} : P4<T>{p[0], p[1], (T)0, p[2]};
+    }
+    for (int64_t j = M; j < M_pad; ++j) h[j] = P4<T>{inf, inf, inf, (T)1};
+    if (c->d_ref) (void)hipFree(c->d_ref);
+    c->d_ref = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_ref, sizeof(P4<T>) * M_pad));
+    HIPCHK(c, hipMemcpyAsync(c->d_ref, h.data(), sizeof(P4<T>) * M_pad, hipMemcpyHostToDevice, c->stream));
+    if (c->d_nrm) (void)hipFree(c->d_nrm);
+    c->d_nrm = nullptr;
+    c->has_normals = normals != nullptr;
+    std::vector<P4<T>> hn;
+    if (normals) {
+        hn.resize((size_t)M);
+        for (int64_t j = 0; j < M; ++j) {
+            const T* n = normals + j * D;
+            hn[j] = (D == 3) ? P4<T>{n[0], n[1], n[2], (T)0} : P4<T>{n[0], n[1], (T)0, (T)0};
+        }
+        HIPCHK(c, hipMalloc(&c->d_nrm, sizeof(P4<T>) * M));
+        HIPCHK(c, hipMemcpyAsync(c->d_nrm, hn.data(), sizeof(P4<T>) * M, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->rows = rows;
+    c->dim = D;
+    c->M = M;
+    c->M_pad = M_pad;
+    c->have_match = false;
+    return PMX_OK;
+}
+
+template <typename T>
+int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0) {
+    if (c->rows == 0) return fail(c, PMX_E_STATE, "pmx_set_reference must be called first");
+    if (rows != c->rows) return fail(c, PMX_E_BAD_PARAM, "reading and reference dimensions differ");
+    if (N < 0) return fail(c, PMX_E_BAD_PARAM, "negative reading size");
+    const int D = rows - 1;
+    std::vector<P4<T>> h((size_t)(N > 0 ? N : 1));
+    for (int64_t i = 0; i < N; ++i) {
+        const T* p = feat + i * rows;
+        h[i] = (D == 3) ? P4<T>{p[0], p[1], p[2], p[3]} : P4<T>{p[0], p[1], (T)0, p[2]};
+    }
+    void* d_raw = nullptr;
+    HIPCHK(c, hipMalloc(&d_raw, sizeof(P4<T>) * (N > 0 ? N : 1)));
+    if (c->d_rd) (void)hipFree(c->d_rd);
+    c->d_rd = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_rd, sizeof(P4<T>) * (N > 0 ? N : 1)));
+    if (N > 0) {
+        HIPCHK(c, hipMemcpyAsync(d_raw, h.data(), sizeof(P4<T>) * N, hipMemcpyHostToDevice, c->stream));
+        Mat4<T> M0 = embed<T>(T0, rows);
+        launch_transform<T>((const P4<T>*)d_raw, (P4<T>*)c->d_rd, N, M0, c->stream);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(d_raw);
+    c->N = N;
+    c->N_total = N;
+    c->N_max = N;
+    if (c->comm && c->nranks > 1) {
+        // global reading size and the largest shard (padding of all-gathers)
+        double* tmp = c->d_result;
+        double hv[2] = {(double)N, 0.0};
+        HIPCHK(c, hipMemcpyAsync(tmp, hv, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        NCCLCHK(c, ncclAllReduce(tmp, tmp, 1, ncclFloat64, ncclSum, c->comm, c->stream));
+        HIPCHK(c, hipMemcpyAsync(tmp + 1, hv, sizeof(double), hipMemcpyHostToDevice, c->stream));
+        NCCLCHK(c, ncclAllReduce(tmp + 1, tmp + 1, 1, ncclFloat64, ncclMax, c->comm, c->stream));
+        HIPCHK(c, hipMemcpyAsync(hv, tmp, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->N_total = (int64_t)hv[0];
+        c->N_max = (int64_t)hv[1];
+    }
+    c->have_match = false;
+    return PMX_OK;
+}
+
+// ------------------------------------------------------------------- match --
+template <typename T>
+int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
+    if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
+    if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
+    if (knn < 1 || knn > 16) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 16] on the GPU path");
+    if (!(maxDist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
+    const int64_t n = c->N * knn;
+    size_t cap = (size_t)c->match_cap * tsize(c);
+    if ((int64_t)c->match_cap < n || !c->d_dists) {
+        size_t capd = 0, capi = 0, capw = 0;
+        if (c->d_dists) (void)hipFree(c->d_dists);
+        if (c->d_ids) (void)hipFree(c->d_ids);
+        if (c->d_w) (void)hipFree(c->d_w);
+        c->d_dists = nullptr;
+        c->d_ids = nullptr;
+        c->d_w = nullptr;
+        int rc;
+        if ((rc = ensure(c, &c->d_dists, &capd, sizeof(T) * (n > 0 ? n : 1)))) return rc;
+        if ((rc = ensure(c, (void**)&c->d_ids, &capi, sizeof(int32_t) * (n > 0 ? n : 1)))) return rc;
+        if ((rc = ensure(c, &c->d_w, &capw, sizeof(T) * (n > 0 ? n : 1)))) return rc;
+        c->match_cap = n;
+        (void)cap;
+    }
+    const int64_t pe = match_part_elems<T>(c->N, c->M_pad, knn, c->cu_count);
+    if (pe > c->part_cap) {
+        size_t a = 0, b = 0;
+        if (c->d_part_d) (void)hipFree(c->d_part_d);
+        if (c->d_part_i) (void)hipFree(c->d_part_i);
+        c->d_part_d = nullptr;
+        c->d_part_i = nullptr;
+        int rc;
+        if ((rc = ensure(c, &c->d_part_d, &a, sizeof(T) * pe))) return rc;
+        if ((rc = ensure(c, (void**)&c->d_part_i, &b, sizeof(int32_t) * pe))) return rc;
+        c->part_cap = pe;
+    }
+    Mat4<T> Tm = embed<T>(Titer, c->rows);
+    for (int i = 0; i < 16; ++i) c->Tstep[i] = (double)Tm.m[i];
+    const T md = (T)maxDist;
+    const T maxR2 = md * md;  // libnabo squares the radius in T [ext]
+    HIPCHK(c, hipMemsetAsync(c->d_iter_err, 0, sizeof(int), c->stream));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) {
+        e0 = get_event(c);
+        e1 = get_event(c);
+    }
+    launch_match<T>((const P4<T>*)c->d_ref, c->M_pad, (const P4<T>*)c->d_rd, c->N, Tm, knn, maxR2, (T*)c->d_dists,
+                    c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1, c->cu_count);
+    HIPCHK(c, hipGetLastError());
+    if (e0 && e1) c->ev_pending.emplace_back(e0, e1);
+    c->knn = knn;
+    c->have_match = true;
+    if (visited) *visited = (uint64_t)c->N * (uint64_t)c->M;
+    return PMX_OK;
+}
+
+// ----------------------------------------------------------------- outliers --
+template <typename T>
+int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const double* ratio_dev) {
+    HIPCHK(c, hipMemsetAsync(c->d_sel, 0, sizeof(SelectState), c->stream));
+    const int passes = select_passes<T>();
+    for (int p = 0; p < passes; ++p) {
+        launch_select_hist<T>(d, n, c->d_hist, c->d_sel, p, c->stream);
+        if (c->comm && c->nranks > 1)
+            NCCLCHK(c, ncclAllReduce(c->d_hist, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), ncclUint32, ncclSum,
+                                     c->comm, c->stream));
+        launch_select_pick<T>(c->d_hist, c->d_sel, p, ratio, ratio_dev, c->stream);
+    }
+    HIPCHK(c, hipGetLastError());
+    return PMX_OK;
+}
+
+int check_match(pmx_ctx* c) {
+    if (!c->have_match) return fail(c, PMX_E_STATE, "pmx_match must be called first");
+    return PMX_OK;
+}
+
+template <typename T>
+int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, double p2) {
+    int rc = check_match(c);
+    if (rc) return rc;
+    const int64_t n = c->N * c->knn;
+    const T* d = (const T*)c->d_dists;
+    T* w = (T*)c->d_w;
+    const int mul = chain_pos > 0;
+    switch (kind) {
+    case 0:  // default: empty chain
+        launch_weights_default<T>(d, w, n, c->stream);
+        break;
+    case 1:  // Null
+        launch_weights_const<T>(w, n, mul, c->stream);
+        break;
+    case 2: {  // MaxDist: w = d <= maxDist^2 (OutlierFiltersImpl.cpp:66-81)
+        if (!(p0 >= 1e-7)) return fail(c, PMX_E_BAD_PARAM, "MaxDistOutlierFilter: maxDist < 1e-7");
+        const T m = (T)p0;
+        const T m2 = (T)std::pow((double)m, 2.0);
+        launch_weights_cmp<T>(d, w, n, m2, 0, mul, c->stream);
+        break;
+    }
+    case 3: {  // MinDist: w = d >= minDist^2 (OutlierFiltersImpl.cpp:87-100)
+        if (!(p0 >= 1e-7)) return fail(c, PMX_E_BAD_PARAM, "MinDistOutlierFilter: minDist < 1e-7");
+        const T m = (T)p0;
+        const T m2 = (T)std::pow((double)m, 2.0);
+        launch_weights_cmp<T>(d, w, n, m2, 1, mul, c->stream);
+        break;
+    }
+    case 4: {  // MedianDist: limit = factor * quantile(0.5)
+        if ((rc = quantile_select<T>(c, d, n, 0.5, nullptr))) return rc;
+        launch_weights_state<T>(d, w, n, c->d_sel, (T)p0, mul, c->stream);
+        break;
+    }
+    case 5: {  // TrimmedDist: limit = quantile(ratio)
+        if (!(p0 >= 1e-7 && p0 <= 1.0)) return fail(c, PMX_E_BAD_PARAM, "TrimmedDistOutlierFilter: ratio out of [1e-7, 1]");
+        if ((rc = quantile_select<T>(c, d, n, p0, nullptr))) return rc;
+        launch_weights_state<T>(d, w, n, c->d_sel, (T)1, mul, c->stream);
+        break;
+    }
+    case 6: {  // VarTrimmedDist
+        const T minR = (T)p0, maxR = (T)p1, lam = (T)p2;
+        if (!(minR < maxR)) return fail(c, PMX_E_BAD_PARAM, "VarTrimmedDistOutlierFilter: minRatio should be smaller than maxRatio");
+        const T* dsrc = d;
+        int64_t nsrc = n;
+        if (c->comm && c->nranks > 1) {
+            const int64_t per = c->N_max * c->knn;
+            const size_t need = sizeof(T) * (size_t)per * (c->nranks + 1);
+            if ((rc = ensure(c, &c->d_gather, &c->gather_bytes, need))) return rc;
+            T* send = (T*)c->d_gather + (size_t)per * c->nranks;
+            // local shard, padded with +inf (excluded by the filter) to the largest shard
+            HIPCHK(c, hipMemcpyAsync(send, d, sizeof(T) * n, hipMemcpyDeviceToDevice, c->stream));
+            if (per > n) {
+                std::vector<T> inf((size_t)(per - n), std::numeric_limits<T>::infinity());
+                HIPCHK(c, hipMemcpyAsync(send + n, inf.data(), sizeof(T) * (per - n), hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+            }
+            NCCLCHK(c, ncclAllGather(send, c->d_gather, (size_t)per, (ncclDataType_t)ncclType<T>(), c->comm, c->stream));
+            dsrc = (const T*)c->d_gather;
+            nsrc = per * c->nranks;
+        }
+        const int points_nbr = (int)(c->N_total * c->knn);
+        const int minEl = (int)std::floor(minR * (T)points_nbr);
+        const int maxEl = (int)std::floor(maxR * (T)points_nbr);
+        const int cnt = maxEl - minEl;
+        if (cnt <= 0) return fail(c, PMX_E_BAD_PARAM, "VarTrimmedDistOutlierFilter: empty ratio range");
+        if (c->deno_pts != points_nbr || c->deno_min != minEl || c->deno_max != maxEl ||
+            !(c->deno_lambda == (double)lam)) {
+            // pow(id / points_nbr, lambda) in T on the host: the same libm call
+            // as the reference's Eigen array pow (OutlierFiltersImpl.cpp:209)
+            std::vector<T> tab((size_t)cnt);
+            for (int j = 0; j < cnt; ++j) {
+                const T id = (T)(minEl + 1 + j);
+                const T ratio = id / (T)points_nbr;
+                tab[j] = std::pow(ratio, lam);
+            }
+            if ((rc = ensure(c, &c->d_deno, &c->deno_bytes, sizeof(T) * cnt))) return rc;
+            HIPCHK(c, hipMemcpyAsync(c->d_deno, tab.data(), sizeof(T) * cnt, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            c->deno_pts = points_nbr;
+            c->deno_min = minEl;
+            c->deno_max = maxEl;
+            c->deno_lambda = (double)lam;
+        }
+        const size_t need = vartrim_scratch_bytes<T>(nsrc);
+        if ((rc = ensure(c, &c->d_vt, &c->vt_bytes, need))) return rc;
+        launch_vartrim<T>(dsrc, nsrc, points_nbr, minR, maxR, (const T*)c->d_deno, c->d_vt, c->vt_bytes, c->d_ratio,
+                          c->d_iter_err, c->stream);
+        HIPCHK(c, hipGetLastError());
+        if ((rc = quantile_select<T>(c, d, n, 0.0, c->d_ratio))) return rc;
+        launch_weights_state<T>(d, w, n, c->d_sel, (T)1, mul, c->stream);
+        break;
+    }
+    default:
+        return fail(c, PMX_E_BAD_PARAM, "unknown outlier filter");
+    }
+    HIPCHK(c, hipGetLastError());
+    return PMX_OK;
+}
+
+// -------------------------------------------------------------- minimizers --
+void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double rm, double rp, double sw,
+                double limit) {
+    if (!st) return;
+    st->kept = (int64_t)kept;
+    st->nonzero_weights = (int64_t)nz;
+    st->rejected_matches = (int64_t)rm;
+    st->rejected_points = (int64_t)rp;
+    st->sum_w = sw;
+    st->limit = limit;
+    st->n_total = c->N_total * c->knn;
+}
+
+template <typename T>
+int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
+    int rc = check_match(c);
+    if (rc) return rc;
+    if (!c->has_normals)
+        return fail(c, PMX_E_BAD_PARAM, "PointToPlaneErrorMinimizer requires \"normals\" on the reference");
+    const int NF = c->dim == 3 ? 6 : 3;
+    const int NV = NF * NF + NF + 5;
+    Mat4<T> Tm = step_mat<T>(c);
+    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)c->d_ref, (const P4<T>*)c->d_nrm,
+                              (const T*)c->d_dists, c->d_ids, (const T*)c->d_w, c->knn, c->N, c->dim, c->d_partials,
+                              c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, c->stream);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = allreduce_f64(c, c->d_result, NV))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_result, c->d_result, sizeof(double) * NV, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_result + 64, c->d_iter_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_result + 65, &c->d_sel->limit, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    resolve_events(c);
+    const double* r = c->h_result;
+    int ierr = 0;
+    std::memcpy(&ierr, &r[64], sizeof(int));
+    const int o = NF * NF + NF;
+    fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 4], r[65]);
+    if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
+    if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
+    if (r[o + 1] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
+    if (r[o + 0] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
+    for (int i = 0; i < NF * NF; ++i) A[i] = r[i];
+    for (int i = 0; i < NF; ++i) b[i] = -r[NF * NF + i];
+    return PMX_OK;
+}
+
+template <typename T>
+int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stats* st) {
+    int rc = check_match(c);
+    if (rc) return rc;
+    Mat4<T> Tm = step_mat<T>(c);
+    launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)c->d_ref, (const T*)c->d_dists, c->d_ids,
+                            (const T*)c->d_w, c->knn, c->N, c->d_partials, c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, c->stream);
+    if ((rc = allreduce_f64(c, c->d_result, 11))) return rc;
+    launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, c->stream);
+    launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)c->d_ref, (const T*)c->d_dists, c->d_ids,
+                            (const T*)c->d_w, c->knn, c->N, (const T*)c->d_means, c->d_partials, c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, c->stream);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = allreduce_f64(c, c->d_result + 16, 9))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_result, c->d_result, sizeof(double) * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_result + 32, c->d_means, sizeof(T) * 6, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_result + 64, c->d_iter_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_result + 65, &c->d_sel->limit, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    resolve_events(c);
+    const double* r = c->h_result;
+    int ierr = 0;
+    std::memcpy(&ierr, &r[64], sizeof(int));
+    fill_stats(c, st, r[7], r[8], r[9], r[10], r[0], r[65]);
+    if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
+    if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
+    if (r[8] == 0.0 || r[7] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
+    T means[6];
+    std::memcpy(means, &r[32], sizeof(T) * 6);
+    const int D = c->dim;
+    for (int i = 0; i < D; ++i) {
+        mean_p[i] = (double)means[i];
+        mean_q[i] = (double)means[3 + i];
+    }
+    for (int i = 0; i < D; ++i)
+        for (int j = 0; j < D; ++j) m[i * D + j] = r[16 + i * 3 + j];
+    return PMX_OK;
+}
+
+template <typename T>
+int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
+    int rc = check_match(c);
+    if (rc) return rc;
+    const int64_t n = c->N * c->knn;
+    if (dists) HIPCHK(c, hipMemcpyAsync(dists, c->d_dists, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
+    if (ids) HIPCHK(c, hipMemcpyAsync(ids, c->d_ids, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
+template <typename T>
+int get_weights_impl(pmx_ctx* c, void* w) {
+    int rc = check_match(c);
+    if (rc) return rc;
+    const int64_t n = c->N * c->knn;
+    HIPCHK(c, hipMemcpyAsync(w, c->d_w, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char* pmx_version(void) { return "pmx 0.1 (HIP, gfx950)"; }
+
+int pmx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* pmx_last_error(const pmx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
+    if (!out) return PMX_E_BAD_PARAM;
+    *out = nullptr;
+    if (dtype != PMX_F32 && dtype != PMX_F64) return PMX_E_BAD_PARAM;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return PMX_E_NO_DEVICE;
+    if (device < 0 || device >= n) return PMX_E_BAD_PARAM;
+    pmx_ctx* c = new pmx_ctx();
+    c->device = device;
+    c->dtype = dtype;
+    auto bad = [&](int code) {
+        pmx_ctx_destroy(c);
+        return code;
+    };
+    if (hipSetDevice(device) != hipSuccess) return bad(PMX_E_HIP);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cu_count = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bad(PMX_E_HIP);
+    // SelectState followed by the per-iteration error word (see launch_select_pick)
+    void* p = nullptr;
+    if (hipMalloc(&p, 256) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(p, 0, 256);
+    c->d_sel = (SelectState*)p;
+    c->d_iter_err = (int*)(c->d_sel + 1);
+    c->d_ratio = (double*)((char*)p + 128);
+    if (hipMalloc((void**)&c->d_hist, 2048 * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_hist, 0, 2048 * sizeof(uint32_t));
+    if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
+    if (hipMalloc((void**)&c->d_result, sizeof(double) * 128) != hipSuccess) return bad(PMX_E_HIP);
+    if (hipMalloc(&c->d_means, 64) != hipSuccess) return bad(PMX_E_HIP);
+    if (hipHostMalloc((void**)&c->h_result, sizeof(double) * 128, hipHostMallocDefault) != hipSuccess)
+        return bad(PMX_E_HIP);
+    *out = c;
+    return PMX_OK;
+}
+
+int pmx_ctx_destroy(pmx_ctx* c) {
+    if (!c) return PMX_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
+                    c->d_part_i, c->d_sel,    c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
+                    c->d_result, c->d_means};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->h_result) (void)hipHostFree(c->h_result);
+    for (auto& pr : c->ev_pending) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return PMX_OK;
+}
+
+int pmx_comm_unique_id(void* out128) {
+    if (!out128) return PMX_E_BAD_PARAM;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return PMX_E_RCCL;
+    std::memcpy(out128, &id, sizeof(id));
+    return PMX_OK;
+}
+
+int pmx_comm_init(pmx_ctx* c, const void* uid128, int nranks, int rank) {
+    if (!c || !uid128 || nranks < 1 || rank < 0 || rank >= nranks) return fail(c, PMX_E_BAD_PARAM, "bad comm args");
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(&id, uid128, sizeof(id));
+    NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return PMX_OK;
+}
+
+#define DISPATCH(c, call_f, call_d) ((c)->dtype == PMX_F64 ? (call_d) : (call_f))
+
+int pmx_set_reference(pmx_ctx* c, const void* feat, int rows, int64_t M, const void* normals) {
+    if (!c || !feat) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c, set_reference_impl<float>(c, (const float*)feat, rows, M, (const float*)normals),
+                    set_reference_impl<double>(c, (const double*)feat, rows, M, (const double*)normals));
+}
+
+int pmx_set_reading(pmx_ctx* c, const void* feat, int rows, int64_t N, const void* T0) {
+    if (!c || (!feat && N > 0) || !T0) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c, set_reading_impl<float>(c, (const float*)feat, rows, N, (const float*)T0),
+                    set_reading_impl<double>(c, (const double*)feat, rows, N, (const double*)T0));
+}
+
+int pmx_match(pmx_ctx* c, const void* T_iter, int knn, double maxDist, double epsilon, uint64_t* visited) {
+    if (!c || !T_iter) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    if (!(epsilon >= 0)) return fail(c, PMX_E_BAD_PARAM, "epsilon must be >= 0");
+    return DISPATCH(c, match_impl<float>(c, (const float*)T_iter, knn, maxDist, visited),
+                    match_impl<double>(c, (const double*)T_iter, knn, maxDist, visited));
+}
+
+#define OUTLIER(c, kind, pos, a, b, d)                                                     \
+    ((c) ? DISPATCH(c, outlier_impl<float>(c, kind, pos, a, b, d), outlier_impl<double>(c, kind, pos, a, b, d)) \
+         : PMX_E_BAD_PARAM)
+
+int pmx_outlier_default(pmx_ctx* c) { return OUTLIER(c, 0, 0, 0, 0, 0); }
+int pmx_outlier_null(pmx_ctx* c, int pos) { return OUTLIER(c, 1, pos, 0, 0, 0); }
+int pmx_outlier_maxdist(pmx_ctx* c, int pos, double m) { return OUTLIER(c, 2, pos, m, 0, 0); }
+int pmx_outlier_mindist(pmx_ctx* c, int pos, double m) { return OUTLIER(c, 3, pos, m, 0, 0); }
+int pmx_outlier_mediandist(pmx_ctx* c, int pos, double f) { return OUTLIER(c, 4, pos, f, 0, 0); }
+int pmx_outlier_trimmed(pmx_ctx* c, int pos, double r) { return OUTLIER(c, 5, pos, r, 0, 0); }
+int pmx_outlier_vartrimmed(pmx_ctx* c, int pos, double a, double b, double l) { return OUTLIER(c, 6, pos, a, b, l); }
+
+int pmx_p2plane_system(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
+    if (!c || !A || !b) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return DISPATCH(c, p2plane_impl<float>(c, A, b, st), p2plane_impl<double>(c, A, b, st));
+}
+
+int pmx_p2point_system(pmx_ctx* c, double* mp, double* mq, double* m, pmx_stats* st) {
+    if (!c || !mp || !mq || !m) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return DISPATCH(c, p2point_impl<float>(c, mp, mq, m, st), p2point_impl<double>(c, mp, mq, m, st));
+}
+
+int pmx_get_matches(pmx_ctx* c, void* dists, int32_t* ids) {
+    if (!c) return PMX_E_BAD_PARAM;
+    return DISPATCH(c, get_matches_impl<float>(c, dists, ids), get_matches_impl<double>(c, dists, ids));
+}
+
+int pmx_get_weights(pmx_ctx* c, void* w) {
+    if (!c || !w) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return DISPATCH(c, get_weights_impl<float>(c, w), get_weights_impl<double>(c, w));
+}
+
+int pmx_get_shape(const pmx_ctx* c, int64_t* n_local, int* knn) {
+    if (!c) return PMX_E_BAD_PARAM;
+    if (n_local) *n_local = c->N;
+    if (knn) *knn = c->knn;
+    return PMX_OK;
+}
+
+int pmx_timing_enable(pmx_ctx* c, int on) {
+    if (!c) return PMX_E_BAD_PARAM;
+    c->timing = on != 0;
+    c->match_ms = 0.0;
+    c->match_launches = 0;
+    return PMX_OK;
+}
+
+int pmx_timing_read(pmx_ctx* c, double* match_ms, int64_t* launches, double* other_ms) {
+    if (!c) return PMX_E_BAD_PARAM;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    resolve_events(c);
+    if (match_ms) *match_ms = c->match_ms;
+    if (launches) *launches = c->match_launches;
+    if (other_ms) *other_ms = 0.0;
+    return PMX_OK;
+}
+
+int pmx_sync(pmx_ctx* c) {
+    if (!c) return PMX_E_BAD_PARAM;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
+}  // extern "C"

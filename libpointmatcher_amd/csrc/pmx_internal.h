@@ -1,0 +1,113 @@
+// pmx_internal.h — shared device types and launcher declarations for libpmx.
+//
+// HBM layout:
+//   reference  P4<T>[M_pad]  (x, y, z, h) — AoS, 16 B (f32) / 32 B (f64) per
+//              point, padded with +inf points to a multiple of kTile so every
+//              LDS tile load is full and branch-free;
+//   normals    P4<T>[M]      (nx, ny, nz, 0);
+//   reading    P4<T>[N]      already transformed by T_refMean_dataIn;
+//   dists / weights T[N * k], ids int32[N * k], point-major (the memory order
+//              of the reference's column-major k x N Eigen matrices).
+// 2-D clouds (rows = 3) are embedded as (x, y, 0, h) with the 3x3 transform
+// embedded in a 4x4; adding the +0 z-term is exact, so distances equal the
+// 2-D sums bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace pmx {
+
+template <typename T>
+struct alignas(4 * sizeof(T)) P4 {
+    T x, y, z, w;
+};
+
+template <typename T>
+struct Mat4 {
+    T m[16];  // row-major
+};
+
+constexpr int kBlock = 256;   // threads per block (4 waves of 64)
+constexpr int kTile = 1024;   // reference points per LDS tile
+constexpr int kSub = 32;      // sub-block of the min-then-rescan k=1 scheme
+
+// device-side select state for quantile filters (one per context)
+struct SelectState {
+    unsigned long long prefix;   // key bits resolved so far
+    unsigned long long rank;     // rank still to find inside the current prefix
+    unsigned long long count;    // number of finite keys (global)
+    double limit;                // resolved threshold (T value)
+    double ratio;                // quantile ratio (T value)
+    int err;                     // PMX_E_EMPTY_QUANTILE etc.
+    int pad;
+};
+
+// ---- match (pmx_match.hip) ----
+template <typename T>
+void launch_match(const P4<T>* ref, int64_t M_pad, const P4<T>* rd, int64_t N, const Mat4<T>& Tm,
+                  int knn, T maxR2, T* dists, int32_t* ids, T* part_d, int32_t* part_i,
+                  int64_t part_cap, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, int cu_count);
+template <typename T>
+int64_t match_part_elems(int64_t N, int64_t M_pad, int knn, int cu_count);
+
+template <typename T>
+void launch_transform(const P4<T>* in, P4<T>* out, int64_t N, const Mat4<T>& Tm, hipStream_t s);
+
+// ---- quantile / weights (pmx_select.hip) ----
+enum WeightOp { kWAssign = 0, kWMul = 1 };
+template <typename T>
+void launch_weights_default(const T* d, T* w, int64_t n, hipStream_t s);
+template <typename T>
+void launch_weights_const(T* w, int64_t n, int mul, hipStream_t s);
+template <typename T>
+void launch_weights_cmp(const T* d, T* w, int64_t n, T thr, int ge, int mul, hipStream_t s);
+// threshold from the select state: w = (d <= scale * state.limit)
+template <typename T>
+void launch_weights_state(const T* d, T* w, int64_t n, const SelectState* st, T scale, int mul,
+                          hipStream_t s);
+
+// one radix-select pass: histogram of digit `pass` among keys matching the
+// resolved prefix.  hist must be zero on entry (select zeroes it on exit).
+template <typename T>
+void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass,
+                        hipStream_t s);
+// resolve the digit of `pass`; pass 0 also computes count and the target
+// rank from ratio (host value, or *ratio_dev when non-null).
+template <typename T>
+void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
+                        const double* ratio_dev, hipStream_t s);
+template <typename T>
+int select_passes();
+int select_bins(int pass, int key_bits);
+
+// VarTrimmed pieces
+template <typename T>
+void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRatio, const T* deno,
+                    void* scratch, size_t scratch_bytes, double* ratio_dev, int* err_dev,
+                    hipStream_t s);
+template <typename T>
+size_t vartrim_scratch_bytes(int64_t n);
+
+// ---- reductions (pmx_reduce.hip) ----
+constexpr int kRedBlocks = 1024;
+constexpr int kNV3 = 36 + 6 + 5;  // A(36) + b(6) + kept, nz, rejM, rejP, sumw
+constexpr int kNV2 = 9 + 3 + 5;
+constexpr int kNVMax = 48;
+template <typename T>
+void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm,
+                            const T* d, const int32_t* ids, const T* w, int k, int64_t N, int dim,
+                            double* partials, hipStream_t s);
+void launch_finalize(const double* partials, int nblocks, int nv, double* out, hipStream_t s);
+template <typename T>
+void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
+                          const int32_t* ids, const T* w, int k, int64_t N, double* partials,
+                          hipStream_t s);
+template <typename T>
+void launch_p2point_means(const double* sums, T* means_dev, int dim, hipStream_t s);
+template <typename T>
+void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
+                          const int32_t* ids, const T* w, int k, int64_t N, const T* means_dev,
+                          double* partials, hipStream_t s);
+
+}  // namespace pmx

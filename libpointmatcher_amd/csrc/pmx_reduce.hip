@@ -1,0 +1,279 @@
+// pmx_reduce.hip — error-minimiser reductions (normal equations) on the device.
+//
+// Replaces ErrorElements (pointmatcher/ErrorMinimizer.cpp:58-193: compaction
+// of the kept pairs + gather of the matched reference points) and the dense
+// parts of PointToPlaneErrorMinimizer::compute_in_place
+// (ErrorMinimizers/PointToPlane.cpp:171-243, crossProduct
+// ErrorMinimizer.cpp:281-315) and PointToPointErrorMinimizer::compute_in_place
+// (ErrorMinimizers/PointToPoint.cpp:61-81).  Nothing is compacted: each lane
+// walks its points, skips dist == inf, counts w == 0 as a rejected match, and
+// for kept pairs gathers q = ref[id], n = normal[id] and adds the T-precision
+// products of the reference's formulas into fp64 accumulators:
+//   F = [p x n ; n]  (3-D),  F = [p_x n_y - p_y n_x ; n]  (2-D)
+//   A_rc += (w F_r) F_c      (full matrix: Eigen's wF * F^T is not symmetrised)
+//   b_r  += (w F_r) dot,     dot = ((dx n_x + dy n_y) + dz n_z), d = p - q
+// Per-block partials (fixed 1024-block grid, fixed lane order) are summed by
+// one finalisation block in block order, so results are deterministic.
+// These kernels are HBM/latency-bound: ~60 B per pair (reading 16, dist 4,
+// id 4, weight 4, gathered point 16, gathered normal 16).
+#include "pmx_internal.h"
+
+namespace pmx {
+
+template <typename T>
+__device__ __forceinline__ void xform3(const Mat4<T>& M, const P4<T>& p, T& x, T& y, T& z) {
+    x = ((M.m[0] * p.x + M.m[1] * p.y) + M.m[2] * p.z) + M.m[3] * p.w;
+    y = ((M.m[4] * p.x + M.m[5] * p.y) + M.m[6] * p.z) + M.m[7] * p.w;
+    z = ((M.m[8] * p.x + M.m[9] * p.y) + M.m[10] * p.z) + M.m[11] * p.w;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// block reduction of NV accumulators; writes partials[blockIdx.x * NV + v]
+template <int NV>
+__device__ __forceinline__ void block_store(double (&acc)[NV], double* __restrict__ partials) {
+    __shared__ double red[4][NV];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double s = wave_sum(acc[v]);
+        if (lane == 0) red[wave][v] = s;
+    }
+    __syncthreads();
+    for (int v = threadIdx.x; v < NV; v += blockDim.x)
+        partials[(int64_t)blockIdx.x * NV + v] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+}
+
+template <typename T, int DIM>
+__global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
+                                                              const P4<T>* __restrict__ ref,
+                                                              const P4<T>* __restrict__ nrm, const T* __restrict__ d,
+                                                              const int32_t* __restrict__ ids,
+                                                              const T* __restrict__ w, int k, int64_t N,
+                                                              double* __restrict__ partials) {
+    constexpr int NF = DIM == 3 ? 6 : 3;
+    constexpr int NA = NF * NF;
+    constexpr int NV = NA + NF + 5;
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const T inf = (T)__builtin_huge_val();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+        T px, py, pz;
+        xform3(Tm, rd[i], px, py, pz);
+        bool exist = false;
+        for (int s = 0; s < k; ++s) {
+            const int64_t e = i * k + s;
+            const T dv = d[e];
+            const T wv = w[e];
+            if (wv != (T)0) acc[NA + NF + 1] += 1.0;  // (w != 0).count()
+            if (dv == inf) continue;
+            if (wv == (T)0) {
+                acc[NA + NF + 2] += 1.0;  // rejected match
+                continue;
+            }
+            exist = true;
+            acc[NA + NF + 0] += 1.0;  // kept
+            acc[NA + NF + 4] += (double)wv;
+            const int32_t id = ids[e];
+            const P4<T> q = ref[id];
+            const P4<T> n = nrm[id];
+            T F[NF];
+            T dot;
+            if (DIM == 3) {
+                F[0] = py * n.z - pz * n.y;
+                F[1] = pz * n.x - px * n.z;
+                F[2] = px * n.y - py * n.x;
+                F[3] = n.x;
+                F[4] = n.y;
+                F[5] = n.z;
+                dot = ((px - q.x) * n.x + (py - q.y) * n.y) + (pz - q.z) * n.z;
+            } else {
+                F[0] = px * n.y - py * n.x;
+                F[1] = n.x;
+                F[2] = n.y;
+                dot = (px - q.x) * n.x + (py - q.y) * n.y;
+            }
+#pragma unroll
+            for (int r = 0; r < NF; ++r) {
+                const T wF = wv * F[r];
+#pragma unroll
+                for (int c = 0; c < NF; ++c) acc[r * NF + c] += (double)(wF * F[c]);
+                acc[NA + r] += (double)(wF * dot);
+            }
+        }
+        if (!exist) acc[NA + NF + 3] += 1.0;  // rejected point
+    }
+    block_store<NV>(acc, partials);
+}
+
+template <typename T>
+void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, const T* d,
+                            const int32_t* ids, const T* w, int k, int64_t N, int dim, double* partials,
+                            hipStream_t s) {
+    if (dim == 3)
+        hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
+                           ids, w, k, N, partials);
+    else
+        hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
+                           ids, w, k, N, partials);
+}
+
+// sum the per-block partials in block order (deterministic)
+__global__ void finalize_kernel(const double* __restrict__ partials, int nblocks, int nv, double* __restrict__ out) {
+    const int v = threadIdx.x;
+    if (v >= nv) return;
+    double s = 0.0;
+    for (int b = 0; b < nblocks; ++b) s += partials[(int64_t)b * nv + v];
+    out[v] = s;
+}
+
+void launch_finalize(const double* partials, int nblocks, int nv, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partials, nblocks, nv, out);
+}
+
+// ------------------------------------------------------------ point-to-point --
+// pass 1: sum w, sum p*w, sum q*w (PointToPoint.cpp:67-72) + ErrorElements counts
+// layout: [0] sw, [1..3] sp, [4..6] sq, [7] kept, [8] nz, [9] rejM, [10] rejP
+template <typename T>
+__global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
+                                                            const P4<T>* __restrict__ ref, const T* __restrict__ d,
+                                                            const int32_t* __restrict__ ids,
+                                                            const T* __restrict__ w, int k, int64_t N,
+                                                            double* __restrict__ partials) {
+    constexpr int NV = 11;
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const T inf = (T)__builtin_huge_val();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+        T px, py, pz;
+        xform3(Tm, rd[i], px, py, pz);
+        bool exist = false;
+        for (int s = 0; s < k; ++s) {
+            const int64_t e = i * k + s;
+            const T dv = d[e];
+            const T wv = w[e];
+            if (wv != (T)0) acc[8] += 1.0;
+            if (dv == inf) continue;
+            if (wv == (T)0) {
+                acc[9] += 1.0;
+                continue;
+            }
+            exist = true;
+            acc[7] += 1.0;
+            const P4<T> q = ref[ids[e]];
+            acc[0] += (double)wv;
+            acc[1] += (double)(px * wv);
+            acc[2] += (double)(py * wv);
+            acc[3] += (double)(pz * wv);
+            acc[4] += (double)(q.x * wv);
+            acc[5] += (double)(q.y * wv);
+            acc[6] += (double)(q.z * wv);
+        }
+        if (!exist) acc[10] += 1.0;
+    }
+    block_store<NV>(acc, partials);
+}
+
+template <typename T>
+void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
+                          const T* w, int k, int64_t N, double* partials, hipStream_t s) {
+    hipLaunchKernelGGL(p2point_pass1_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, w, k, N,
+                       partials);
+}
+
+// means in T: w_sum_inv = 1 / w.sum(); mean = sum * w_sum_inv (PointToPoint.cpp:67-72)
+template <typename T>
+__global__ void p2point_means_kernel(const double* __restrict__ sums, T* __restrict__ means, int dim) {
+    if (threadIdx.x != 0) return;
+    const T winv = (T)1 / (T)sums[0];
+    for (int r = 0; r < 3; ++r) {
+        means[r] = r < dim ? (T)sums[1 + r] * winv : (T)0;
+        means[3 + r] = r < dim ? (T)sums[4 + r] * winv : (T)0;
+    }
+}
+
+template <typename T>
+void launch_p2point_means(const double* sums, T* means_dev, int dim, hipStream_t s) {
+    hipLaunchKernelGGL(p2point_means_kernel<T>, dim3(1), dim3(64), 0, s, sums, means_dev, dim);
+}
+
+// pass 2: m = sum (qc * w) pc^T  (PointToPoint.cpp:76-81), 3x3 (2-D uses the
+// top-left 2x2; z terms are exactly zero)
+template <typename T>
+__global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
+                                                            const P4<T>* __restrict__ ref, const T* __restrict__ d,
+                                                            const int32_t* __restrict__ ids,
+                                                            const T* __restrict__ w, int k, int64_t N,
+                                                            const T* __restrict__ means,
+                                                            double* __restrict__ partials) {
+    constexpr int NV = 9;
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const T inf = (T)__builtin_huge_val();
+    const T mp[3] = {means[0], means[1], means[2]};
+    const T mq[3] = {means[3], means[4], means[5]};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+        T p[3];
+        xform3(Tm, rd[i], p[0], p[1], p[2]);
+        for (int s = 0; s < k; ++s) {
+            const int64_t e = i * k + s;
+            const T wv = w[e];
+            if (d[e] == inf || wv == (T)0) continue;
+            const P4<T> q4 = ref[ids[e]];
+            const T q[3] = {q4.x, q4.y, q4.z};
+            T pc[3], qc[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                pc[r] = p[r] - mp[r];
+                qc[r] = q[r] - mq[r];
+            }
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const T qw = qc[r] * wv;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[r * 3 + c] += (double)(qw * pc[c]);
+            }
+        }
+    }
+    block_store<NV>(acc, partials);
+}
+
+template <typename T>
+void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
+                          const T* w, int k, int64_t N, const T* means_dev, double* partials, hipStream_t s) {
+    hipLaunchKernelGGL(p2point_pass2_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, w, k, N,
+                       means_dev, partials);
+}
+
+template void launch_p2plane_partial<float>(const P4<float>*, const Mat4<float>&, const P4<float>*,
+                                            const P4<float>*, const float*, const int32_t*, const float*, int,
+                                            int64_t, int, double*, hipStream_t);
+template void launch_p2plane_partial<double>(const P4<double>*, const Mat4<double>&, const P4<double>*,
+                                             const P4<double>*, const double*, const int32_t*, const double*, int,
+                                             int64_t, int, double*, hipStream_t);
+template void launch_p2point_pass1<float>(const P4<float>*, const Mat4<float>&, const P4<float>*, const float*,
+                                          const int32_t*, const float*, int, int64_t, double*, hipStream_t);
+template void launch_p2point_pass1<double>(const P4<double>*, const Mat4<double>&, const P4<double>*,
+                                           const double*, const int32_t*, const double*, int, int64_t, double*,
+                                           hipStream_t);
+template void launch_p2point_means<float>(const double*, float*, int, hipStream_t);
+template void launch_p2point_means<double>(const double*, double*, int, hipStream_t);
+template void launch_p2point_pass2<float>(const P4<float>*, const Mat4<float>&, const P4<float>*, const float*,
+                                          const int32_t*, const float*, int, int64_t, const float*, double*,
+                                          hipStream_t);
+template void launch_p2point_pass2<double>(const P4<double>*, const Mat4<double>&, const P4<double>*,
+                                           const double*, const int32_t*, const double*, int, int64_t,
+                                           const double*, double*, hipStream_t);
+
+}  // namespace pmx

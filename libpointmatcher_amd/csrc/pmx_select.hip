@@ -1,0 +1,525 @@
+// pmx_select.hip — outlier weighting on the device.
+//
+// Replaces OutlierFiltersImpl.cpp:51-223 and Matches::getDistsQuantile
+// (Matches.cpp:60-87).  The reference copies the finite distances into a
+// std::vector and runs nth_element; here the exact order statistic is found
+// by a most-significant-digit radix select on the IEEE bit patterns (squared
+// distances are >= +0, so the unsigned bit order is the numeric order; +inf
+// and NaN keys are excluded exactly as `dists != inf` excludes them).  Each
+// pass is one streaming histogram kernel (k*N*sizeof(T) bytes, HBM-bound) and
+// one single-block "pick" kernel; with several ranks the 2048-bin histogram is
+// all-reduced between the two (pmx_capi.hip), which makes the select exact
+// over the global, sharded match set.
+//
+// Index rule (Matches.cpp:83-86): target = (size_t)((T)count * ratio) over the
+// finite distances, ratio == 1 -> maximum; the weight is (dist <= value).
+//
+// VarTrimmedDist (OutlierFiltersImpl.cpp:166-220): compaction of the finite
+// positive distances, a device LSD radix sort, the sequential std::partial_sum
+// in T (one wave, bit-identical to the CPU), the FRMS curve and a first-index
+// argmin, then the same radix select with the optimised ratio.
+#include "pmx_internal.h"
+
+#include <cmath>
+
+namespace pmx {
+
+template <typename T>
+struct KeyOf;
+template <>
+struct KeyOf<float> {
+    using K = uint32_t;
+    static constexpr int bits = 32;
+    static __device__ __forceinline__ K key(float v) { return __float_as_uint(v); }
+    static __device__ __forceinline__ float val(K k) { return __uint_as_float(k); }
+    static constexpr K inf_key = 0x7F800000u;
+};
+template <>
+struct KeyOf<double> {
+    using K = unsigned long long;
+    static constexpr int bits = 64;
+    static __device__ __forceinline__ K key(double v) { return (K)__double_as_longlong(v); }
+    static __device__ __forceinline__ double val(K k) { return __longlong_as_double((long long)k); }
+    static constexpr K inf_key = 0x7FF0000000000000ull;
+};
+
+// digit layout: 11-bit digits from the top, the last one(s) 10-bit
+// f32: [31:21] [20:10] [9:0]          f64: [63:53] [52:42] [41:31] [30:20] [19:10] [9:0]
+__host__ __device__ inline void digit_of(int key_bits, int pass, int& shift, int& bits) {
+    if (key_bits == 32) {
+        const int sh[3] = {21, 10, 0};
+        const int bt[3] = {11, 11, 10};
+        shift = sh[pass];
+        bits = bt[pass];
+    } else {
+        const int sh[6] = {53, 42, 31, 20, 10, 0};
+        const int bt[6] = {11, 11, 11, 11, 10, 10};
+        shift = sh[pass];
+        bits = bt[pass];
+    }
+}
+
+int select_bins(int pass, int key_bits) {
+    int sh, bt;
+    digit_of(key_bits, pass, sh, bt);
+    return 1 << bt;
+}
+template <>
+int select_passes<float>() {
+    return 3;
+}
+template <>
+int select_passes<double>() {
+    return 6;
+}
+
+// ------------------------------------------------------------- histogram --
+template <typename T>
+__global__ __launch_bounds__(256) void select_hist_kernel(const T* __restrict__ d, int64_t n,
+                                                          uint32_t* __restrict__ hist,
+                                                          const SelectState* __restrict__ st, int pass) {
+    using KO = KeyOf<T>;
+    using K = typename KO::K;
+    __shared__ uint32_t lh[2048];
+    int shift, bits;
+    digit_of(KO::bits, pass, shift, bits);
+    const int nb = 1 << bits;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) lh[i] = 0;
+    __syncthreads();
+    const bool skip = st->err != 0;
+    const K prefix = (K)st->prefix;
+    const int hs = shift + bits;
+    if (!skip) {
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const K k = KO::key(d[i]);
+            if (k >= KO::inf_key) continue;  // +inf (and NaN) excluded, Matches.cpp:71
+            if (pass > 0 && (k >> hs) != prefix) continue;
+            atomicAdd(&lh[(uint32_t)(k >> shift) & (uint32_t)(nb - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+        const uint32_t c = lh[i];
+        if (c) atomicAdd(&hist[i], c);
+    }
+}
+
+template <typename T>
+void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass, hipStream_t s) {
+    int64_t g = (n + 256 * 8 - 1) / (256 * 8);
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(select_hist_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, n, hist, st, pass);
+}
+
+// ------------------------------------------------------------------ pick --
+// one block of 256 threads; each thread owns 8 consecutive bins
+template <typename T>
+__global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__ hist, SelectState* __restrict__ st,
+                                                          int pass, double ratio_host,
+                                                          const double* __restrict__ ratio_dev,
+                                                          int* __restrict__ iter_err, int last) {
+    using KO = KeyOf<T>;
+    using K = typename KO::K;
+    __shared__ unsigned long long part[256];
+    __shared__ unsigned long long s_rank;
+    __shared__ int s_err;
+    int shift, bits;
+    digit_of(KO::bits, pass, shift, bits);
+    const int nb = 1 << bits;
+    const int per = nb / 256;  // 8 or 4
+    const int t = threadIdx.x;
+    unsigned long long mine = 0;
+    for (int j = 0; j < per; ++j) mine += hist[t * per + j];
+    part[t] = mine;
+    __syncthreads();
+    // inclusive scan (Hillis-Steele) over 256 partials
+    for (int off = 1; off < 256; off <<= 1) {
+        unsigned long long v = t >= off ? part[t - off] : 0ull;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    if (t == 0) {
+        s_err = st->err;
+        if (pass == 0 && s_err == 0) {
+            const unsigned long long count = part[255];
+            st->count = count;
+            st->prefix = 0;
+            const T q = ratio_dev ? (T)(*ratio_dev) : (T)ratio_host;
+            st->ratio = (double)q;
+            if (count == 0) {
+                s_err = -2;  // PMX_E_EMPTY_QUANTILE: ConvergenceError("no outlier to filter")
+            } else if (q < (T)0 || q > (T)1) {
+                s_err = -3;  // ConvergenceError("quantile must be between 0 and 1")
+            } else if (q == (T)1) {
+                st->rank = count - 1;  // max_element
+            } else {
+                unsigned long long r = (unsigned long long)((T)count * q);
+                if (r >= count) r = count - 1;  // reference reads out of range (UB); clamp
+                st->rank = r;
+            }
+            if (s_err) {
+                st->err = s_err;
+                *iter_err = s_err;
+                st->limit = __builtin_nan("");
+            }
+        }
+        s_rank = st->rank;
+    }
+    __syncthreads();
+    if (s_err == 0) {
+        const unsigned long long rank = s_rank;
+        const unsigned long long excl = t > 0 ? part[t - 1] : 0ull;
+        if (rank >= excl && rank < part[t]) {
+            unsigned long long cum = excl;
+            for (int j = 0; j < per; ++j) {
+                const unsigned long long c = hist[t * per + j];
+                if (rank < cum + c) {
+                    const K digit = (K)(t * per + j);
+                    const K prefix = ((K)st->prefix << bits) | digit;
+                    st->prefix = (unsigned long long)prefix;
+                    st->rank = rank - cum;
+                    if (last) st->limit = (double)KO::val(prefix);
+                    break;
+                }
+                cum += c;
+            }
+        }
+    }
+    __syncthreads();
+    for (int j = 0; j < per; ++j) hist[t * per + j] = 0;  // ready for the next pass
+}
+
+template <typename T>
+void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio, const double* ratio_dev,
+                        hipStream_t s) {
+    // iter_err lives right after the state (see pmx_capi.hip)
+    int* iter_err = reinterpret_cast<int*>(st + 1);
+    const int last = pass == select_passes<T>() - 1;
+    hipLaunchKernelGGL(select_pick_kernel<T>, dim3(1), dim3(256), 0, s, hist, st, pass, ratio, ratio_dev,
+                       iter_err, last);
+}
+
+// ---------------------------------------------------------------- weights --
+template <typename T>
+__global__ void w_default_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        w[i] = d[i] == (T)__builtin_huge_val() ? (T)0 : (T)1;
+}
+template <typename T>
+__global__ void w_const_kernel(T* __restrict__ w, int64_t n, int mul) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        w[i] = mul ? w[i] * (T)1 : (T)1;
+}
+template <typename T>
+__global__ void w_cmp_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n, T thr, int ge, int mul) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const T v = (ge ? (d[i] >= thr) : (d[i] <= thr)) ? (T)1 : (T)0;
+        w[i] = mul ? w[i] * v : v;
+    }
+}
+template <typename T>
+__global__ void w_state_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n,
+                               const SelectState* __restrict__ st, T scale, int mul) {
+    const T thr = scale * (T)st->limit;  // MedianDist: factor * median (OutlierFiltersImpl.cpp:121-122)
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const T v = d[i] <= thr ? (T)1 : (T)0;
+        w[i] = mul ? w[i] * v : v;
+    }
+}
+
+static unsigned grid_for(int64_t n) {
+    int64_t g = (n + 1023) / 1024;
+    if (g < 1) g = 1;
+    if (g > 4096) g = 4096;
+    return (unsigned)g;
+}
+
+template <typename T>
+void launch_weights_default(const T* d, T* w, int64_t n, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(w_default_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, w, n);
+}
+template <typename T>
+void launch_weights_const(T* w, int64_t n, int mul, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(w_const_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, w, n, mul);
+}
+template <typename T>
+void launch_weights_cmp(const T* d, T* w, int64_t n, T thr, int ge, int mul, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(w_cmp_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, w, n, thr, ge, mul);
+}
+template <typename T>
+void launch_weights_state(const T* d, T* w, int64_t n, const SelectState* st, T scale, int mul, hipStream_t s) {
+    if (n > 0)
+        hipLaunchKernelGGL(w_state_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, w, n, st, scale, mul);
+}
+
+// ============================================================ VarTrimmed ==
+// scratch layout (bytes, 256-aligned pieces):
+//   [hdr: 64 B]   int count, int err
+//   keysA[n], keysB[n]   sort ping-pong (K)
+//   cum[n]               sequential partial sums (T)
+//   counts[256 * tiles], offsets[256 * tiles]  (uint32)
+// deno: host-computed table pow(id / points_nbr, lambda) in T (the same libm
+// call as the reference's Eigen pow, OutlierFiltersImpl.cpp:209)
+constexpr int kRsItems = 16;
+constexpr int kRsTile = 256 * kRsItems;
+
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+template <typename T>
+size_t vartrim_scratch_bytes(int64_t n) {
+    using K = typename KeyOf<T>::K;
+    const int64_t tiles = (n + kRsTile - 1) / kRsTile + 1;
+    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(4 * 256 * tiles);
+}
+
+template <typename T>
+__global__ void vt_compact_kernel(const T* __restrict__ d, int64_t n, typename KeyOf<T>::K* __restrict__ keys,
+                                  int* __restrict__ count) {
+    using KO = KeyOf<T>;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const T v = d[i];
+        if (v != (T)__builtin_huge_val() && v > (T)0) {  // OutlierFiltersImpl.cpp:186-188
+            const int p = atomicAdd(count, 1);
+            keys[p] = KO::key(v);
+        }
+    }
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void rs_count_kernel(const K* __restrict__ keys, const int* __restrict__ count,
+                                                       int shift, int tiles, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t lc[256];
+    lc[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t c = *count;
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    for (int it = 0; it < kRsItems; ++it) {
+        const int64_t i = base + it * 256 + threadIdx.x;
+        if (i < c) atomicAdd(&lc[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    counts[(int64_t)threadIdx.x * tiles + blockIdx.x] = lc[threadIdx.x];
+}
+
+// exclusive scan over 256*tiles counts (digit-major), one block of 1024
+__global__ __launch_bounds__(1024) void rs_scan_kernel(const uint32_t* __restrict__ counts, int64_t total,
+                                                       uint32_t* __restrict__ offsets) {
+    __shared__ uint32_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (total + 1023) / 1024;
+    const int64_t lo = t * per;
+    const int64_t hi = lo + per < total ? lo + per : total;
+    uint32_t s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += counts[i];
+    part[t] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = t > 0 ? part[t - 1] : 0u;
+    for (int64_t i = lo; i < hi; ++i) {
+        offsets[i] = run;
+        run += counts[i];
+    }
+}
+
+// stable scatter: keys of a tile are ranked in index order (round-major,
+// then lane) with wave ballots; per-digit running offsets live in LDS
+template <typename K>
+__global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ in, K* __restrict__ out,
+                                                         const int* __restrict__ count, int shift, int tiles,
+                                                         const uint32_t* __restrict__ offsets) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[4][256];
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    run[t] = offsets[(int64_t)t * tiles + blockIdx.x];
+    for (int w = 0; w < 4; ++w) wcnt[w][t] = 0;
+    __syncthreads();
+    const int64_t c = *count;
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int it = 0; it < kRsItems; ++it) {
+        const int64_t i = base + it * 256 + t;
+        const bool valid = i < c;
+        K key = valid ? in[i] : (K)0;
+        const uint32_t dg = (uint32_t)(key >> shift) & 255u;
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const unsigned long long bb = __ballot(valid && ((dg >> b) & 1u));
+            peers &= ((dg >> b) & 1u) ? bb : ~bb;
+        }
+        const int rank = __popcll(peers & lt);
+        if (valid && rank == 0) wcnt[wave][dg] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = run[dg] + (uint32_t)rank;
+            for (int w = 0; w < wave; ++w) pos += wcnt[w][dg];
+            out[pos] = key;
+        }
+        __syncthreads();
+        run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+        wcnt[0][t] = 0;
+        wcnt[1][t] = 0;
+        wcnt[2][t] = 0;
+        wcnt[3][t] = 0;
+        __syncthreads();
+    }
+}
+
+// std::partial_sum in T, strictly sequential (one wave; lane l publishes the
+// running sum after adding element l of each 64-chunk)
+template <typename T>
+__global__ __launch_bounds__(64) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
+                                                       const int* __restrict__ count, T* __restrict__ cum) {
+    using KO = KeyOf<T>;
+    const int lane = threadIdx.x;
+    const int64_t c = *count;
+    T acc = 0;
+    for (int64_t b = 0; b < c; b += 64) {
+        const int64_t i = b + lane;
+        const T v = i < c ? KO::val(keys[i]) : (T)0;
+        T mine = 0;
+        const int lim = (c - b) < 64 ? (int)(c - b) : 64;
+        for (int l = 0; l < lim; ++l) {
+            const T x = __shfl(v, l);
+            acc = acc + x;  // 0 + x == x exactly, so cum[0] = v[0] as in partial_sum
+            if (lane == l) mine = acc;
+        }
+        if (i < c) cum[i] = mine;
+    }
+}
+
+// FRMS_j = (cum[minEl+j] * (1/id)) * ((1/deno)^2), first argmin; writes the
+// optimised ratio (OutlierFiltersImpl.cpp:202-217)
+template <typename T>
+__global__ __launch_bounds__(1024) void vt_frms_kernel(const T* __restrict__ cum, const int* __restrict__ count,
+                                                       const T* __restrict__ deno, int minEl, int maxEl,
+                                                       int points_nbr, double* __restrict__ ratio_dev,
+                                                       int* __restrict__ err, int* __restrict__ iter_err) {
+    __shared__ T sv[1024];
+    __shared__ int si[1024];
+    const int t = threadIdx.x;
+    const int c = *count;
+    int hi = maxEl < c ? maxEl : c;  // reference reads past the filtered count (UB); build clamps
+    const int n = hi - minEl;
+    if (c == 0 || n <= 0) {
+        if (t == 0) {
+            const int e = c == 0 ? -2 : -3;
+            *err = e;
+            *iter_err = e;
+            *ratio_dev = __builtin_nan("");
+        }
+        return;
+    }
+    T bv = (T)__builtin_huge_val();
+    int bi = 0x7fffffff;
+    for (int j = t; j < n; j += 1024) {
+        const T id = (T)(minEl + 1 + j);
+        const T inv_id = (T)1 / id;
+        const T invd = (T)1 / deno[j];
+        const T f = (cum[minEl + j] * inv_id) * (invd * invd);
+        if (f < bv || (f == bv && j < bi)) {
+            bv = f;
+            bi = j;
+        }
+    }
+    sv[t] = bv;
+    si[t] = bi;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+        if (t < off) {
+            const T ov = sv[t + off];
+            const int oi = si[t + off];
+            if (ov < sv[t] || (ov == sv[t] && oi < si[t])) {
+                sv[t] = ov;
+                si[t] = oi;
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const int minIndex = si[0] == 0x7fffffff ? 0 : si[0];
+        *ratio_dev = (double)(T)((float)(minIndex + minEl) / (float)points_nbr);
+    }
+}
+
+template <typename T>
+void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRatio, const T* deno, void* scratch,
+                    size_t scratch_bytes, double* ratio_dev, int* err_dev, hipStream_t s) {
+    (void)scratch_bytes;
+    using K = typename KeyOf<T>::K;
+    char* p = static_cast<char*>(scratch);
+    int* hdr = reinterpret_cast<int*>(p);
+    p += 256;
+    K* keysA = reinterpret_cast<K*>(p);
+    p += al256(sizeof(K) * n);
+    K* keysB = reinterpret_cast<K*>(p);
+    p += al256(sizeof(K) * n);
+    T* cum = reinterpret_cast<T*>(p);
+    p += al256(sizeof(T) * n);
+    const int64_t tiles = (n + kRsTile - 1) / kRsTile + 1;
+    uint32_t* counts = reinterpret_cast<uint32_t*>(p);
+    p += al256(4 * 256 * tiles);
+    uint32_t* offsets = reinterpret_cast<uint32_t*>(p);
+    p += al256(4 * 256 * tiles);
+
+    (void)hipMemsetAsync(hdr, 0, 256, s);
+    if (n > 0)
+        hipLaunchKernelGGL(vt_compact_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr);
+    const int key_bits = KeyOf<T>::bits;
+    K* src = keysA;
+    K* dst = keysB;
+    for (int shift = 0; shift < key_bits; shift += 8) {
+        hipLaunchKernelGGL(rs_count_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, hdr, shift, (int)tiles,
+                           counts);
+        hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, counts, (int64_t)256 * tiles, offsets);
+        hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, dst, hdr, shift,
+                           (int)tiles, offsets);
+        K* tmp = src;
+        src = dst;
+        dst = tmp;
+    }
+    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(64), 0, s, src, hdr, cum);
+    const int minEl = (int)std::floor(minRatio * (T)points_nbr);
+    const int maxEl = (int)std::floor(maxRatio * (T)points_nbr);
+    hipLaunchKernelGGL(vt_frms_kernel<T>, dim3(1), dim3(1024), 0, s, cum, hdr, deno, minEl, maxEl, points_nbr,
+                       ratio_dev, hdr + 1, err_dev);
+}
+
+// explicit instantiations
+template void launch_select_hist<float>(const float*, int64_t, uint32_t*, const SelectState*, int, hipStream_t);
+template void launch_select_hist<double>(const double*, int64_t, uint32_t*, const SelectState*, int, hipStream_t);
+template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, const double*, hipStream_t);
+template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, hipStream_t);
+template void launch_weights_default<float>(const float*, float*, int64_t, hipStream_t);
+template void launch_weights_default<double>(const double*, double*, int64_t, hipStream_t);
+template void launch_weights_const<float>(float*, int64_t, int, hipStream_t);
+template void launch_weights_const<double>(double*, int64_t, int, hipStream_t);
+template void launch_weights_cmp<float>(const float*, float*, int64_t, float, int, int, hipStream_t);
+template void launch_weights_cmp<double>(const double*, double*, int64_t, double, int, int, hipStream_t);
+template void launch_weights_state<float>(const float*, float*, int64_t, const SelectState*, float, int,
+                                          hipStream_t);
+template void launch_weights_state<double>(const double*, double*, int64_t, const SelectState*, double, int,
+                                           hipStream_t);
+template void launch_vartrim<float>(const float*, int64_t, int, float, float, const float*, void*, size_t, double*,
+                                    int*, hipStream_t);
+template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,
+                                     double*, int*, hipStream_t);
+template size_t vartrim_scratch_bytes<float>(int64_t);
+template size_t vartrim_scratch_bytes<double>(int64_t);
+
+}  // namespace pmx

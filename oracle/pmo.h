@@ -1,0 +1,143 @@
+/*
+ * pmo — CPU ORACLE for the libpointmatcher ICP inner loop.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is a plain-C restatement of the reference
+ * CPU path (libpointmatcher v1.3.1 + the documented semantics of libnabo and
+ * Eigen, which are not vendored in /root/reference).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and
+ * only as the checker / the CPU baseline.  The product (libpointmatcher_amd)
+ * never links or calls it.
+ *
+ * Parity pinning: the reference's C++ cannot be compiled here (Eigen3, Boost
+ * and libnabo are absent), so this restatement is pinned by the reference's
+ * own known-answer tests and fixtures (utest/utest.cpp validT2d/validT3d,
+ * icpSingular, icpIdentity, utest/ui/Outliers.cpp VarTrimmed KAT, the
+ * examples/data/icp_data *.ref_trans regression fixtures) and cross-checked
+ * against numpy/scipy (cKDTree) golden vectors — see tests/.
+ *
+ * Every function cites the reference file:line it restates (paths relative to
+ * the reference repository root).
+ */
+#ifndef PMO_H
+#define PMO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes (mirrors the exception types of the reference). */
+enum {
+    PMO_OK = 0,
+    PMO_E_NO_POINTS = -1,       /* ConvergenceError("ErrorMnimizer: no point to minimize") ErrorMinimizer.cpp:75-77 */
+    PMO_E_EMPTY_QUANTILE = -2,  /* ConvergenceError("no outlier to filter") Matches.cpp:76-77 */
+    PMO_E_BAD_PARAM = -3,       /* InvalidParameter / ConvergenceError("quantile must be between 0 and 1") */
+    PMO_E_TRANSFORMATION = -4,  /* TransformationError TransformationsImpl.cpp:62-63 */
+    PMO_E_NAN = -5,             /* ConvergenceError("abs rotation norm not a number") TransformationCheckersImpl.cpp:154-157 */
+};
+
+/* Outlier filter types (OutlierFiltersImpl.h). */
+enum {
+    PMO_OF_NULL = 0,        /* NullOutlierFilter            OutlierFiltersImpl.cpp:51-58 */
+    PMO_OF_MAXDIST = 1,     /* MaxDistOutlierFilter(maxDist)  :66-84 */
+    PMO_OF_MINDIST = 2,     /* MinDistOutlierFilter(minDist)  :87-103 */
+    PMO_OF_MEDIANDIST = 3,  /* MedianDistOutlierFilter(factor) :108-128 */
+    PMO_OF_TRIMMED = 4,     /* TrimmedDistOutlierFilter(ratio) :132-150 */
+    PMO_OF_VARTRIMMED = 5,  /* VarTrimmedDistOutlierFilter(minRatio,maxRatio,lambda) :153-223 */
+};
+
+enum { PMO_MIN_P2PLANE = 0, PMO_MIN_P2POINT = 1 };
+enum { PMO_KNN_BRUTE = 0, PMO_KNN_KDTREE = 1 };
+/* accumulation mode of the minimizer sums:
+ *   0 = T-precision products accumulated in double (the build's semantics)
+ *   1 = T-precision products accumulated sequentially in T (reference-like,
+ *       used only to quantify the float-accumulation gap). */
+enum { PMO_ACC_F64 = 0, PMO_ACC_T = 1 };
+
+#define PMO_MAX_FILTERS 8
+
+typedef struct pmo_cfg {
+    /* matcher: KDTreeMatcher params (MatchersImpl.h:80-88) */
+    int knn;
+    double maxDist;          /* radius (not squared); +inf = none */
+    int knn_method;          /* PMO_KNN_BRUTE | PMO_KNN_KDTREE */
+    int knn_threads;         /* >1 = parallel over queries (CPU baseline only) */
+    /* outlier chain (OutlierFilter.cpp:63-103) */
+    int n_filters;
+    int filter_type[PMO_MAX_FILTERS];
+    double filter_p[PMO_MAX_FILTERS][3];
+    /* error minimizer */
+    int minimizer;           /* PMO_MIN_* */
+    int acc_mode;            /* PMO_ACC_* */
+    /* transformation checkers (TransformationCheckersImpl.cpp:45-158) */
+    int counter_max;         /* <0 = no Counter checker */
+    int diff_enabled;
+    double diff_rot, diff_trans;
+    int diff_smooth;
+} pmo_cfg;
+
+typedef struct pmo_stats {
+    int64_t iterations;          /* IterationsCount  ICP.cpp:432 */
+    int64_t kept;                /* P of the last iteration (ErrorElements columns) */
+    int64_t nonzero_weights;     /* (w != 0).count()  ErrorMinimizer.cpp:75 */
+    int64_t rejected_matches;    /* nbRejectedMatches ErrorMinimizer.cpp:191 */
+    int64_t rejected_points;     /* nbRejectedPoints  ErrorMinimizer.cpp:192 */
+    int64_t touched;             /* PointCountTouched ICP.cpp:433 */
+    double sum_w;                /* sum of kept weights */
+    double point_used_ratio;     /* ErrorMinimizer.cpp:139 */
+    double weighted_point_used_ratio; /* OverlapRatio ErrorMinimizer.cpp:140 */
+    int max_iter_reached;        /* ICP.cpp:426 */
+    int error;                   /* PMO_E_* */
+    double last_limit;           /* last quantile threshold (diagnostic) */
+} pmo_stats;
+
+/* ---------- float (T = float) ---------- */
+/* rows = D+1 (homogeneous row included); points are stored point-major,
+ * i.e. the memory layout of the reference's column-major (D+1) x N
+ * features matrix.  normals are D values per point. */
+int64_t pmo_knn_f32(const float* ref, int rows, int64_t M, const float* query, int64_t N,
+                    int k, float maxDist, int method, int threads, float* dists, int32_t* ids);
+int pmo_quantile_f32(const float* dists, int64_t n, float q, float* out);
+int pmo_outlier_f32(int type, const double* p, const float* dists, int k, int64_t N, float* w);
+int pmo_outlier_chain_f32(int n, const int* types, const double* params, const float* dists,
+                          int k, int64_t N, float* w);
+int pmo_vartrimmed_ratio_f32(const float* dists, int64_t n, float minRatio, float maxRatio,
+                             float lambda, float* ratio_out);
+void pmo_transform_f32(const float* T, int rows, const float* pts, int64_t N, float* out);
+int pmo_p2plane_system_f32(int rows, const float* reading_t, const float* ref, const float* normals,
+                           const float* dists, const int32_t* ids, const float* w, int k, int64_t N,
+                           int acc_mode, double* A, double* b, pmo_stats* st);
+int pmo_p2plane_solve_f32(int rows, const double* A, const double* b, float* dT);
+int pmo_p2point_f32(int rows, const float* reading_t, const float* ref, const float* dists,
+                    const int32_t* ids, const float* w, int k, int64_t N, int acc_mode,
+                    float* dT, pmo_stats* st);
+int pmo_icp_f32(const pmo_cfg* cfg, const float* reading, int rows, int64_t N,
+                const float* ref, int64_t M, const float* ref_normals,
+                const float* T_init, float* T_out, pmo_stats* st, float* trace);
+
+/* ---------- double (T = double) ---------- */
+int64_t pmo_knn_f64(const double* ref, int rows, int64_t M, const double* query, int64_t N,
+                    int k, double maxDist, int method, int threads, double* dists, int32_t* ids);
+int pmo_quantile_f64(const double* dists, int64_t n, double q, double* out);
+int pmo_outlier_f64(int type, const double* p, const double* dists, int k, int64_t N, double* w);
+int pmo_outlier_chain_f64(int n, const int* types, const double* params, const double* dists,
+                          int k, int64_t N, double* w);
+int pmo_vartrimmed_ratio_f64(const double* dists, int64_t n, double minRatio, double maxRatio,
+                             double lambda, double* ratio_out);
+void pmo_transform_f64(const double* T, int rows, const double* pts, int64_t N, double* out);
+int pmo_p2plane_system_f64(int rows, const double* reading_t, const double* ref, const double* normals,
+                           const double* dists, const int32_t* ids, const double* w, int k, int64_t N,
+                           int acc_mode, double* A, double* b, pmo_stats* st);
+int pmo_p2plane_solve_f64(int rows, const double* A, const double* b, double* dT);
+int pmo_p2point_f64(int rows, const double* reading_t, const double* ref, const double* dists,
+                    const int32_t* ids, const double* w, int k, int64_t N, int acc_mode,
+                    double* dT, pmo_stats* st);
+int pmo_icp_f64(const pmo_cfg* cfg, const double* reading, int rows, int64_t N,
+                const double* ref, int64_t M, const double* ref_normals,
+                const double* T_init, double* T_out, pmo_stats* st, double* trace);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

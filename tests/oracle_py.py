@@ -1,0 +1,211 @@
+"""ctypes wrapper around the CPU oracle (oracle/build/libpmo.so).
+
+TEST INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py as the checker.  The product package
+(libpointmatcher_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "build", "libpmo.so")
+
+# error codes (oracle/pmo.h)
+OK, E_NO_POINTS, E_EMPTY_QUANTILE, E_BAD_PARAM, E_TRANSFORMATION, E_NAN = 0, -1, -2, -3, -4, -5
+OF = {"NullOutlierFilter": 0, "MaxDistOutlierFilter": 1, "MinDistOutlierFilter": 2,
+      "MedianDistOutlierFilter": 3, "TrimmedDistOutlierFilter": 4, "VarTrimmedDistOutlierFilter": 5}
+OF_PARAMS = {0: [], 1: [("maxDist", 1.0)], 2: [("minDist", 1.0)], 3: [("factor", 3.0)],
+             4: [("ratio", 0.85)], 5: [("minRatio", 0.05), ("maxRatio", 0.99), ("lambda", 2.35)]}
+MIN = {"PointToPlaneErrorMinimizer": 0, "PointToPointErrorMinimizer": 1}
+
+
+class Cfg(C.Structure):
+    _fields_ = [("knn", C.c_int), ("maxDist", C.c_double), ("knn_method", C.c_int),
+                ("knn_threads", C.c_int), ("n_filters", C.c_int),
+                ("filter_type", C.c_int * 8), ("filter_p", (C.c_double * 3) * 8),
+                ("minimizer", C.c_int), ("acc_mode", C.c_int), ("counter_max", C.c_int),
+                ("diff_enabled", C.c_int), ("diff_rot", C.c_double), ("diff_trans", C.c_double),
+                ("diff_smooth", C.c_int)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("iterations", C.c_int64), ("kept", C.c_int64), ("nonzero_weights", C.c_int64),
+                ("rejected_matches", C.c_int64), ("rejected_points", C.c_int64),
+                ("touched", C.c_int64), ("sum_w", C.c_double), ("point_used_ratio", C.c_double),
+                ("weighted_point_used_ratio", C.c_double), ("max_iter_reached", C.c_int),
+                ("error", C.c_int), ("last_limit", C.c_double)]
+
+    def asdict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+    return _lib
+
+
+def _sfx(dtype):
+    return "f32" if np.dtype(dtype) == np.float32 else "f64"
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def knn(ref, query, k=1, max_dist=np.inf, method="kdtree", threads=1):
+    """ref, query: (n, rows) arrays (rows = D+1).  Returns dists (N,k), ids (N,k), touched."""
+    dt = ref.dtype
+    ref = np.ascontiguousarray(ref)
+    query = np.ascontiguousarray(query, dtype=dt)
+    N, rows = query.shape
+    dists = np.empty((N, k), dt)
+    ids = np.empty((N, k), np.int32)
+    f = getattr(lib(), "pmo_knn_" + _sfx(dt))
+    f.restype = C.c_int64
+    scal = C.c_float if dt == np.float32 else C.c_double
+    touched = f(_p(ref), rows, C.c_int64(ref.shape[0]), _p(query), C.c_int64(N), k,
+                scal(max_dist), 1 if method == "kdtree" else 0, threads, _p(dists), _p(ids))
+    return dists, ids, touched
+
+
+def quantile(dists, q):
+    d = np.ascontiguousarray(dists).ravel()
+    out = np.zeros(1, d.dtype)
+    f = getattr(lib(), "pmo_quantile_" + _sfx(d.dtype))
+    scal = C.c_float if d.dtype == np.float32 else C.c_double
+    rc = f(_p(d), C.c_int64(d.size), scal(q), _p(out))
+    return rc, out[0]
+
+
+def outlier_chain(filters, dists):
+    """filters: list of (name, {param: value}); dists (N,k)."""
+    d = np.ascontiguousarray(dists)
+    N, k = d.shape
+    types, params = _filters(filters)
+    w = np.empty_like(d)
+    f = getattr(lib(), "pmo_outlier_chain_" + _sfx(d.dtype))
+    rc = f(len(filters), _p(types), _p(params), _p(d), k, C.c_int64(N), _p(w))
+    return rc, w
+
+
+def vartrimmed_ratio(dists, min_ratio, max_ratio, lam):
+    d = np.ascontiguousarray(dists).ravel()
+    out = np.zeros(1, d.dtype)
+    scal = C.c_float if d.dtype == np.float32 else C.c_double
+    f = getattr(lib(), "pmo_vartrimmed_ratio_" + _sfx(d.dtype))
+    rc = f(_p(d), C.c_int64(d.size), scal(min_ratio), scal(max_ratio), scal(lam), _p(out))
+    return rc, out[0]
+
+
+def transform(T, pts):
+    pts = np.ascontiguousarray(pts)
+    T = np.ascontiguousarray(T, dtype=pts.dtype)
+    out = np.empty_like(pts)
+    getattr(lib(), "pmo_transform_" + _sfx(pts.dtype))(_p(T), pts.shape[1], _p(pts),
+                                                         C.c_int64(pts.shape[0]), _p(out))
+    return out
+
+
+def p2plane_system(reading_t, ref, normals, dists, ids, w, acc_mode=0):
+    rows = reading_t.shape[1]
+    n = 6 if rows == 4 else 3
+    A = np.zeros(n * n)
+    b = np.zeros(n)
+    st = Stats()
+    N, k = dists.shape
+    rc = getattr(lib(), "pmo_p2plane_system_" + _sfx(reading_t.dtype))(
+        rows, _p(reading_t), _p(ref), _p(np.ascontiguousarray(normals)), _p(dists), _p(ids), _p(w),
+        k, C.c_int64(N), acc_mode, _p(A), _p(b), C.byref(st))
+    return rc, A.reshape(n, n), b, st
+
+
+def p2plane_solve(A, b, rows, dtype):
+    dT = np.zeros((rows, rows), dtype)
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    rc = getattr(lib(), "pmo_p2plane_solve_" + _sfx(dtype))(rows, _p(A), _p(b), _p(dT))
+    return rc, dT
+
+
+def p2point(reading_t, ref, dists, ids, w, acc_mode=0):
+    rows = reading_t.shape[1]
+    N, k = dists.shape
+    dT = np.zeros((rows, rows), reading_t.dtype)
+    st = Stats()
+    rc = getattr(lib(), "pmo_p2point_" + _sfx(reading_t.dtype))(
+        rows, _p(reading_t), _p(ref), _p(dists), _p(ids), _p(w), k, C.c_int64(N), acc_mode,
+        _p(dT), C.byref(st))
+    return rc, dT, st
+
+
+def _filters(filters):
+    types = np.zeros(8, np.int32)
+    params = np.zeros((8, 3), np.float64)
+    for i, (name, p) in enumerate(filters):
+        t = OF[name]
+        types[i] = t
+        for j, (pn, default) in enumerate(OF_PARAMS[t]):
+            params[i, j] = float(p.get(pn, default))
+    return types, params
+
+
+def make_cfg(knn=1, max_dist=np.inf, method="kdtree", threads=1, filters=(("TrimmedDistOutlierFilter", {"ratio": 0.85}),),
+             minimizer="PointToPlaneErrorMinimizer", counter_max=40, differential=None, acc_mode=0):
+    cfg = Cfg()
+    cfg.knn = knn
+    cfg.maxDist = max_dist
+    cfg.knn_method = 1 if method == "kdtree" else 0
+    cfg.knn_threads = threads
+    cfg.n_filters = len(filters)
+    types, params = _filters(filters)
+    for i in range(8):
+        cfg.filter_type[i] = int(types[i])
+        for j in range(3):
+            cfg.filter_p[i][j] = float(params[i, j])
+    cfg.minimizer = MIN[minimizer]
+    cfg.acc_mode = acc_mode
+    cfg.counter_max = counter_max if counter_max is not None else -1
+    if differential:
+        cfg.diff_enabled = 1
+        cfg.diff_rot = differential.get("minDiffRotErr", 0.001)
+        cfg.diff_trans = differential.get("minDiffTransErr", 0.001)
+        cfg.diff_smooth = int(differential.get("smoothLength", 3))
+    return cfg
+
+
+def icp(cfg, reading, reference, normals=None, T_init=None, trace=False):
+    """reading, reference: (n, rows) arrays incl. homogeneous row.  Returns (rc, T, stats, trace)."""
+    dt = reference.dtype
+    reading = np.ascontiguousarray(reading, dtype=dt)
+    reference = np.ascontiguousarray(reference)
+    rows = reading.shape[1]
+    if T_init is None:
+        T_init = np.eye(rows, dtype=dt)
+    T_init = np.ascontiguousarray(T_init, dtype=dt)
+    T_out = np.zeros((rows, rows), dt)
+    st = Stats()
+    maxit = max(cfg.counter_max, 1) if cfg.counter_max >= 0 else 4096
+    tr = np.zeros((maxit, rows, rows), dt) if trace else None
+    nrm = np.ascontiguousarray(normals, dtype=dt) if normals is not None else None
+    rc = getattr(lib(), "pmo_icp_" + _sfx(dt))(
+        C.byref(cfg), _p(reading), rows, C.c_int64(reading.shape[0]), _p(reference),
+        C.c_int64(reference.shape[0]), _p(nrm), _p(T_init), _p(T_out), C.byref(st), _p(tr))
+    if trace:
+        tr = tr[: st.iterations]
+    return rc, T_out, st, tr

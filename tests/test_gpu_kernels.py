@@ -1,0 +1,225 @@
+"""Kernel-level parity of the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (bit-exact for index work, exact for T-precision distances):
+  - match: ids identical, distances bitwise identical (same no-FMA formula,
+    lowest-index ties) — MatchersImpl.cpp:85-101 + libnabo semantics;
+  - outlier weights: identical (exact order statistics, Matches.cpp:60-87);
+  - normal equations: the per-pair T products are identical; only the fp64
+    summation order differs -> relative 1e-12.
+"""
+import numpy as np
+import pytest
+
+from libpointmatcher_amd import _capi as P
+from libpointmatcher_amd.synth import random_cloud, reference_cloud, reading_cloud, t_gt
+
+pytestmark = pytest.mark.gpu
+
+
+def small_T(rows, dtype, seed=0, ang=0.05, tr=0.02):
+    rng = np.random.default_rng(seed)
+    T = np.eye(rows)
+    if rows == 4:
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+        T[:3, :3] = np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+        T[:3, 3] = rng.normal(size=3) * tr
+    else:
+        c, s = np.cos(ang), np.sin(ang)
+        T[:2, :2] = [[c, -s], [s, c]]
+        T[:2, 2] = rng.normal(size=2) * tr
+    return T.astype(dtype)
+
+
+def run_match(ref, rd, T, k=1, max_dist=np.inf, dtype=np.float32, T0=None):
+    ctx = P.Context(0, dtype)
+    ctx.set_reference(ref)
+    ctx.set_reading(rd, T0)
+    ctx.match(T, knn=k, max_dist=max_dist)
+    d, i = ctx.get_matches()
+    ctx.close()
+    return d, i
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("k", [1, 2, 4, 7])
+@pytest.mark.parametrize("N,M", [(1000, 3000), (5000, 2500), (777, 1025)])
+def test_match_vs_oracle(oracle, dtype, k, N, M):
+    ref = random_cloud(M, seed=1, dtype=dtype)
+    rd = random_cloud(N, seed=2, dtype=dtype)
+    T = small_T(4, dtype, seed=3)
+    d, i = run_match(ref, rd, T, k=k, dtype=dtype)
+    step = oracle.transform(T, rd)
+    od, oi, _ = oracle.knn(ref, step, k=k, method="brute")
+    assert np.array_equal(i, oi)
+    assert np.array_equal(d.view(np.uint32 if dtype == np.float32 else np.uint64),
+                          od.view(np.uint32 if dtype == np.float32 else np.uint64))
+
+
+def test_match_large_chunked(oracle):
+    # N small vs M large: the reference is split into chunks + merge kernel
+    ref = random_cloud(200_000, seed=4)
+    rd = random_cloud(3000, seed=5)
+    T = small_T(4, np.float32, seed=6)
+    for k in (1, 4):
+        d, i = run_match(ref, rd, T, k=k)
+        od, oi, _ = oracle.knn(ref, oracle.transform(T, rd), k=k, method="kdtree")
+        assert np.array_equal(i, oi) and np.array_equal(d, od)
+
+
+def test_match_ties_lowest_index(oracle):
+    # duplicated reference points: every query has exact ties
+    base = random_cloud(1500, seed=7)
+    ref = np.concatenate([base, base, base])
+    rd = base[::3].copy()
+    T = np.eye(4, dtype=np.float32)
+    for k in (1, 3, 5):
+        d, i = run_match(ref, rd, T, k=k)
+        od, oi, _ = oracle.knn(ref, rd, k=k, method="brute")
+        assert np.array_equal(i, oi) and np.array_equal(d, od)
+    d, i = run_match(ref, rd, T, k=1)
+    assert np.all(i[:, 0] == np.arange(0, 1500, 3))  # self-match, lowest index
+    assert np.all(d == 0)
+
+
+def test_match_maxdist_and_2d(oracle):
+    ref = random_cloud(4000, seed=8)
+    rd = random_cloud(3000, seed=9, scale=1.3)
+    T = small_T(4, np.float32, seed=10)
+    for k in (1, 3):
+        d, i = run_match(ref, rd, T, k=k, max_dist=0.05)
+        od, oi, _ = oracle.knn(ref, oracle.transform(T, rd), k=k, max_dist=0.05, method="brute")
+        assert np.array_equal(i, oi) and np.array_equal(d, od)
+        assert (i == -1).any() and np.all(np.isinf(d[i == -1]))
+    # 2-D (rows = 3)
+    ref2 = random_cloud(3000, rows=3, seed=11)
+    rd2 = random_cloud(2000, rows=3, seed=12)
+    T2 = small_T(3, np.float32, seed=13)
+    for k in (1, 2):
+        d, i = run_match(ref2, rd2, T2, k=k)
+        od, oi, _ = oracle.knn(ref2, oracle.transform(T2, rd2), k=k, method="brute")
+        assert np.array_equal(i, oi) and np.array_equal(d, od)
+
+
+def test_reading_T0_applied_once(oracle):
+    ref = random_cloud(3000, seed=14)
+    rd = random_cloud(2000, seed=15)
+    T0 = small_T(4, np.float32, seed=16, ang=0.3, tr=0.5)
+    T = small_T(4, np.float32, seed=17)
+    d, i = run_match(ref, rd, T, T0=T0)
+    step = oracle.transform(T, oracle.transform(T0, rd))
+    od, oi, _ = oracle.knn(ref, step, method="brute")
+    assert np.array_equal(i, oi) and np.array_equal(d, od)
+
+
+FILTERS = [
+    [],
+    [("TrimmedDistOutlierFilter", {"ratio": 0.85})],
+    [("TrimmedDistOutlierFilter", {"ratio": 1.0})],
+    [("TrimmedDistOutlierFilter", {"ratio": 0.3})],
+    [("MaxDistOutlierFilter", {"maxDist": 0.04})],
+    [("MinDistOutlierFilter", {"minDist": 0.01})],
+    [("MedianDistOutlierFilter", {"factor": 3.0})],
+    [("NullOutlierFilter", {})],
+    [("VarTrimmedDistOutlierFilter", {"minRatio": 0.05, "maxRatio": 0.99, "lambda": 2.35})],
+    [("VarTrimmedDistOutlierFilter", {"minRatio": 0.6, "maxRatio": 0.8, "lambda": 0.9})],
+    [("MaxDistOutlierFilter", {"maxDist": 0.05}), ("TrimmedDistOutlierFilter", {"ratio": 0.7})],
+]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("fi", range(len(FILTERS)))
+@pytest.mark.parametrize("k", [1, 3])
+def test_outlier_chain_vs_oracle(oracle, dtype, fi, k):
+    filters = FILTERS[fi]
+    ref, nrm = reference_cloud(20000, dtype)
+    rd = reading_cloud(15000, dtype)
+    T = np.eye(4, dtype=dtype)
+    ctx = P.Context(0, dtype)
+    ctx.set_reference(ref - np.array([0, 0, 0, 0], dtype=dtype), nrm)
+    ctx.set_reading(rd)
+    ctx.match(T, knn=k)
+    if not filters:
+        ctx.outlier_default()
+    for pos, (name, p) in enumerate(filters):
+        ctx.outlier(name, pos, **p)
+    w = ctx.get_weights()
+    d, i = ctx.get_matches()
+    ctx.close()
+    rc, ow = oracle.outlier_chain(filters, d)
+    assert rc == 0
+    assert np.array_equal(w, ow)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("k", [1, 4])
+def test_p2plane_system_vs_oracle(oracle, dtype, k):
+    ref, nrm = reference_cloud(30000, dtype)
+    rd = reading_cloud(20000, dtype)
+    T = small_T(4, dtype, seed=20, ang=0.01, tr=0.01)
+    ctx = P.Context(0, dtype)
+    ctx.set_reference(ref, nrm)
+    ctx.set_reading(rd)
+    ctx.match(T, knn=k)
+    ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
+    A, b, st = ctx.p2plane_system()
+    d, i = ctx.get_matches()
+    w = ctx.get_weights()
+    ctx.close()
+    step = oracle.transform(T, rd)
+    rc, oA, ob, ost = oracle.p2plane_system(step, ref, nrm, d, i, w)
+    assert rc == 0
+    np.testing.assert_allclose(A, oA, rtol=1e-12, atol=1e-12 * np.abs(oA).max())
+    np.testing.assert_allclose(b, ob, rtol=1e-12, atol=1e-12 * np.abs(ob).max())
+    assert st.kept == ost.kept and st.nonzero_weights == ost.nonzero_weights
+    assert st.rejected_matches == ost.rejected_matches and st.rejected_points == ost.rejected_points
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_p2point_system_vs_oracle(oracle, dtype):
+    ref, nrm = reference_cloud(30000, dtype)
+    rd = reading_cloud(20000, dtype)
+    T = small_T(4, dtype, seed=21, ang=0.01, tr=0.01)
+    ctx = P.Context(0, dtype)
+    ctx.set_reference(ref, nrm)
+    ctx.set_reading(rd)
+    ctx.match(T, knn=1)
+    ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
+    mp, mq, m, st = ctx.p2point_system()
+    d, i = ctx.get_matches()
+    w = ctx.get_weights()
+    ctx.close()
+    # oracle: full P2Point step, compare the resulting transform
+    step = oracle.transform(T, rd)
+    rc, dT, ost = oracle.p2point(step, ref, d, i, w)
+    assert rc == 0 and st.kept == ost.kept
+    # rebuild with numpy SVD from the GPU moments: rotation must agree
+    U, S, Vt = np.linalg.svd(m)
+    R = U @ Vt
+    if np.linalg.det(R) < 0:
+        Vt[-1] *= -1
+        R = U @ Vt
+    tol = 1e-5 if dtype == np.float32 else 1e-12
+    assert np.abs(R - dT[:3, :3]).max() < tol
+    assert np.abs((mq - R @ mp) - dT[:3, 3]).max() < tol
+
+
+def test_errors_surface_as_reference_exceptions():
+    ref = random_cloud(2000, seed=30)
+    rd = random_cloud(1000, seed=31, scale=50.0)
+    ctx = P.Context(0, np.float32)
+    ctx.set_reference(ref, np.zeros((2000, 3), np.float32))
+    ctx.set_reading(rd)
+    # radius excludes everything -> all dists inf -> empty quantile
+    ctx.match(np.eye(4, dtype=np.float32), knn=1, max_dist=1e-6)
+    ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
+    with pytest.raises(P.ConvergenceError, match="no outlier to filter"):
+        ctx.p2plane_system()
+    ctx.match(np.eye(4, dtype=np.float32), knn=1, max_dist=1e-6)
+    ctx.outlier_default()
+    with pytest.raises(P.ConvergenceError, match="no point to minimize"):
+        ctx.p2plane_system()
+    with pytest.raises(P.InvalidParameter):
+        ctx.match(np.eye(4, dtype=np.float32), knn=0)
+    ctx.close()
