@@ -1,0 +1,207 @@
+"""Benchmark: ICP iterations/s and matched-pairs/s on the BASELINE.json workload.
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c3] [--matcher brute]
+
+A "step" is one ICP iteration of the hot path — fused transform + k-NN
+match, outlier weighting, normal equations, the host 6x6 solve and the
+checker — over the synthetic cloud of the configuration.
+Default workload = BASELINE config 3: 1M -> 1M float, k = 1, TrimmedDist
+ratio 0.85, point-to-plane, one GPU.  With N GPUs (torchrun, one process per
+GPU) every rank holds its own 1M-point reading shard against the replicated
+1M reference (weak scaling) and each iteration all-reduces the quantile
+histograms and the normal equations over RCCL.
+
+Timing: W untimed iterations, then exactly K iterations between a barrier +
+device synchronisation on both sides; the max over ranks is reported.  The
+clouds are resident in HBM before the timed region.  The match kernel's
+device time is measured with HIP events on the context stream (pmx_timing_*).
+The CPU baseline (rank 0, N = 1 only) is the oracle's libnabo-style kd-tree
+restatement of the reference CPU path on the same inputs (a bounded number of
+iterations), timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (N per rank, M, dtype, knn, filters, minimizer)
+    "c2": (100_000, 100_000, np.float32, 1, [("TrimmedDistOutlierFilter", {"ratio": 0.85})], "PointToPlaneErrorMinimizer"),
+    "c3": (1_000_000, 1_000_000, np.float32, 1, [("TrimmedDistOutlierFilter", {"ratio": 0.85})], "PointToPlaneErrorMinimizer"),
+    "c4": (1_000_000, 1_000_000, np.float32, 4, [("MaxDistOutlierFilter", {"maxDist": 0.05})], "PointToPlaneErrorMinimizer"),
+    "c5": (10_000_000, 1_000_000, np.float64, 1, [], "PointToPointErrorMinimizer"),
+}
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
+FP32_VALU_TFLOPS = 157.3   # MI355X FP32 vector peak (spec)
+FP64_VALU_TFLOPS = 78.6
+
+
+def chain_yaml(knn, filters, minimizer, search_type, maxit):
+    lines = ["matcher:", "  KDTreeMatcher:", f"    knn: {knn}", "    epsilon: 0", f"    searchType: {search_type}",
+             "outlierFilters:"]
+    for name, p in filters:
+        lines.append(f"  - {name}:")
+        lines += [f"      {k}: {v}" for k, v in p.items()]
+    lines += ["errorMinimizer:", f"  {minimizer}", "transformationCheckers:", "  - CounterTransformationChecker:",
+              f"      maxIterationCount: {maxit}", "inspector:", "  NullInspector", "logger:", "  NullLogger"]
+    return "\n".join(lines) + "\n"
+
+
+def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer, iters, threads):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+
+    cfg = O.make_cfg(knn=knn, filters=tuple(filters), minimizer=minimizer, counter_max=iters, threads=threads,
+                     method="kdtree")
+    t0 = time.perf_counter()
+    rc, T, st, _ = O.icp(cfg, reading, reference, normals=normals if minimizer.startswith("PointToPlane") else None)
+    wall = time.perf_counter() - t0
+    if rc != 0:
+        return None
+    loop = st.loop_seconds
+    n = reading.shape[0]
+    return {"value": n * knn * st.iterations / loop, "unit": "matched-pairs/s", "cores": threads,
+            "kind": "port", "iters_per_s": st.iterations / loop,
+            "sample": f"{cfg_name} inputs ({n}->{reference.shape[0]}), {st.iterations} ICP iterations, "
+                      f"kd-tree (libnabo-style, exact) oracle restatement of the reference CPU path, "
+                      f"{threads} thread(s), loop {loop:.2f} s (setup+loop {wall:.2f} s)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--matcher", default="brute", choices=["brute", "grid"],
+                    help="KDTreeMatcher searchType 0 (brute force) or 1 (spatial grid)")
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch
+        import torch.distributed as tdist
+
+        tdist.init_process_group("gloo", init_method="env://")  # control plane only
+    from libpointmatcher_amd import _capi
+    from libpointmatcher_amd.icp import ICP
+    from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+
+    N, M, dtype, knn, filters, minimizer = CONFIGS[args.config]
+    reference, normals = reference_cloud(M, dtype)
+    # each rank's shard of the global reading (weak scaling: N per rank)
+    if dist:
+        full = reading_cloud(N * world, dtype)
+        reading = np.ascontiguousarray(full[rank * N:(rank + 1) * N])
+        del full
+    else:
+        reading = reading_cloud(N, dtype)
+
+    search_type = 0 if args.matcher == "brute" else 1
+    total_it = args.warmup + args.steps + 10
+    icp = ICP(dtype, device=local_rank)
+    icp.load_yaml(chain_yaml(knn, filters, minimizer, search_type, total_it))
+    if dist:
+        import torch
+
+        uid = bytearray(_capi.Context.unique_id() if rank == 0 else bytes(128))
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        tdist.broadcast(t, src=0)
+        icp.comm_init(bytes(t.tolist()), world, rank)
+
+    icp.prepare(reading, reference, normals if minimizer.startswith("PointToPlane") else None)
+    icp.iterate(args.warmup)
+    icp.timing(True)
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    icp.iterate(args.steps)   # each iteration ends with the system copy-back: device is synchronised
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    match_ms, launches = icp.timing_read()
+    st = icp.stats()
+    if dist:
+        import torch
+
+        e = torch.tensor([elapsed], dtype=torch.float64)
+        tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    pairs = N * world * knn * args.steps
+    avg_match_s = match_ms * 1e-3 / max(launches, 1)
+    esz = np.dtype(dtype).itemsize
+    # algorithmic bytes of one match launch: the reading shard (4 T per point),
+    # the reference (4 T per point) and the k (dist, id) outputs per query
+    alg_bytes = N * 4 * esz + M * 4 * esz + N * knn * (esz + 4)
+    achieved_gbs = alg_bytes / avg_match_s / 1e9
+    flops = 8.0 * N * M  # 3 sub + 3 mul + 2 add per pair
+    peak_tf = FP32_VALU_TFLOPS if esz == 4 else FP64_VALU_TFLOPS
+    metric = "ICP iterations/sec + matched-pairs/sec, 1M→1M pts, k=1, point-to-plane"
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            metric = json.load(f)["metric"]
+    except Exception:
+        pass
+    result = {
+        "metric": metric,
+        "value": pairs / elapsed,
+        "unit": "matched-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if esz == 4 else "f64",
+        "data": "synthetic (box+sphere surface, seeds 1/2, sigma 0.01, SURVEY.md §8(d))",
+        "config": {"workload": f"BASELINE {args.config}: {N * world}->{M} {'float' if esz == 4 else 'double'}, "
+                               f"k={knn}, {', '.join(f[0] for f in filters) or 'no outlier filter'}, {minimizer}",
+                   "matcher": f"KDTreeMatcher searchType={search_type} ({args.matcher}, exact)",
+                   "reading_per_gpu": N, "reference": M, "parallelism": f"reading sharded x{world}, RCCL all-reduce"},
+        "icp_iterations_per_s": args.steps / elapsed,
+        "kept_pairs_last_iter": st.kept,
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "match (k-NN + fused transform)", "avg_launch_ms": avg_match_s * 1e3,
+                     "algorithmic_bytes_per_launch": alg_bytes},
+        "compute_roofline": {"bound": "valu", "achieved": flops / avg_match_s / 1e12, "peak": peak_tf,
+                             "unit": "TFLOP/s", "frac": flops / avg_match_s / 1e12 / peak_tf,
+                             "note": "brute-force match is VALU-bound (8 FLOP/pair); the HBM fraction is small by construction"},
+    }
+    if args.matcher == "grid":
+        result["compute_roofline"]["note"] = "grid matcher evaluates far fewer than N*M pairs; FLOP figure is brute-force-equivalent"
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cb = cpu_baseline(args.config, reading, reference, normals, knn, filters, minimizer, args.cpu_iters, threads)
+        result["cpu_baseline"] = cb
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    icp.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

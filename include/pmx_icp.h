@@ -1,0 +1,84 @@
+/*
+ * pmx_icp.h — C ABI of the host ICP chain (libpmx_icp.so).
+ *
+ * A flat front-end over the C++ restatement of PointMatcher<T>::ICP
+ * (libpointmatcher_amd/csrc/host/pm_icp.h) for non-C++ callers (the Python
+ * tests and bench, a ctypes / cgo / JNI binding).  The chain is configured
+ * exactly like the reference: ICPChainBase::setDefault (ICP.cpp:99-113) or a
+ * libpointmatcher YAML chain (ICPChainBase::loadFromYaml, ICP.cpp:116-167).
+ *
+ * Clouds: rows x n point-major T arrays (rows = D + 1, homogeneous row last);
+ * reference normals D x M point-major or NULL.  Transforms: rows x rows
+ * row-major T.
+ *
+ * Errors: 0 on success, otherwise the negative code of the exception the
+ * reference would throw; pmx_icp_last_error() holds its message.
+ */
+#ifndef PMX_ICP_H
+#define PMX_ICP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pmx_icp pmx_icp;
+
+enum {
+    PMX_ICP_OK = 0,
+    PMX_ICP_CONVERGENCE_ERROR = -1,   /* PointMatcher<T>::ConvergenceError */
+    PMX_ICP_INVALID_PARAMETER = -3,   /* Parametrizable::InvalidParameter */
+    PMX_ICP_TRANSFORMATION_ERROR = -4,/* TransformationError */
+    PMX_ICP_INVALID_ELEMENT = -5,     /* InvalidElement (unknown module name) */
+    PMX_ICP_INVALID_MODULE_TYPE = -6, /* ICPChainBase::InvalidModuleType */
+    PMX_ICP_CONFIGURATION_ERROR = -7, /* ConfigurationError / YAML syntax */
+    PMX_ICP_RUNTIME_ERROR = -10       /* std::runtime_error (incl. HIP/RCCL failures) */
+};
+
+typedef struct pmx_icp_stats {
+    int64_t iterations;            /* IterationsCount */
+    int64_t point_count_touched;   /* PointCountTouched (pair evaluations) */
+    double overlap_ratio;          /* OverlapRatio = weightedPointUsedRatio */
+    double point_used_ratio;
+    int64_t kept;                  /* ErrorElements columns of the last iteration */
+    int64_t rejected_matches, rejected_points;
+    double convergence_duration;   /* s, wall clock of the loop */
+    double reference_preprocessing_duration;
+    double reading_preprocessing_duration;
+    int max_iterations_reached;
+} pmx_icp_stats;
+
+/* dtype: 0 = float, 1 = double; device: HIP ordinal */
+int pmx_icp_create(int dtype, int device, pmx_icp** out);
+void pmx_icp_destroy(pmx_icp* icp);
+const char* pmx_icp_last_error(const pmx_icp* icp);
+
+int pmx_icp_set_default(pmx_icp* icp);
+int pmx_icp_load_yaml(pmx_icp* icp, const char* yaml_text);
+/* multi-GPU: call before the first compute; uid from pmx_comm_unique_id */
+int pmx_icp_comm_init(pmx_icp* icp, const void* uid128, int nranks, int rank);
+int pmx_icp_keep_trace(pmx_icp* icp, int on);
+
+/* ICP::compute (ICP.cpp:265-449): T_out = transform of reading into reference */
+int pmx_icp_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
+                    const void* ref_normals, const void* T_init, void* T_out);
+
+/* the same loop in phases (bench: time the iterations alone) */
+int pmx_icp_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
+                    const void* ref_normals, const void* T_init);
+/* run up to n iterations; *done = 1 once a checker stopped the loop */
+int pmx_icp_iterate(pmx_icp* icp, int n, int* done);
+int pmx_icp_finish(pmx_icp* icp, void* T_out);
+
+int pmx_icp_stats_get(const pmx_icp* icp, pmx_icp_stats* out);
+/* T_iter after each iteration (rows x rows each), returns count written */
+int pmx_icp_trace_get(const pmx_icp* icp, void* out, int max_iters);
+/* HIP-event device time of the match kernel over the last iterations */
+int pmx_icp_timing(pmx_icp* icp, int on);
+int pmx_icp_timing_read(pmx_icp* icp, double* match_ms, int64_t* match_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

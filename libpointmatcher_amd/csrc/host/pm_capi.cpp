@@ -1,0 +1,238 @@
+// pm_capi.cpp — extern "C" front-end of the host ICP chain (include/pmx_icp.h).
+#include <cstring>
+#include <memory>
+
+#include "pm_icp.h"
+#include "pmx_icp.h"
+
+using namespace pm;
+
+struct pmx_icp {
+    int dtype = 0;
+    std::unique_ptr<PointMatcher<float>::ICP> f;
+    std::unique_ptr<PointMatcher<double>::ICP> d;
+    std::string err;
+};
+
+namespace {
+
+template <typename F>
+int guarded(pmx_icp* icp, F&& fn) {
+    try {
+        fn();
+        return PMX_ICP_OK;
+    } catch (const ConvergenceError& e) {
+        icp->err = e.what();
+        return PMX_ICP_CONVERGENCE_ERROR;
+    } catch (const InvalidParameter& e) {
+        icp->err = e.what();
+        return PMX_ICP_INVALID_PARAMETER;
+    } catch (const TransformationError& e) {
+        icp->err = e.what();
+        return PMX_ICP_TRANSFORMATION_ERROR;
+    } catch (const InvalidElement& e) {
+        icp->err = e.what();
+        return PMX_ICP_INVALID_ELEMENT;
+    } catch (const InvalidModuleType& e) {
+        icp->err = e.what();
+        return PMX_ICP_INVALID_MODULE_TYPE;
+    } catch (const ConfigurationError& e) {
+        icp->err = e.what();
+        return PMX_ICP_CONFIGURATION_ERROR;
+    } catch (const std::exception& e) {
+        icp->err = e.what();
+        return PMX_ICP_RUNTIME_ERROR;
+    }
+}
+
+template <typename T>
+DataPoints<T> make_cloud(const void* feat, int rows, int64_t n, const void* normals) {
+    DataPoints<T> c;
+    c.rows = rows;
+    c.n = n;
+    const T* p = static_cast<const T*>(feat);
+    c.features.assign(p, p + (size_t)rows * n);
+    const char* xyz[] = {"x", "y", "z"};
+    for (int r = 0; r < rows - 1; ++r) c.featureLabels.push_back({xyz[r], 1});
+    c.featureLabels.push_back({"pad", 1});
+    if (normals) c.addDescriptor("normals", rows - 1, static_cast<const T*>(normals));
+    return c;
+}
+
+template <typename T>
+typename PointMatcher<T>::ICP& get(pmx_icp* icp);
+template <>
+PointMatcher<float>::ICP& get<float>(pmx_icp* icp) {
+    return *icp->f;
+}
+template <>
+PointMatcher<double>::ICP& get<double>(pmx_icp* icp) {
+    return *icp->d;
+}
+
+template <typename T>
+void prepare_impl(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
+                  const void* nrm, const void* T_init) {
+    auto rd = make_cloud<T>(reading, rows, N, nullptr);
+    auto ref = make_cloud<T>(reference, rows, M, nrm);
+    std::vector<T> Ti((size_t)rows * rows, (T)0);
+    if (T_init) {
+        const T* p = static_cast<const T*>(T_init);
+        Ti.assign(p, p + (size_t)rows * rows);
+    } else {
+        for (int i = 0; i < rows; ++i) Ti[i * rows + i] = 1;
+    }
+    get<T>(icp).prepare(rd, ref, Ti);
+}
+
+template <typename T>
+void finish_impl(pmx_icp* icp, void* T_out) {
+    auto out = get<T>(icp).finish();
+    std::memcpy(T_out, out.data(), sizeof(T) * out.size());
+}
+
+template <typename T>
+void stats_impl(const pmx_icp* icp, pmx_icp_stats* s) {
+    auto& I = get<T>(const_cast<pmx_icp*>(icp));
+    std::memset(s, 0, sizeof(*s));
+    s->iterations = I.iterationCount;
+    s->point_count_touched = I.matcher ? (int64_t)I.matcher->getVisitCount() : 0;
+    if (I.errorMinimizer) {
+        s->overlap_ratio = (double)I.errorMinimizer->getWeightedPointUsedRatio();
+        s->point_used_ratio = (double)I.errorMinimizer->getPointUsedRatio();
+        s->kept = I.errorMinimizer->keptPoints;
+        s->rejected_matches = I.errorMinimizer->nbRejectedMatches;
+        s->rejected_points = I.errorMinimizer->nbRejectedPoints;
+    }
+    s->convergence_duration = I.convergenceDuration;
+    s->reference_preprocessing_duration = I.referencePreprocessingDuration;
+    s->reading_preprocessing_duration = I.readingPreprocessingDuration;
+    s->max_iterations_reached = I.maxNumIterationsReached ? 1 : 0;
+}
+
+}  // namespace
+
+#define BOTH(icp, expr_f, expr_d) ((icp)->dtype == 1 ? (expr_d) : (expr_f))
+
+extern "C" {
+
+int pmx_icp_create(int dtype, int device, pmx_icp** out) {
+    if (!out || (dtype != 0 && dtype != 1)) return PMX_ICP_INVALID_PARAMETER;
+    pmx_icp* icp = new pmx_icp();
+    icp->dtype = dtype;
+    if (dtype == 1)
+        icp->d.reset(new PointMatcher<double>::ICP(device));
+    else
+        icp->f.reset(new PointMatcher<float>::ICP(device));
+    *out = icp;
+    return PMX_ICP_OK;
+}
+
+void pmx_icp_destroy(pmx_icp* icp) { delete icp; }
+
+const char* pmx_icp_last_error(const pmx_icp* icp) { return icp ? icp->err.c_str() : "null"; }
+
+int pmx_icp_set_default(pmx_icp* icp) {
+    return guarded(icp, [&] { BOTH(icp, icp->f->setDefault(), icp->d->setDefault()); });
+}
+
+int pmx_icp_load_yaml(pmx_icp* icp, const char* text) {
+    return guarded(icp, [&] {
+        const std::string s(text ? text : "");
+        BOTH(icp, icp->f->loadFromYaml(s), icp->d->loadFromYaml(s));
+    });
+}
+
+int pmx_icp_comm_init(pmx_icp* icp, const void* uid, int nranks, int rank) {
+    return guarded(icp, [&] {
+        Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
+        if (dev.ctx) throw std::runtime_error("pmx_icp_comm_init must precede the first compute");
+        dev.nranks = nranks;
+        dev.rank = rank;
+        const unsigned char* p = static_cast<const unsigned char*>(uid);
+        dev.uid.assign(p, p + 128);
+    });
+}
+
+int pmx_icp_keep_trace(pmx_icp* icp, int on) {
+    return guarded(icp, [&] { BOTH(icp, icp->f->keepTrace = on != 0, icp->d->keepTrace = on != 0); });
+}
+
+int pmx_icp_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
+                    const void* nrm, const void* T_init) {
+    return guarded(icp, [&] {
+        BOTH(icp, prepare_impl<float>(icp, reading, rows, N, reference, M, nrm, T_init),
+             prepare_impl<double>(icp, reading, rows, N, reference, M, nrm, T_init));
+    });
+}
+
+int pmx_icp_iterate(pmx_icp* icp, int n, int* done) {
+    return guarded(icp, [&] {
+        bool more = true;
+        for (int i = 0; i < n && more; ++i) more = BOTH(icp, icp->f->step(), icp->d->step());
+        if (done) *done = more ? 0 : 1;
+    });
+}
+
+int pmx_icp_finish(pmx_icp* icp, void* T_out) {
+    return guarded(icp, [&] { BOTH(icp, finish_impl<float>(icp, T_out), finish_impl<double>(icp, T_out)); });
+}
+
+int pmx_icp_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
+                    const void* nrm, const void* T_init, void* T_out) {
+    int rc = pmx_icp_prepare(icp, reading, rows, N, reference, M, nrm, T_init);
+    if (rc) return rc;
+    int done = 0;
+    while (!done) {
+        rc = pmx_icp_iterate(icp, 1 << 20, &done);
+        if (rc) return rc;
+    }
+    return pmx_icp_finish(icp, T_out);
+}
+
+int pmx_icp_stats_get(const pmx_icp* icp, pmx_icp_stats* out) {
+    if (!icp || !out) return PMX_ICP_INVALID_PARAMETER;
+    if (icp->dtype == 1)
+        stats_impl<double>(icp, out);
+    else
+        stats_impl<float>(icp, out);
+    return PMX_ICP_OK;
+}
+
+int pmx_icp_trace_get(const pmx_icp* icp, void* out, int max_iters) {
+    if (!icp || !out) return 0;
+    int n = 0;
+    if (icp->dtype == 1) {
+        for (auto& t : icp->d->trace) {
+            if (n >= max_iters) break;
+            std::memcpy((double*)out + (size_t)n * t.size(), t.data(), sizeof(double) * t.size());
+            ++n;
+        }
+    } else {
+        for (auto& t : icp->f->trace) {
+            if (n >= max_iters) break;
+            std::memcpy((float*)out + (size_t)n * t.size(), t.data(), sizeof(float) * t.size());
+            ++n;
+        }
+    }
+    return n;
+}
+
+int pmx_icp_timing(pmx_icp* icp, int on) {
+    return guarded(icp, [&] {
+        Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
+        dev.ensure();
+        dev.check(pmx_timing_enable(dev.ctx, on));
+    });
+}
+
+int pmx_icp_timing_read(pmx_icp* icp, double* ms, int64_t* launches) {
+    return guarded(icp, [&] {
+        Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
+        dev.ensure();
+        double other = 0;
+        dev.check(pmx_timing_read(dev.ctx, ms, launches, &other));
+    });
+}
+
+}  // extern "C"

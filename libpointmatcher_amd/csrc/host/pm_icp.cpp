@@ -1,0 +1,866 @@
+// pm_icp.cpp — modules, registry and the ICP loop of the GPU path.
+//
+// Module names, parameter names, defaults and bounds are those of the
+// reference so that libpointmatcher YAML chain files load unchanged:
+//   KDTreeMatcher                 MatchersImpl.h:74-103
+//   Null/MaxDist/MinDist/MedianDist/TrimmedDist/VarTrimmedDist OutlierFilter
+//                                 OutlierFiltersImpl.h:51-172
+//   PointToPlane / PointToPoint ErrorMinimizer
+//                                 ErrorMinimizers/PointToPlane.h:61-90, PointToPoint.h
+//   Counter / Differential / Bound TransformationChecker
+//                                 TransformationCheckersImpl.h:60-130
+//   IdentityDataPointsFilter, NullInspector, NullLogger (+ no-op stand-ins for
+//   the VTK/Performance inspectors and FileLogger, accepted for config
+//   compatibility)
+#include "pm_icp.h"
+
+#include <cstring>
+#include <iostream>
+
+namespace pm {
+
+// ------------------------------------------------------------------ Device --
+Device::~Device() {
+    if (ctx) pmx_ctx_destroy(ctx);
+}
+
+void Device::ensure() {
+    if (ctx) return;
+    const int rc = pmx_ctx_create(device, dtype, &ctx);
+    if (rc != PMX_OK) {
+        ctx = nullptr;
+        throw std::runtime_error("pmx_ctx_create failed (" + std::to_string(rc) + "): no usable HIP device " +
+                                 std::to_string(device) + " (" + std::to_string(pmx_device_count()) + " visible)");
+    }
+    if (nranks > 1) {
+        if (uid.size() != 128) throw std::runtime_error("multi-rank ICP needs a 128-byte RCCL unique id");
+        check(pmx_comm_init(ctx, uid.data(), nranks, rank));
+    }
+}
+
+void Device::check(int rc) const {
+    if (rc == PMX_OK) return;
+    const std::string msg = ctx ? pmx_last_error(ctx) : "no device context";
+    switch (rc) {
+    case PMX_E_NO_POINTS:
+    case PMX_E_EMPTY_QUANTILE:
+        throw ConvergenceError(msg);
+    case PMX_E_BAD_PARAM:
+        throw InvalidParameter(msg);
+    default:
+        throw std::runtime_error("pmx error " + std::to_string(rc) + ": " + msg);
+    }
+}
+
+template <typename T>
+static int dtype_of() {
+    return sizeof(T) == 8 ? PMX_F64 : PMX_F32;
+}
+
+// ----------------------------------------------------------------- Matches --
+template <typename T>
+void PointMatcher<T>::Matches::mirror() const {
+    if (mirrored) return;
+    dists.resize((size_t)n * knn);
+    ids.resize((size_t)n * knn);
+    dev->check(pmx_get_matches(dev->ctx, dists.data(), ids.data()));
+    mirrored = true;
+}
+
+template <typename T>
+T PointMatcher<T>::Matches::getDistsQuantile(T quantile) const {
+    mirror();
+    std::vector<T> v;
+    v.reserve(dists.size());
+    for (T d : dists)
+        if (d != std::numeric_limits<T>::infinity()) v.push_back(d);
+    if (v.empty()) throw ConvergenceError("no outlier to filter");
+    if (quantile < (T)0 || quantile > (T)1) throw ConvergenceError("quantile must be between 0 and 1");
+    if (quantile == (T)1) return *std::max_element(v.begin(), v.end());
+    size_t idx = (size_t)((T)v.size() * quantile);
+    if (idx >= v.size()) idx = v.size() - 1;
+    std::nth_element(v.begin(), v.begin() + idx, v.end());
+    return v[idx];
+}
+
+// ================================================================= modules ==
+namespace {
+
+template <typename T>
+using PM = PointMatcher<T>;
+
+// ---- KDTreeMatcher on the GPU (exact search; see pmx_match.hip) ----------
+template <typename T>
+struct KDTreeMatcherGPU : PM<T>::Matcher {
+    typedef typename PM<T>::Matches Matches;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("knn", "number of nearest neighbors to consider it the reference", "1", "1", "2147483647",
+                     &Parametrizable::Comp<unsigned>),
+                PDoc("epsilon", "approximation to use for the nearest-neighbor search", "0", "0", "inf",
+                     &Parametrizable::Comp<T>),
+                PDoc("searchType", "Nabo search type (the GPU search is exact for every type)", "1", "0", "2",
+                     &Parametrizable::Comp<unsigned>),
+                PDoc("maxDist", "maximum distance to consider for neighbors", "inf", "0", "inf",
+                     &Parametrizable::Comp<T>)};
+    }
+    int knn;
+    T epsilon;
+    int searchType;
+    T maxDist;
+    explicit KDTreeMatcherGPU(const Parametrizable::Parameters& p)
+        : PM<T>::Matcher("KDTreeMatcher", doc(), p),
+          knn(this->template get<int>("knn")),
+          epsilon(this->template get<T>("epsilon")),
+          searchType(this->template get<int>("searchType")),
+          maxDist(this->template get<T>("maxDist")) {}
+
+    void init(Device& dev, const DataPoints<T>& ref) override {
+        dev.ensure();
+        std::vector<T> nrm;
+        const T* np = nullptr;
+        if (ref.descriptorExists("normals")) {
+            int span = 0;
+            nrm = ref.descriptor("normals", &span);
+            if (span < ref.rows - 1) throw InvalidElement("normals descriptor has fewer rows than the dimension");
+            if (span != ref.rows - 1) {
+                std::vector<T> t((size_t)(ref.rows - 1) * ref.n);
+                for (int64_t i = 0; i < ref.n; ++i)
+                    for (int r = 0; r < ref.rows - 1; ++r) t[i * (ref.rows - 1) + r] = nrm[i * span + r];
+                nrm.swap(t);
+            }
+            np = nrm.data();
+        }
+        dev.check(pmx_set_reference(dev.ctx, ref.features.data(), ref.rows, ref.n, np));
+    }
+    Matches findClosests(Device& dev, const std::vector<T>& T_iter) override {
+        uint64_t visited = 0;
+        dev.check(pmx_match(dev.ctx, T_iter.data(), knn, (double)maxDist, (double)epsilon, &visited));
+        this->visitCounter += visited;
+        Matches m;
+        m.dev = &dev;
+        m.knn = knn;
+        int64_t n = 0;
+        pmx_get_shape(dev.ctx, &n, nullptr);
+        m.n = n;
+        return m;
+    }
+};
+
+// ---- outlier filters ------------------------------------------------------
+template <typename T>
+struct NullOF : PM<T>::OutlierFilter {
+    explicit NullOF(const Parametrizable::Parameters&) {}
+    void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
+        d.check(pmx_outlier_null(d.ctx, pos));
+    }
+};
+template <typename T>
+struct MaxDistOF : PM<T>::OutlierFilter {
+    T maxDist;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("maxDist", "threshold distance (Euclidean norm)", "1", "0.0000001", "inf", &Parametrizable::Comp<T>)};
+    }
+    explicit MaxDistOF(const Parametrizable::Parameters& p)
+        : PM<T>::OutlierFilter("MaxDistOutlierFilter", doc(), p), maxDist(this->template get<T>("maxDist")) {}
+    void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
+        d.check(pmx_outlier_maxdist(d.ctx, pos, (double)maxDist));
+    }
+};
+template <typename T>
+struct MinDistOF : PM<T>::OutlierFilter {
+    T minDist;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("minDist", "threshold distance (Euclidean norm)", "1", "0.0000001", "inf", &Parametrizable::Comp<T>)};
+    }
+    explicit MinDistOF(const Parametrizable::Parameters& p)
+        : PM<T>::OutlierFilter("MinDistOutlierFilter", doc(), p), minDist(this->template get<T>("minDist")) {}
+    void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
+        d.check(pmx_outlier_mindist(d.ctx, pos, (double)minDist));
+    }
+};
+template <typename T>
+struct MedianDistOF : PM<T>::OutlierFilter {
+    T factor;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("factor", "points farther away factor * median will be considered outliers.", "3", "0.0000001",
+                     "inf", &Parametrizable::Comp<T>)};
+    }
+    explicit MedianDistOF(const Parametrizable::Parameters& p)
+        : PM<T>::OutlierFilter("MedianDistOutlierFilter", doc(), p), factor(this->template get<T>("factor")) {}
+    void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
+        d.check(pmx_outlier_mediandist(d.ctx, pos, (double)factor));
+    }
+};
+template <typename T>
+struct TrimmedDistOF : PM<T>::OutlierFilter {
+    T ratio;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("ratio", "percentage to keep", "0.85", "0.0000001", "1.0", &Parametrizable::Comp<T>)};
+    }
+    explicit TrimmedDistOF(const Parametrizable::Parameters& p)
+        : PM<T>::OutlierFilter("TrimmedDistOutlierFilter", doc(), p), ratio(this->template get<T>("ratio")) {}
+    void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
+        d.check(pmx_outlier_trimmed(d.ctx, pos, (double)ratio));
+    }
+};
+template <typename T>
+struct VarTrimmedDistOF : PM<T>::OutlierFilter {
+    T minRatio, maxRatio, lambda;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("minRatio", "min ratio", "0.05", "0.0000001", "1", &Parametrizable::Comp<T>),
+                PDoc("maxRatio", "max ratio", "0.99", "0.0000001", "1", &Parametrizable::Comp<T>),
+                PDoc("lambda", "lambda (part of the term that balance the rmsd: 1/ratio^lambda", "2.35")};
+    }
+    explicit VarTrimmedDistOF(const Parametrizable::Parameters& p)
+        : PM<T>::OutlierFilter("VarTrimmedDistOutlierFilter", doc(), p),
+          minRatio(this->template get<T>("minRatio")),
+          maxRatio(this->template get<T>("maxRatio")),
+          lambda(this->template get<T>("lambda")) {
+        if (minRatio >= maxRatio)  // OutlierFiltersImpl.cpp:160-163
+            throw InvalidParameter("VarTrimmedDistOutlierFilter: minRatio (" + std::to_string(minRatio) +
+                                   ") should be smaller than maxRatio (" + std::to_string(maxRatio) + ")");
+    }
+    void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
+        d.check(pmx_outlier_vartrimmed(d.ctx, pos, (double)minRatio, (double)maxRatio, (double)lambda));
+    }
+};
+
+// ---- error minimisers -----------------------------------------------------
+template <typename T>
+void build_p2plane_transform(int rows, const T* x, std::vector<T>& out) {
+    // PointToPlane.cpp:245-312
+    out.assign((size_t)rows * rows, (T)0);
+    if (rows == 4) {
+        const T z = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
+        const T ang = std::sqrt(z);
+        T axis[3];
+        if (z > (T)0) {
+            const T sq = std::sqrt(z);
+            for (int i = 0; i < 3; ++i) axis[i] = x[i] / sq;
+        } else {
+            for (int i = 0; i < 3; ++i) axis[i] = x[i];
+        }
+        T R[9];
+        dense::angle_axis(ang, axis, R);
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) out[r * 4 + c] = R[r * 3 + c];
+            out[r * 4 + 3] = x[3 + r];
+        }
+        out[15] = 1;
+        bool nan = false;
+        for (T v : out)
+            if (v != v) nan = true;
+        if (nan)  // degenerate: identical clouds -> NaN rotation -> identity (PointToPlane.cpp:286-292)
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) out[r * 4 + c] = r == c ? (T)1 : (T)0;
+    } else {
+        const T s = std::sin(x[0]), c = std::cos(x[0]);
+        out = {c, -s, x[1], s, c, x[2], 0, 0, 1};
+    }
+}
+
+template <typename T>
+struct PointToPlaneEM : PM<T>::ErrorMinimizer {
+    bool force2D, force4DOF;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("force2D",
+                     "If set to true(1), the minimization will be forced to give a solution in 2D (i.e., on the "
+                     "XY-plane) even with 3D inputs.",
+                     "0", "0", "1", &Parametrizable::Comp<bool>),
+                PDoc("force4DOF",
+                     "If set to true(1), the minimization will optimize only yaw and translation, pitch and roll "
+                     "will follow the prior.",
+                     "0", "0", "1", &Parametrizable::Comp<bool>)};
+    }
+    explicit PointToPlaneEM(const Parametrizable::Parameters& p)
+        : PM<T>::ErrorMinimizer("PointToPlaneErrorMinimizer", doc(), p),
+          force2D(this->template get<T>("force2D") != (T)0),
+          force4DOF(this->template get<T>("force4DOF") != (T)0) {
+        if (force2D && force4DOF)
+            throw ConfigurationError("Force 2D cannot be used together with force4DOF.");
+    }
+    std::vector<T> compute(Device& d, int rows) override {
+        if (force2D || force4DOF)
+            throw ConfigurationError("PointToPlaneErrorMinimizer: force2D / force4DOF are outside the GPU path");
+        const int n = rows == 4 ? 6 : 3;
+        double A[36], b[6];
+        pmx_stats st;
+        d.check(pmx_p2plane_system(d.ctx, A, b, &st));
+        this->setStats(st);
+        T At[36], bt[6], x[6];
+        for (int i = 0; i < n * n; ++i) At[i] = (T)A[i];
+        for (int i = 0; i < n; ++i) bt[i] = (T)b[i];
+        dense::solve_underdetermined(At, bt, n, x);
+        std::vector<T> out;
+        build_p2plane_transform(rows, x, out);
+        return out;
+    }
+};
+
+template <typename T>
+struct PointToPointEM : PM<T>::ErrorMinimizer {
+    explicit PointToPointEM(const Parametrizable::Parameters&) { this->className = "PointToPointErrorMinimizer"; }
+    std::vector<T> compute(Device& d, int rows) override {
+        // PointToPoint.cpp:61-101
+        const int D = rows - 1;
+        double mp[3], mq[3], md[9];
+        pmx_stats st;
+        d.check(pmx_p2point_system(d.ctx, mp, mq, md, &st));
+        this->setStats(st);
+        T m[9], U[9], S[3], V[9], R[9], Vt[9];
+        for (int i = 0; i < D * D; ++i) m[i] = (T)md[i];
+        dense::jacobi_svd(m, D, U, S, V);
+        for (int r = 0; r < D; ++r)
+            for (int c = 0; c < D; ++c) Vt[r * D + c] = V[c * D + r];
+        auto mul = [&]() {
+            for (int r = 0; r < D; ++r)
+                for (int c = 0; c < D; ++c) {
+                    T s = 0;
+                    for (int k = 0; k < D; ++k) s = s + U[r * D + k] * Vt[k * D + c];
+                    R[r * D + c] = s;
+                }
+        };
+        mul();
+        const T det = D == 3 ? R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                                   R[2] * (R[3] * R[7] - R[4] * R[6])
+                             : R[0] * R[3] - R[1] * R[2];
+        if (det < (T)0) {
+            for (int c = 0; c < D; ++c) Vt[(D - 1) * D + c] = -Vt[(D - 1) * D + c];
+            mul();
+        }
+        std::vector<T> out((size_t)rows * rows, (T)0);
+        for (int r = 0; r < D; ++r) {
+            T s = 0;
+            for (int c = 0; c < D; ++c) s = s + R[r * D + c] * (T)mp[c];
+            for (int c = 0; c < D; ++c) out[r * rows + c] = R[r * D + c];
+            out[r * rows + D] = (T)mq[r] - s;
+        }
+        out[D * rows + D] = 1;
+        return out;
+    }
+};
+
+// ---- transformation checkers ------------------------------------------------
+template <typename T>
+void rot3(const std::vector<T>& M, int rows, T* m3) {
+    // topLeftCorner(3,3) — in 2-D this is the whole 3x3 homogeneous matrix,
+    // exactly as the reference's check() uses it
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) m3[r * 3 + c] = M[r * rows + c];
+}
+
+template <typename T>
+struct CounterTC : PM<T>::TransformationChecker {
+    unsigned maxIterationCount;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("maxIterationCount", "maximum number of iterations ", "40", "0", "2147483647",
+                     &Parametrizable::Comp<unsigned>)};
+    }
+    explicit CounterTC(const Parametrizable::Parameters& p)
+        : PM<T>::TransformationChecker("CounterTransformationChecker", doc(), p),
+          maxIterationCount(this->template get<unsigned>("maxIterationCount")) {
+        this->limits = {(T)maxIterationCount};
+        this->conditionVariableNames = {"Iteration"};
+        this->limitNames = {"Max iteration"};
+    }
+    void init(const std::vector<T>&, int, bool&) override { this->conditionVariables = {(T)0}; }
+    void check(const std::vector<T>&, int, bool& iterate) override {
+        this->conditionVariables[0] = this->conditionVariables[0] + (T)1;
+        if (this->conditionVariables[0] >= this->limits[0]) {  // TransformationCheckersImpl.cpp:71-75
+            iterate = false;
+            throw typename PM<T>::MaxNumIterationsReached();
+        }
+    }
+};
+
+template <typename T>
+struct DifferentialTC : PM<T>::TransformationChecker {
+    T minDiffRotErr, minDiffTransErr;
+    unsigned smoothLength;
+    std::vector<std::array<T, 4>> rotations;
+    std::vector<std::array<T, 3>> translations;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("minDiffRotErr", "threshold for rotation error (radian)", "0.001", "0.", "6.2831854",
+                     &Parametrizable::Comp<T>),
+                PDoc("minDiffTransErr", "threshold for translation error", "0.001", "0.", "inf", &Parametrizable::Comp<T>),
+                PDoc("smoothLength", "number of iterations over which to average the differencial error", "3", "0",
+                     "2147483647", &Parametrizable::Comp<unsigned>)};
+    }
+    explicit DifferentialTC(const Parametrizable::Parameters& p)
+        : PM<T>::TransformationChecker("DifferentialTransformationChecker", doc(), p),
+          minDiffRotErr(this->template get<T>("minDiffRotErr")),
+          minDiffTransErr(this->template get<T>("minDiffTransErr")),
+          smoothLength(this->template get<unsigned>("smoothLength")) {
+        this->limits = {minDiffRotErr, minDiffTransErr};
+    }
+    void push(const std::vector<T>& M, int rows, bool init2d) {
+        T m3[9], q[4];
+        if (init2d) {
+            // TransformationCheckersImpl.cpp:107-110: 2-D init uses [R 0; 0 1]
+            for (int i = 0; i < 9; ++i) m3[i] = (i % 4 == 0) ? (T)1 : (T)0;
+            m3[0] = M[0];
+            m3[1] = M[1];
+            m3[3] = M[3];
+            m3[4] = M[4];
+        } else {
+            rot3(M, rows, m3);
+        }
+        dense::quat_from_matrix(m3, q);
+        rotations.push_back({q[0], q[1], q[2], q[3]});
+        std::array<T, 3> t{0, 0, 0};
+        for (int r = 0; r < rows - 1; ++r) t[r] = M[r * rows + rows - 1];
+        translations.push_back(t);
+    }
+    void init(const std::vector<T>& M, int rows, bool&) override {
+        this->conditionVariables = {(T)0, (T)0};
+        rotations.clear();
+        translations.clear();
+        push(M, rows, rows != 4);
+    }
+    void check(const std::vector<T>& M, int rows, bool& iterate) override {
+        push(M, rows, false);
+        T cv0 = 0, cv1 = 0;
+        if (rotations.size() > smoothLength) {
+            for (size_t i = rotations.size() - 1; i >= rotations.size() - smoothLength; i--) {
+                cv0 = cv0 + std::fabs(dense::angular_distance(rotations[i].data(), rotations[i - 1].data()));
+                T nn = 0;
+                for (int r = 0; r < rows - 1; ++r) {
+                    const T d = translations[i][r] - translations[i - 1][r];
+                    nn = nn + d * d;
+                }
+                cv1 = cv1 + std::fabs(std::sqrt(nn));
+            }
+            cv0 = cv0 / (T)smoothLength;
+            cv1 = cv1 / (T)smoothLength;
+            if (cv0 < this->limits[0] && cv1 < this->limits[1]) iterate = false;
+        }
+        this->conditionVariables = {cv0, cv1};
+        if (cv0 != cv0) throw ConvergenceError("abs rotation norm not a number");
+        if (cv1 != cv1) throw ConvergenceError("abs translation norm not a number");
+    }
+};
+
+template <typename T>
+struct BoundTC : PM<T>::TransformationChecker {
+    T maxRotationNorm, maxTranslationNorm;
+    std::array<T, 4> q0{};
+    T rot2d0 = 0;
+    std::array<T, 3> t0{};
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("maxRotationNorm", "rotation bound", "1", "0", "inf", &Parametrizable::Comp<T>),
+                PDoc("maxTranslationNorm", "translation bound", "1", "0", "inf", &Parametrizable::Comp<T>)};
+    }
+    explicit BoundTC(const Parametrizable::Parameters& p)
+        : PM<T>::TransformationChecker("BoundTransformationChecker", doc(), p),
+          maxRotationNorm(this->template get<T>("maxRotationNorm")),
+          maxTranslationNorm(this->template get<T>("maxTranslationNorm")) {
+        this->limits = {maxRotationNorm, maxTranslationNorm};
+    }
+    void init(const std::vector<T>& M, int rows, bool&) override {
+        this->conditionVariables = {(T)0, (T)0};
+        if (rows == 4) {
+            T m3[9];
+            rot3(M, rows, m3);
+            dense::quat_from_matrix(m3, q0.data());
+        } else {
+            rot2d0 = std::acos(M[0]);
+        }
+        for (int r = 0; r < rows - 1; ++r) t0[r] = M[r * rows + rows - 1];
+    }
+    void check(const std::vector<T>& M, int rows, bool&) override {
+        T cv0;
+        if (rows == 4) {
+            T m3[9], q[4];
+            rot3(M, rows, m3);
+            dense::quat_from_matrix(m3, q);
+            cv0 = dense::angular_distance(q, q0.data());
+        } else {
+            T v = std::acos(M[0]) - rot2d0;
+            while (v > (T)3.14159265358979323846) v -= (T)(2 * 3.14159265358979323846);
+            while (v < (T)-M_PI) v += (T)(2 * 3.14159265358979323846);
+            cv0 = v;
+        }
+        T nn = 0;
+        for (int r = 0; r < rows - 1; ++r) {
+            const T d = M[r * rows + rows - 1] - t0[r];
+            nn = nn + d * d;
+        }
+        const T cv1 = std::sqrt(nn);
+        this->conditionVariables = {cv0, cv1};
+        if (cv0 > this->limits[0] || cv1 > this->limits[1]) {
+            std::ostringstream oss;
+            oss << "limit out of bounds: rot: " << cv0 << "/" << this->limits[0] << " tr: " << cv1 << "/"
+                << this->limits[1];
+            throw ConvergenceError(oss.str());
+        }
+    }
+};
+
+// ---- data filters / inspectors / loggers -----------------------------------
+template <typename T>
+struct IdentityDPF : PM<T>::DataPointsFilter {
+    explicit IdentityDPF(const Parametrizable::Parameters&) { this->className = "IdentityDataPointsFilter"; }
+    void inPlaceFilter(DataPoints<T>&) override {}
+};
+
+// Reference data filters that are outside the hot path:
+// registered with the reference's parameter docs so chain files validate
+// exactly as in the reference (bounds, unused parameters, module types), but
+// applying one throws — they never run silently.
+template <typename T>
+struct UnsupportedDPF : PM<T>::DataPointsFilter {
+    UnsupportedDPF(const std::string& name, const Parametrizable::ParametersDoc& d, const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter(name, d, p) {
+        for (auto& pd : d) this->getParamValueString(pd.name);
+    }
+    void inPlaceFilter(DataPoints<T>&) override {
+        throw ConfigurationError(this->className +
+                                 " is outside the MI355X ICP path; pre-filter the clouds (and provide reference "
+                                 "normals) before calling ICP");
+    }
+};
+
+template <typename T>
+void register_unsupported_filters(Registrar<typename PM<T>::DataPointsFilter>& R) {
+    typedef Parametrizable::Parameters Ps;
+    typedef Parametrizable P;
+    auto add = [&](const std::string& name, Parametrizable::ParametersDoc d) {
+        R.reg(name, [name, d](const Ps& p) { return std::make_shared<UnsupportedDPF<T>>(name, d, p); }, true);
+    };
+    add("RandomSamplingDataPointsFilter",
+        {PDoc("prob", "probability to keep a point, one over decimation factor ", "0.75", "0", "1", &P::Comp<T>)});
+    add("SamplingSurfaceNormalDataPointsFilter",
+        {PDoc("ratio", "ratio of points to keep with random subsampling", "0.5", "0.0000001", "1.0", &P::Comp<T>),
+         PDoc("knn", "how many points are used to compute the normals", "7", "3", "2147483647", &P::Comp<unsigned>),
+         PDoc("samplingMethod", "0: random subsampling, 1: bin subsampling", "0", "0", "1", &P::Comp<unsigned>),
+         PDoc("maxBoxDim", "maximum length of a box above which the box is discarded", "inf"),
+         PDoc("averageExistingDescriptors", "keep and average existing descriptors", "1"),
+         PDoc("keepNormals", "add normals as descriptors", "1"), PDoc("keepDensities", "add densities", "0"),
+         PDoc("keepEigenValues", "add eigen values", "0"), PDoc("keepEigenVectors", "add eigen vectors", "0")});
+    add("SurfaceNormalDataPointsFilter",
+        {PDoc("knn", "number of nearest neighbors to consider, including the point itself", "5", "3", "2147483647",
+              &P::Comp<unsigned>),
+         PDoc("maxDist", "maximum distance to consider for neighbors", "inf", "0", "inf", &P::Comp<T>),
+         PDoc("epsilon", "approximation to use for the nearest-neighbor search", "0", "0", "inf", &P::Comp<T>),
+         PDoc("keepNormals", "add normals", "1"), PDoc("keepDensities", "add densities", "0"),
+         PDoc("keepEigenValues", "add eigen values", "0"), PDoc("keepEigenVectors", "add eigen vectors", "0"),
+         PDoc("keepMatchedIds", "add matched ids", "0"), PDoc("keepMeanDist", "add mean distance", "0"),
+         PDoc("sortEigen", "sort eigenvalues", "0"), PDoc("smoothNormals", "average normals", "0")});
+    add("MaxDistDataPointsFilter",
+        {PDoc("dim", "dimension on which the filter will be applied. x=0, y=1, z=2, radius=-1", "-1", "-1", "2",
+              &P::Comp<int>),
+         PDoc("maxDist", "maximum distance authorized", "1", "-inf", "inf", &P::Comp<T>)});
+    add("MinDistDataPointsFilter",
+        {PDoc("dim", "dimension on which the filter will be applied. x=0, y=1, z=2, radius=-1", "-1", "-1", "2",
+              &P::Comp<int>),
+         PDoc("minDist", "minimum value authorized", "1", "-inf", "inf", &P::Comp<T>)});
+}
+
+// no-op stand-in accepting a reference module's parameters (reads them all so
+// the "set but not used" check passes)
+template <typename Base>
+struct NoOp : Base {
+    NoOp(const std::string& name, const Parametrizable::ParametersDoc& d, const Parametrizable::Parameters& p)
+        : Base(name, d, p) {
+        for (auto& pd : d) this->getParamValueString(pd.name);
+    }
+};
+
+template <typename T>
+Parametrizable::ParametersDoc perf_doc() {
+    return {PDoc("baseFileName", "base file name for the statistics files (if empty, disabled)", ""),
+            PDoc("dumpPerfOnExit", "dump performance statistics to stderr on exit", "0"),
+            PDoc("dumpStats", "dump the statistics on first and last step", "0")};
+}
+template <typename T>
+Parametrizable::ParametersDoc vtk_doc() {
+    return {PDoc("baseFileName", "base file name for the VTK files ", "point-matcher-output"),
+            PDoc("dumpPerfOnExit", "dump performance statistics to stderr on exit", "0"),
+            PDoc("dumpStats", "dump the statistics on first and last step", "0"),
+            PDoc("dumpIterationInfo", "dump iteration info", "0"),
+            PDoc("dumpDataLinks", "dump data links at each iteration", "0"),
+            PDoc("dumpReading", "dump the reading cloud at each iteration", "0"),
+            PDoc("dumpReference", "dump the reference cloud at each iteration", "0"),
+            PDoc("writeBinary", "write binary VTK files", "0")};
+}
+inline Parametrizable::ParametersDoc filelogger_doc() {
+    return {PDoc("infoFileName", "name of the file to output infos to", ""),
+            PDoc("warningFileName", "name of the file to output warnings to", ""),
+            PDoc("displayLocation", "display the location of message in source code", "0")};
+}
+
+}  // namespace
+
+// --------------------------------------------------------------- registry --
+template <typename T>
+PointMatcher<T>::PointMatcher() {
+    typedef Parametrizable::Parameters Ps;
+    MatcherRegistrar.reg("KDTreeMatcher", [](const Ps& p) { return std::make_shared<KDTreeMatcherGPU<T>>(p); }, true,
+                         "This matcher matches a point from the reading to its closest neighbors in the reference.");
+    OutlierFilterRegistrar.reg("NullOutlierFilter", [](const Ps& p) { return std::make_shared<NullOF<T>>(p); }, false);
+    OutlierFilterRegistrar.reg("MaxDistOutlierFilter", [](const Ps& p) { return std::make_shared<MaxDistOF<T>>(p); }, true);
+    OutlierFilterRegistrar.reg("MinDistOutlierFilter", [](const Ps& p) { return std::make_shared<MinDistOF<T>>(p); }, true);
+    OutlierFilterRegistrar.reg("MedianDistOutlierFilter", [](const Ps& p) { return std::make_shared<MedianDistOF<T>>(p); },
+                               true);
+    OutlierFilterRegistrar.reg("TrimmedDistOutlierFilter", [](const Ps& p) { return std::make_shared<TrimmedDistOF<T>>(p); },
+                               true);
+    OutlierFilterRegistrar.reg("VarTrimmedDistOutlierFilter",
+                               [](const Ps& p) { return std::make_shared<VarTrimmedDistOF<T>>(p); }, true);
+    ErrorMinimizerRegistrar.reg("PointToPlaneErrorMinimizer",
+                                [](const Ps& p) { return std::make_shared<PointToPlaneEM<T>>(p); }, true);
+    ErrorMinimizerRegistrar.reg("PointToPointErrorMinimizer",
+                                [](const Ps& p) { return std::make_shared<PointToPointEM<T>>(p); }, false);
+    TransformationCheckerRegistrar.reg("CounterTransformationChecker",
+                                       [](const Ps& p) { return std::make_shared<CounterTC<T>>(p); }, true);
+    TransformationCheckerRegistrar.reg("DifferentialTransformationChecker",
+                                       [](const Ps& p) { return std::make_shared<DifferentialTC<T>>(p); }, true);
+    TransformationCheckerRegistrar.reg("BoundTransformationChecker",
+                                       [](const Ps& p) { return std::make_shared<BoundTC<T>>(p); }, true);
+    DataPointsFilterRegistrar.reg("IdentityDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<IdentityDPF<T>>(p); }, false);
+    register_unsupported_filters<T>(DataPointsFilterRegistrar);
+    InspectorRegistrar.reg("NullInspector", [](const Ps& p) {
+        return std::make_shared<NoOp<Inspector>>("NullInspector", Parametrizable::ParametersDoc(), p);
+    }, false);
+    InspectorRegistrar.reg("PerformanceInspector", [](const Ps& p) {
+        return std::make_shared<NoOp<Inspector>>("PerformanceInspector", perf_doc<T>(), p);
+    }, true);
+    InspectorRegistrar.reg("VTKFileInspector", [](const Ps& p) {
+        return std::make_shared<NoOp<Inspector>>("VTKFileInspector", vtk_doc<T>(), p);
+    }, true);
+    LoggerRegistrar.reg("NullLogger", [](const Ps& p) {
+        return std::make_shared<NoOp<Logger>>("NullLogger", Parametrizable::ParametersDoc(), p);
+    }, false);
+    LoggerRegistrar.reg("FileLogger", [](const Ps& p) {
+        return std::make_shared<NoOp<Logger>>("FileLogger", filelogger_doc(), p);
+    }, true);
+}
+
+template <typename T>
+const PointMatcher<T>& PointMatcher<T>::get() {
+    static const PointMatcher<T> instance;
+    return instance;
+}
+
+template <typename T>
+void PointMatcher<T>::ErrorMinimizer::setStats(const pmx_stats& st) {
+    const double kn = (double)st.n_total;
+    keptPoints = st.kept;
+    pointUsedRatio = (T)((double)st.kept / kn);
+    weightedPointUsedRatio = (T)(st.sum_w / kn);
+    nbRejectedMatches = st.rejected_matches;
+    nbRejectedPoints = st.rejected_points;
+}
+
+template <typename T>
+void PointMatcher<T>::OutlierFilters::compute(Device& dev, const Matches& m) {
+    if (this->empty()) {
+        dev.check(pmx_outlier_default(dev.ctx));
+        return;
+    }
+    int pos = 0;
+    for (auto& f : *this) f->compute(dev, m, pos++);
+}
+
+template <typename T>
+void PointMatcher<T>::TransformationCheckers::init(const TransformationParameters& T_, int rows, bool& iterate) {
+    for (auto& c : *this) c->init(T_, rows, iterate);
+}
+template <typename T>
+void PointMatcher<T>::TransformationCheckers::check(const TransformationParameters& T_, int rows, bool& iterate) {
+    for (auto& c : *this) c->check(T_, rows, iterate);
+}
+
+// ==================================================================== ICP ==
+template <typename T>
+PointMatcher<T>::ICP::ICP(int device) {
+    dev.device = device;
+    dev.dtype = dtype_of<T>();
+}
+
+template <typename T>
+void PointMatcher<T>::ICP::cleanup() {
+    readingDataPointsFilters.clear();
+    readingStepDataPointsFilters.clear();
+    referenceDataPointsFilters.clear();
+    matcher.reset();
+    outlierFilters.clear();
+    errorMinimizer.reset();
+    transformationCheckers.clear();
+    inspector.reset();
+}
+
+template <typename T>
+void PointMatcher<T>::ICP::setDefault() {
+    // ICP.cpp:99-113.  RandomSampling and SamplingSurfaceNormal (the default
+    // reading / reference data filters) are outside the GPU path: the
+    // reference cloud must carry "normals" (SURVEY.md §8(f) row 1).
+    cleanup();
+    const PointMatcher& pm = PointMatcher::get();
+    outlierFilters.push_back(pm.OutlierFilterRegistrar.create("TrimmedDistOutlierFilter"));
+    matcher = pm.MatcherRegistrar.create("KDTreeMatcher");
+    errorMinimizer = pm.ErrorMinimizerRegistrar.create("PointToPlaneErrorMinimizer");
+    transformationCheckers.push_back(pm.TransformationCheckerRegistrar.create("CounterTransformationChecker"));
+    transformationCheckers.push_back(pm.TransformationCheckerRegistrar.create("DifferentialTransformationChecker"));
+    inspector = pm.InspectorRegistrar.create("NullInspector");
+}
+
+template <typename T>
+void PointMatcher<T>::ICP::loadFromYaml(const std::string& text) {
+    cleanup();
+    const YNode doc = parse_yaml(text);
+    if (doc.kind != YNode::Map && doc.kind != YNode::Null) throw ConfigurationError("YAML chain must be a map");
+    const PointMatcher& pm = PointMatcher::get();
+    std::set<std::string> used;
+    auto many = [&](const std::string& key, auto& reg, auto& vec) {
+        used.insert(key);
+        const YNode* n = doc.find(key);
+        if (!n) return;
+        for (const YNode& item : n->seq) vec.push_back(reg.createFromYAML(item));
+    };
+    auto one = [&](const std::string& key, auto& reg, auto& ptr) {
+        used.insert(key);
+        const YNode* n = doc.find(key);
+        if (n)
+            ptr = reg.createFromYAML(*n);
+        else
+            ptr.reset();
+    };
+    one("logger", pm.LoggerRegistrar, logger);  // ICP.cpp:131-135 (logger first)
+    many("readingDataPointsFilters", pm.DataPointsFilterRegistrar, readingDataPointsFilters);
+    many("readingStepDataPointsFilters", pm.DataPointsFilterRegistrar, readingStepDataPointsFilters);
+    many("referenceDataPointsFilters", pm.DataPointsFilterRegistrar, referenceDataPointsFilters);
+    one("matcher", pm.MatcherRegistrar, matcher);
+    many("outlierFilters", pm.OutlierFilterRegistrar, outlierFilters);
+    one("errorMinimizer", pm.ErrorMinimizerRegistrar, errorMinimizer);
+    many("transformationCheckers", pm.TransformationCheckerRegistrar, transformationCheckers);
+    one("inspector", pm.InspectorRegistrar, inspector);
+    for (const auto& kv : doc.map)  // ICP.cpp:158-166
+        if (!used.count(kv.first)) throw InvalidModuleType("Module type " + kv.first + " does not exist");
+}
+
+template <typename T>
+typename PointMatcher<T>::TransformationParameters PointMatcher<T>::ICP::operator()(const DataPoints& reading,
+                                                                                     const DataPoints& reference) {
+    const int dim = reading.rows;
+    TransformationParameters I((size_t)dim * dim, (T)0);
+    for (int i = 0; i < dim; ++i) I[i * dim + i] = 1;
+    return compute(reading, reference, I);
+}
+
+template <typename T>
+typename PointMatcher<T>::TransformationParameters PointMatcher<T>::ICP::compute(
+    const DataPoints& reading, const DataPoints& reference, const TransformationParameters& T_init) {
+    prepare(reading, reference, T_init);
+    while (step()) {
+    }
+    return finish();
+}
+
+template <typename T>
+static double since(const std::chrono::steady_clock::time_point& t) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+}
+
+template <typename T>
+void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints& referenceIn,
+                                   const TransformationParameters& T_init) {
+    // ICP::compute, ICP.cpp:265-313
+    if (!matcher) throw std::runtime_error("You must setup a matcher before running ICP");
+    if (!errorMinimizer) throw std::runtime_error("You must setup an error minimizer before running ICP");
+    if (!inspector) throw std::runtime_error("You must setup an inspector before running ICP");
+    auto t = std::chrono::steady_clock::now();
+    const int dim = referenceIn.rows;
+    if (dim != 3 && dim != 4) throw std::runtime_error("clouds must be 2-D or 3-D (3 or 4 homogeneous rows)");
+    DataPoints reference(referenceIn);
+    referenceDataPointsFilters.init();
+    referenceDataPointsFilters.apply(reference);
+    const int64_t M = reference.n;
+    if (M <= 0) throw ConvergenceError("empty reference");
+    // mean of the reference columns in T (sequential), ICP.cpp:291-292
+    T_refIn_refMean_.assign((size_t)dim * dim, (T)0);
+    for (int i = 0; i < dim; ++i) T_refIn_refMean_[i * dim + i] = 1;
+    for (int r = 0; r < dim - 1; ++r) {
+        T s = 0;
+        for (int64_t j = 0; j < M; ++j) s = s + reference.features[j * dim + r];
+        const T mean = s / (T)M;
+        T_refIn_refMean_[r * dim + dim - 1] = mean;
+        for (int64_t j = 0; j < M; ++j) reference.features[j * dim + r] = reference.features[j * dim + r] - mean;
+    }
+    dev.ensure();
+    matcher->init(dev, reference);  // ICP.cpp:302
+    referencePreprocessingDuration = since<T>(t);
+    prefilteredReferencePtsCount = M;
+
+    // computeWithTransformedReference, ICP.cpp:317-370
+    if ((int64_t)T_init.size() != (int64_t)dim * dim)
+        throw std::runtime_error("The shape of initial transformation matrix must be NxN. Where N is the number of "
+                                 "rows in the read/reference scans.");
+    if (readingIn.rows != dim) throw std::runtime_error("reading and reference dimensions differ");
+    t = std::chrono::steady_clock::now();
+    DataPoints reading(readingIn);
+    readingDataPointsFilters.init();
+    readingDataPointsFilters.apply(reading);
+    if (!readingStepDataPointsFilters.empty())
+        throw ConfigurationError("readingStepDataPointsFilters are outside the GPU path (the step reading is never "
+                                 "materialised on the host)");
+    // T_refMean_dataIn = T_refIn_refMean^-1 * T_init (the inverse of a pure
+    // translation is exact), ICP.cpp:345-346
+    TransformationParameters inv((size_t)dim * dim, (T)0);
+    for (int i = 0; i < dim; ++i) inv[i * dim + i] = 1;
+    for (int r = 0; r < dim - 1; ++r) inv[r * dim + dim - 1] = -T_refIn_refMean_[r * dim + dim - 1];
+    T_refMean_dataIn_.assign((size_t)dim * dim, (T)0);
+    dense::matmul(inv.data(), T_init.data(), dim, T_refMean_dataIn_.data());
+    if (std::fabs((T)1 - dense::det_rot(T_refMean_dataIn_.data(), dim)) > (T)0.001)
+        throw TransformationError("RigidTransformation: Error, rotation matrix is not orthogonal.");
+    // transformations.apply(reading, T_refMean_dataIn): done on the device
+    dev.check(pmx_set_reading(dev.ctx, reading.features.data(), dim, reading.n, T_refMean_dataIn_.data()));
+    rows_ = dim;
+    T_iter_.assign((size_t)dim * dim, (T)0);
+    for (int i = 0; i < dim; ++i) T_iter_[i * dim + i] = 1;
+    iterate_ = true;
+    maxNumIterationsReached = false;
+    transformationCheckers.init(T_iter_, dim, iterate_);
+    iterationCount = 0;
+    trace.clear();
+    readingPreprocessingDuration = since<T>(t);
+    prefilteredReadingPtsCount = reading.n;
+    t0_ = std::chrono::steady_clock::now();
+}
+
+template <typename T>
+bool PointMatcher<T>::ICP::step() {
+    // one pass of the loop body, ICP.cpp:371-430
+    if (!iterate_) return false;
+    const int dim = rows_;
+    if (std::fabs((T)1 - dense::det_rot(T_iter_.data(), dim)) > (T)0.001)  // TransformationsImpl.cpp:62-63
+        throw TransformationError("RigidTransformation: Error, rotation matrix is not orthogonal.");
+    const Matches matches = matcher->findClosests(dev, T_iter_);
+    outlierFilters.compute(dev, matches);
+    const TransformationParameters dT = errorMinimizer->compute(dev, dim);
+    dense::matmul(dT.data(), T_iter_.data(), dim, T_iter_.data());
+    try {
+        transformationCheckers.check(T_iter_, dim, iterate_);
+    } catch (const MaxNumIterationsReached&) {
+        iterate_ = false;
+        maxNumIterationsReached = true;
+    }
+    ++iterationCount;
+    if (keepTrace) trace.push_back(T_iter_);
+    return iterate_;
+}
+
+template <typename T>
+typename PointMatcher<T>::TransformationParameters PointMatcher<T>::ICP::finish() {
+    convergenceDuration = since<T>(t0_);
+    const int dim = rows_;
+    TransformationParameters tmp((size_t)dim * dim), out((size_t)dim * dim);
+    dense::matmul(T_refIn_refMean_.data(), T_iter_.data(), dim, tmp.data());
+    dense::matmul(tmp.data(), T_refMean_dataIn_.data(), dim, out.data());
+    return out;  // ICP.cpp:448
+}
+
+template struct PointMatcher<float>;
+template struct PointMatcher<double>;
+
+}  // namespace pm

@@ -1,0 +1,201 @@
+// pm_icp.h — PointMatcher<T> restated for the device-resident GPU path.
+//
+// The class layout follows pointmatcher/PointMatcher.h (Matcher :470-485,
+// OutlierFilter :496-514, ErrorMinimizer :527-569, TransformationChecker
+// :580-610, ICPChainBase / ICP :652-764) and the loop of
+// pointmatcher/ICP.cpp:265-449.  The differences are the ones device
+// residency forces:
+//   * Matches and OutlierWeights live in HBM (inside the pmx_ctx the ICP
+//     object owns); host copies are made lazily (Matches::mirror()).
+//   * The step transform is not applied to a host copy of the reading
+//     (ICP.cpp:373-381): it is passed to the matcher and fused into the match
+//     kernel; the minimiser kernels re-apply it bit-identically.
+//   * Plugins receive the device context explicitly.
+#pragma once
+
+#include <array>
+#include <chrono>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pm_core.h"
+#include "pmx.h"
+
+namespace pm {
+
+// device handle shared by the modules of one ICP object
+struct Device {
+    pmx_ctx* ctx = nullptr;
+    int device = 0;
+    int dtype = PMX_F32;
+    int nranks = 1;
+    int rank = 0;
+    std::vector<unsigned char> uid;  // RCCL unique id when nranks > 1
+    ~Device();
+    void ensure();
+    void check(int rc) const;  // PMX_E_* -> reference exception types
+};
+
+template <typename T>
+struct PointMatcher {
+    typedef pm::DataPoints<T> DataPoints;
+    typedef std::vector<T> TransformationParameters;  // rows x rows, row-major
+    typedef Parametrizable::Parameters Parameters;
+    typedef Parametrizable::ParametersDoc ParametersDoc;
+
+    // Matches (PointMatcher.h:371-391): k x N squared distances + ids, on the
+    // device; mirror() copies them to the host.
+    struct Matches {
+        Device* dev = nullptr;
+        int knn = 0;
+        int64_t n = 0;
+        mutable bool mirrored = false;
+        mutable std::vector<T> dists;
+        mutable std::vector<int32_t> ids;
+        void mirror() const;
+        T getDistsQuantile(T quantile) const;  // Matches.cpp:60-87 (host, on the mirror)
+    };
+
+    // ---------------------------------------------------------- Matcher --
+    struct Matcher : Parametrizable {
+        uint64_t visitCounter = 0;
+        Matcher() {}
+        Matcher(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
+        virtual ~Matcher() {}
+        void resetVisitCount() { visitCounter = 0; }
+        uint64_t getVisitCount() const { return visitCounter; }
+        virtual void init(Device& dev, const DataPoints& filteredReference) = 0;
+        virtual Matches findClosests(Device& dev, const TransformationParameters& T_iter) = 0;
+    };
+
+    // ---------------------------------------------------- OutlierFilter --
+    struct OutlierFilter : Parametrizable {
+        OutlierFilter() {}
+        OutlierFilter(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
+        virtual ~OutlierFilter() {}
+        // multiply this filter's weights into the device weights
+        // (chain_pos 0 assigns) — OutlierFilter.cpp:90-99
+        virtual void compute(Device& dev, const Matches& m, int chain_pos) = 0;
+    };
+    struct OutlierFilters : std::vector<std::shared_ptr<OutlierFilter>> {
+        void compute(Device& dev, const Matches& m);  // OutlierFilter.cpp:63-103
+    };
+
+    // --------------------------------------------------- ErrorMinimizer --
+    struct ErrorMinimizer : Parametrizable {
+        // ErrorElements statistics (ErrorMinimizer.cpp:133-192)
+        T pointUsedRatio = -1;
+        T weightedPointUsedRatio = -1;
+        int64_t nbRejectedMatches = -1;
+        int64_t nbRejectedPoints = -1;
+        int64_t keptPoints = 0;
+        ErrorMinimizer() {}
+        ErrorMinimizer(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
+        virtual ~ErrorMinimizer() {}
+        virtual TransformationParameters compute(Device& dev, int rows) = 0;
+        T getPointUsedRatio() const { return pointUsedRatio; }
+        T getWeightedPointUsedRatio() const { return weightedPointUsedRatio; }
+        virtual T getOverlap() const { return weightedPointUsedRatio; }
+        void setStats(const pmx_stats& st);
+    };
+
+    // --------------------------------------------- TransformationChecker --
+    struct TransformationChecker : Parametrizable {
+        std::vector<T> limits, conditionVariables;
+        std::vector<std::string> limitNames, conditionVariableNames;
+        TransformationChecker() {}
+        TransformationChecker(const std::string& n, const ParametersDoc& d, const Parameters& p)
+            : Parametrizable(n, d, p) {}
+        virtual ~TransformationChecker() {}
+        virtual void init(const TransformationParameters& T_, int rows, bool& iterate) = 0;
+        virtual void check(const TransformationParameters& T_, int rows, bool& iterate) = 0;
+    };
+    struct TransformationCheckers : std::vector<std::shared_ptr<TransformationChecker>> {
+        void init(const TransformationParameters& T_, int rows, bool& iterate);
+        void check(const TransformationParameters& T_, int rows, bool& iterate);
+    };
+    struct MaxNumIterationsReached {};
+
+    // ---------------------------------------- data filters / inspector / logger --
+    struct DataPointsFilter : Parametrizable {
+        DataPointsFilter() {}
+        DataPointsFilter(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
+        virtual ~DataPointsFilter() {}
+        virtual void init() {}
+        virtual void inPlaceFilter(DataPoints& cloud) = 0;
+    };
+    struct DataPointsFilters : std::vector<std::shared_ptr<DataPointsFilter>> {
+        void init() {
+            for (auto& f : *this) f->init();
+        }
+        void apply(DataPoints& c) {
+            for (auto& f : *this) f->inPlaceFilter(c);
+        }
+    };
+    struct Inspector : Parametrizable {
+        Inspector() {}
+        Inspector(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
+        virtual ~Inspector() {}
+    };
+    struct Logger : Parametrizable {
+        Logger() {}
+        Logger(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
+        virtual ~Logger() {}
+    };
+
+    // ---------------------------------------------------------- registry --
+    Registrar<Matcher> MatcherRegistrar;
+    Registrar<OutlierFilter> OutlierFilterRegistrar;
+    Registrar<ErrorMinimizer> ErrorMinimizerRegistrar;
+    Registrar<TransformationChecker> TransformationCheckerRegistrar;
+    Registrar<DataPointsFilter> DataPointsFilterRegistrar;
+    Registrar<Inspector> InspectorRegistrar;
+    Registrar<Logger> LoggerRegistrar;
+    PointMatcher();
+    static const PointMatcher& get();
+
+    // --------------------------------------------------------------- ICP --
+    struct ICP {
+        DataPointsFilters readingDataPointsFilters, readingStepDataPointsFilters, referenceDataPointsFilters;
+        std::shared_ptr<Matcher> matcher;
+        OutlierFilters outlierFilters;
+        std::shared_ptr<ErrorMinimizer> errorMinimizer;
+        TransformationCheckers transformationCheckers;
+        std::shared_ptr<Inspector> inspector;
+        std::shared_ptr<Logger> logger;
+        Device dev;
+
+        ICP(int device = 0);
+        void cleanup();
+        void setDefault();                       // ICP.cpp:99-113
+        void loadFromYaml(const std::string& text);  // ICP.cpp:116-167
+
+        TransformationParameters operator()(const DataPoints& reading, const DataPoints& reference);
+        TransformationParameters compute(const DataPoints& reading, const DataPoints& reference,
+                                         const TransformationParameters& T_init);  // ICP.cpp:265-313
+
+        // the loop of computeWithTransformedReference (ICP.cpp:317-449) in three
+        // phases, so a caller can time the iterations alone
+        void prepare(const DataPoints& reading, const DataPoints& reference, const TransformationParameters& T_init);
+        bool step();                          // one iteration; false when a checker stopped
+        TransformationParameters finish();    // T_refIn_refMean * T_iter * T_refMean_dataIn
+
+        // statistics (Inspector::addStat names, ICP.cpp:305-307, 363-365, 432-436)
+        int64_t iterationCount = 0;
+        bool maxNumIterationsReached = false;
+        double convergenceDuration = 0, referencePreprocessingDuration = 0, readingPreprocessingDuration = 0;
+        int64_t prefilteredReadingPtsCount = 0, prefilteredReferencePtsCount = 0;
+        std::vector<TransformationParameters> trace;  // T_iter after each iteration
+        bool keepTrace = false;
+        bool getMaxNumIterationsReached() const { return maxNumIterationsReached; }
+
+      private:
+        int rows_ = 0;
+        bool iterate_ = false;
+        TransformationParameters T_refIn_refMean_, T_refMean_dataIn_, T_iter_;
+        std::chrono::steady_clock::time_point t0_;
+    };
+};
+
+}  // namespace pm

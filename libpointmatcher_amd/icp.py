@@ -1,0 +1,187 @@
+"""ctypes binding of the host ICP chain (include/pmx_icp.h, lib/libpmx_icp.so).
+
+    icp = ICP(np.float32)
+    icp.load_yaml(open("chain.yaml").read())     # or icp.set_default()
+    T = icp.compute(reading, reference, ref_normals)
+
+Clouds are (n, rows) arrays with the homogeneous row last (rows = D + 1) —
+the memory layout of the reference's column-major (D+1) x n features.
+Errors raise the Python mirrors of the reference exception types.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _capi
+from ._capi import ConvergenceError, InvalidParameter, TransformationError
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "lib", "libpmx_icp.so")
+
+
+class InvalidElement(RuntimeError):
+    """InvalidElement (pointmatcher/Registrar.h:69-72): unknown module name."""
+
+
+class InvalidModuleType(RuntimeError):
+    """ICPChainBase::InvalidModuleType (pointmatcher/ICP.cpp:158-166)."""
+
+
+class ConfigurationError(RuntimeError):
+    """PointMatcherSupport::ConfigurationError / YAML syntax."""
+
+
+_ERR = {-1: ConvergenceError, -3: InvalidParameter, -4: TransformationError, -5: InvalidElement,
+        -6: InvalidModuleType, -7: ConfigurationError, -10: RuntimeError}
+
+
+class IcpStats(C.Structure):
+    _fields_ = [("iterations", C.c_int64), ("point_count_touched", C.c_int64),
+                ("overlap_ratio", C.c_double), ("point_used_ratio", C.c_double), ("kept", C.c_int64),
+                ("rejected_matches", C.c_int64), ("rejected_points", C.c_int64),
+                ("convergence_duration", C.c_double), ("reference_preprocessing_duration", C.c_double),
+                ("reading_preprocessing_duration", C.c_double), ("max_iterations_reached", C.c_int)]
+
+    def asdict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _capi.lib()  # libpmx.so first (RTLD_GLOBAL)
+        if not os.path.exists(LIB):
+            raise _capi.PmxError(f"{LIB} not built")
+        l = C.CDLL(LIB)
+        l.pmx_icp_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        l.pmx_icp_destroy.argtypes = [C.c_void_p]
+        l.pmx_icp_last_error.argtypes = [C.c_void_p]
+        l.pmx_icp_last_error.restype = C.c_char_p
+        l.pmx_icp_set_default.argtypes = [C.c_void_p]
+        l.pmx_icp_load_yaml.argtypes = [C.c_void_p, C.c_char_p]
+        l.pmx_icp_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        l.pmx_icp_keep_trace.argtypes = [C.c_void_p, C.c_int]
+        l.pmx_icp_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int64,
+                                      C.c_void_p, C.c_void_p, C.c_void_p]
+        l.pmx_icp_prepare.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int64,
+                                      C.c_void_p, C.c_void_p]
+        l.pmx_icp_iterate.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        l.pmx_icp_finish.argtypes = [C.c_void_p, C.c_void_p]
+        l.pmx_icp_stats_get.argtypes = [C.c_void_p, C.POINTER(IcpStats)]
+        l.pmx_icp_trace_get.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        l.pmx_icp_timing.argtypes = [C.c_void_p, C.c_int]
+        l.pmx_icp_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+        _lib = l
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class ICP:
+    """PointMatcher<T>::ICP on the MI355X path (one object per rank / thread)."""
+
+    def __init__(self, dtype=np.float32, device=0):
+        self.dtype = np.dtype(dtype)
+        self._l = lib()
+        h = C.c_void_p()
+        rc = self._l.pmx_icp_create(1 if self.dtype == np.float64 else 0, device, C.byref(h))
+        if rc:
+            raise RuntimeError("pmx_icp_create failed")
+        self.h = h
+        self.rows = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._l.pmx_icp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc:
+            msg = self._l.pmx_icp_last_error(self.h).decode()
+            raise _ERR.get(rc, RuntimeError)(msg)
+
+    # --- configuration
+    def set_default(self):
+        self._chk(self._l.pmx_icp_set_default(self.h))
+
+    def load_yaml(self, text: str):
+        self._chk(self._l.pmx_icp_load_yaml(self.h, text.encode()))
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = (C.c_char * 128).from_buffer_copy(uid)
+        self._chk(self._l.pmx_icp_comm_init(self.h, buf, nranks, rank))
+
+    def keep_trace(self, on=True):
+        self._chk(self._l.pmx_icp_keep_trace(self.h, 1 if on else 0))
+
+    # --- run
+    def _args(self, reading, reference, normals, T_init):
+        rd = np.ascontiguousarray(reading, dtype=self.dtype)
+        ref = np.ascontiguousarray(reference, dtype=self.dtype)
+        nrm = np.ascontiguousarray(normals, dtype=self.dtype) if normals is not None else None
+        rows = rd.shape[1]
+        if ref.shape[1] != rows:
+            raise ValueError("reading and reference must have the same number of rows")
+        Ti = np.ascontiguousarray(np.eye(rows) if T_init is None else T_init, dtype=self.dtype)
+        self.rows = rows
+        self._keep = (rd, ref, nrm, Ti)
+        return rd, ref, nrm, Ti, rows
+
+    def compute(self, reading, reference, normals=None, T_init=None):
+        rd, ref, nrm, Ti, rows = self._args(reading, reference, normals, T_init)
+        out = np.zeros((rows, rows), self.dtype)
+        self._chk(self._l.pmx_icp_compute(self.h, _p(rd), rows, rd.shape[0], _p(ref), ref.shape[0], _p(nrm),
+                                          _p(Ti), _p(out)))
+        return out
+
+    __call__ = compute
+
+    def prepare(self, reading, reference, normals=None, T_init=None):
+        rd, ref, nrm, Ti, rows = self._args(reading, reference, normals, T_init)
+        self._chk(self._l.pmx_icp_prepare(self.h, _p(rd), rows, rd.shape[0], _p(ref), ref.shape[0], _p(nrm),
+                                          _p(Ti)))
+
+    def iterate(self, n=1):
+        done = C.c_int(0)
+        self._chk(self._l.pmx_icp_iterate(self.h, n, C.byref(done)))
+        return bool(done.value)
+
+    def finish(self):
+        out = np.zeros((self.rows, self.rows), self.dtype)
+        self._chk(self._l.pmx_icp_finish(self.h, _p(out)))
+        return out
+
+    # --- introspection
+    def stats(self):
+        s = IcpStats()
+        self._l.pmx_icp_stats_get(self.h, C.byref(s))
+        return s
+
+    def trace(self, max_iters=100000):
+        it = self.stats().iterations
+        out = np.zeros((max(it, 1), self.rows, self.rows), self.dtype)
+        n = self._l.pmx_icp_trace_get(self.h, _p(out), min(it, max_iters))
+        return out[:n]
+
+    def timing(self, on=True):
+        self._chk(self._l.pmx_icp_timing(self.h, 1 if on else 0))
+
+    def timing_read(self):
+        ms = C.c_double()
+        n = C.c_int64()
+        self._chk(self._l.pmx_icp_timing_read(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value

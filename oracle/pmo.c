@@ -15,11 +15,19 @@
 /* contraction must stay off: distances are ((dx*dx + dy*dy) + dz*dz) */
 #endif
 
+#include <time.h>
+static double pmo_now(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 /* ---- T = double ---- */
 #define T double
 #define SUF(x) x##_f64
 static inline double tmin_f64(void) { return DBL_MIN; }
 static inline double teps_f64(void) { return DBL_EPSILON; }
+static inline double tpow_f64(double a, double b) { return pow(a, b); }
 #include "pmo_dense.inc"
 #include "pmo_impl.inc"
 #undef T
@@ -30,6 +38,7 @@ static inline double teps_f64(void) { return DBL_EPSILON; }
 #define SUF(x) x##_f32
 static inline float tmin_f32(void) { return FLT_MIN; }
 static inline float teps_f32(void) { return FLT_EPSILON; }
+static inline float tpow_f32(float a, float b) { return powf(a, b); }
 #include "pmo_dense.inc"
 #include "pmo_impl.inc"
 #undef T

@@ -90,6 +90,7 @@ typedef struct pmo_stats {
     int max_iter_reached;        /* ICP.cpp:426 */
     int error;                   /* PMO_E_* */
     double last_limit;           /* last quantile threshold (diagnostic) */
+    double loop_seconds;         /* wall time of the iteration loop (CPU baseline) */
 } pmo_stats;
 
 /* ---------- float (T = float) ---------- */

@@ -38,7 +38,7 @@ class Stats(C.Structure):
                 ("rejected_matches", C.c_int64), ("rejected_points", C.c_int64),
                 ("touched", C.c_int64), ("sum_w", C.c_double), ("point_used_ratio", C.c_double),
                 ("weighted_point_used_ratio", C.c_double), ("max_iter_reached", C.c_int),
-                ("error", C.c_int), ("last_limit", C.c_double)]
+                ("error", C.c_int), ("last_limit", C.c_double), ("loop_seconds", C.c_double)]
 
     def asdict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -1,0 +1,194 @@
+"""The CPU oracle pinned against the reference's own known answers and fixtures,
+and cross-checked against numpy/scipy (runs without a GPU).
+
+Pins (tests/golden/kat.json, transcribed from the reference tests):
+  - validT3d / validT2d: utest/utest.cpp:346-356 with utest/utest.h:49-85
+  - icpSingular / icpIdentity: utest/utest.cpp:162-220
+  - VarTrimmed KAT: utest/ui/Outliers.cpp:126-152
+  - icp_data/*.ref_trans: utest/utest.cpp:81-160 (< 3 % median displacement)
+"""
+import numpy as np
+import pytest
+
+from helpers import hom, pca_normals, planar_grid, rel_displacement, validate2d, validate3d
+
+DIFF = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
+
+
+# --------------------------------------------------------------------- kNN --
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("k", [1, 3])
+def test_knn_kdtree_equals_brute_and_scipy(oracle, dtype, k):
+    from scipy.spatial import cKDTree
+
+    rng = np.random.default_rng(0)
+    ref = hom(rng.uniform(-1, 1, (3000, 3)), dtype)
+    q = hom(rng.uniform(-1.2, 1.2, (800, 3)), dtype)
+    d1, i1, t1 = oracle.knn(ref, q, k=k, method="kdtree")
+    d2, i2, t2 = oracle.knn(ref, q, k=k, method="brute")
+    assert np.array_equal(i1, i2) and np.array_equal(d1, d2)
+    assert t2 == 3000 * 800 and t1 < t2  # the tree prunes
+    sd, si = cKDTree(ref[:, :3].astype(np.float64)).query(q[:, :3].astype(np.float64), k=k)
+    si = si.reshape(800, k)
+    assert np.array_equal(si, i1)
+    np.testing.assert_allclose(d1, sd.reshape(800, k) ** 2, rtol=1e-5 if dtype == np.float32 else 1e-12)
+
+
+def test_knn_ties_and_radius(oracle):
+    base = hom(np.random.default_rng(1).uniform(-1, 1, (500, 3)), np.float32)
+    ref = np.concatenate([base, base])
+    d, i, _ = oracle.knn(ref, base, k=2, method="kdtree")
+    assert np.all(i[:, 0] == np.arange(500)) and np.all(i[:, 1] == np.arange(500, 1000))
+    assert np.all(d == 0)
+    d, i, _ = oracle.knn(ref, base + np.float32(5), k=1, max_dist=0.1, method="brute")
+    assert np.all(i == -1) and np.all(np.isinf(d))
+
+
+# ---------------------------------------------------------------- quantile --
+def test_quantile_index_rule(oracle):
+    # Matches.cpp:83-86: idx = (size_t)((T)size * q) over the finite values
+    for n in (100_000, 1_000_000):
+        v = np.arange(n, dtype=np.float32)
+        rng = np.random.default_rng(n)
+        rng.shuffle(v)
+        rc, val = oracle.quantile(v, np.float32(0.85))
+        assert rc == 0 and val == np.float32(int(np.float32(n) * np.float32(0.85)))
+    v = np.array([3, np.inf, 1, 2, np.inf], np.float32)
+    assert oracle.quantile(v, 1.0) == (0, 3.0)           # q == 1 -> max over finite
+    assert oracle.quantile(v, 0.5)[1] == 2.0            # idx = (size_t)(3 * 0.5) = 1
+    assert oracle.quantile(np.full(4, np.inf, np.float32), 0.5)[0] == oracle.E_EMPTY_QUANTILE
+    assert oracle.quantile(v, 1.5)[0] == oracle.E_BAD_PARAM
+
+
+def test_vartrimmed_kat(oracle, golden):
+    _, kat = golden
+    vt = kat["vartrim"]
+    d = np.array(vt["dists"], np.float32).reshape(5, 1)
+    for lam, key in ((0.0, "lambda0_w"), (1.0, "lambda1_w")):
+        rc, w = oracle.outlier_chain([("VarTrimmedDistOutlierFilter",
+                                       {"minRatio": vt["minRatio"], "maxRatio": vt["maxRatio"], "lambda": lam})], d)
+        assert rc == 0
+        exp = vt[key]
+        assert w[0, 0] == exp[0] and w[1, 0] == exp[1]
+    # hand derivation: lambda 0 -> ratio 0, lambda 1 -> ratio 0.8
+    assert oracle.vartrimmed_ratio(d, 1e-7, 1.0, 0.0)[1] == np.float32(0.0)
+    assert oracle.vartrimmed_ratio(d, 1e-7, 1.0, 1.0)[1] == np.float32(0.8)
+
+
+def test_outlier_filters_semantics(oracle):
+    d = np.array([[0.01], [0.04], [np.inf], [0.09], [0.0]], np.float32)
+    # empty chain: w = dist != inf (OutlierFilter.cpp:70-85)
+    assert oracle.outlier_chain([], d)[1].ravel().tolist() == [1, 1, 0, 1, 1]
+    # MaxDist compares against the squared radius (OutlierFiltersImpl.cpp:69)
+    assert oracle.outlier_chain([("MaxDistOutlierFilter", {"maxDist": 0.2})], d)[1].ravel().tolist() == [1, 1, 0, 0, 1]
+    assert oracle.outlier_chain([("MinDistOutlierFilter", {"minDist": 0.15})], d)[1].ravel().tolist() == [0, 1, 1, 1, 0]
+    # chain product
+    w = oracle.outlier_chain([("MaxDistOutlierFilter", {"maxDist": 0.25}),
+                              ("TrimmedDistOutlierFilter", {"ratio": 0.5})], d)[1].ravel().tolist()
+    # trimmed over the 4 finite dists: idx (size_t)(4 * 0.5) = 2 -> 0.04
+    assert w == [1, 1, 0, 0, 1]
+
+
+# ------------------------------------------------------------ minimisers --
+def test_p2plane_system_matches_numpy(oracle):
+    rng = np.random.default_rng(3)
+    n = 2000
+    p = hom(rng.normal(size=(n, 3)), np.float32)
+    q = hom(rng.normal(size=(n, 3)), np.float32)
+    nrm = rng.normal(size=(n, 3))
+    nrm = (nrm / np.linalg.norm(nrm, axis=1, keepdims=True)).astype(np.float32)
+    ids = np.arange(n, dtype=np.int32).reshape(n, 1)
+    d = np.ones((n, 1), np.float32)
+    w = rng.integers(0, 2, size=(n, 1)).astype(np.float32)
+    rc, A, b, st = oracle.p2plane_system(p, q, nrm, d, ids, w)
+    assert rc == 0 and st.kept == int(w.sum())
+    P3, Q3 = p[:, :3].astype(np.float64), q[:, :3].astype(np.float64)
+    F = np.hstack([np.cross(P3, nrm), nrm])
+    keep = w[:, 0] != 0
+    An = (F[keep].T * w[keep, 0]) @ F[keep]
+    dot = np.sum((P3 - Q3) * nrm, axis=1)
+    bn = -(F[keep].T * w[keep, 0]) @ dot[keep]
+    np.testing.assert_allclose(A, An, rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(b, bn, rtol=1e-5, atol=1e-4)
+    # full-rank solve equals numpy's
+    rc, dT = oracle.p2plane_solve(A, b, 4, np.float64)
+    x = np.linalg.solve(A, b)
+    assert np.allclose(dT[:3, 3], x[3:], atol=1e-10)
+
+
+def test_p2plane_solve_min_norm_singular(oracle):
+    # rank-deficient system: only tz, rx, ry constrained (icpSingular geometry)
+    A = np.zeros((6, 6))
+    A[0, 0] = A[1, 1] = 2.0
+    A[5, 5] = 4.0
+    b = np.array([0, 0, 0, 0, 0, 4.0])
+    rc, dT = oracle.p2plane_solve(A, b, 4, np.float32)
+    assert rc == 0
+    assert np.allclose(dT, np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 1], [0, 0, 0, 1]]), atol=1e-6)
+
+
+# -------------------------------------------------------------- reference KATs --
+@pytest.mark.parametrize("minimizer", ["PointToPointErrorMinimizer", "PointToPlaneErrorMinimizer"])
+def test_kat_validT3d_car_cloud(oracle, golden, minimizer):
+    g, kat = golden
+    cfg = oracle.make_cfg(filters=(("TrimmedDistOutlierFilter", {"ratio": 0.85}),), minimizer=minimizer,
+                          differential=DIFF)
+    rc, T, st, _ = oracle.icp(cfg, hom(g["car401"]), hom(g["car400"]), normals=g["car400_normals"])
+    assert rc == 0
+    ok, dt, da = validate3d(T, np.array(kat["validT3d"]), kat["tol3d"])
+    assert ok, (dt, da)
+
+
+def test_kat_validT2d_boxes(oracle, golden):
+    g, kat = golden
+    cfg = oracle.make_cfg(filters=(("TrimmedDistOutlierFilter", {"ratio": 0.85}),),
+                          minimizer="PointToPointErrorMinimizer", differential=DIFF)
+    rc, T, st, _ = oracle.icp(cfg, hom(g["box2"]), hom(g["box1"]))
+    assert rc == 0
+    ok, dt, da = validate2d(T, np.array(kat["validT2d"]), kat["tol2d"])
+    assert ok, (dt, da)
+
+
+def test_kat_icp_singular(oracle):
+    pts0, pts1 = planar_grid()
+    nrm = np.tile(np.array([[0, 0, 1]], np.float32), (pts1.shape[0], 1))
+    cfg = oracle.make_cfg(filters=(("TrimmedDistOutlierFilter", {"ratio": 1.0}),), differential=DIFF)
+    rc, T, st, _ = oracle.icp(cfg, pts0, pts1, normals=nrm)
+    assert rc == 0
+    exp = np.eye(4)
+    exp[2, 3] = 1
+    # Eigen isApprox(float): ||a - b|| <= 1e-5 * min(||a||, ||b||)
+    assert np.linalg.norm(T - exp) <= 1e-5 * min(np.linalg.norm(T), np.linalg.norm(exp))
+
+
+def test_kat_icp_identity(oracle, golden):
+    g, _ = golden
+    pts = g["vtk0"]
+    nrm = pca_normals(pts.astype(np.float64)).astype(np.float32)
+    cfg = oracle.make_cfg(filters=(("TrimmedDistOutlierFilter", {"ratio": 1.0}),), differential=DIFF)
+    rc, T, st, _ = oracle.icp(cfg, hom(pts), hom(pts), normals=nrm)
+    assert rc == 0
+    assert np.linalg.norm(T - np.eye(4)) <= 1e-4 * 2.0
+
+
+def test_regression_icp_data_ref_trans(oracle, golden):
+    g, kat = golden
+    refT = np.array(kat["icp_data_ref_trans"]["defaultPointToPointMinDistDataPointsFilter"])
+    cfg = oracle.make_cfg(filters=(("TrimmedDistOutlierFilter", {"ratio": 0.75}),),
+                          minimizer="PointToPointErrorMinimizer", counter_max=150, differential=DIFF)
+    rc, T, st, _ = oracle.icp(cfg, hom(g["vtk1"]), hom(g["vtk0"]))
+    assert rc == 0
+    assert rel_displacement(T, refT, g["vtk1"]) < kat["icp_data_rel_tol"]
+
+
+def test_float_accumulation_gap_is_small(oracle, golden):
+    """The build accumulates the normal equations in fp64 where the reference
+    sums T products in T; quantify the gap on the car-cloud KAT."""
+    g, _ = golden
+    out = []
+    for acc in (0, 1):
+        cfg = oracle.make_cfg(differential=None, counter_max=30, acc_mode=acc)
+        rc, T, st, _ = oracle.icp(cfg, hom(g["car401"]), hom(g["car400"]), normals=g["car400_normals"])
+        assert rc == 0
+        out.append(T)
+    assert np.linalg.norm(out[0] - out[1]) < 1e-4
