@@ -81,7 +81,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--matcher", default="brute", choices=["brute", "grid"],
+    ap.add_argument("--matcher", default="grid", choices=["brute", "grid"],
                     help="KDTreeMatcher searchType 0 (brute force) or 1 (spatial grid)")
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0)

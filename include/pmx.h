@@ -74,6 +74,7 @@ typedef struct pmx_stats {
     double sum_w;               /* sum of kept weights (weightedPointUsedRatio * k * N) */
     double limit;               /* last quantile threshold (diagnostic, T value) */
     int64_t n_total;            /* k * N over all ranks */
+    int64_t visited;            /* pair evaluations of the iteration's match (PointCountTouched) */
 } pmx_stats;
 
 /* ------------------------------------------------------------ context --- */
@@ -106,11 +107,19 @@ int pmx_set_reference(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const
 int pmx_set_reading(pmx_ctx* ctx, const void* feat, int rows, int64_t N, const void* T0);
 
 /* ------------------------------------------------------------- match --- */
+/* search structure, mirroring KDTreeMatcher's searchType
+ * (MatchersImpl.h:85; libnabo: 0 brute force, 1/2 kd-tree): 0 = brute force
+ * over all N*M pairs (LDS-tiled), 1 or 2 = uniform grid with exact shell
+ * search (default).  Both return identical results (same arithmetic, same
+ * lowest-index tie rule).  Takes effect at the next pmx_match. */
+int pmx_set_search(pmx_ctx* ctx, int search_type);
+
 /* T_iter: rows x rows row-major T.  knn >= 1 (<= 16 on this path),
  * maxDist: radius (inclusive, squared in T; +inf = none), epsilon: the
  * search is exact, so any epsilon >= 0 is satisfied.  visited (may be NULL)
- * receives the pair evaluations of this call (PointCountTouched).  Results
- * stay on the device. */
+ * receives the pair evaluations of this call when they are known at launch
+ * (brute force: N*M; grid: 0 — the exact count is returned in
+ * pmx_stats.visited by the next system call).  Results stay on the device. */
 int pmx_match(pmx_ctx* ctx, const void* T_iter, int knn, double maxDist, double epsilon,
               uint64_t* visited);
 

@@ -47,7 +47,8 @@ class PmxError(RuntimeError):
 class Stats(C.Structure):
     _fields_ = [("kept", C.c_int64), ("nonzero_weights", C.c_int64),
                 ("rejected_matches", C.c_int64), ("rejected_points", C.c_int64),
-                ("sum_w", C.c_double), ("limit", C.c_double), ("n_total", C.c_int64)]
+                ("sum_w", C.c_double), ("limit", C.c_double), ("n_total", C.c_int64),
+                ("visited", C.c_int64)]
 
     def asdict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -57,7 +58,7 @@ _lib = None
 
 EXPORTS = [
     "pmx_ctx_create", "pmx_ctx_destroy", "pmx_last_error", "pmx_device_count", "pmx_version",
-    "pmx_comm_unique_id", "pmx_comm_init", "pmx_set_reference", "pmx_set_reading", "pmx_match",
+    "pmx_comm_unique_id", "pmx_comm_init", "pmx_set_reference", "pmx_set_reading", "pmx_set_search", "pmx_match",
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
@@ -80,6 +81,7 @@ def lib():
         l.pmx_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         l.pmx_set_reference.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
         l.pmx_set_reading.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
+        l.pmx_set_search.argtypes = [C.c_void_p, C.c_int]
         l.pmx_match.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double,
                                 C.POINTER(C.c_uint64)]
         l.pmx_outlier_default.argtypes = [C.c_void_p]
@@ -183,6 +185,10 @@ class Context:
         self._chk(self._l.pmx_set_reading(self.h, _ptr(feat), rows, feat.shape[0], _ptr(T0)))
 
     # --- per-iteration
+    def set_search(self, search_type: int):
+        """0 = brute force, 1/2 = exact grid search (KDTreeMatcher searchType)."""
+        self._chk(self._l.pmx_set_search(self.h, int(search_type)))
+
     def match(self, T, knn=1, max_dist=np.inf, epsilon=0.0):
         T = self._arr(T)
         v = C.c_uint64(0)

@@ -130,12 +130,13 @@ struct KDTreeMatcherGPU : PM<T>::Matcher {
             }
             np = nrm.data();
         }
+        dev.check(pmx_set_search(dev.ctx, searchType));  // 0: brute force, 1/2: exact grid search
         dev.check(pmx_set_reference(dev.ctx, ref.features.data(), ref.rows, ref.n, np));
     }
     Matches findClosests(Device& dev, const std::vector<T>& T_iter) override {
-        uint64_t visited = 0;
-        dev.check(pmx_match(dev.ctx, T_iter.data(), knn, (double)maxDist, (double)epsilon, &visited));
-        this->visitCounter += visited;
+        // PointCountTouched is added from the minimiser's pmx_stats.visited
+        // once the (asynchronous) match has completed, see ICP::step
+        dev.check(pmx_match(dev.ctx, T_iter.data(), knn, (double)maxDist, (double)epsilon, nullptr));
         Matches m;
         m.dev = &dev;
         m.knn = knn;
@@ -650,6 +651,7 @@ void PointMatcher<T>::ErrorMinimizer::setStats(const pmx_stats& st) {
     weightedPointUsedRatio = (T)(st.sum_w / kn);
     nbRejectedMatches = st.rejected_matches;
     nbRejectedPoints = st.rejected_points;
+    lastVisited = st.visited;
 }
 
 template <typename T>
@@ -838,6 +840,7 @@ bool PointMatcher<T>::ICP::step() {
     const Matches matches = matcher->findClosests(dev, T_iter_);
     outlierFilters.compute(dev, matches);
     const TransformationParameters dT = errorMinimizer->compute(dev, dim);
+    matcher->visitCounter += (uint64_t)errorMinimizer->lastVisited;  // MatchersImpl.cpp:98
     dense::matmul(dT.data(), T_iter_.data(), dim, T_iter_.data());
     try {
         transformationCheckers.check(T_iter_, dim, iterate_);

@@ -90,6 +90,7 @@ struct PointMatcher {
         int64_t nbRejectedMatches = -1;
         int64_t nbRejectedPoints = -1;
         int64_t keptPoints = 0;
+        int64_t lastVisited = 0;  // pair evaluations of the iteration's match
         ErrorMinimizer() {}
         ErrorMinimizer(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
         virtual ~ErrorMinimizer() {}

@@ -10,6 +10,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -34,6 +35,19 @@ struct pmx_ctx {
     void* d_ref = nullptr;
     void* d_nrm = nullptr;
     bool has_normals = false;
+
+    // uniform grid over the reference (exact shell search, pmx_grid.hip)
+    int search_type = 1;
+    void* d_gpts = nullptr;
+    int32_t* d_gidx = nullptr;
+    uint32_t* d_gstart = nullptr;
+    double g_lo[3] = {0, 0, 0};
+    double g_h = 1.0;
+    int g_dim[3] = {1, 1, 1};
+    bool grid_ready = false;
+    int32_t* d_order = nullptr;  // reading visit order (sorted by initial cell)
+    unsigned long long* d_visited = nullptr;
+    uint64_t visited_host = 0;   // brute force: known at launch
 
     // reading shard
     int64_t N = 0, N_total = 0, N_max = 0;
@@ -174,6 +188,172 @@ hipEvent_t get_event(pmx_ctx* c) {
     return e;
 }
 
+// -------------------------------------------------------------------- grid --
+// Uniform grid of the (centred) reference for the exact shell search.  The
+// cell size targets ~8 points per occupied cell: the occupied-cell count at
+// two trial sizes gives the data's local dimension (surface ~2, volume ~3),
+// from which the size for the target density follows.  Points are counting-
+// sorted by cell (x fastest) so every x-row of cells is one contiguous range.
+constexpr int64_t kMaxCells = (int64_t)1 << 26;
+
+struct GridShape {
+    double lo[3], h;
+    int g[3];
+    int64_t cells() const { return (int64_t)g[0] * g[1] * g[2]; }
+};
+
+static GridShape grid_shape(const double lo[3], const double ext[3], double h) {
+    GridShape s;
+    for (int a = 0; a < 3; ++a) {
+        s.lo[a] = lo[a];
+        const double gg = std::floor(ext[a] / h) + 1.0;
+        s.g[a] = gg > 1e9 ? 1000000000 : (int)gg;
+    }
+    s.h = h;
+    return s;
+}
+
+template <typename T>
+static int64_t cell_of(const GridShape& s, const P4<T>& p) {
+    const double q[3] = {(double)p.x, (double)p.y, (double)p.z};
+    int64_t ci[3];
+    for (int a = 0; a < 3; ++a) {
+        double f = std::floor((q[a] - s.lo[a]) / s.h);
+        if (f < 0) f = 0;
+        if (f > s.g[a] - 1) f = s.g[a] - 1;
+        ci[a] = (int64_t)f;
+    }
+    return (ci[2] * s.g[1] + ci[1]) * s.g[0] + ci[0];
+}
+
+template <typename T>
+static bool finite_pt(const P4<T>& p) {
+    return std::isfinite((double)p.x) && std::isfinite((double)p.y) && std::isfinite((double)p.z);
+}
+
+template <typename T>
+int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M) {
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    int64_t valid = 0;
+    for (int64_t j = 0; j < M; ++j) {
+        if (!finite_pt(pts[j])) continue;  // inf / NaN points can never be a neighbour
+        const double q[3] = {(double)pts[j].x, (double)pts[j].y, (double)pts[j].z};
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], q[a]);
+            hi[a] = std::max(hi[a], q[a]);
+        }
+        ++valid;
+    }
+    if (valid == 0)
+        for (int a = 0; a < 3; ++a) lo[a] = hi[a] = 0;
+    double ext[3], maxe = 0;
+    for (int a = 0; a < 3; ++a) {
+        ext[a] = hi[a] - lo[a];
+        maxe = std::max(maxe, ext[a]);
+    }
+    if (!(maxe > 0)) maxe = 1;
+    auto occupied = [&](double h) -> int64_t {
+        GridShape s = grid_shape(lo, ext, h);
+        if (s.cells() > ((int64_t)1 << 28)) return -1;
+        std::vector<uint8_t> bm((size_t)s.cells(), 0);
+        int64_t occ = 0;
+        for (int64_t j = 0; j < M; ++j) {
+            if (!finite_pt(pts[j])) continue;
+            uint8_t& b = bm[(size_t)cell_of(s, pts[j])];
+            occ += b == 0;
+            b = 1;
+        }
+        return occ;
+    };
+    double h = maxe / 64.0;
+    if (valid > 0) {
+        const double h0 = maxe / 64.0, h1 = h0 / 2.0;
+        const int64_t o0 = std::max<int64_t>(1, occupied(h0));
+        const int64_t o1 = std::max<int64_t>(1, occupied(h1));
+        double dim = std::log2((double)o1 / (double)o0);
+        dim = std::min(3.0, std::max(1.0, dim));
+        const double ppc1 = (double)valid / (double)o1;
+        h = h1 * std::pow(8.0 / ppc1, 1.0 / dim);
+        h = std::max(h, maxe / 4096.0);
+    }
+    GridShape s = grid_shape(lo, ext, h);
+    while (s.cells() > kMaxCells) {
+        h *= 1.25;
+        s = grid_shape(lo, ext, h);
+    }
+    const int64_t C = s.cells();
+    std::vector<uint32_t> start((size_t)C + 1, 0);
+    std::vector<int64_t> cellid((size_t)M, -1);
+    for (int64_t j = 0; j < M; ++j)
+        if (finite_pt(pts[j])) {
+            cellid[j] = cell_of(s, pts[j]);
+            start[(size_t)cellid[j] + 1]++;
+        }
+    for (int64_t i = 0; i < C; ++i) start[i + 1] += start[i];
+    std::vector<uint32_t> fill(start.begin(), start.end() - 1);
+    std::vector<P4<T>> gp((size_t)std::max<int64_t>(valid, 1));
+    std::vector<int32_t> gi((size_t)std::max<int64_t>(valid, 1));
+    for (int64_t j = 0; j < M; ++j) {  // stable: index order inside a cell
+        if (cellid[j] < 0) continue;
+        const uint32_t p = fill[(size_t)cellid[j]]++;
+        gp[p] = pts[j];
+        gi[p] = (int32_t)j;
+    }
+    for (void** b : {&c->d_gpts, (void**)&c->d_gidx, (void**)&c->d_gstart})
+        if (*b) {
+            (void)hipFree(*b);
+            *b = nullptr;
+        }
+    HIPCHK(c, hipMalloc(&c->d_gpts, sizeof(P4<T>) * gp.size()));
+    HIPCHK(c, hipMalloc((void**)&c->d_gidx, sizeof(int32_t) * gi.size()));
+    HIPCHK(c, hipMalloc((void**)&c->d_gstart, sizeof(uint32_t) * start.size()));
+    HIPCHK(c, hipMemcpyAsync(c->d_gpts, gp.data(), sizeof(P4<T>) * gp.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_gidx, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_gstart, start.data(), sizeof(uint32_t) * start.size(), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int a = 0; a < 3; ++a) {
+        c->g_lo[a] = s.lo[a];
+        c->g_dim[a] = s.g[a];
+    }
+    c->g_h = s.h;
+    c->grid_ready = true;
+    return PMX_OK;
+}
+
+// visit order of the reading: sorted by the cell of the initially transformed
+// point, so lanes of a wave walk neighbouring cells (performance only)
+template <typename T>
+int build_order(pmx_ctx* c, const std::vector<P4<T>>& raw, int64_t N, const Mat4<T>& M0) {
+    if (c->d_order) (void)hipFree(c->d_order);
+    c->d_order = nullptr;
+    if (!c->grid_ready || N <= 0) return PMX_OK;
+    GridShape s;
+    for (int a = 0; a < 3; ++a) {
+        s.lo[a] = c->g_lo[a];
+        s.g[a] = c->g_dim[a];
+    }
+    s.h = c->g_h;
+    std::vector<uint64_t> key((size_t)N);
+    for (int64_t i = 0; i < N; ++i) {
+        const P4<T>& p = raw[i];
+        P4<double> q;
+        q.x = ((double)M0.m[0] * p.x + (double)M0.m[1] * p.y) + (double)M0.m[2] * p.z + (double)M0.m[3] * p.w;
+        q.y = ((double)M0.m[4] * p.x + (double)M0.m[5] * p.y) + (double)M0.m[6] * p.z + (double)M0.m[7] * p.w;
+        q.z = ((double)M0.m[8] * p.x + (double)M0.m[9] * p.y) + (double)M0.m[10] * p.z + (double)M0.m[11] * p.w;
+        q.w = 1;
+        const uint64_t cell = finite_pt(q) ? (uint64_t)cell_of(s, q) : (uint64_t)s.cells();
+        key[i] = (cell << 32) | (uint64_t)i;
+    }
+    std::sort(key.begin(), key.end());
+    std::vector<int32_t> order((size_t)N);
+    for (int64_t i = 0; i < N; ++i) order[i] = (int32_t)(key[i] & 0xffffffffu);
+    HIPCHK(c, hipMalloc((void**)&c->d_order, sizeof(int32_t) * N));
+    HIPCHK(c, hipMemcpyAsync(c->d_order, order.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
 // ------------------------------------------------------------------ clouds --
 template <typename T>
 int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals) {
@@ -212,7 +392,8 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     c->M = M;
     c->M_pad = M_pad;
     c->have_match = false;
-    return PMX_OK;
+    c->grid_ready = false;
+    return build_grid<T>(c, h, M);
 }
 
 template <typename T>
@@ -236,6 +417,8 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
         Mat4<T> M0 = embed<T>(T0, rows);
         launch_transform<T>((const P4<T>*)d_raw, (P4<T>*)c->d_rd, N, M0, c->stream);
         HIPCHK(c, hipGetLastError());
+        int rc = build_order<T>(c, h, N, M0);
+        if (rc) return rc;
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     (void)hipFree(d_raw);
@@ -305,13 +488,25 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         e0 = get_event(c);
         e1 = get_event(c);
     }
-    launch_match<T>((const P4<T>*)c->d_ref, c->M_pad, (const P4<T>*)c->d_rd, c->N, Tm, knn, maxR2, (T*)c->d_dists,
-                    c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1, c->cu_count);
+    HIPCHK(c, hipMemsetAsync(c->d_visited, 0, sizeof(unsigned long long), c->stream));
+    if (c->search_type == 0 || !c->grid_ready) {
+        launch_match<T>((const P4<T>*)c->d_ref, c->M_pad, (const P4<T>*)c->d_rd, c->N, Tm, knn, maxR2,
+                        (T*)c->d_dists, c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1,
+                        c->cu_count);
+        c->visited_host = (uint64_t)c->N * (uint64_t)c->M;
+    } else {
+        if (e0) (void)hipEventRecord(e0, c->stream);
+        launch_grid_match<T>((const P4<T>*)c->d_gpts, c->d_gidx, c->d_gstart, c->g_lo, c->g_h, c->g_dim,
+                             (const P4<T>*)c->d_rd, c->d_order, c->N, Tm, knn, maxR2, (T*)c->d_dists, c->d_ids,
+                             c->d_visited, c->stream);
+        if (e1) (void)hipEventRecord(e1, c->stream);
+        c->visited_host = 0;
+    }
     HIPCHK(c, hipGetLastError());
     if (e0 && e1) c->ev_pending.emplace_back(e0, e1);
     c->knn = knn;
     c->have_match = true;
-    if (visited) *visited = (uint64_t)c->N * (uint64_t)c->M;
+    if (visited) *visited = c->visited_host;
     return PMX_OK;
 }
 
@@ -447,6 +642,9 @@ void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double 
     st->sum_w = sw;
     st->limit = limit;
     st->n_total = c->N_total * c->knn;
+    unsigned long long v = 0;
+    std::memcpy(&v, &c->h_result[66], sizeof(v));
+    st->visited = c->visited_host ? (int64_t)c->visited_host : (int64_t)v;
 }
 
 template <typename T>
@@ -467,6 +665,8 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     HIPCHK(c, hipMemcpyAsync(c->h_result, c->d_result, sizeof(double) * NV, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_result + 64, c->d_iter_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_result + 65, &c->d_sel->limit, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_result + 66, c->d_visited, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     resolve_events(c);
     const double* r = c->h_result;
@@ -502,6 +702,8 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
     HIPCHK(c, hipMemcpyAsync(c->h_result + 32, c->d_means, sizeof(T) * 6, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_result + 64, c->d_iter_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_result + 65, &c->d_sel->limit, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_result + 66, c->d_visited, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     resolve_events(c);
     const double* r = c->h_result;
@@ -585,6 +787,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     c->d_sel = (SelectState*)p;
     c->d_iter_err = (int*)(c->d_sel + 1);
     c->d_ratio = (double*)((char*)p + 128);
+    c->d_visited = (unsigned long long*)((char*)p + 192);
     if (hipMalloc((void**)&c->d_hist, 2048 * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_hist, 0, 2048 * sizeof(uint32_t));
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
@@ -602,7 +805,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_sel,    c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
-                    c->d_result, c->d_means};
+                    c->d_result, c->d_means, c->d_gpts, c->d_gidx, c->d_gstart, c->d_order};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_result) (void)hipHostFree(c->h_result);
@@ -696,6 +899,13 @@ int pmx_get_shape(const pmx_ctx* c, int64_t* n_local, int* knn) {
     if (!c) return PMX_E_BAD_PARAM;
     if (n_local) *n_local = c->N;
     if (knn) *knn = c->knn;
+    return PMX_OK;
+}
+
+int pmx_set_search(pmx_ctx* c, int search_type) {
+    if (!c) return PMX_E_BAD_PARAM;
+    if (search_type < 0 || search_type > 2) return fail(c, PMX_E_BAD_PARAM, "searchType must be 0, 1 or 2");
+    c->search_type = search_type;
     return PMX_OK;
 }
 

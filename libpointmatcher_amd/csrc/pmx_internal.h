@@ -54,6 +54,12 @@ int64_t match_part_elems(int64_t N, int64_t M_pad, int knn, int cu_count);
 template <typename T>
 void launch_transform(const P4<T>* in, P4<T>* out, int64_t N, const Mat4<T>& Tm, hipStream_t s);
 
+// ---- grid match (pmx_grid.hip) ----
+template <typename T>
+void launch_grid_match(const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo, double h,
+                       const int* g, const P4<T>* rd, const int32_t* order, int64_t N, const Mat4<T>& Tm, int knn,
+                       T maxR2, T* dists, int32_t* ids, unsigned long long* visited, hipStream_t s);
+
 // ---- quantile / weights (pmx_select.hip) ----
 enum WeightOp { kWAssign = 0, kWMul = 1 };
 template <typename T>

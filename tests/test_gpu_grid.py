@@ -1,0 +1,104 @@
+"""Exact grid search (searchType 1/2) == brute force (searchType 0) == oracle,
+bit for bit, on the geometries where a shell search can go wrong: queries
+outside the reference bounding box, planar / 2-D data (degenerate z extent),
+duplicated points (ties), non-finite reference points, a radius, large k,
+and surface data at the benchmark density.
+"""
+import numpy as np
+import pytest
+
+from libpointmatcher_amd import _capi as P
+from libpointmatcher_amd.synth import random_cloud, reading_cloud, reference_cloud
+
+pytestmark = pytest.mark.gpu
+
+
+def match(ref, rd, T, k, search, max_dist=np.inf, dtype=np.float32):
+    ctx = P.Context(0, dtype)
+    ctx.set_search(search)
+    ctx.set_reference(ref)
+    ctx.set_reading(rd)
+    ctx.match(T, knn=k, max_dist=max_dist)
+    d, i = ctx.get_matches()
+    ctx.close()
+    return d, i
+
+
+def same(a, b):
+    return np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def check(oracle, ref, rd, T, k, max_dist=np.inf, dtype=np.float32):
+    g = match(ref, rd, T, k, 1, max_dist, dtype)
+    b = match(ref, rd, T, k, 0, max_dist, dtype)
+    o = oracle.knn(ref, oracle.transform(T, rd), k=k, max_dist=max_dist, method="kdtree")[:2]
+    assert same(g, b), "grid != brute"
+    assert same(g, o), "grid != oracle"
+
+
+@pytest.mark.parametrize("k", [1, 3, 9])
+def test_surface_density(oracle, k):
+    ref, _ = reference_cloud(200_000)
+    rd = reading_cloud(50_000)
+    check(oracle, ref, rd, np.eye(4, dtype=np.float32), k)
+
+
+def test_queries_outside_bbox(oracle):
+    ref = random_cloud(20_000, seed=1)
+    rd = random_cloud(5_000, seed=2, scale=4.0)  # most queries far outside [-1, 1]^3
+    for k in (1, 4):
+        check(oracle, ref, rd, np.eye(4, dtype=np.float32), k)
+
+
+def test_planar_and_2d(oracle):
+    rng = np.random.default_rng(3)
+    ref = np.hstack([rng.uniform(-5, 5, (30_000, 2)), np.zeros((30_000, 1)), np.ones((30_000, 1))]).astype(np.float32)
+    rd = np.hstack([rng.uniform(-6, 6, (8_000, 2)), rng.normal(0, 0.5, (8_000, 1)), np.ones((8_000, 1))]).astype(np.float32)
+    check(oracle, ref, rd, np.eye(4, dtype=np.float32), 1)
+    check(oracle, ref, rd, np.eye(4, dtype=np.float32), 5)
+    ref2 = random_cloud(20_000, rows=3, seed=4)
+    rd2 = random_cloud(5_000, rows=3, seed=5, scale=1.5)
+    check(oracle, ref2, rd2, np.eye(3, dtype=np.float32), 2)
+
+
+def test_ties_duplicates_and_nonfinite(oracle):
+    base = random_cloud(5_000, seed=6)
+    ref = np.concatenate([base, base, base[:1000]])
+    ref[17, 0] = np.inf
+    ref[99, 1] = np.nan
+    rd = base[::2].copy()
+    for k in (1, 3):
+        check(oracle, ref, rd, np.eye(4, dtype=np.float32), k)
+
+
+def test_radius_and_double(oracle):
+    ref = random_cloud(30_000, seed=7, dtype=np.float64)
+    rd = random_cloud(10_000, seed=8, dtype=np.float64, scale=1.2)
+    check(oracle, ref, rd, np.eye(4), 1, max_dist=0.02, dtype=np.float64)
+    check(oracle, ref, rd, np.eye(4), 4, max_dist=0.05, dtype=np.float64)
+
+
+def test_tiny_reference(oracle):
+    for M in (1, 2, 7):
+        ref = random_cloud(M, seed=9)
+        rd = random_cloud(300, seed=10, scale=3.0)
+        check(oracle, ref, rd, np.eye(4, dtype=np.float32), min(2, M))
+
+
+def test_grid_visits_far_fewer_pairs():
+    ref, nrm = reference_cloud(200_000)
+    rd = reading_cloud(100_000)
+    stats = []
+    for search in (0, 1):
+        ctx = P.Context(0, np.float32)
+        ctx.set_search(search)
+        ctx.set_reference(ref, nrm)
+        ctx.set_reading(rd)
+        ctx.match(np.eye(4, dtype=np.float32), knn=1)
+        ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
+        A, b, st = ctx.p2plane_system()
+        stats.append((st.visited, A.copy(), b.copy()))
+        ctx.close()
+    assert stats[0][0] == 200_000 * 100_000
+    assert stats[1][0] < stats[0][0] / 500
+    assert np.array_equal(stats[0][1], stats[1][1]) and np.array_equal(stats[0][2], stats[1][2])

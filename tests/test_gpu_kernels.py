@@ -32,8 +32,9 @@ def small_T(rows, dtype, seed=0, ang=0.05, tr=0.02):
     return T.astype(dtype)
 
 
-def run_match(ref, rd, T, k=1, max_dist=np.inf, dtype=np.float32, T0=None):
+def run_match(ref, rd, T, k=1, max_dist=np.inf, dtype=np.float32, T0=None, search=1):
     ctx = P.Context(0, dtype)
+    ctx.set_search(search)
     ctx.set_reference(ref)
     ctx.set_reading(rd, T0)
     ctx.match(T, knn=k, max_dist=max_dist)
@@ -42,14 +43,15 @@ def run_match(ref, rd, T, k=1, max_dist=np.inf, dtype=np.float32, T0=None):
     return d, i
 
 
+@pytest.mark.parametrize("search", [0, 1])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("k", [1, 2, 4, 7])
 @pytest.mark.parametrize("N,M", [(1000, 3000), (5000, 2500), (777, 1025)])
-def test_match_vs_oracle(oracle, dtype, k, N, M):
+def test_match_vs_oracle(oracle, dtype, k, N, M, search):
     ref = random_cloud(M, seed=1, dtype=dtype)
     rd = random_cloud(N, seed=2, dtype=dtype)
     T = small_T(4, dtype, seed=3)
-    d, i = run_match(ref, rd, T, k=k, dtype=dtype)
+    d, i = run_match(ref, rd, T, k=k, dtype=dtype, search=search)
     step = oracle.transform(T, rd)
     od, oi, _ = oracle.knn(ref, step, k=k, method="brute")
     assert np.array_equal(i, oi)
