@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -21,6 +22,16 @@
 #include "../../include/pmx.h"
 
 using namespace pmx;
+
+// iteration block layout (see pmx_ctx_create)
+constexpr size_t kBlkSel = 1024;
+constexpr size_t kBlkIterErr = kBlkSel + sizeof(SelectState);
+constexpr size_t kBlkRatio = 1152;
+constexpr size_t kBlkVisited = 1216;
+constexpr size_t kBlkMeans = 1280;
+constexpr size_t kBlkCopy = 1344;
+constexpr size_t kBlkBytes = 2048;
+static_assert(kBlkIterErr + sizeof(int) <= kBlkRatio, "iteration block layout");
 
 struct pmx_ctx {
     int device = 0;
@@ -273,7 +284,9 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M) {
         double dim = std::log2((double)o1 / (double)o0);
         dim = std::min(3.0, std::max(1.0, dim));
         const double ppc1 = (double)valid / (double)o1;
-        h = h1 * std::pow(8.0 / ppc1, 1.0 / dim);
+        double target = 16.0;  // points per occupied cell (measured optimum; PMX_GRID_PPC: tuning knob)
+        if (const char* e = std::getenv("PMX_GRID_PPC")) target = std::max(0.5, std::atof(e));
+        h = h1 * std::pow(target / ppc1, 1.0 / dim);
         h = std::max(h, maxe / 4096.0);
     }
     GridShape s = grid_shape(lo, ext, h);
@@ -328,6 +341,7 @@ int build_order(pmx_ctx* c, const std::vector<P4<T>>& raw, int64_t N, const Mat4
     if (c->d_order) (void)hipFree(c->d_order);
     c->d_order = nullptr;
     if (!c->grid_ready || N <= 0) return PMX_OK;
+    if (std::getenv("PMX_GRID_NOORDER")) return PMX_OK;  // tuning knob: identity visit order
     GridShape s;
     for (int a = 0; a < 3; ++a) {
         s.lo[a] = c->g_lo[a];
@@ -482,13 +496,13 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
     for (int i = 0; i < 16; ++i) c->Tstep[i] = (double)Tm.m[i];
     const T md = (T)maxDist;
     const T maxR2 = md * md;  // libnabo squares the radius in T [ext]
-    HIPCHK(c, hipMemsetAsync(c->d_iter_err, 0, sizeof(int), c->stream));
+    // reset the per-iteration error word, VarTrimmed ratio and pair counter
+    HIPCHK(c, hipMemsetAsync((char*)c->d_result + kBlkIterErr, 0, kBlkVisited + 8 - kBlkIterErr, c->stream));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = get_event(c);
         e1 = get_event(c);
     }
-    HIPCHK(c, hipMemsetAsync(c->d_visited, 0, sizeof(unsigned long long), c->stream));
     if (c->search_type == 0 || !c->grid_ready) {
         launch_match<T>((const P4<T>*)c->d_ref, c->M_pad, (const P4<T>*)c->d_rd, c->N, Tm, knn, maxR2,
                         (T*)c->d_dists, c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1,
@@ -632,6 +646,24 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
 }
 
 // -------------------------------------------------------------- minimizers --
+// one D2H copy of the iteration block, then a stream sync
+int readback(pmx_ctx* c) {
+    HIPCHK(c, hipMemcpyAsync(c->h_result, c->d_result, kBlkCopy, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    resolve_events(c);
+    return PMX_OK;
+}
+int host_iter_err(const pmx_ctx* c) {
+    int e = 0;
+    std::memcpy(&e, (const char*)c->h_result + kBlkIterErr, sizeof(int));
+    return e;
+}
+double host_limit(const pmx_ctx* c) {
+    double v = 0;
+    std::memcpy(&v, (const char*)c->h_result + kBlkSel + offsetof(SelectState, limit), sizeof(double));
+    return v;
+}
+
 void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double rm, double rp, double sw,
                 double limit) {
     if (!st) return;
@@ -643,7 +675,7 @@ void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double 
     st->limit = limit;
     st->n_total = c->N_total * c->knn;
     unsigned long long v = 0;
-    std::memcpy(&v, &c->h_result[66], sizeof(v));
+    std::memcpy(&v, (const char*)c->h_result + kBlkVisited, sizeof(v));
     st->visited = c->visited_host ? (int64_t)c->visited_host : (int64_t)v;
 }
 
@@ -662,18 +694,11 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, c->stream);
     HIPCHK(c, hipGetLastError());
     if ((rc = allreduce_f64(c, c->d_result, NV))) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->h_result, c->d_result, sizeof(double) * NV, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_result + 64, c->d_iter_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_result + 65, &c->d_sel->limit, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_result + 66, c->d_visited, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    resolve_events(c);
+    if ((rc = readback(c))) return rc;
     const double* r = c->h_result;
-    int ierr = 0;
-    std::memcpy(&ierr, &r[64], sizeof(int));
+    const int ierr = host_iter_err(c);
     const int o = NF * NF + NF;
-    fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 4], r[65]);
+    fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 4], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[o + 1] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
@@ -698,23 +723,15 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
     launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, c->stream);
     HIPCHK(c, hipGetLastError());
     if ((rc = allreduce_f64(c, c->d_result + 16, 9))) return rc;
-    HIPCHK(c, hipMemcpyAsync(c->h_result, c->d_result, sizeof(double) * 32, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_result + 32, c->d_means, sizeof(T) * 6, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_result + 64, c->d_iter_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_result + 65, &c->d_sel->limit, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_result + 66, c->d_visited, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    resolve_events(c);
+    if ((rc = readback(c))) return rc;
     const double* r = c->h_result;
-    int ierr = 0;
-    std::memcpy(&ierr, &r[64], sizeof(int));
-    fill_stats(c, st, r[7], r[8], r[9], r[10], r[0], r[65]);
+    const int ierr = host_iter_err(c);
+    fill_stats(c, st, r[7], r[8], r[9], r[10], r[0], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[8] == 0.0 || r[7] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
     T means[6];
-    std::memcpy(means, &r[32], sizeof(T) * 6);
+    std::memcpy(means, (const char*)c->h_result + kBlkMeans, sizeof(T) * 6);
     const int D = c->dim;
     for (int i = 0; i < D; ++i) {
         mean_p[i] = (double)means[i];
@@ -780,21 +797,25 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bad(PMX_E_HIP);
-    // SelectState followed by the per-iteration error word (see launch_select_pick)
+    // One small "iteration block" holds everything the host reads back per
+    // iteration, so a single D2H copy returns it (see kBlk*):
+    //   [0, 1024)     reduction results (128 doubles)
+    //   [1024, ...)   SelectState, then the per-iteration error word
+    //   [1152]        VarTrimmed ratio, [1216] pair-evaluation counter
+    //   [1280, 1344)  point-to-point means (6 T)
     void* p = nullptr;
-    if (hipMalloc(&p, 256) != hipSuccess) return bad(PMX_E_HIP);
-    (void)hipMemset(p, 0, 256);
-    c->d_sel = (SelectState*)p;
+    if (hipMalloc(&p, kBlkBytes) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(p, 0, kBlkBytes);
+    c->d_result = (double*)p;
+    c->d_sel = (SelectState*)((char*)p + kBlkSel);
     c->d_iter_err = (int*)(c->d_sel + 1);
-    c->d_ratio = (double*)((char*)p + 128);
-    c->d_visited = (unsigned long long*)((char*)p + 192);
+    c->d_ratio = (double*)((char*)p + kBlkRatio);
+    c->d_visited = (unsigned long long*)((char*)p + kBlkVisited);
+    c->d_means = (char*)p + kBlkMeans;
     if (hipMalloc((void**)&c->d_hist, 2048 * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_hist, 0, 2048 * sizeof(uint32_t));
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
-    if (hipMalloc((void**)&c->d_result, sizeof(double) * 128) != hipSuccess) return bad(PMX_E_HIP);
-    if (hipMalloc(&c->d_means, 64) != hipSuccess) return bad(PMX_E_HIP);
-    if (hipHostMalloc((void**)&c->h_result, sizeof(double) * 128, hipHostMallocDefault) != hipSuccess)
-        return bad(PMX_E_HIP);
+    if (hipHostMalloc((void**)&c->h_result, kBlkBytes, hipHostMallocDefault) != hipSuccess) return bad(PMX_E_HIP);
     *out = c;
     return PMX_OK;
 }
@@ -804,8 +825,8 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
-                    c->d_part_i, c->d_sel,    c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
-                    c->d_result, c->d_means, c->d_gpts, c->d_gidx, c->d_gstart, c->d_order};
+                    c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
+                    c->d_result, c->d_gpts, c->d_gidx, c->d_gstart, c->d_order};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_result) (void)hipHostFree(c->h_result);

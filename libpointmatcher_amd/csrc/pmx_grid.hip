@@ -67,17 +67,35 @@ __device__ __forceinline__ void ginsert(T (&kd)[KT], int32_t (&ki)[KT], T d, int
 }
 
 template <typename T, int KT>
+__device__ __forceinline__ void consider(const int32_t* __restrict__ gidx, uint32_t j, T d, T (&kd)[KT],
+                                         int32_t (&ki)[KT]) {
+    if (d <= kd[KT - 1]) {
+        const int32_t id = gidx[j];
+        if (d < kd[KT - 1] || id < ki[KT - 1]) ginsert<T, KT>(kd, ki, d, id);
+    }
+}
+
+// Scan one contiguous point range.  The scan is latency-bound (each lane
+// walks its own cells), so points are fetched eight at a time with
+// independent loads before any of them is used.
+template <typename T, int KT>
 __device__ __forceinline__ void scan_range(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                                            uint32_t a, uint32_t b, T qx, T qy, T qz, T (&kd)[KT],
                                            int32_t (&ki)[KT], uint32_t& visits) {
     visits += b - a;
-    for (uint32_t j = a; j < b; ++j) {
-        const T d = gsqd(qx, qy, qz, gpts[j]);
-        if (d <= kd[KT - 1]) {
-            const int32_t id = gidx[j];
-            if (d < kd[KT - 1] || id < ki[KT - 1]) ginsert<T, KT>(kd, ki, d, id);
-        }
+    uint32_t j = a;
+    constexpr int U = 8;
+    for (; j + U <= b; j += U) {
+        P4<T> p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) p[u] = gpts[j + u];
+        T d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = gsqd(qx, qy, qz, p[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) consider<T, KT>(gidx, j + u, d[u], kd, ki);
     }
+    for (; j < b; ++j) consider<T, KT>(gidx, j, gsqd(qx, qy, qz, gpts[j]), kd, ki);
 }
 
 struct GridGeom {
@@ -119,8 +137,29 @@ __global__ __launch_bounds__(256) void grid_match_kernel(const P4<T>* __restrict
         }
         if (!qnan) {
             const double margin = 1.0 - 1e-5;
-            for (int R = 0;; ++R) {
-                // walk the shell at Chebyshev radius R (the whole block for R == 0)
+            {
+                // phase 1: the whole 3x3x3 block (R = 0 and 1).  The nine row
+                // bounds are loaded together from always-valid (clamped)
+                // addresses and masked afterwards, then the rows are scanned.
+                uint32_t ra[9], rb[9];
+                const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
+#pragma unroll
+                for (int r = 0; r < 9; ++r) {
+                    const int z = c[2] + r / 3 - 1, y = c[1] + r % 3 - 1;
+                    const bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
+                    const int zc = min(max(z, 0), G.g[2] - 1), yc = min(max(y, 0), G.g[1] - 1);
+                    const int64_t row = ((int64_t)zc * G.g[1] + yc) * G.g[0];
+                    const uint32_t va = start[row + x0];
+                    const uint32_t vb = start[row + x1 + 1];
+                    ra[r] = ok ? va : 0u;
+                    rb[r] = ok ? vb : 0u;
+                }
+#pragma unroll
+                for (int r = 0; r < 9; ++r) scan_range<T, KT>(gpts, gidx, ra[r], rb[r], qx, qy, qz, kd, ki, visits);
+            }
+            for (int R = 1;; ++R) {
+              if (R >= 2) {
+                // walk the shell at Chebyshev radius R
                 const int y0 = max(c[1] - R, 0), y1 = min(c[1] + R, G.g[1] - 1);
                 const int z0 = max(c[2] - R, 0), z1 = min(c[2] + R, G.g[2] - 1);
                 const int x0 = max(c[0] - R, 0), x1 = min(c[0] + R, G.g[0] - 1);
@@ -129,7 +168,7 @@ __global__ __launch_bounds__(256) void grid_match_kernel(const P4<T>* __restrict
                     for (int y = y0; y <= y1; ++y) {
                         const bool yface = (y == c[1] - R) || (y == c[1] + R);
                         const int64_t row = ((int64_t)z * G.g[1] + y) * G.g[0];
-                        if (zface || yface || R == 0) {
+                        if (zface || yface) {
                             scan_range<T, KT>(gpts, gidx, start[row + x0], start[row + x1 + 1], qx, qy, qz, kd, ki,
                                               visits);
                         } else {
@@ -142,6 +181,7 @@ __global__ __launch_bounds__(256) void grid_match_kernel(const P4<T>* __restrict
                         }
                     }
                 }
+              }
                 // lower bound on the distance to any unvisited cell
                 double lb = 1e300;
                 bool any = false;

@@ -125,17 +125,23 @@ void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref
                            ids, w, k, N, partials);
 }
 
-// sum the per-block partials in block order (deterministic)
-__global__ void finalize_kernel(const double* __restrict__ partials, int nblocks, int nv, double* __restrict__ out) {
-    const int v = threadIdx.x;
-    if (v >= nv) return;
+// Sum the per-block partials: one block per accumulator, each thread adds a
+// fixed strided subset in order, then a fixed-shape tree — the summation
+// order never changes, so results are bitwise reproducible.
+__global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ partials, int nblocks, int nv,
+                                                       double* __restrict__ out) {
+    __shared__ double red[4];
+    const int v = blockIdx.x;
     double s = 0.0;
-    for (int b = 0; b < nblocks; ++b) s += partials[(int64_t)b * nv + v];
-    out[v] = s;
+    for (int b = threadIdx.x; b < nblocks; b += 256) s += partials[(int64_t)b * nv + v];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[v] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 void launch_finalize(const double* partials, int nblocks, int nv, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, s, partials, nblocks, nv, out);
+    hipLaunchKernelGGL(finalize_kernel, dim3(nv), dim3(256), 0, s, partials, nblocks, nv, out);
 }
 
 // ------------------------------------------------------------ point-to-point --
