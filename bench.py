@@ -86,13 +86,19 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist", action="store_true",
+                    help="use the torchrun/RCCL multi-rank path even at world size 1 (rehearsal on one GPU)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    dist = world > 1 or args.dist
     if dist:
+        # torch is imported BEFORE libpmx is loaded: torch bundles its own HIP
+        # runtime and RCCL (same SONAMEs), and loading it after libpmx would put
+        # two HIP runtimes in the process.  In this order libpmx binds to the
+        # already-loaded ones.
         import torch
         import torch.distributed as tdist
 
