@@ -75,6 +75,8 @@ typedef struct pmx_stats {
     double limit;               /* last quantile threshold (diagnostic, T value) */
     int64_t n_total;            /* k * N over all ranks */
     int64_t visited;            /* pair evaluations of the iteration's match (PointCountTouched) */
+    int64_t fallback_queries;   /* grid tile search: queries re-run by the per-lane shell search
+                                   (diagnostic; local to this rank) */
 } pmx_stats;
 
 /* ------------------------------------------------------------ context --- */

@@ -48,7 +48,7 @@ class Stats(C.Structure):
     _fields_ = [("kept", C.c_int64), ("nonzero_weights", C.c_int64),
                 ("rejected_matches", C.c_int64), ("rejected_points", C.c_int64),
                 ("sum_w", C.c_double), ("limit", C.c_double), ("n_total", C.c_int64),
-                ("visited", C.c_int64)]
+                ("visited", C.c_int64), ("fallback_queries", C.c_int64)]
 
     def asdict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

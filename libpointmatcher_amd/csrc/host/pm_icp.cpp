@@ -308,7 +308,7 @@ struct PointToPointEM : PM<T>::ErrorMinimizer {
         pmx_stats st;
         d.check(pmx_p2point_system(d.ctx, mp, mq, md, &st));
         this->setStats(st);
-        T m[9], U[9], S[3], V[9], R[9], Vt[9];
+        T m[9], U[9], S[3], V[9], R[9] = {}, Vt[9];
         for (int i = 0; i < D * D; ++i) m[i] = (T)md[i];
         dense::jacobi_svd(m, D, U, S, V);
         for (int r = 0; r < D; ++r)

@@ -49,15 +49,23 @@ struct pmx_ctx {
 
     // uniform grid over the reference (exact shell search, pmx_grid.hip)
     int search_type = 1;
+    int grid_mode = 1;            // 1 = per-lane shell search (default), 0 = LDS tiles (PMX_GRID_MODE=tile)
+    uint32_t tile_max = 4096;     // largest per-wave box scanned from LDS (PMX_GRID_TILE_MAX)
+    bool no_visits = false;       // experiment knob: skip the pair counter (PMX_NO_VISITS)
     void* d_gpts = nullptr;
+    void* d_gnrm = nullptr;       // normals in grid order
     int32_t* d_gidx = nullptr;
     uint32_t* d_gstart = nullptr;
     double g_lo[3] = {0, 0, 0};
     double g_h = 1.0;
     int g_dim[3] = {1, 1, 1};
     bool grid_ready = false;
-    int32_t* d_order = nullptr;  // reading visit order (sorted by initial cell)
-    unsigned long long* d_visited = nullptr;
+    std::vector<int32_t> slot_query;  // slot -> reading index (empty = identity)
+    uint32_t* d_waves = nullptr;      // tile-kernel wave table: first slot of each wave (+ N)
+    int64_t n_waves = 0;
+    bool ids_grid = false;            // last match wrote grid positions
+    unsigned long long* d_visited = nullptr;  // [pairs, fallbacks] in the iteration block
+    unsigned long long* d_vpart = nullptr;    // spread per-wave counters (pmx_grid.hip)
     uint64_t visited_host = 0;   // brute force: known at launch
 
     // reading shard
@@ -201,7 +209,7 @@ hipEvent_t get_event(pmx_ctx* c) {
 
 // -------------------------------------------------------------------- grid --
 // Uniform grid of the (centred) reference for the exact shell search.  The
-// cell size targets ~8 points per occupied cell: the occupied-cell count at
+// cell size targets ~4 points per occupied cell: the occupied-cell count at
 // two trial sizes gives the data's local dimension (surface ~2, volume ~3),
 // from which the size for the target density follows.  Points are counting-
 // sorted by cell (x fastest) so every x-row of cells is one contiguous range.
@@ -243,7 +251,7 @@ static bool finite_pt(const P4<T>& p) {
 }
 
 template <typename T>
-int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M) {
+int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::vector<P4<T>>& nrm) {
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     int64_t valid = 0;
     for (int64_t j = 0; j < M; ++j) {
@@ -284,7 +292,10 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M) {
         double dim = std::log2((double)o1 / (double)o0);
         dim = std::min(3.0, std::max(1.0, dim));
         const double ppc1 = (double)valid / (double)o1;
-        double target = 16.0;  // points per occupied cell (measured optimum; PMX_GRID_PPC: tuning knob)
+        // points per occupied cell: 2-4 is the measured optimum of the per-lane
+        // search on MI355X (C3: 0.106 ms at 2-4, 0.117 at 6, 0.148 at 1,
+        // 0.19 at 16); PMX_GRID_PPC is the tuning knob
+        double target = 4.0;
         if (const char* e = std::getenv("PMX_GRID_PPC")) target = std::max(0.5, std::atof(e));
         h = h1 * std::pow(target / ppc1, 1.0 / dim);
         h = std::max(h, maxe / 4096.0);
@@ -312,7 +323,7 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M) {
         gp[p] = pts[j];
         gi[p] = (int32_t)j;
     }
-    for (void** b : {&c->d_gpts, (void**)&c->d_gidx, (void**)&c->d_gstart})
+    for (void** b : {&c->d_gpts, &c->d_gnrm, (void**)&c->d_gidx, (void**)&c->d_gstart})
         if (*b) {
             (void)hipFree(*b);
             *b = nullptr;
@@ -321,6 +332,13 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M) {
     HIPCHK(c, hipMalloc((void**)&c->d_gidx, sizeof(int32_t) * gi.size()));
     HIPCHK(c, hipMalloc((void**)&c->d_gstart, sizeof(uint32_t) * start.size()));
     HIPCHK(c, hipMemcpyAsync(c->d_gpts, gp.data(), sizeof(P4<T>) * gp.size(), hipMemcpyHostToDevice, c->stream));
+    std::vector<P4<T>> gn;
+    if (!nrm.empty()) {
+        gn.resize(gp.size());
+        for (int64_t p = 0; p < valid; ++p) gn[(size_t)p] = nrm[(size_t)gi[(size_t)p]];
+        HIPCHK(c, hipMalloc(&c->d_gnrm, sizeof(P4<T>) * gn.size()));
+        HIPCHK(c, hipMemcpyAsync(c->d_gnrm, gn.data(), sizeof(P4<T>) * gn.size(), hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(c, hipMemcpyAsync(c->d_gidx, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->d_gstart, start.data(), sizeof(uint32_t) * start.size(), hipMemcpyHostToDevice,
                              c->stream));
@@ -334,21 +352,43 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M) {
     return PMX_OK;
 }
 
-// visit order of the reading: sorted by the cell of the initially transformed
-// point, so lanes of a wave walk neighbouring cells (performance only)
+// 21-bit Morton spread (bit i -> bit 3i)
+static inline uint64_t spread3(uint64_t v) {
+    v &= 0x1fffffull;
+    v = (v | v << 32) & 0x1f00000000ffffull;
+    v = (v | v << 16) & 0x1f0000ff0000ffull;
+    v = (v | v << 8) & 0x100f00f00f00f00full;
+    v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+    v = (v | v << 2) & 0x1249249249249249ull;
+    return v;
+}
+
+// Slot order of the reading: Morton order of the cell of the initially
+// transformed point, so the 64 queries of a wave form a compact cluster
+// (small shared LDS box in the tile kernel) and result writes are coalesced.
+// Performance only: every kernel is order-independent up to fp64 summation
+// order, and the mirrors undo the permutation.
+//
+// Waves of the tile kernel: a wave takes up to 64 consecutive slots but never
+// crosses the boundary of an aligned Morton block of 2^L cells per side, so
+// its queries never straddle two distant regions (a straddling wave would
+// share one huge LDS box).  L is the smallest level whose wave count stays
+// within `fill` (default 1.25, PMX_GRID_WAVE_FILL) of ceil(N / 64).
 template <typename T>
-int build_order(pmx_ctx* c, const std::vector<P4<T>>& raw, int64_t N, const Mat4<T>& M0) {
-    if (c->d_order) (void)hipFree(c->d_order);
-    c->d_order = nullptr;
-    if (!c->grid_ready || N <= 0) return PMX_OK;
-    if (std::getenv("PMX_GRID_NOORDER")) return PMX_OK;  // tuning knob: identity visit order
+std::vector<int32_t> build_order(const pmx_ctx* c, const std::vector<P4<T>>& raw, int64_t N, const Mat4<T>& M0,
+                                 std::vector<uint32_t>& waves) {
+    std::vector<int32_t> order;
+    waves.clear();
+    if (!c->grid_ready || N <= 0) return order;
+    if (std::getenv("PMX_GRID_NOORDER")) return order;  // tuning knob: identity slot order
     GridShape s;
     for (int a = 0; a < 3; ++a) {
         s.lo[a] = c->g_lo[a];
         s.g[a] = c->g_dim[a];
     }
     s.h = c->g_h;
-    std::vector<uint64_t> key((size_t)N);
+    const bool morton = s.g[0] <= (1 << 21) && s.g[1] <= (1 << 21) && s.g[2] <= (1 << 21);
+    std::vector<std::pair<uint64_t, int32_t>> key((size_t)N);
     for (int64_t i = 0; i < N; ++i) {
         const P4<T>& p = raw[i];
         P4<double> q;
@@ -356,16 +396,43 @@ int build_order(pmx_ctx* c, const std::vector<P4<T>>& raw, int64_t N, const Mat4
         q.y = ((double)M0.m[4] * p.x + (double)M0.m[5] * p.y) + (double)M0.m[6] * p.z + (double)M0.m[7] * p.w;
         q.z = ((double)M0.m[8] * p.x + (double)M0.m[9] * p.y) + (double)M0.m[10] * p.z + (double)M0.m[11] * p.w;
         q.w = 1;
-        const uint64_t cell = finite_pt(q) ? (uint64_t)cell_of(s, q) : (uint64_t)s.cells();
-        key[i] = (cell << 32) | (uint64_t)i;
+        uint64_t k = ~0ull;
+        if (finite_pt(q)) {
+            const int64_t cell = cell_of(s, q);
+            if (morton) {
+                const int64_t cx = cell % s.g[0], cy = (cell / s.g[0]) % s.g[1], cz = cell / ((int64_t)s.g[0] * s.g[1]);
+                k = spread3((uint64_t)cx) | (spread3((uint64_t)cy) << 1) | (spread3((uint64_t)cz) << 2);
+            } else {
+                k = (uint64_t)cell;
+            }
+        }
+        key[(size_t)i] = {k, (int32_t)i};
     }
     std::sort(key.begin(), key.end());
-    std::vector<int32_t> order((size_t)N);
-    for (int64_t i = 0; i < N; ++i) order[i] = (int32_t)(key[i] & 0xffffffffu);
-    HIPCHK(c, hipMalloc((void**)&c->d_order, sizeof(int32_t) * N));
-    HIPCHK(c, hipMemcpyAsync(c->d_order, order.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return PMX_OK;
+    order.resize((size_t)N);
+    for (int64_t i = 0; i < N; ++i) order[(size_t)i] = key[(size_t)i].second;
+    if (morton) {
+        double fill = 1.25;
+        if (const char* e = std::getenv("PMX_GRID_WAVE_FILL")) fill = std::max(1.0, std::atof(e));
+        const int64_t full = (N + 63) / 64;
+        auto cut = [&](int L, std::vector<uint32_t>* out) -> int64_t {
+            int64_t W = 0;
+            for (int64_t i = 0; i < N;) {
+                const uint64_t blk = L >= 21 ? 0 : key[(size_t)i].first >> (3 * L);
+                int64_t j = i + 1;
+                while (j < N && j - i < 64 && (L >= 21 ? 0 : key[(size_t)j].first >> (3 * L)) == blk) ++j;
+                if (out) out->push_back((uint32_t)i);
+                ++W;
+                i = j;
+            }
+            return W;
+        };
+        int L = 0;
+        while (L < 21 && (double)cut(L, nullptr) > fill * (double)full) ++L;
+        cut(L, &waves);
+        waves.push_back((uint32_t)N);
+    }
+    return order;
 }
 
 // ------------------------------------------------------------------ clouds --
@@ -407,7 +474,9 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     c->M_pad = M_pad;
     c->have_match = false;
     c->grid_ready = false;
-    return build_grid<T>(c, h, M);
+    // a resident reading keeps its slot order (any permutation is correct;
+    // it was only chosen for the previous grid's locality)
+    return build_grid<T>(c, h, M, hn);
 }
 
 template <typename T>
@@ -421,6 +490,23 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
         const T* p = feat + i * rows;
         h[i] = (D == 3) ? P4<T>{p[0], p[1], p[2], p[3]} : P4<T>{p[0], p[1], (T)0, p[2]};
     }
+    Mat4<T> M0 = embed<T>(T0, rows);
+    std::vector<uint32_t> waves;
+    c->slot_query = build_order<T>(c, h, N, M0, waves);
+    if (!c->slot_query.empty()) {
+        std::vector<P4<T>> hs((size_t)N);
+        for (int64_t s = 0; s < N; ++s) hs[(size_t)s] = h[(size_t)c->slot_query[(size_t)s]];
+        h.swap(hs);
+    }
+    if (c->d_waves) (void)hipFree(c->d_waves);
+    c->d_waves = nullptr;
+    c->n_waves = 0;
+    if (!waves.empty()) {
+        HIPCHK(c, hipMalloc((void**)&c->d_waves, sizeof(uint32_t) * waves.size()));
+        HIPCHK(c, hipMemcpyAsync(c->d_waves, waves.data(), sizeof(uint32_t) * waves.size(), hipMemcpyHostToDevice,
+                                 c->stream));
+        c->n_waves = (int64_t)waves.size() - 1;
+    }
     void* d_raw = nullptr;
     HIPCHK(c, hipMalloc(&d_raw, sizeof(P4<T>) * (N > 0 ? N : 1)));
     if (c->d_rd) (void)hipFree(c->d_rd);
@@ -428,11 +514,8 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     HIPCHK(c, hipMalloc(&c->d_rd, sizeof(P4<T>) * (N > 0 ? N : 1)));
     if (N > 0) {
         HIPCHK(c, hipMemcpyAsync(d_raw, h.data(), sizeof(P4<T>) * N, hipMemcpyHostToDevice, c->stream));
-        Mat4<T> M0 = embed<T>(T0, rows);
         launch_transform<T>((const P4<T>*)d_raw, (P4<T>*)c->d_rd, N, M0, c->stream);
         HIPCHK(c, hipGetLastError());
-        int rc = build_order<T>(c, h, N, M0);
-        if (rc) return rc;
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     (void)hipFree(d_raw);
@@ -497,7 +580,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
     const T md = (T)maxDist;
     const T maxR2 = md * md;  // libnabo squares the radius in T [ext]
     // reset the per-iteration error word, VarTrimmed ratio and pair counter
-    HIPCHK(c, hipMemsetAsync((char*)c->d_result + kBlkIterErr, 0, kBlkVisited + 8 - kBlkIterErr, c->stream));
+    // (visited and fallback counters: [kBlkVisited, kBlkVisited + 16))
+    HIPCHK(c, hipMemsetAsync((char*)c->d_result + kBlkIterErr, 0, kBlkVisited + 16 - kBlkIterErr, c->stream));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = get_event(c);
@@ -508,13 +592,16 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                         (T*)c->d_dists, c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1,
                         c->cu_count);
         c->visited_host = (uint64_t)c->N * (uint64_t)c->M;
+        c->ids_grid = false;
     } else {
         if (e0) (void)hipEventRecord(e0, c->stream);
-        launch_grid_match<T>((const P4<T>*)c->d_gpts, c->d_gidx, c->d_gstart, c->g_lo, c->g_h, c->g_dim,
-                             (const P4<T>*)c->d_rd, c->d_order, c->N, Tm, knn, maxR2, (T*)c->d_dists, c->d_ids,
+        launch_grid_match<T>(c->grid_mode, (const P4<T>*)c->d_gpts, c->d_gidx, c->d_gstart, c->g_lo, c->g_h,
+                             c->g_dim, (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2,
+                             c->tile_max, (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart,
                              c->d_visited, c->stream);
         if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
+        c->ids_grid = true;
     }
     HIPCHK(c, hipGetLastError());
     if (e0 && e1) c->ev_pending.emplace_back(e0, e1);
@@ -543,6 +630,23 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
 int check_match(pmx_ctx* c) {
     if (!c->have_match) return fail(c, PMX_E_STATE, "pmx_match must be called first");
     return PMX_OK;
+}
+
+// the reference layout the current match ids index
+const void* match_ref(const pmx_ctx* c) { return c->ids_grid ? c->d_gpts : c->d_ref; }
+
+// slot-major device array -> query-major host array (the reference's order)
+template <typename V>
+void unpermute(const pmx_ctx* c, const std::vector<V>& src, V* dst, int k) {
+    const int64_t N = c->N;
+    if (c->slot_query.empty()) {
+        std::memcpy(dst, src.data(), sizeof(V) * (size_t)(N * k));
+        return;
+    }
+    for (int64_t s = 0; s < N; ++s) {
+        const int64_t qi = c->slot_query[(size_t)s];
+        for (int j = 0; j < k; ++j) dst[qi * k + j] = src[(size_t)(s * k + j)];
+    }
 }
 
 template <typename T>
@@ -677,6 +781,8 @@ void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double 
     unsigned long long v = 0;
     std::memcpy(&v, (const char*)c->h_result + kBlkVisited, sizeof(v));
     st->visited = c->visited_host ? (int64_t)c->visited_host : (int64_t)v;
+    std::memcpy(&v, (const char*)c->h_result + kBlkVisited + 8, sizeof(v));
+    st->fallback_queries = c->visited_host ? 0 : (int64_t)v;
 }
 
 template <typename T>
@@ -688,9 +794,9 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     const int NF = c->dim == 3 ? 6 : 3;
     const int NV = NF * NF + NF + 5;
     Mat4<T> Tm = step_mat<T>(c);
-    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)c->d_ref, (const P4<T>*)c->d_nrm,
-                              (const T*)c->d_dists, c->d_ids, (const T*)c->d_w, c->knn, c->N, c->dim, c->d_partials,
-                              c->stream);
+    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c),
+                              (const P4<T>*)(c->ids_grid ? c->d_gnrm : c->d_nrm), (const T*)c->d_dists, c->d_ids,
+                              (const T*)c->d_w, c->knn, c->N, c->dim, c->d_partials, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, c->stream);
     HIPCHK(c, hipGetLastError());
     if ((rc = allreduce_f64(c, c->d_result, NV))) return rc;
@@ -713,12 +819,12 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
     int rc = check_match(c);
     if (rc) return rc;
     Mat4<T> Tm = step_mat<T>(c);
-    launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)c->d_ref, (const T*)c->d_dists, c->d_ids,
+    launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
                             (const T*)c->d_w, c->knn, c->N, c->d_partials, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, c->stream);
     if ((rc = allreduce_f64(c, c->d_result, 11))) return rc;
     launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, c->stream);
-    launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)c->d_ref, (const T*)c->d_dists, c->d_ids,
+    launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
                             (const T*)c->d_w, c->knn, c->N, (const T*)c->d_means, c->d_partials, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, c->stream);
     HIPCHK(c, hipGetLastError());
@@ -747,9 +853,30 @@ int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
     int rc = check_match(c);
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
-    if (dists) HIPCHK(c, hipMemcpyAsync(dists, c->d_dists, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
-    if (ids) HIPCHK(c, hipMemcpyAsync(ids, c->d_ids, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (n <= 0) return PMX_OK;
+    std::vector<T> hd;
+    std::vector<int32_t> hi;
+    if (dists) {
+        hd.resize((size_t)n);
+        HIPCHK(c, hipMemcpyAsync(hd.data(), c->d_dists, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
+    }
+    int32_t* d_map = nullptr;
+    if (ids) {
+        hi.resize((size_t)n);
+        const int32_t* src = c->d_ids;
+        if (c->ids_grid) {  // grid positions -> reference indices
+            HIPCHK(c, hipMalloc((void**)&d_map, sizeof(int32_t) * n));
+            launch_pos_to_index(c->d_ids, c->d_gidx, d_map, n, c->stream);
+            HIPCHK(c, hipGetLastError());
+            src = d_map;
+        }
+        HIPCHK(c, hipMemcpyAsync(hi.data(), src, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    }
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (d_map) (void)hipFree(d_map);
+    HIPCHK(c, e);
+    if (dists) unpermute<T>(c, hd, (T*)dists, c->knn);
+    if (ids) unpermute<int32_t>(c, hi, ids, c->knn);
     return PMX_OK;
 }
 
@@ -758,8 +885,11 @@ int get_weights_impl(pmx_ctx* c, void* w) {
     int rc = check_match(c);
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
-    HIPCHK(c, hipMemcpyAsync(w, c->d_w, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
+    if (n <= 0) return PMX_OK;
+    std::vector<T> hw((size_t)n);
+    HIPCHK(c, hipMemcpyAsync(hw.data(), c->d_w, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    unpermute<T>(c, hw, (T*)w, c->knn);
     return PMX_OK;
 }
 
@@ -788,6 +918,10 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     pmx_ctx* c = new pmx_ctx();
     c->device = device;
     c->dtype = dtype;
+    // tuning knobs (defaults are the measured optimum on MI355X)
+    if (const char* e = std::getenv("PMX_GRID_MODE")) c->grid_mode = std::strcmp(e, "tile") == 0 ? 0 : 1;
+    if (const char* e = std::getenv("PMX_GRID_TILE_MAX")) c->tile_max = (uint32_t)std::max(0, std::atoi(e));
+    c->no_visits = std::getenv("PMX_NO_VISITS") != nullptr;
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
@@ -812,6 +946,8 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     c->d_ratio = (double*)((char*)p + kBlkRatio);
     c->d_visited = (unsigned long long*)((char*)p + kBlkVisited);
     c->d_means = (char*)p + kBlkMeans;
+    if (hipMalloc((void**)&c->d_vpart, grid_counter_bytes()) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_vpart, 0, grid_counter_bytes());
     if (hipMalloc((void**)&c->d_hist, 2048 * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_hist, 0, 2048 * sizeof(uint32_t));
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
@@ -826,7 +962,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
-                    c->d_result, c->d_gpts, c->d_gidx, c->d_gstart, c->d_order};
+                    c->d_result, c->d_gpts, c->d_gnrm, c->d_gidx, c->d_gstart, c->d_waves, c->d_vpart};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_result) (void)hipHostFree(c->h_result);

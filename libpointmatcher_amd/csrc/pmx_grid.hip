@@ -4,29 +4,44 @@
 // MatchersImpl.cpp:85-101 with libnabo's exact search): distances are the
 // bit-identical ((dx*dx + dy*dy) + dz*dz) in T without FMA, candidates are
 // ordered by (distance, original index) so ties resolve to the lowest index,
-// k-lists are sorted ascending.  Only the set of pairs evaluated changes:
-// instead of all N*M pairs, each query visits the cells of growing cubic
-// shells around its own cell and stops once the k-th best distance is
-// provably below every unvisited point:
-//
-//   LB_R = min over axes and existing sides of the distance from q to the
-//          faces of the (2R+1)^3 block of visited cells (computed in double);
-//   stop when  d_k < LB_R^2 * (1 - 1e-5)   (and the list is full).
-//
-// The 1e-5 relative margin dominates every rounding involved (T distances
-// carry a few ulp; cell assignment is done in double), so an unvisited point
-// can never produce a distance <= d_k: the result equals the brute-force one
-// exactly, ties included.  With a finite radius the search also stops once
-// LB_R^2 (1 - 1e-5) > maxDist^2.
+// k-lists are sorted ascending.  Only the set of pairs evaluated changes.
 //
 // Layout (built once per Matcher::init on the host, pmx_capi.hip):
 //   gpts  P4<T>[M]        reference points sorted by cell (x fastest)
 //   gidx  int32[M]        their original indices
 //   start uint32[C + 1]   first point of each cell (C = gx * gy * gz)
-// Each x-row of cells is one contiguous point range, so a shell is walked as
-// a handful of contiguous scans.  Queries are visited in the order of their
-// initial cell (a permutation computed at pmx_set_reading) so neighbouring
-// lanes walk neighbouring cells.
+// Each x-row of cells is one contiguous point range.  Match ids produced
+// here are POSITIONS in gpts (the reductions gather gpts / sorted normals
+// coherently); gidx maps them back to reference indices for ties and for
+// the host mirror.  The reading arrives in slot order (Morton order of the
+// initial cell, pmx_set_reading), so consecutive lanes hold nearby queries
+// and every output write is coalesced.
+//
+// Per-lane shell search (default): each lane visits the cells of growing
+// cubic shells around its query's cell (the 3x3x3 block first, its nine row
+// bounds prefetched together) and stops at the LB test below with the box of
+// visited cells.  Measured best at ~2-4 points per occupied cell (C3:
+// 0.106 ms per 1M queries); it is bound by the dependent gather latency of
+// the row scans, not by pair evaluation.
+//
+// Tile kernel (PMX_GRID_MODE=tile, pmx_grid_tile.inc).  One wave = up to 64
+// queries inside one aligned Morton block (the wave table of
+// pmx_set_reading).  The wave takes the bounding box of its queries' cells, grows it
+// by one cell, copies the box's reference points (ny * nz contiguous row
+// ranges) into LDS, and every lane scans the whole LDS list (broadcast reads,
+// no divergence); the box grows by one cell per round until every lane is
+// certified.  A lane's result is exact when its k-th distance is below the
+// squared distance to the nearest box face that is not a grid boundary:
+//
+//   LB = min over interior box faces of |q - face|   (in double)
+//   certified when  d_k < LB^2 (1 - 1e-5)   or  LB^2 (1 - 1e-5) > maxDist^2.
+//
+// The 1e-5 relative margin dominates every rounding involved (T distances
+// carry a few ulp; cell assignment is done in double), so no point outside
+// the box can produce a distance <= d_k.  Lanes of waves whose box grows too
+// large run the per-lane shell search.  It evaluates 5x more pairs than the
+// per-lane search from LDS (broadcast reads) and measures 0.187 ms at C3: a
+// candidate for QPT > 1 and for very dense references.
 #include "pmx_internal.h"
 
 namespace pmx {
@@ -49,14 +64,35 @@ __device__ __forceinline__ T gsqd(T qx, T qy, T qz, const P4<T>& r) {
     return d;
 }
 
+// position <-> the w lane of an LDS point (bit pattern, never used as a number)
+__device__ __forceinline__ float pos_w(uint32_t p, float) { return __uint_as_float(p); }
+__device__ __forceinline__ double pos_w(uint32_t p, double) { return __longlong_as_double((long long)p); }
+__device__ __forceinline__ uint32_t w_pos(float w) { return __float_as_uint(w); }
+__device__ __forceinline__ uint32_t w_pos(double w) { return (uint32_t)__double_as_longlong(w); }
+
+constexpr int32_t kNoPos = 0x7fffffff;
+
+__device__ __forceinline__ float vmin(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ double vmin(double a, double b) { return fmin(a, b); }
+
+// (equal distance) does candidate position a come before the held position b?
+// Ties are broken on the ORIGINAL reference index, as the brute force does.
+__device__ __forceinline__ bool tie_first(const int32_t* __restrict__ gidx, int32_t a, int32_t b) {
+    if (b == kNoPos) return true;
+    if (a == kNoPos) return false;
+    return gidx[a] < gidx[b];
+}
+
 template <typename T, int KT>
-__device__ __forceinline__ void ginsert(T (&kd)[KT], int32_t (&ki)[KT], T d, int32_t id) {
-    // lexicographic (d, id) insertion; candidates arrive in arbitrary index order
+__device__ __forceinline__ void ginsert(const int32_t* __restrict__ gidx, T (&kd)[KT], int32_t (&ki)[KT], T d,
+                                        int32_t pos) {
+    // lexicographic (d, original index) insertion
     kd[KT - 1] = d;
-    ki[KT - 1] = id;
+    ki[KT - 1] = pos;
 #pragma unroll
     for (int s = KT - 1; s > 0; --s) {
-        const bool sw = kd[s] < kd[s - 1] || (kd[s] == kd[s - 1] && ki[s] < ki[s - 1]);
+        bool sw = kd[s] < kd[s - 1];
+        if (!sw && kd[s] == kd[s - 1]) sw = tie_first(gidx, ki[s], ki[s - 1]);
         const T td = sw ? kd[s - 1] : kd[s];
         const int32_t ti = sw ? ki[s - 1] : ki[s];
         kd[s - 1] = sw ? kd[s] : kd[s - 1];
@@ -67,17 +103,15 @@ __device__ __forceinline__ void ginsert(T (&kd)[KT], int32_t (&ki)[KT], T d, int
 }
 
 template <typename T, int KT>
-__device__ __forceinline__ void consider(const int32_t* __restrict__ gidx, uint32_t j, T d, T (&kd)[KT],
+__device__ __forceinline__ void consider(const int32_t* __restrict__ gidx, int32_t pos, T d, T (&kd)[KT],
                                          int32_t (&ki)[KT]) {
     if (d <= kd[KT - 1]) {
-        const int32_t id = gidx[j];
-        if (d < kd[KT - 1] || id < ki[KT - 1]) ginsert<T, KT>(kd, ki, d, id);
+        if (d < kd[KT - 1] || tie_first(gidx, pos, ki[KT - 1])) ginsert<T, KT>(gidx, kd, ki, d, pos);
     }
 }
 
-// Scan one contiguous point range.  The scan is latency-bound (each lane
-// walks its own cells), so points are fetched eight at a time with
-// independent loads before any of them is used.
+// Scan one contiguous point range of gpts (per-lane search).  Latency-bound:
+// points are fetched eight at a time with independent loads.
 template <typename T, int KT>
 __device__ __forceinline__ void scan_range(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                                            uint32_t a, uint32_t b, T qx, T qy, T qz, T (&kd)[KT],
@@ -93,9 +127,9 @@ __device__ __forceinline__ void scan_range(const P4<T>* __restrict__ gpts, const
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = gsqd(qx, qy, qz, p[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) consider<T, KT>(gidx, j + u, d[u], kd, ki);
+        for (int u = 0; u < U; ++u) consider<T, KT>(gidx, (int32_t)(j + u), d[u], kd, ki);
     }
-    for (; j < b; ++j) consider<T, KT>(gidx, j, gsqd(qx, qy, qz, gpts[j]), kd, ki);
+    for (; j < b; ++j) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, gpts[j]), kd, ki);
 }
 
 struct GridGeom {
@@ -104,128 +138,205 @@ struct GridGeom {
     int g[3];
 };
 
+__device__ __forceinline__ void cell_of_q(const GridGeom& G, const double q[3], int c[3], bool& qnan) {
+    qnan = false;
+    for (int a = 0; a < 3; ++a) {
+        const double f = (q[a] - G.lo[a]) * G.inv_h;
+        if (!(f == f)) qnan = true;
+        c[a] = f < 0.0 ? 0 : (f >= (double)G.g[a] ? G.g[a] - 1 : (int)f);
+    }
+}
+
+// exact shell search for one query (from scratch); kd/ki must be initialised
 template <typename T, int KT>
-__global__ __launch_bounds__(256) void grid_match_kernel(const P4<T>* __restrict__ gpts,
-                                                         const int32_t* __restrict__ gidx,
-                                                         const uint32_t* __restrict__ start, GridGeom G,
-                                                         const P4<T>* __restrict__ rd,
-                                                         const int32_t* __restrict__ order, int64_t N,
-                                                         Mat4<T> Tm, int k, T maxR2, T* __restrict__ out_d,
-                                                         int32_t* __restrict__ out_i,
-                                                         unsigned long long* __restrict__ visited) {
+__device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
+                            const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy, T qz,
+                            const double q[3], const int c[3], T maxR2, T (&kd)[KT], int32_t (&ki)[KT],
+                            uint32_t& visits) {
+    const double margin = 1.0 - 1e-5;
+    {
+        // phase 1: the whole 3x3x3 block (R = 0 and 1).  The nine row
+        // bounds are loaded together from always-valid (clamped)
+        // addresses and masked afterwards, then the rows are scanned.
+        uint32_t ra[9], rb[9];
+        const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            const int z = c[2] + r / 3 - 1, y = c[1] + r % 3 - 1;
+            const bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
+            const int zc = min(max(z, 0), G.g[2] - 1), yc = min(max(y, 0), G.g[1] - 1);
+            const int64_t row = ((int64_t)zc * G.g[1] + yc) * G.g[0];
+            const uint32_t va = start[row + x0];
+            const uint32_t vb = start[row + x1 + 1];
+            ra[r] = ok ? va : 0u;
+            rb[r] = ok ? vb : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < 9; ++r) scan_range<T, KT>(gpts, gidx, ra[r], rb[r], qx, qy, qz, kd, ki, visits);
+    }
+    for (int R = 1;; ++R) {
+        if (R >= 2) {
+            // walk the shell at Chebyshev radius R
+            const int y0 = max(c[1] - R, 0), y1 = min(c[1] + R, G.g[1] - 1);
+            const int z0 = max(c[2] - R, 0), z1 = min(c[2] + R, G.g[2] - 1);
+            const int x0 = max(c[0] - R, 0), x1 = min(c[0] + R, G.g[0] - 1);
+            for (int z = z0; z <= z1; ++z) {
+                const bool zface = (z == c[2] - R) || (z == c[2] + R);
+                for (int y = y0; y <= y1; ++y) {
+                    const bool yface = (y == c[1] - R) || (y == c[1] + R);
+                    const int64_t row = ((int64_t)z * G.g[1] + y) * G.g[0];
+                    if (zface || yface) {
+                        scan_range<T, KT>(gpts, gidx, start[row + x0], start[row + x1 + 1], qx, qy, qz, kd, ki,
+                                          visits);
+                    } else {
+                        if (c[0] - R >= 0)
+                            scan_range<T, KT>(gpts, gidx, start[row + c[0] - R], start[row + c[0] - R + 1], qx, qy,
+                                              qz, kd, ki, visits);
+                        if (c[0] + R <= G.g[0] - 1)
+                            scan_range<T, KT>(gpts, gidx, start[row + c[0] + R], start[row + c[0] + R + 1], qx, qy,
+                                              qz, kd, ki, visits);
+                    }
+                }
+            }
+        }
+        // lower bound on the distance to any unvisited cell
+        double lb = 1e300;
+        bool any = false;
+        for (int a = 0; a < 3; ++a) {
+            if (c[a] - R - 1 >= 0) {
+                const double face = G.lo[a] + (double)(c[a] - R) * G.h;
+                lb = fmin(lb, q[a] - face);
+                any = true;
+            }
+            if (c[a] + R + 1 <= G.g[a] - 1) {
+                const double face = G.lo[a] + (double)(c[a] + R + 1) * G.h;
+                lb = fmin(lb, face - q[a]);
+                any = true;
+            }
+        }
+        if (!any) break;  // the whole grid has been visited
+        if (lb > 0.0) {
+            const double lb2 = lb * lb * margin;
+            if ((double)kd[KT - 1] < lb2 && ki[KT - 1] != kNoPos) break;
+            if (lb2 > (double)maxR2) break;
+        }
+    }
+}
+
+template <typename T, int KT>
+__device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&kd)[KT], const int32_t (&ki)[KT],
+                                          T* __restrict__ out_d, int32_t* __restrict__ out_i) {
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {  // static indexing keeps kd/ki in registers
+        if (s < k) {
+            T d = kd[s];
+            int32_t id = ki[s];
+            if (id == kNoPos || !(d <= maxR2)) {
+                d = (T)__builtin_huge_val();
+                id = -1;
+            }
+            out_d[j * k + s] = d;
+            out_i[j * k + s] = id;
+        }
+    }
+}
+
+// Pair / fallback counters.  One device-scope atomic per wave on a single
+// address serialises (~110 us for 16K waves at C3), so every wave adds into
+// one of kVSlots counters, each on its own 128-byte line; counter_sum_kernel
+// folds them into the iteration block after the match.
+constexpr int kVSlots = 256;
+constexpr int kVStride = 16;  // unsigned long longs: 128 bytes
+__device__ __forceinline__ unsigned long long* vslot(unsigned long long* vpart, int which) {
+    const unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    return vpart + ((size_t)which * kVSlots + (wave & (kVSlots - 1))) * kVStride;
+}
+__device__ __forceinline__ void add_visits(uint32_t visits, unsigned long long* vpart) {
+    unsigned long long v = visits;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0 && vpart && v) atomicAdd(vslot(vpart, 0), v);
+}
+
+__global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long* __restrict__ vpart,
+                                                              unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long red[2][kVSlots / 64];
+    const int t = threadIdx.x;
+    unsigned long long a = vpart[(size_t)t * kVStride], b = vpart[(size_t)(kVSlots + t) * kVStride];
+    vpart[(size_t)t * kVStride] = 0;  // ready for the next match
+    vpart[(size_t)(kVSlots + t) * kVStride] = 0;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+    }
+    if ((t & 63) == 0) {
+        red[0][t >> 6] = a;
+        red[1][t >> 6] = b;
+    }
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long sa = 0, sb = 0;
+        for (int w = 0; w < kVSlots / 64; ++w) {
+            sa += red[0][w];
+            sb += red[1][w];
+        }
+        out[0] = sa;
+        out[1] = sb;
+    }
+}
+size_t grid_counter_bytes() { return sizeof(unsigned long long) * 2 * kVSlots * kVStride; }
+
+// ------------------------------------------------------- per-lane kernel --
+template <typename T, int KT>
+__global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
+                                                        const int32_t* __restrict__ gidx,
+                                                        const uint32_t* __restrict__ start, GridGeom G,
+                                                        const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
+                                                        T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
+                                                        unsigned long long* __restrict__ visited) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t visits = 0;
     if (j < N) {
-        const int64_t qi = order ? (int64_t)order[j] : j;
         T qx, qy, qz;
-        gxform(Tm, rd[qi], qx, qy, qz);
+        gxform(Tm, rd[j], qx, qy, qz);
         T kd[KT];
         int32_t ki[KT];
 #pragma unroll
         for (int s = 0; s < KT; ++s) {
             kd[s] = (T)__builtin_huge_val();
-            ki[s] = 0x7fffffff;
+            ki[s] = kNoPos;
         }
         const double q[3] = {(double)qx, (double)qy, (double)qz};
         int c[3];
-        bool qnan = false;
-        for (int a = 0; a < 3; ++a) {
-            const double f = (q[a] - G.lo[a]) * G.inv_h;
-            if (!(f == f)) qnan = true;
-            int ci = f < 0.0 ? 0 : (f >= (double)G.g[a] ? G.g[a] - 1 : (int)f);
-            c[a] = ci;
-        }
-        if (!qnan) {
-            const double margin = 1.0 - 1e-5;
-            {
-                // phase 1: the whole 3x3x3 block (R = 0 and 1).  The nine row
-                // bounds are loaded together from always-valid (clamped)
-                // addresses and masked afterwards, then the rows are scanned.
-                uint32_t ra[9], rb[9];
-                const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
-#pragma unroll
-                for (int r = 0; r < 9; ++r) {
-                    const int z = c[2] + r / 3 - 1, y = c[1] + r % 3 - 1;
-                    const bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
-                    const int zc = min(max(z, 0), G.g[2] - 1), yc = min(max(y, 0), G.g[1] - 1);
-                    const int64_t row = ((int64_t)zc * G.g[1] + yc) * G.g[0];
-                    const uint32_t va = start[row + x0];
-                    const uint32_t vb = start[row + x1 + 1];
-                    ra[r] = ok ? va : 0u;
-                    rb[r] = ok ? vb : 0u;
-                }
-#pragma unroll
-                for (int r = 0; r < 9; ++r) scan_range<T, KT>(gpts, gidx, ra[r], rb[r], qx, qy, qz, kd, ki, visits);
-            }
-            for (int R = 1;; ++R) {
-              if (R >= 2) {
-                // walk the shell at Chebyshev radius R
-                const int y0 = max(c[1] - R, 0), y1 = min(c[1] + R, G.g[1] - 1);
-                const int z0 = max(c[2] - R, 0), z1 = min(c[2] + R, G.g[2] - 1);
-                const int x0 = max(c[0] - R, 0), x1 = min(c[0] + R, G.g[0] - 1);
-                for (int z = z0; z <= z1; ++z) {
-                    const bool zface = (z == c[2] - R) || (z == c[2] + R);
-                    for (int y = y0; y <= y1; ++y) {
-                        const bool yface = (y == c[1] - R) || (y == c[1] + R);
-                        const int64_t row = ((int64_t)z * G.g[1] + y) * G.g[0];
-                        if (zface || yface) {
-                            scan_range<T, KT>(gpts, gidx, start[row + x0], start[row + x1 + 1], qx, qy, qz, kd, ki,
-                                              visits);
-                        } else {
-                            if (c[0] - R >= 0)
-                                scan_range<T, KT>(gpts, gidx, start[row + c[0] - R], start[row + c[0] - R + 1], qx,
-                                                  qy, qz, kd, ki, visits);
-                            if (c[0] + R <= G.g[0] - 1)
-                                scan_range<T, KT>(gpts, gidx, start[row + c[0] + R], start[row + c[0] + R + 1], qx,
-                                                  qy, qz, kd, ki, visits);
-                        }
-                    }
-                }
-              }
-                // lower bound on the distance to any unvisited cell
-                double lb = 1e300;
-                bool any = false;
-                for (int a = 0; a < 3; ++a) {
-                    if (c[a] - R - 1 >= 0) {
-                        const double face = G.lo[a] + (double)(c[a] - R) * G.h;
-                        lb = fmin(lb, q[a] - face);
-                        any = true;
-                    }
-                    if (c[a] + R + 1 <= G.g[a] - 1) {
-                        const double face = G.lo[a] + (double)(c[a] + R + 1) * G.h;
-                        lb = fmin(lb, face - q[a]);
-                        any = true;
-                    }
-                }
-                if (!any) break;  // the whole grid has been visited
-                if (lb > 0.0) {
-                    const double lb2 = lb * lb * margin;
-                    if ((double)kd[KT - 1] < lb2 && ki[KT - 1] != 0x7fffffff) break;
-                    if (lb2 > (double)maxR2) break;
-                }
-            }
-        }
-        for (int s = 0; s < k; ++s) {
-            T d = kd[s];
-            int32_t id = ki[s];
-            if (id == 0x7fffffff || !(d <= maxR2)) {
-                d = (T)__builtin_huge_val();
-                id = -1;
-            }
-            out_d[qi * k + s] = d;
-            out_i[qi * k + s] = id;
-        }
+        bool qnan;
+        cell_of_q(G, q, c, qnan);
+        if (!qnan) lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, kd, ki, visits);
+        write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i);
     }
-    // PointCountTouched: one atomic per wave
-    unsigned long long v = visits;
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if ((threadIdx.x & 63) == 0 && visited) atomicAdd(visited, v);
+    add_visits(visits, visited);
+}
+
+// ------------------------------------------------------------ tile kernel --
+#include "pmx_grid_tile.inc"
+
+template <typename T, int KT>
+static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
+                      const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
+                      T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited, hipStream_t s) {
+    if (mode == 1) {
+        hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
+                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited);
+    } else {
+        const int64_t W = waves ? n_waves : (N + 63) / 64;
+        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
+                           waves, Tm, knn, maxR2, max_pts, dists, ids, visited);
+    }
 }
 
 template <typename T>
-void launch_grid_match(const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo, double h,
-                       const int* g, const P4<T>* rd, const int32_t* order, int64_t N, const Mat4<T>& Tm, int knn,
-                       T maxR2, T* dists, int32_t* ids, unsigned long long* visited, hipStream_t s) {
+void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
+                       double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
+                       const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
+                       unsigned long long* visited, unsigned long long* vout, hipStream_t s) {
     if (N <= 0) return;
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -234,29 +345,45 @@ void launch_grid_match(const P4<T>* gpts, const int32_t* gidx, const uint32_t* s
     }
     G.h = h;
     G.inv_h = 1.0 / h;
-    const dim3 grid((unsigned)((N + 255) / 256));
+#define PMX_KT(KT) \
+    launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, s)
     if (knn == 1)
-        hipLaunchKernelGGL((grid_match_kernel<T, 1>), grid, dim3(256), 0, s, gpts, gidx, start, G, rd, order, N, Tm,
-                           knn, maxR2, dists, ids, visited);
+        PMX_KT(1);
     else if (knn <= 2)
-        hipLaunchKernelGGL((grid_match_kernel<T, 2>), grid, dim3(256), 0, s, gpts, gidx, start, G, rd, order, N, Tm,
-                           knn, maxR2, dists, ids, visited);
+        PMX_KT(2);
     else if (knn <= 4)
-        hipLaunchKernelGGL((grid_match_kernel<T, 4>), grid, dim3(256), 0, s, gpts, gidx, start, G, rd, order, N, Tm,
-                           knn, maxR2, dists, ids, visited);
+        PMX_KT(4);
     else if (knn <= 8)
-        hipLaunchKernelGGL((grid_match_kernel<T, 8>), grid, dim3(256), 0, s, gpts, gidx, start, G, rd, order, N, Tm,
-                           knn, maxR2, dists, ids, visited);
+        PMX_KT(8);
     else
-        hipLaunchKernelGGL((grid_match_kernel<T, 16>), grid, dim3(256), 0, s, gpts, gidx, start, G, rd, order, N,
-                           Tm, knn, maxR2, dists, ids, visited);
+        PMX_KT(16);
+#undef PMX_KT
+    if (visited && vout) hipLaunchKernelGGL(counter_sum_kernel, dim3(1), dim3(kVSlots), 0, s, visited, vout);
 }
 
-template void launch_grid_match<float>(const P4<float>*, const int32_t*, const uint32_t*, const double*, double,
-                                       const int*, const P4<float>*, const int32_t*, int64_t, const Mat4<float>&, int,
-                                       float, float*, int32_t*, unsigned long long*, hipStream_t);
-template void launch_grid_match<double>(const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
-                                        const int*, const P4<double>*, const int32_t*, int64_t, const Mat4<double>&,
-                                        int, double, double*, int32_t*, unsigned long long*, hipStream_t);
+template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, const uint32_t*, const double*, double,
+                                       const int*, const P4<float>*, int64_t, const uint32_t*, int64_t,
+                                       const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
+                                       unsigned long long*, unsigned long long*, hipStream_t);
+template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
+                                        const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
+                                        const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
+                                        unsigned long long*, unsigned long long*, hipStream_t);
+
+// map match ids (grid positions, -1 = none) back to reference indices
+__global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,
+                                    int32_t* __restrict__ out, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int32_t p = pos[i];
+        out[i] = p < 0 ? -1 : gidx[p];
+    }
+}
+void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, int64_t n, hipStream_t s) {
+    if (n <= 0) return;
+    int64_t g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(pos_to_index_kernel, dim3((unsigned)g), dim3(256), 0, s, pos, gidx, out, n);
+}
 
 }  // namespace pmx

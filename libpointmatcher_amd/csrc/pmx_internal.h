@@ -5,9 +5,14 @@
 //              point, padded with +inf points to a multiple of kTile so every
 //              LDS tile load is full and branch-free;
 //   normals    P4<T>[M]      (nx, ny, nz, 0);
-//   reading    P4<T>[N]      already transformed by T_refMean_dataIn;
-//   dists / weights T[N * k], ids int32[N * k], point-major (the memory order
-//              of the reference's column-major k x N Eigen matrices).
+//   grid       the reference (and its normals) sorted by cell, + cell starts;
+//   reading    P4<T>[N]      already transformed by T_refMean_dataIn, in SLOT
+//              order (Morton order of the initial cell; slot -> query index
+//              kept on the host for the mirrors);
+//   dists / weights T[N * k], ids int32[N * k], slot-major (the memory order
+//              of the reference's column-major k x N Eigen matrices, up to the
+//              slot permutation).  ids are reference indices after a brute-
+//              force match and grid positions after a grid match.
 // 2-D clouds (rows = 3) are embedded as (x, y, 0, h) with the 3x3 transform
 // embedded in a 4x4; adding the +0 z-term is exact, so distances equal the
 // 2-D sums bit for bit.
@@ -55,10 +60,16 @@ template <typename T>
 void launch_transform(const P4<T>* in, P4<T>* out, int64_t N, const Mat4<T>& Tm, hipStream_t s);
 
 // ---- grid match (pmx_grid.hip) ----
+// mode 0 = wave-cooperative LDS tiles (default), 1 = per-lane shell search.
+// ids written are positions in gpts; launch_pos_to_index maps them back.
 template <typename T>
-void launch_grid_match(const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo, double h,
-                       const int* g, const P4<T>* rd, const int32_t* order, int64_t N, const Mat4<T>& Tm, int knn,
-                       T maxR2, T* dists, int32_t* ids, unsigned long long* visited, hipStream_t s);
+void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
+                       double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
+                       const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
+                       unsigned long long* vpart, unsigned long long* vout, hipStream_t s);
+// spread pair / fallback counters of the grid kernels (bytes; zero-initialised once)
+size_t grid_counter_bytes();
+void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, int64_t n, hipStream_t s);
 
 // ---- quantile / weights (pmx_select.hip) ----
 enum WeightOp { kWAssign = 0, kWMul = 1 };

@@ -177,12 +177,20 @@ def _worker(rank, world, port, outdir, dtype_name):
 
 @pytest.fixture(scope="module", params=["float32", "float64"])
 def two_rank_results(request, tmp_path_factory):
-    import torch.multiprocessing as mp
+    # plain multiprocessing: the parent never imports torch, so torch's bundled
+    # HIP runtime is not loaded next to the /opt/rocm one libpmx links
+    import multiprocessing as mp
 
     O.build()
     out = tmp_path_factory.mktemp("mr_" + request.param)
-    mp.start_processes(_worker, args=(2, _free_port(), str(out), request.param), nprocs=2, join=True,
-                       start_method="spawn")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(i, 2, port, str(out), request.param)) for i in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     r = [dict(np.load(out / f"rank{i}.npz")) for i in range(2)]
     return np.dtype(request.param), r
 
