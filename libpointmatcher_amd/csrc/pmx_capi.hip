@@ -52,6 +52,7 @@ struct pmx_ctx {
     int grid_mode = 1;            // 1 = per-lane shell search (default), 0 = LDS tiles (PMX_GRID_MODE=tile)
     uint32_t tile_max = 4096;     // largest per-wave box scanned from LDS (PMX_GRID_TILE_MAX)
     bool no_visits = false;       // experiment knob: skip the pair counter (PMX_NO_VISITS)
+    bool select_split = false;    // experiment knob: hist + pick kernels per pass (PMX_SELECT_SPLIT)
     void* d_gpts = nullptr;
     void* d_gnrm = nullptr;       // normals in grid order
     int32_t* d_gidx = nullptr;
@@ -84,10 +85,20 @@ struct pmx_ctx {
     double Tstep[16] = {0};  // step transform (embedded 4x4, T values)
     bool have_match = false;
 
-    // quantile select: SelectState followed by the per-iteration error word
+    // outlier weight chain (WChain): predicates recorded by the filter calls
+    int chain_n = 0;
+    int chain_type[kMaxChain] = {};
+    double chain_thr[kMaxChain] = {};
+    bool w_valid = false;  // d_w holds the chain's weights (mirror only)
+
+    // quantile select: SelectState followed by the per-iteration error word;
+    // chain positions >= 1 use their own states (d_sel_more)
+    SelectState* d_sel_more = nullptr;
+    SelectState* sel_slot(int pos) const { return pos == 0 ? d_sel : d_sel_more + (pos - 1); }
     SelectState* d_sel = nullptr;
     int* d_iter_err = nullptr;
     uint32_t* d_hist = nullptr;
+    unsigned int* d_ticket = nullptr;  // inside the d_hist allocation
     double* d_ratio = nullptr;
 
     // VarTrimmed scratch + cached pow table
@@ -579,9 +590,12 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
     for (int i = 0; i < 16; ++i) c->Tstep[i] = (double)Tm.m[i];
     const T md = (T)maxDist;
     const T maxR2 = md * md;  // libnabo squares the radius in T [ext]
-    // reset the per-iteration error word, VarTrimmed ratio and pair counter
-    // (visited and fallback counters: [kBlkVisited, kBlkVisited + 16))
-    HIPCHK(c, hipMemsetAsync((char*)c->d_result + kBlkIterErr, 0, kBlkVisited + 16 - kBlkIterErr, c->stream));
+    // reset the per-iteration error word and the pair / fallback counters
+    // ([kBlkVisited, kBlkVisited + 16)); the grid match's counter-sum kernel
+    // does both itself, which saves a fill launch per iteration
+    const bool grid = !(c->search_type == 0 || !c->grid_ready);
+    if (!grid || c->no_visits)
+        HIPCHK(c, hipMemsetAsync((char*)c->d_result + kBlkIterErr, 0, kBlkVisited + 16 - kBlkIterErr, c->stream));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = get_event(c);
@@ -598,7 +612,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)c->d_gpts, c->d_gidx, c->d_gstart, c->g_lo, c->g_h,
                              c->g_dim, (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2,
                              c->tile_max, (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart,
-                             c->d_visited, c->stream);
+                             c->d_visited, c->d_iter_err, c->stream);
         if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
         c->ids_grid = true;
@@ -607,21 +621,28 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
     if (e0 && e1) c->ev_pending.emplace_back(e0, e1);
     c->knn = knn;
     c->have_match = true;
+    c->chain_n = 0;  // new matches: the outlier chain starts over
+    c->w_valid = false;
     if (visited) *visited = c->visited_host;
     return PMX_OK;
 }
 
 // ----------------------------------------------------------------- outliers --
 template <typename T>
-int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const double* ratio_dev) {
-    HIPCHK(c, hipMemsetAsync(c->d_sel, 0, sizeof(SelectState), c->stream));
+int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const double* ratio_dev, SelectState* st) {
+    // (no state reset: pass 0 starts a fresh select)
     const int passes = select_passes<T>();
     for (int p = 0; p < passes; ++p) {
-        launch_select_hist<T>(d, n, c->d_hist, c->d_sel, p, c->stream);
-        if (c->comm && c->nranks > 1)
-            NCCLCHK(c, ncclAllReduce(c->d_hist, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), ncclUint32, ncclSum,
-                                     c->comm, c->stream));
-        launch_select_pick<T>(c->d_hist, c->d_sel, p, ratio, ratio_dev, c->stream);
+        if ((c->comm && c->nranks > 1) || c->select_split) {
+            // the histogram is all-reduced between the two halves of a pass
+            launch_select_hist<T>(d, n, c->d_hist, st, p, c->stream);
+            if (c->comm && c->nranks > 1)
+                NCCLCHK(c, ncclAllReduce(c->d_hist, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), ncclUint32,
+                                         ncclSum, c->comm, c->stream));
+            launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, c->stream);
+        } else {
+            launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, c->stream);
+        }
     }
     HIPCHK(c, hipGetLastError());
     return PMX_OK;
@@ -649,44 +670,73 @@ void unpermute(const pmx_ctx* c, const std::vector<V>& src, V* dst, int k) {
     }
 }
 
+// record predicate `pos` of the weight chain (position 0 starts a new chain)
+void chain_set(pmx_ctx* c, int pos, int type, double thr) {
+    c->chain_n = pos + 1;
+    c->chain_type[pos] = type;
+    c->chain_thr[pos] = thr;
+    c->w_valid = false;
+}
+
+template <typename T>
+WChain<T> chain_of(const pmx_ctx* c) {
+    WChain<T> w;
+    if (c->chain_n == 0) {  // no filter applied: the empty chain's default (dist != inf)
+        w.n = 1;
+        w.type[0] = kWPDefault;
+        return w;
+    }
+    w.n = c->chain_n;
+    for (int i = 0; i < c->chain_n; ++i) {
+        w.type[i] = c->chain_type[i];
+        w.thr[i] = (T)c->chain_thr[i];
+        w.st[i] = c->sel_slot(i);
+    }
+    return w;
+}
+
+// OutlierFilters::compute (OutlierFilter.cpp:63-103): filter `chain_pos` of
+// the chain.  Quantile filters resolve their threshold on the device now;
+// the 0/1 weights themselves are evaluated inline by the minimiser.
 template <typename T>
 int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, double p2) {
     int rc = check_match(c);
     if (rc) return rc;
+    if (chain_pos < 0 || chain_pos >= kMaxChain) return fail(c, PMX_E_BAD_PARAM, "outlier chain longer than 8 filters");
+    if (chain_pos > c->chain_n) return fail(c, PMX_E_BAD_PARAM, "outlier chain positions must be consecutive");
     const int64_t n = c->N * c->knn;
     const T* d = (const T*)c->d_dists;
-    T* w = (T*)c->d_w;
-    const int mul = chain_pos > 0;
+    SelectState* slot = c->sel_slot(chain_pos);
     switch (kind) {
-    case 0:  // default: empty chain
-        launch_weights_default<T>(d, w, n, c->stream);
+    case 0:  // default: empty chain, w = (dist != inf)
+        chain_set(c, chain_pos, kWPDefault, 0.0);
         break;
     case 1:  // Null
-        launch_weights_const<T>(w, n, mul, c->stream);
+        chain_set(c, chain_pos, kWPNull, 0.0);
         break;
     case 2: {  // MaxDist: w = d <= maxDist^2 (OutlierFiltersImpl.cpp:66-81)
         if (!(p0 >= 1e-7)) return fail(c, PMX_E_BAD_PARAM, "MaxDistOutlierFilter: maxDist < 1e-7");
         const T m = (T)p0;
         const T m2 = (T)std::pow((double)m, 2.0);
-        launch_weights_cmp<T>(d, w, n, m2, 0, mul, c->stream);
+        chain_set(c, chain_pos, kWPLe, (double)m2);
         break;
     }
     case 3: {  // MinDist: w = d >= minDist^2 (OutlierFiltersImpl.cpp:87-100)
         if (!(p0 >= 1e-7)) return fail(c, PMX_E_BAD_PARAM, "MinDistOutlierFilter: minDist < 1e-7");
         const T m = (T)p0;
         const T m2 = (T)std::pow((double)m, 2.0);
-        launch_weights_cmp<T>(d, w, n, m2, 1, mul, c->stream);
+        chain_set(c, chain_pos, kWPGe, (double)m2);
         break;
     }
     case 4: {  // MedianDist: limit = factor * quantile(0.5)
-        if ((rc = quantile_select<T>(c, d, n, 0.5, nullptr))) return rc;
-        launch_weights_state<T>(d, w, n, c->d_sel, (T)p0, mul, c->stream);
+        if ((rc = quantile_select<T>(c, d, n, 0.5, nullptr, slot))) return rc;
+        chain_set(c, chain_pos, kWPState, (double)(T)p0);
         break;
     }
     case 5: {  // TrimmedDist: limit = quantile(ratio)
         if (!(p0 >= 1e-7 && p0 <= 1.0)) return fail(c, PMX_E_BAD_PARAM, "TrimmedDistOutlierFilter: ratio out of [1e-7, 1]");
-        if ((rc = quantile_select<T>(c, d, n, p0, nullptr))) return rc;
-        launch_weights_state<T>(d, w, n, c->d_sel, (T)1, mul, c->stream);
+        if ((rc = quantile_select<T>(c, d, n, p0, nullptr, slot))) return rc;
+        chain_set(c, chain_pos, kWPState, 1.0);
         break;
     }
     case 6: {  // VarTrimmedDist
@@ -738,8 +788,8 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
         launch_vartrim<T>(dsrc, nsrc, points_nbr, minR, maxR, (const T*)c->d_deno, c->d_vt, c->vt_bytes, c->d_ratio,
                           c->d_iter_err, c->stream);
         HIPCHK(c, hipGetLastError());
-        if ((rc = quantile_select<T>(c, d, n, 0.0, c->d_ratio))) return rc;
-        launch_weights_state<T>(d, w, n, c->d_sel, (T)1, mul, c->stream);
+        if ((rc = quantile_select<T>(c, d, n, 0.0, c->d_ratio, slot))) return rc;
+        chain_set(c, chain_pos, kWPState, 1.0);
         break;
     }
     default:
@@ -792,25 +842,30 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     if (!c->has_normals)
         return fail(c, PMX_E_BAD_PARAM, "PointToPlaneErrorMinimizer requires \"normals\" on the reference");
     const int NF = c->dim == 3 ? 6 : 3;
-    const int NV = NF * NF + NF + 5;
+    const int NS = NF * (NF + 1) / 2;
+    const int NV = p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c),
                               (const P4<T>*)(c->ids_grid ? c->d_gnrm : c->d_nrm), (const T*)c->d_dists, c->d_ids,
-                              (const T*)c->d_w, c->knn, c->N, c->dim, c->d_partials, c->stream);
+                              chain_of<T>(c), c->knn, c->N, c->dim, c->d_partials, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, c->stream);
     HIPCHK(c, hipGetLastError());
     if ((rc = allreduce_f64(c, c->d_result, NV))) return rc;
     if ((rc = readback(c))) return rc;
     const double* r = c->h_result;
     const int ierr = host_iter_err(c);
-    const int o = NF * NF + NF;
-    fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 4], host_limit(c));
+    const int o = NS + NF;
+    // 0/1 weights: sum of kept weights == kept count
+    fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 0], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[o + 1] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
     if (r[o + 0] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
-    for (int i = 0; i < NF * NF; ++i) A[i] = r[i];
-    for (int i = 0; i < NF; ++i) b[i] = -r[NF * NF + i];
+    // mirror the upper triangle (exactly symmetric, see pmx_reduce.hip)
+    int a = 0;
+    for (int i = 0; i < NF; ++i)
+        for (int j = i; j < NF; ++j, ++a) A[i * NF + j] = A[j * NF + i] = r[a];
+    for (int i = 0; i < NF; ++i) b[i] = -r[NS + i];
     return PMX_OK;
 }
 
@@ -819,13 +874,14 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
     int rc = check_match(c);
     if (rc) return rc;
     Mat4<T> Tm = step_mat<T>(c);
+    const WChain<T> chain = chain_of<T>(c);
     launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
-                            (const T*)c->d_w, c->knn, c->N, c->d_partials, c->stream);
+                            chain, c->knn, c->N, c->d_partials, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, c->stream);
     if ((rc = allreduce_f64(c, c->d_result, 11))) return rc;
     launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, c->stream);
     launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
-                            (const T*)c->d_w, c->knn, c->N, (const T*)c->d_means, c->d_partials, c->stream);
+                            chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, c->stream);
     HIPCHK(c, hipGetLastError());
     if ((rc = allreduce_f64(c, c->d_result + 16, 9))) return rc;
@@ -886,6 +942,11 @@ int get_weights_impl(pmx_ctx* c, void* w) {
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
     if (n <= 0) return PMX_OK;
+    if (!c->w_valid) {  // materialise the chain's 0/1 weights
+        launch_weights_chain<T>((const T*)c->d_dists, (T*)c->d_w, n, chain_of<T>(c), c->stream);
+        HIPCHK(c, hipGetLastError());
+        c->w_valid = true;
+    }
     std::vector<T> hw((size_t)n);
     HIPCHK(c, hipMemcpyAsync(hw.data(), c->d_w, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -922,11 +983,17 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_MODE")) c->grid_mode = std::strcmp(e, "tile") == 0 ? 0 : 1;
     if (const char* e = std::getenv("PMX_GRID_TILE_MAX")) c->tile_max = (uint32_t)std::max(0, std::atoi(e));
     c->no_visits = std::getenv("PMX_NO_VISITS") != nullptr;
+    c->select_split = std::getenv("PMX_SELECT_SPLIT") != nullptr;
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
     };
     if (hipSetDevice(device) != hipSuccess) return bad(PMX_E_HIP);
+    if (const char* e = std::getenv("PMX_SYNC")) {  // host wait policy for the per-iteration sync
+        if (std::strcmp(e, "spin") == 0) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+        if (std::strcmp(e, "yield") == 0) (void)hipSetDeviceFlags(hipDeviceScheduleYield);
+        if (std::strcmp(e, "block") == 0) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
@@ -946,10 +1013,14 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     c->d_ratio = (double*)((char*)p + kBlkRatio);
     c->d_visited = (unsigned long long*)((char*)p + kBlkVisited);
     c->d_means = (char*)p + kBlkMeans;
+    if (hipMalloc((void**)&c->d_sel_more, sizeof(SelectState) * (kMaxChain - 1)) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_sel_more, 0, sizeof(SelectState) * (kMaxChain - 1));
     if (hipMalloc((void**)&c->d_vpart, grid_counter_bytes()) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_vpart, 0, grid_counter_bytes());
-    if (hipMalloc((void**)&c->d_hist, 2048 * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
-    (void)hipMemset(c->d_hist, 0, 2048 * sizeof(uint32_t));
+    // 2048 histogram bins, then the fused select pass's ticket counter
+    if (hipMalloc((void**)&c->d_hist, (2048 + 64) * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_hist, 0, (2048 + 64) * sizeof(uint32_t));
+    c->d_ticket = c->d_hist + 2048;
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
     if (hipHostMalloc((void**)&c->h_result, kBlkBytes, hipHostMallocDefault) != hipSuccess) return bad(PMX_E_HIP);
     *out = c;
@@ -962,7 +1033,8 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
-                    c->d_result, c->d_gpts, c->d_gnrm, c->d_gidx, c->d_gstart, c->d_waves, c->d_vpart};
+                    c->d_result, c->d_gpts, c->d_gnrm, c->d_gidx, c->d_gstart, c->d_waves, c->d_vpart,
+                    c->d_sel_more};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_result) (void)hipHostFree(c->h_result);

@@ -257,8 +257,11 @@ __device__ __forceinline__ void add_visits(uint32_t visits, unsigned long long* 
     if ((threadIdx.x & 63) == 0 && vpart && v) atomicAdd(vslot(vpart, 0), v);
 }
 
+// (also clears the iteration's error word: it runs first after the match,
+// before any filter can raise one)
 __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long* __restrict__ vpart,
-                                                              unsigned long long* __restrict__ out) {
+                                                              unsigned long long* __restrict__ out,
+                                                              int* __restrict__ iter_err) {
     __shared__ unsigned long long red[2][kVSlots / 64];
     const int t = threadIdx.x;
     unsigned long long a = vpart[(size_t)t * kVStride], b = vpart[(size_t)(kVSlots + t) * kVStride];
@@ -281,6 +284,7 @@ __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long
         }
         out[0] = sa;
         out[1] = sb;
+        if (iter_err) *iter_err = 0;
     }
 }
 size_t grid_counter_bytes() { return sizeof(unsigned long long) * 2 * kVSlots * kVStride; }
@@ -336,7 +340,7 @@ template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
-                       unsigned long long* visited, unsigned long long* vout, hipStream_t s) {
+                       unsigned long long* visited, unsigned long long* vout, int* iter_err, hipStream_t s) {
     if (N <= 0) return;
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -358,17 +362,18 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     else
         PMX_KT(16);
 #undef PMX_KT
-    if (visited && vout) hipLaunchKernelGGL(counter_sum_kernel, dim3(1), dim3(kVSlots), 0, s, visited, vout);
+    if (visited && vout)
+        hipLaunchKernelGGL(counter_sum_kernel, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err);
 }
 
 template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, const uint32_t*, const double*, double,
                                        const int*, const P4<float>*, int64_t, const uint32_t*, int64_t,
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
-                                       unsigned long long*, unsigned long long*, hipStream_t);
+                                       unsigned long long*, unsigned long long*, int*, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
-                                        unsigned long long*, unsigned long long*, hipStream_t);
+                                        unsigned long long*, unsigned long long*, int*, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

@@ -66,10 +66,59 @@ template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
-                       unsigned long long* vpart, unsigned long long* vout, hipStream_t s);
+                       unsigned long long* vpart, unsigned long long* vout, int* iter_err, hipStream_t s);
 // spread pair / fallback counters of the grid kernels (bytes; zero-initialised once)
 size_t grid_counter_bytes();
 void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, int64_t n, hipStream_t s);
+
+// ---- outlier weights as a predicate chain ----
+// Every supported OutlierFilter produces 0/1 weights and a chain multiplies
+// them (OutlierFilter.cpp:63-103), so the chain is a conjunction of
+// predicates on the distance.  It is evaluated inline by the reductions (no
+// weight array is written or read on the hot path) and materialised only for
+// the host mirror (pmx_get_weights).
+enum WPred { kWPDefault = 0, kWPNull = 1, kWPLe = 2, kWPGe = 3, kWPState = 4 };
+constexpr int kMaxChain = 8;
+template <typename T>
+struct WChain {
+    int n = 0;
+    int type[kMaxChain] = {};
+    T thr[kMaxChain] = {};                        // kWPLe / kWPGe: threshold; kWPState: scale
+    const SelectState* st[kMaxChain] = {};        // kWPState: resolved quantile (limit)
+};
+// per-thread resolved thresholds (kWPState: scale * limit in T, as the
+// reference's `factor * quantile`, OutlierFiltersImpl.cpp:121-122)
+// A conjunction of `d <= t` / `d >= t` / `d != inf` predicates is one
+// interval test: keep = (d != inf if required) && lo <= d && d <= hi with
+// hi = min of the upper thresholds, lo = max of the lower ones.  A NaN
+// threshold (failed quantile) rejects everything, as `d <= NaN` does; the
+// min/max below propagate it.
+template <typename T>
+struct WRange {
+    T lo, hi;
+    bool finite;
+};
+template <typename T>
+__device__ __forceinline__ WRange<T> chain_resolve(const WChain<T>& c) {
+    WRange<T> r{-(T)__builtin_huge_val(), (T)__builtin_huge_val(), false};
+    for (int i = 0; i < c.n; ++i) {  // uniform, once per thread
+        const int t = c.type[i];
+        if (t == kWPDefault) {
+            r.finite = true;
+        } else if (t == kWPGe) {
+            const T v = c.thr[i];
+            r.lo = (v != v || r.lo != r.lo) ? v + r.lo : (v > r.lo ? v : r.lo);
+        } else if (t == kWPLe || t == kWPState) {
+            const T v = t == kWPState ? c.thr[i] * (T)c.st[i]->limit : c.thr[i];
+            r.hi = (v != v || r.hi != r.hi) ? v + r.hi : (v < r.hi ? v : r.hi);
+        }
+    }
+    return r;
+}
+template <typename T>
+__device__ __forceinline__ bool chain_keep(const WRange<T>& r, T d) {
+    return (!r.finite || d != (T)__builtin_huge_val()) && d >= r.lo && d <= r.hi;
+}
 
 // ---- quantile / weights (pmx_select.hip) ----
 enum WeightOp { kWAssign = 0, kWMul = 1 };
@@ -93,7 +142,11 @@ void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState
 // rank from ratio (host value, or *ratio_dev when non-null).
 template <typename T>
 void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
-                        const double* ratio_dev, hipStream_t s);
+                        const double* ratio_dev, int* iter_err, hipStream_t s);
+// hist + pick in one launch (single rank; ticket: zeroed uint32, reset on exit)
+template <typename T>
+void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
+                        const double* ratio_dev, unsigned int* ticket, int* iter_err, hipStream_t s);
 template <typename T>
 int select_passes();
 int select_bins(int pass, int key_bits);
@@ -108,23 +161,26 @@ size_t vartrim_scratch_bytes(int64_t n);
 
 // ---- reductions (pmx_reduce.hip) ----
 constexpr int kRedBlocks = 1024;
-constexpr int kNV3 = 36 + 6 + 5;  // A(36) + b(6) + kept, nz, rejM, rejP, sumw
-constexpr int kNV2 = 9 + 3 + 5;
 constexpr int kNVMax = 48;
+// point-to-plane result layout: upper triangle of A (NS), b (NF), then kept,
+// nonzero weights, rejected matches, rejected points
+constexpr int p2plane_nv(int dim) { return dim == 3 ? 21 + 6 + 4 : 6 + 3 + 4; }
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm,
-                            const T* d, const int32_t* ids, const T* w, int k, int64_t N, int dim,
+                            const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, hipStream_t s);
 void launch_finalize(const double* partials, int nblocks, int nv, double* out, hipStream_t s);
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
-                          const int32_t* ids, const T* w, int k, int64_t N, double* partials,
+                          const int32_t* ids, const WChain<T>& chain, int k, int64_t N, double* partials,
                           hipStream_t s);
 template <typename T>
 void launch_p2point_means(const double* sums, T* means_dev, int dim, hipStream_t s);
 template <typename T>
 void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
-                          const int32_t* ids, const T* w, int k, int64_t N, const T* means_dev,
+                          const int32_t* ids, const WChain<T>& chain, int k, int64_t N, const T* means_dev,
                           double* partials, hipStream_t s);
+template <typename T>
+void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, hipStream_t s);
 
 }  // namespace pmx

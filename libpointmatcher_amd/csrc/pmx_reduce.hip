@@ -6,16 +6,19 @@
 // (ErrorMinimizers/PointToPlane.cpp:171-243, crossProduct
 // ErrorMinimizer.cpp:281-315) and PointToPointErrorMinimizer::compute_in_place
 // (ErrorMinimizers/PointToPoint.cpp:61-81).  Nothing is compacted: each lane
-// walks its points, skips dist == inf, counts w == 0 as a rejected match, and
-// for kept pairs gathers q = ref[id], n = normal[id] and adds the T-precision
-// products of the reference's formulas into fp64 accumulators:
+// walks its slots, evaluates the outlier chain on the distance (weights are
+// 0/1, see WChain), skips dist == inf, counts weight 0 as a rejected match,
+// and for kept pairs gathers q = ref[id], n = normal[id] (grid order after a
+// grid match: coherent) and adds the T-precision products of the reference's
+// formulas into fp64 accumulators:
 //   F = [p x n ; n]  (3-D),  F = [p_x n_y - p_y n_x ; n]  (2-D)
-//   A_rc += (w F_r) F_c      (full matrix: Eigen's wF * F^T is not symmetrised)
-//   b_r  += (w F_r) dot,     dot = ((dx n_x + dy n_y) + dz n_z), d = p - q
-// Per-block partials (fixed 1024-block grid, fixed lane order) are summed by
-// one finalisation block in block order, so results are deterministic.
-// These kernels are HBM/latency-bound: ~60 B per pair (reading 16, dist 4,
-// id 4, weight 4, gathered point 16, gathered normal 16).
+//   A_rc += (w F_r) F_c,   b_r += (w F_r) dot,   dot = ((dx n_x + dy n_y) + dz n_z)
+// With w = 1, (w F_r) F_c == F_r F_c == F_c F_r bit for bit, so Eigen's
+// wF * F^T is exactly symmetric: only the upper triangle (21 / 6 terms) is
+// accumulated and the host mirrors it.  Per-block partials (fixed 1024-block
+// grid, fixed lane order) are summed by finalize_kernel in block order, so
+// results are deterministic.  ~56 B per pair (reading 16, dist 4, id 4,
+// gathered point 16, gathered normal 16).
 #include "pmx_internal.h"
 
 namespace pmx {
@@ -49,19 +52,21 @@ __device__ __forceinline__ void block_store(double (&acc)[NV], double* __restric
         partials[(int64_t)blockIdx.x * NV + v] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
 }
 
+// result layout: [0, NS) upper triangle of A row-major (r <= c), [NS, NS+NF) b,
+// then kept, nonzero weights, rejected matches, rejected points
 template <typename T, int DIM>
 __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
                                                               const P4<T>* __restrict__ ref,
                                                               const P4<T>* __restrict__ nrm, const T* __restrict__ d,
-                                                              const int32_t* __restrict__ ids,
-                                                              const T* __restrict__ w, int k, int64_t N,
-                                                              double* __restrict__ partials) {
+                                                              const int32_t* __restrict__ ids, WChain<T> chain,
+                                                              int k, int64_t N, double* __restrict__ partials) {
     constexpr int NF = DIM == 3 ? 6 : 3;
-    constexpr int NA = NF * NF;
-    constexpr int NV = NA + NF + 5;
+    constexpr int NS = NF * (NF + 1) / 2;
+    constexpr int NV = NS + NF + 4;
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const WRange<T> wr = chain_resolve(chain);
     const T inf = (T)__builtin_huge_val();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
@@ -71,16 +76,15 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
         for (int s = 0; s < k; ++s) {
             const int64_t e = i * k + s;
             const T dv = d[e];
-            const T wv = w[e];
-            if (wv != (T)0) acc[NA + NF + 1] += 1.0;  // (w != 0).count()
+            const bool keep = chain_keep(wr,dv);
+            if (keep) acc[NS + NF + 1] += 1.0;  // (w != 0).count()
             if (dv == inf) continue;
-            if (wv == (T)0) {
-                acc[NA + NF + 2] += 1.0;  // rejected match
+            if (!keep) {
+                acc[NS + NF + 2] += 1.0;  // rejected match
                 continue;
             }
             exist = true;
-            acc[NA + NF + 0] += 1.0;  // kept
-            acc[NA + NF + 4] += (double)wv;
+            acc[NS + NF + 0] += 1.0;  // kept (= sum of the 0/1 weights)
             const int32_t id = ids[e];
             const P4<T> q = ref[id];
             const P4<T> n = nrm[id];
@@ -100,29 +104,29 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                 F[2] = n.y;
                 dot = (px - q.x) * n.x + (py - q.y) * n.y;
             }
+            int a = 0;
 #pragma unroll
             for (int r = 0; r < NF; ++r) {
-                const T wF = wv * F[r];
 #pragma unroll
-                for (int c = 0; c < NF; ++c) acc[r * NF + c] += (double)(wF * F[c]);
-                acc[NA + r] += (double)(wF * dot);
+                for (int c = r; c < NF; ++c) acc[a++] += (double)(F[r] * F[c]);
+                acc[NS + r] += (double)(F[r] * dot);
             }
         }
-        if (!exist) acc[NA + NF + 3] += 1.0;  // rejected point
+        if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
     }
     block_store<NV>(acc, partials);
 }
 
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, const T* d,
-                            const int32_t* ids, const T* w, int k, int64_t N, int dim, double* partials,
+                            const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim, double* partials,
                             hipStream_t s) {
     if (dim == 3)
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
-                           ids, w, k, N, partials);
+                           ids, chain, k, N, partials);
     else
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
-                           ids, w, k, N, partials);
+                           ids, chain, k, N, partials);
 }
 
 // Sum the per-block partials: one block per accumulator, each thread adds a
@@ -150,13 +154,13 @@ void launch_finalize(const double* partials, int nblocks, int nv, double* out, h
 template <typename T>
 __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
                                                             const P4<T>* __restrict__ ref, const T* __restrict__ d,
-                                                            const int32_t* __restrict__ ids,
-                                                            const T* __restrict__ w, int k, int64_t N,
-                                                            double* __restrict__ partials) {
+                                                            const int32_t* __restrict__ ids, WChain<T> chain, int k,
+                                                            int64_t N, double* __restrict__ partials) {
     constexpr int NV = 11;
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const WRange<T> wr = chain_resolve(chain);
     const T inf = (T)__builtin_huge_val();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
@@ -166,23 +170,24 @@ __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restr
         for (int s = 0; s < k; ++s) {
             const int64_t e = i * k + s;
             const T dv = d[e];
-            const T wv = w[e];
-            if (wv != (T)0) acc[8] += 1.0;
+            const bool keep = chain_keep(wr,dv);
+            if (keep) acc[8] += 1.0;
             if (dv == inf) continue;
-            if (wv == (T)0) {
+            if (!keep) {
                 acc[9] += 1.0;
                 continue;
             }
             exist = true;
             acc[7] += 1.0;
             const P4<T> q = ref[ids[e]];
-            acc[0] += (double)wv;
-            acc[1] += (double)(px * wv);
-            acc[2] += (double)(py * wv);
-            acc[3] += (double)(pz * wv);
-            acc[4] += (double)(q.x * wv);
-            acc[5] += (double)(q.y * wv);
-            acc[6] += (double)(q.z * wv);
+            // w = 1: p * w == p exactly
+            acc[0] += 1.0;
+            acc[1] += (double)px;
+            acc[2] += (double)py;
+            acc[3] += (double)pz;
+            acc[4] += (double)q.x;
+            acc[5] += (double)q.y;
+            acc[6] += (double)q.z;
         }
         if (!exist) acc[10] += 1.0;
     }
@@ -191,8 +196,8 @@ __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restr
 
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
-                          const T* w, int k, int64_t N, double* partials, hipStream_t s) {
-    hipLaunchKernelGGL(p2point_pass1_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, w, k, N,
+                          const WChain<T>& chain, int k, int64_t N, double* partials, hipStream_t s) {
+    hipLaunchKernelGGL(p2point_pass1_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, chain, k, N,
                        partials);
 }
 
@@ -217,14 +222,14 @@ void launch_p2point_means(const double* sums, T* means_dev, int dim, hipStream_t
 template <typename T>
 __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
                                                             const P4<T>* __restrict__ ref, const T* __restrict__ d,
-                                                            const int32_t* __restrict__ ids,
-                                                            const T* __restrict__ w, int k, int64_t N,
-                                                            const T* __restrict__ means,
+                                                            const int32_t* __restrict__ ids, WChain<T> chain, int k,
+                                                            int64_t N, const T* __restrict__ means,
                                                             double* __restrict__ partials) {
     constexpr int NV = 9;
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const WRange<T> wr = chain_resolve(chain);
     const T inf = (T)__builtin_huge_val();
     const T mp[3] = {means[0], means[1], means[2]};
     const T mq[3] = {means[3], means[4], means[5]};
@@ -234,8 +239,8 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
         xform3(Tm, rd[i], p[0], p[1], p[2]);
         for (int s = 0; s < k; ++s) {
             const int64_t e = i * k + s;
-            const T wv = w[e];
-            if (d[e] == inf || wv == (T)0) continue;
+            const T dv = d[e];
+            if (dv == inf || !chain_keep(wr,dv)) continue;
             const P4<T> q4 = ref[ids[e]];
             const T q[3] = {q4.x, q4.y, q4.z};
             T pc[3], qc[3];
@@ -246,9 +251,8 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
             }
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-                const T qw = qc[r] * wv;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) acc[r * 3 + c] += (double)(qw * pc[c]);
+                for (int c = 0; c < 3; ++c) acc[r * 3 + c] += (double)(qc[r] * pc[c]);  // (qc * 1) pc
             }
         }
     }
@@ -257,29 +261,40 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
 
 template <typename T>
 void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
-                          const T* w, int k, int64_t N, const T* means_dev, double* partials, hipStream_t s) {
-    hipLaunchKernelGGL(p2point_pass2_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, w, k, N,
+                          const WChain<T>& chain, int k, int64_t N, const T* means_dev, double* partials,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(p2point_pass2_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, chain, k, N,
                        means_dev, partials);
 }
 
-template void launch_p2plane_partial<float>(const P4<float>*, const Mat4<float>&, const P4<float>*,
-                                            const P4<float>*, const float*, const int32_t*, const float*, int,
-                                            int64_t, int, double*, hipStream_t);
-template void launch_p2plane_partial<double>(const P4<double>*, const Mat4<double>&, const P4<double>*,
-                                             const P4<double>*, const double*, const int32_t*, const double*, int,
-                                             int64_t, int, double*, hipStream_t);
-template void launch_p2point_pass1<float>(const P4<float>*, const Mat4<float>&, const P4<float>*, const float*,
-                                          const int32_t*, const float*, int, int64_t, double*, hipStream_t);
-template void launch_p2point_pass1<double>(const P4<double>*, const Mat4<double>&, const P4<double>*,
-                                           const double*, const int32_t*, const double*, int, int64_t, double*,
-                                           hipStream_t);
-template void launch_p2point_means<float>(const double*, float*, int, hipStream_t);
-template void launch_p2point_means<double>(const double*, double*, int, hipStream_t);
-template void launch_p2point_pass2<float>(const P4<float>*, const Mat4<float>&, const P4<float>*, const float*,
-                                          const int32_t*, const float*, int, int64_t, const float*, double*,
-                                          hipStream_t);
-template void launch_p2point_pass2<double>(const P4<double>*, const Mat4<double>&, const P4<double>*,
-                                           const double*, const int32_t*, const double*, int, int64_t,
-                                           const double*, double*, hipStream_t);
+// materialise the chain's 0/1 weights (host mirror only)
+template <typename T>
+__global__ void weights_chain_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n, WChain<T> chain) {
+    const WRange<T> wr = chain_resolve(chain);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        w[i] = chain_keep(wr,d[i]) ? (T)1 : (T)0;
+}
+template <typename T>
+void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, hipStream_t s) {
+    if (n <= 0) return;
+    int64_t g = (n + 1023) / 1024;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(weights_chain_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, w, n, chain);
+}
+
+#define PMX_INST(T)                                                                                                  \
+    template void launch_p2plane_partial<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const P4<T>*, const T*,      \
+                                            const int32_t*, const WChain<T>&, int, int64_t, int, double*,           \
+                                            hipStream_t);                                                             \
+    template void launch_p2point_pass1<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
+                                          const WChain<T>&, int, int64_t, double*, hipStream_t);                     \
+    template void launch_p2point_means<T>(const double*, T*, int, hipStream_t);                                      \
+    template void launch_p2point_pass2<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
+                                          const WChain<T>&, int, int64_t, const T*, double*, hipStream_t);           \
+    template void launch_weights_chain<T>(const T*, T*, int64_t, const WChain<T>&, hipStream_t);
+PMX_INST(float)
+PMX_INST(double)
+#undef PMX_INST
 
 }  // namespace pmx

@@ -20,7 +20,9 @@
 // argmin, then the same radix select with the optimised ratio.
 #include "pmx_internal.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace pmx {
 
@@ -74,64 +76,172 @@ int select_passes<double>() {
 }
 
 // ------------------------------------------------------------- histogram --
+constexpr int kSelPer = 16;  // keys per thread per tile
+
+// kSelPer consecutive values from i0 (16-byte vector loads when the whole run
+// is in range; +inf pads past n and is excluded like any infinite distance)
 template <typename T>
-__global__ __launch_bounds__(256) void select_hist_kernel(const T* __restrict__ d, int64_t n,
-                                                          uint32_t* __restrict__ hist,
-                                                          const SelectState* __restrict__ st, int pass) {
+__device__ __forceinline__ void load_keys(const T* __restrict__ d, int64_t i0, int64_t n, T (&v)[kSelPer]) {
+    if (i0 + kSelPer <= n) {
+        using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+        constexpr int E = 16 / sizeof(T);
+        const V* p = reinterpret_cast<const V*>(d + i0);  // i0 * sizeof(T) is a multiple of 64
+#pragma unroll
+        for (int q = 0; q < kSelPer / E; ++q) {
+            const V x = p[q];
+            const T* xe = reinterpret_cast<const T*>(&x);
+#pragma unroll
+            for (int e = 0; e < E; ++e) v[q * E + e] = xe[e];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kSelPer; ++j) v[j] = i0 + j < n ? d[i0 + j] : (T)__builtin_huge_val();
+    }
+}
+// Block-local histogram of digit `pass` over the keys that match the
+// resolved prefix, flushed into the global histogram with one atomic per
+// non-empty bin.  Pass 0 starts a fresh select (the state is not read).
+template <typename T>
+__device__ __forceinline__ void hist_phase(const T* __restrict__ d, int64_t n, uint32_t* __restrict__ hist,
+                                           const SelectState* __restrict__ st, int pass, uint32_t* lh, int agg) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
-    __shared__ uint32_t lh[2048];
     int shift, bits;
     digit_of(KO::bits, pass, shift, bits);
     const int nb = 1 << bits;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) lh[i] = 0;
     __syncthreads();
-    const bool skip = st->err != 0;
-    const K prefix = (K)st->prefix;
+    const bool skip = pass > 0 && st->err != 0;
+    const K prefix = pass > 0 ? (K)st->prefix : (K)0;
     const int hs = shift + bits;
     if (!skip) {
-        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-            const K k = KO::key(d[i]);
-            if (k >= KO::inf_key) continue;  // +inf (and NaN) excluded, Matches.cpp:71
-            if (pass > 0 && (k >> hs) != prefix) continue;
-            atomicAdd(&lh[(uint32_t)(k >> shift) & (uint32_t)(nb - 1)], 1u);
+        // Neighbouring slots hold neighbouring queries with similar distances,
+        // so the lanes of a wave mostly hit the same few bins: the wave
+        // aggregates equal bins (ballot) and one lane adds the count.
+        // Each thread loads kSelPer consecutive keys at once (vector loads,
+        // all in flight: the pass is latency-bound otherwise).
+        const int lane = threadIdx.x & 63;
+        const int64_t tile = (int64_t)blockDim.x * kSelPer;
+        for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {  // uniform
+            const int64_t i0 = base + (int64_t)threadIdx.x * kSelPer;
+            T v[kSelPer];
+            load_keys<T>(d, i0, n, v);
+#pragma unroll
+            for (int j = 0; j < kSelPer; ++j) {
+                const K k = KO::key(v[j]);
+                int bin = -1;
+                // +inf (and NaN, and the padding past n) excluded, Matches.cpp:71;
+                // later passes keep the resolved prefix
+                if (k < KO::inf_key && (pass == 0 || (k >> hs) == prefix))
+                    bin = (int)((uint32_t)(k >> shift) & (uint32_t)(nb - 1));
+                if (!agg) {
+                    if (bin >= 0) atomicAdd(&lh[bin], 1u);
+                    continue;
+                }
+                unsigned long long todo = __ballot(bin >= 0);
+                while (todo) {  // wave-uniform: one round per distinct bin
+                    const int leader = __builtin_ctzll(todo);
+                    const int lb = __builtin_amdgcn_readlane(bin, leader);  // SGPR, no LDS round trip
+                    const unsigned long long same = __ballot(bin == lb);
+                    if (lane == leader) atomicAdd(&lh[lb], (uint32_t)__popcll(same));
+                    todo &= ~same;
+                }
+            }
         }
     }
     __syncthreads();
+    // flush with returning atomics and wait for the returns: once they are
+    // back the adds are performed at the device coherence point, which is
+    // what the fused pass's ticket relies on (no release fence, which would
+    // write back the whole L2)
+    uint32_t ret = 0;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) {
         const uint32_t c = lh[i];
-        if (c) atomicAdd(&hist[i], c);
+        if (c) ret |= atomicAdd(&hist[i], c);
     }
+    asm volatile("" ::"v"(ret));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void select_hist_kernel(const T* __restrict__ d, int64_t n,
+                                                          uint32_t* __restrict__ hist,
+                                                          const SelectState* __restrict__ st, int pass, int agg) {
+    __shared__ uint32_t lh[2048];
+    hist_phase<T>(d, n, hist, st, pass, lh, agg);
+}
+
+// wave aggregation of equal bins before the LDS atomic (PMX_SELECT_AGG=1: on).
+// Off by default: measured on MI355X (C3, 1M distances) pass 0 takes 11.4 us
+// with plain LDS atomics and 39.7 us aggregated — the distances of
+// neighbouring slots are noisy, so a wave sees ~20-30 distinct bins and the
+// per-bin rounds cost more than the LDS bank conflicts they save.
+static int select_agg() {
+    static const int v = [] {
+        const char* e = std::getenv("PMX_SELECT_AGG");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+// Few blocks: every block flushes its non-empty bins with global atomics, and
+// the first digits of squared distances fall into a handful of bins, so more
+// blocks mostly add same-address atomic traffic.
+static int64_t select_blocks(int64_t n) {
+    static const int64_t cap = [] {
+        const char* e = std::getenv("PMX_SELECT_BLOCKS");  // tuning knob
+        return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)256;
+    }();
+    int64_t g = (n + 256 * kSelPer - 1) / (256 * kSelPer);
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return g;
 }
 
 template <typename T>
 void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass, hipStream_t s) {
-    int64_t g = (n + 256 * 8 - 1) / (256 * 8);
-    if (g < 1) g = 1;
-    if (g > 2048) g = 2048;
-    hipLaunchKernelGGL(select_hist_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, n, hist, st, pass);
+    hipLaunchKernelGGL(select_hist_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
+                       pass, select_agg());
 }
 
 // ------------------------------------------------------------------ pick --
-// one block of 256 threads; each thread owns 8 consecutive bins
-template <typename T>
-__global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__ hist, SelectState* __restrict__ st,
-                                                          int pass, double ratio_host,
-                                                          const double* __restrict__ ratio_dev,
-                                                          int* __restrict__ iter_err, int last) {
+// histogram bin reads/resets; kCoherent: device-scope atomics (the fused pass
+// kernel reads bins other blocks - on other XCDs - have just added to)
+template <bool kCoherent>
+__device__ __forceinline__ uint32_t hbin(uint32_t* h) {
+    // (a fetch-add of 0 is performed where the other blocks' adds were)
+    if constexpr (kCoherent) return __hip_atomic_fetch_add(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *h;
+}
+template <bool kCoherent>
+__device__ __forceinline__ void hzero(uint32_t* h) {
+    if constexpr (kCoherent) {
+        __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *h = 0;
+    }
+}
+
+// one block of 256 threads; each thread owns 8 consecutive bins.  Pass 0
+// starts a fresh select state (count, rank from the ratio, error).
+template <typename T, bool kCoherent>
+__device__ __forceinline__ void pick_phase(uint32_t* __restrict__ hist, SelectState* __restrict__ st, int pass,
+                                           double ratio_host, const double* __restrict__ ratio_dev,
+                                           int* __restrict__ iter_err, int last, unsigned long long* part,
+                                           unsigned long long& s_rank, int& s_err) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
-    __shared__ unsigned long long part[256];
-    __shared__ unsigned long long s_rank;
-    __shared__ int s_err;
     int shift, bits;
     digit_of(KO::bits, pass, shift, bits);
     const int nb = 1 << bits;
     const int per = nb / 256;  // 8 or 4
     const int t = threadIdx.x;
+    // this thread's bins, read once (independent reads, all in flight)
+    uint32_t hv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) hv[j] = j < per ? hbin<kCoherent>(&hist[t * per + j]) : 0u;
     unsigned long long mine = 0;
-    for (int j = 0; j < per; ++j) mine += hist[t * per + j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mine += hv[j];
     part[t] = mine;
     __syncthreads();
     // inclusive scan (Hillis-Steele) over 256 partials
@@ -142,9 +252,10 @@ __global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__
         __syncthreads();
     }
     if (t == 0) {
-        s_err = st->err;
-        if (pass == 0 && s_err == 0) {
+        s_err = pass == 0 ? 0 : st->err;
+        if (pass == 0) {
             const unsigned long long count = part[255];
+            st->err = 0;
             st->count = count;
             st->prefix = 0;
             const T q = ratio_dev ? (T)(*ratio_dev) : (T)ratio_host;
@@ -174,8 +285,10 @@ __global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__
         const unsigned long long excl = t > 0 ? part[t - 1] : 0ull;
         if (rank >= excl && rank < part[t]) {
             unsigned long long cum = excl;
-            for (int j = 0; j < per; ++j) {
-                const unsigned long long c = hist[t * per + j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j >= per) break;
+                const unsigned long long c = hv[j];
                 if (rank < cum + c) {
                     const K digit = (K)(t * per + j);
                     const K prefix = ((K)st->prefix << bits) | digit;
@@ -189,17 +302,60 @@ __global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__
         }
     }
     __syncthreads();
-    for (int j = 0; j < per; ++j) hist[t * per + j] = 0;  // ready for the next pass
+    for (int j = 0; j < per; ++j) hzero<kCoherent>(&hist[t * per + j]);  // ready for the next pass
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__ hist, SelectState* __restrict__ st,
+                                                          int pass, double ratio_host,
+                                                          const double* __restrict__ ratio_dev,
+                                                          int* __restrict__ iter_err, int last) {
+    __shared__ unsigned long long part[256];
+    __shared__ unsigned long long s_rank;
+    __shared__ int s_err;
+    pick_phase<T, false>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err);
+}
+
+// One radix-select pass in one launch (single rank): every block builds and
+// flushes its histogram; the last block to finish (ticket counter) resolves
+// the digit.  Saves a launch per pass and the separate pick kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void select_pass_kernel(const T* __restrict__ d, int64_t n,
+                                                          uint32_t* __restrict__ hist, SelectState* __restrict__ st,
+                                                          int pass, double ratio_host,
+                                                          const double* __restrict__ ratio_dev,
+                                                          int* __restrict__ iter_err, int last,
+                                                          unsigned int* __restrict__ ticket, int agg) {
+    __shared__ uint32_t lh[2048];
+    __shared__ unsigned long long part[256];
+    __shared__ unsigned long long s_rank;
+    __shared__ int s_err;
+    __shared__ bool s_last;
+    hist_phase<T>(d, n, hist, st, pass, lh, agg);
+    __syncthreads();  // every thread's flush has returned
+    if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    // the last block: every other block's flush was performed before its
+    // ticket; the bins are read with device-scope atomics (pick_phase)
+    pick_phase<T, true>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err);
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename T>
 void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio, const double* ratio_dev,
-                        hipStream_t s) {
-    // iter_err lives right after the state (see pmx_capi.hip)
-    int* iter_err = reinterpret_cast<int*>(st + 1);
+                        int* iter_err, hipStream_t s) {
     const int last = pass == select_passes<T>() - 1;
     hipLaunchKernelGGL(select_pick_kernel<T>, dim3(1), dim3(256), 0, s, hist, st, pass, ratio, ratio_dev,
                        iter_err, last);
+}
+
+template <typename T>
+void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
+                        const double* ratio_dev, unsigned int* ticket, int* iter_err, hipStream_t s) {
+    const int last = pass == select_passes<T>() - 1;
+    hipLaunchKernelGGL(select_pass_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
+                       pass, ratio, ratio_dev, iter_err, last, ticket, select_agg());
 }
 
 // ---------------------------------------------------------------- weights --
@@ -503,8 +659,12 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
 // explicit instantiations
 template void launch_select_hist<float>(const float*, int64_t, uint32_t*, const SelectState*, int, hipStream_t);
 template void launch_select_hist<double>(const double*, int64_t, uint32_t*, const SelectState*, int, hipStream_t);
-template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, const double*, hipStream_t);
-template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, hipStream_t);
+template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, const double*, int*, hipStream_t);
+template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, hipStream_t);
+template void launch_select_pass<float>(const float*, int64_t, uint32_t*, SelectState*, int, double, const double*,
+                                        unsigned int*, int*, hipStream_t);
+template void launch_select_pass<double>(const double*, int64_t, uint32_t*, SelectState*, int, double, const double*,
+                                         unsigned int*, int*, hipStream_t);
 template void launch_weights_default<float>(const float*, float*, int64_t, hipStream_t);
 template void launch_weights_default<double>(const double*, double*, int64_t, hipStream_t);
 template void launch_weights_const<float>(float*, int64_t, int, hipStream_t);
