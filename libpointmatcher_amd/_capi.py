@@ -13,7 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(HERE, "lib")
-LIBPMX = os.path.join(LIBDIR, "libpmx.so")
+# PMX_LIB_VARIANT: a kernel-variant build under lib/<variant>/ (tuning
+# experiments through this module only; the host chain links lib/libpmx.so)
+LIBPMX = os.path.join(LIBDIR, os.environ.get("PMX_LIB_VARIANT", ""), "libpmx.so")
 LIBPMX_ICP = os.path.join(LIBDIR, "libpmx_icp.so")
 
 PMX_F32, PMX_F64 = 0, 1

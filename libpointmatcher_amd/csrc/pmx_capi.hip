@@ -33,6 +33,25 @@ constexpr size_t kBlkCopy = 1344;
 constexpr size_t kBlkBytes = 2048;
 static_assert(kBlkIterErr + sizeof(int) <= kBlkRatio, "iteration block layout");
 
+// one resolution of the uniform grid over the reference (pmx_grid.hip)
+struct GridLevel {
+    void* gpts = nullptr;        // P4<T>[valid] sorted by cell (x fastest)
+    void* gnrm = nullptr;        // normals in the same order
+    int32_t* gidx = nullptr;     // original reference index of each position
+    uint32_t* gstart = nullptr;  // first position of each cell, + end
+    double lo[3] = {0, 0, 0};
+    double h = 1.0;
+    int dim[3] = {1, 1, 1};
+    double ppc = 0.0;
+    void release() {
+        for (void* b : {gpts, gnrm, (void*)gidx, (void*)gstart})
+            if (b) (void)hipFree(b);
+        gpts = gnrm = nullptr;
+        gidx = nullptr;
+        gstart = nullptr;
+    }
+};
+
 struct pmx_ctx {
     int device = 0;
     int dtype = PMX_F32;
@@ -53,14 +72,21 @@ struct pmx_ctx {
     uint32_t tile_max = 4096;     // largest per-wave box scanned from LDS (PMX_GRID_TILE_MAX)
     bool no_visits = false;       // experiment knob: skip the pair counter (PMX_NO_VISITS)
     bool select_split = false;    // experiment knob: hist + pick kernels per pass (PMX_SELECT_SPLIT)
-    void* d_gpts = nullptr;
-    void* d_gnrm = nullptr;       // normals in grid order
-    int32_t* d_gidx = nullptr;
-    uint32_t* d_gstart = nullptr;
-    double g_lo[3] = {0, 0, 0};
-    double g_h = 1.0;
-    int g_dim[3] = {1, 1, 1};
+    // Grid levels of increasing cell size (points per occupied cell:
+    // level_ppc, PMX_GRID_LEVELS).  Every level answers exactly; the level of
+    // the next match is chosen from the last match's pair count (adaptive:
+    // converged iterations want small cells, misaligned ones or large k want
+    // large cells, see choose_level).
+    std::vector<GridLevel> levels;
+    std::vector<double> level_ppc{2.0, 4.0, 8.0, 16.0, 32.0, 64.0};
+    int level = 0;      // level of the next grid match
+    int ids_level = 0;  // level whose positions the current match ids are
+    std::vector<double> level_cells;   // last cells-per-query seen at each level
+    std::vector<int64_t> level_seen;   // match count when it was seen (0: never)
+    int64_t match_count = 0;
+    bool adaptive = true;
     bool grid_ready = false;
+    const GridLevel& lv(int i) const { return levels[(size_t)i]; }
     std::vector<int32_t> slot_query;  // slot -> reading index (empty = identity)
     uint32_t* d_waves = nullptr;      // tile-kernel wave table: first slot of each wave (+ N)
     int64_t n_waves = 0;
@@ -262,6 +288,10 @@ static bool finite_pt(const P4<T>& p) {
 }
 
 template <typename T>
+int build_level(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::vector<P4<T>>& nrm,
+                const double lo[3], const double ext[3], double maxe, int64_t valid, double h, GridLevel& out);
+
+template <typename T>
 int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::vector<P4<T>>& nrm) {
     double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
     int64_t valid = 0;
@@ -295,22 +325,42 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::
         }
         return occ;
     };
-    double h = maxe / 64.0;
+    double dim = 3.0, ppc1 = 1.0, h1 = maxe / 128.0;
     if (valid > 0) {
-        const double h0 = maxe / 64.0, h1 = h0 / 2.0;
+        const double h0 = maxe / 64.0;
         const int64_t o0 = std::max<int64_t>(1, occupied(h0));
         const int64_t o1 = std::max<int64_t>(1, occupied(h1));
-        double dim = std::log2((double)o1 / (double)o0);
+        dim = std::log2((double)o1 / (double)o0);
         dim = std::min(3.0, std::max(1.0, dim));
-        const double ppc1 = (double)valid / (double)o1;
-        // points per occupied cell: 2-4 is the measured optimum of the per-lane
-        // search on MI355X (C3: 0.106 ms at 2-4, 0.117 at 6, 0.148 at 1,
-        // 0.19 at 16); PMX_GRID_PPC is the tuning knob
-        double target = 4.0;
-        if (const char* e = std::getenv("PMX_GRID_PPC")) target = std::max(0.5, std::atof(e));
-        h = h1 * std::pow(target / ppc1, 1.0 / dim);
-        h = std::max(h, maxe / 4096.0);
+        ppc1 = (double)valid / (double)o1;
     }
+    for (auto& L : c->levels) L.release();
+    c->levels.clear();
+    c->level = 0;
+    c->match_count = 0;
+    c->level_cells.assign(c->level_ppc.size(), 0.0);
+    c->level_seen.assign(c->level_ppc.size(), 0);
+    for (double target : c->level_ppc) {
+        GridLevel L;
+        int rc = build_level<T>(c, pts, M, nrm, lo, ext, maxe, valid, valid > 0 ? h1 * std::pow(target / ppc1, 1.0 / dim)
+                                                                            : maxe / 64.0,
+                                L);
+        if (rc) {
+            L.release();
+            return rc;
+        }
+        L.ppc = target;
+        c->levels.push_back(L);
+    }
+    c->grid_ready = true;
+    return PMX_OK;
+}
+
+// one level of the grid: cell size h (clamped to the 2^26-cell budget)
+template <typename T>
+int build_level(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::vector<P4<T>>& nrm,
+                const double lo[3], const double ext[3], double maxe, int64_t valid, double h, GridLevel& out) {
+    h = std::max(h, maxe / 4096.0);
     GridShape s = grid_shape(lo, ext, h);
     while (s.cells() > kMaxCells) {
         h *= 1.25;
@@ -334,32 +384,26 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::
         gp[p] = pts[j];
         gi[p] = (int32_t)j;
     }
-    for (void** b : {&c->d_gpts, &c->d_gnrm, (void**)&c->d_gidx, (void**)&c->d_gstart})
-        if (*b) {
-            (void)hipFree(*b);
-            *b = nullptr;
-        }
-    HIPCHK(c, hipMalloc(&c->d_gpts, sizeof(P4<T>) * gp.size()));
-    HIPCHK(c, hipMalloc((void**)&c->d_gidx, sizeof(int32_t) * gi.size()));
-    HIPCHK(c, hipMalloc((void**)&c->d_gstart, sizeof(uint32_t) * start.size()));
-    HIPCHK(c, hipMemcpyAsync(c->d_gpts, gp.data(), sizeof(P4<T>) * gp.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMalloc(&out.gpts, sizeof(P4<T>) * gp.size()));
+    HIPCHK(c, hipMalloc((void**)&out.gidx, sizeof(int32_t) * gi.size()));
+    HIPCHK(c, hipMalloc((void**)&out.gstart, sizeof(uint32_t) * start.size()));
+    HIPCHK(c, hipMemcpyAsync(out.gpts, gp.data(), sizeof(P4<T>) * gp.size(), hipMemcpyHostToDevice, c->stream));
     std::vector<P4<T>> gn;
     if (!nrm.empty()) {
         gn.resize(gp.size());
         for (int64_t p = 0; p < valid; ++p) gn[(size_t)p] = nrm[(size_t)gi[(size_t)p]];
-        HIPCHK(c, hipMalloc(&c->d_gnrm, sizeof(P4<T>) * gn.size()));
-        HIPCHK(c, hipMemcpyAsync(c->d_gnrm, gn.data(), sizeof(P4<T>) * gn.size(), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMalloc(&out.gnrm, sizeof(P4<T>) * gn.size()));
+        HIPCHK(c, hipMemcpyAsync(out.gnrm, gn.data(), sizeof(P4<T>) * gn.size(), hipMemcpyHostToDevice, c->stream));
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_gidx, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_gstart, start.data(), sizeof(uint32_t) * start.size(), hipMemcpyHostToDevice,
+    HIPCHK(c, hipMemcpyAsync(out.gidx, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out.gstart, start.data(), sizeof(uint32_t) * start.size(), hipMemcpyHostToDevice,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int a = 0; a < 3; ++a) {
-        c->g_lo[a] = s.lo[a];
-        c->g_dim[a] = s.g[a];
+        out.lo[a] = s.lo[a];
+        out.dim[a] = s.g[a];
     }
-    c->g_h = s.h;
-    c->grid_ready = true;
+    out.h = s.h;
     return PMX_OK;
 }
 
@@ -392,12 +436,12 @@ std::vector<int32_t> build_order(const pmx_ctx* c, const std::vector<P4<T>>& raw
     waves.clear();
     if (!c->grid_ready || N <= 0) return order;
     if (std::getenv("PMX_GRID_NOORDER")) return order;  // tuning knob: identity slot order
-    GridShape s;
+    GridShape s;  // Morton order over the finest level's cells
     for (int a = 0; a < 3; ++a) {
-        s.lo[a] = c->g_lo[a];
-        s.g[a] = c->g_dim[a];
+        s.lo[a] = c->lv(0).lo[a];
+        s.g[a] = c->lv(0).dim[a];
     }
-    s.h = c->g_h;
+    s.h = c->lv(0).h;
     const bool morton = s.g[0] <= (1 << 21) && s.g[1] <= (1 << 21) && s.g[2] <= (1 << 21);
     std::vector<std::pair<uint64_t, int32_t>> key((size_t)N);
     for (int64_t i = 0; i < N; ++i) {
@@ -609,13 +653,15 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         c->ids_grid = false;
     } else {
         if (e0) (void)hipEventRecord(e0, c->stream);
-        launch_grid_match<T>(c->grid_mode, (const P4<T>*)c->d_gpts, c->d_gidx, c->d_gstart, c->g_lo, c->g_h,
-                             c->g_dim, (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2,
-                             c->tile_max, (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart,
-                             c->d_visited, c->d_iter_err, c->stream);
+        const GridLevel& L = c->lv(c->level);
+        launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
+                             (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
+                             (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
+                             c->d_iter_err, c->stream);
         if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
         c->ids_grid = true;
+        c->ids_level = c->level;
     }
     HIPCHK(c, hipGetLastError());
     if (e0 && e1) c->ev_pending.emplace_back(e0, e1);
@@ -654,7 +700,32 @@ int check_match(pmx_ctx* c) {
 }
 
 // the reference layout the current match ids index
-const void* match_ref(const pmx_ctx* c) { return c->ids_grid ? c->d_gpts : c->d_ref; }
+const void* match_ref(const pmx_ctx* c) { return c->ids_grid ? c->lv(c->ids_level).gpts : c->d_ref; }
+const void* match_nrm(const pmx_ctx* c) { return c->ids_grid ? c->lv(c->ids_level).gnrm : c->d_nrm; }
+
+// Adaptive grid level for the next match, from the pairs this match
+// evaluated per query and per point-per-cell (~ occupied cells visited):
+// beyond ~24 cells the search walked outer shells (misaligned clouds, large
+// k) and the next coarser level is cheaper; below ~5 a finer one is.  Any
+// level gives the identical exact result.
+void choose_level(pmx_ctx* c, uint64_t visited) {
+    if (!c->adaptive || !c->ids_grid || c->levels.size() < 2 || c->N <= 0 || c->knn <= 0) return;
+    const int l = c->ids_level;
+    const double cells = (double)visited / ((double)c->N * c->lv(l).ppc);
+    ++c->match_count;
+    c->level_cells[(size_t)l] = cells;
+    c->level_seen[(size_t)l] = c->match_count;
+    int next = l;
+    if (cells > 32.0 && l + 1 < (int)c->levels.size()) {
+        next = l + 1;  // outer shells dominate: larger cells
+    } else if (cells < 16.0 && l > 0) {
+        // the 3x3x3 block sufficed: smaller cells evaluate fewer pairs, unless
+        // the finer level was just seen walking shells (no ping-pong)
+        const bool recent = c->level_seen[(size_t)l - 1] > 0 && c->match_count - c->level_seen[(size_t)l - 1] <= 3;
+        if (!(recent && c->level_cells[(size_t)l - 1] > 32.0)) next = l - 1;
+    }
+    c->level = next;
+}
 
 // slot-major device array -> query-major host array (the reference's order)
 template <typename V>
@@ -835,6 +906,14 @@ void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double 
     st->fallback_queries = c->visited_host ? 0 : (int64_t)v;
 }
 
+// after a readback: adapt the grid level of the next match
+void after_readback(pmx_ctx* c) {
+    if (c->visited_host || c->no_visits) return;
+    unsigned long long v = 0;
+    std::memcpy(&v, (const char*)c->h_result + kBlkVisited, sizeof(v));
+    choose_level(c, v);
+}
+
 template <typename T>
 int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     int rc = check_match(c);
@@ -846,12 +925,13 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     const int NV = p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c),
-                              (const P4<T>*)(c->ids_grid ? c->d_gnrm : c->d_nrm), (const T*)c->d_dists, c->d_ids,
+                              (const P4<T>*)match_nrm(c), (const T*)c->d_dists, c->d_ids,
                               chain_of<T>(c), c->knn, c->N, c->dim, c->d_partials, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, c->stream);
     HIPCHK(c, hipGetLastError());
     if ((rc = allreduce_f64(c, c->d_result, NV))) return rc;
     if ((rc = readback(c))) return rc;
+    after_readback(c);
     const double* r = c->h_result;
     const int ierr = host_iter_err(c);
     const int o = NS + NF;
@@ -886,6 +966,7 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
     HIPCHK(c, hipGetLastError());
     if ((rc = allreduce_f64(c, c->d_result + 16, 9))) return rc;
     if ((rc = readback(c))) return rc;
+    after_readback(c);
     const double* r = c->h_result;
     const int ierr = host_iter_err(c);
     fill_stats(c, st, r[7], r[8], r[9], r[10], r[0], host_limit(c));
@@ -922,7 +1003,7 @@ int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
         const int32_t* src = c->d_ids;
         if (c->ids_grid) {  // grid positions -> reference indices
             HIPCHK(c, hipMalloc((void**)&d_map, sizeof(int32_t) * n));
-            launch_pos_to_index(c->d_ids, c->d_gidx, d_map, n, c->stream);
+            launch_pos_to_index(c->d_ids, c->lv(c->ids_level).gidx, d_map, n, c->stream);
             HIPCHK(c, hipGetLastError());
             src = d_map;
         }
@@ -980,10 +1061,26 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     c->device = device;
     c->dtype = dtype;
     // tuning knobs (defaults are the measured optimum on MI355X)
-    if (const char* e = std::getenv("PMX_GRID_MODE")) c->grid_mode = std::strcmp(e, "tile") == 0 ? 0 : 1;
+    if (const char* e = std::getenv("PMX_GRID_MODE"))
+        c->grid_mode = std::strcmp(e, "tile") == 0 ? 0 : std::strcmp(e, "octant") == 0 ? 2 : 1;
     if (const char* e = std::getenv("PMX_GRID_TILE_MAX")) c->tile_max = (uint32_t)std::max(0, std::atoi(e));
     c->no_visits = std::getenv("PMX_NO_VISITS") != nullptr;
     c->select_split = std::getenv("PMX_SELECT_SPLIT") != nullptr;
+    // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
+    // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
+    if (const char* e = std::getenv("PMX_GRID_LEVELS")) {
+        std::vector<double> v;
+        for (const char* p = e; *p;) {
+            char* end = nullptr;
+            const double x = std::strtod(p, &end);
+            if (end == p) break;
+            if (x >= 0.25) v.push_back(x);
+            p = *end == ',' ? end + 1 : end;
+        }
+        if (!v.empty()) c->level_ppc = v;
+    }
+    if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
+    if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
@@ -1033,10 +1130,11 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
-                    c->d_result, c->d_gpts, c->d_gnrm, c->d_gidx, c->d_gstart, c->d_waves, c->d_vpart,
+                    c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (auto& L : c->levels) L.release();
     if (c->h_result) (void)hipHostFree(c->h_result);
     for (auto& pr : c->ev_pending) {
         (void)hipEventDestroy(pr.first);

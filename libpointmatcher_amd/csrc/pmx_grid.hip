@@ -111,25 +111,40 @@ __device__ __forceinline__ void consider(const int32_t* __restrict__ gidx, int32
 }
 
 // Scan one contiguous point range of gpts (per-lane search).  Latency-bound:
-// points are fetched eight at a time with independent loads.
+// points are fetched kScanU at a time with independent loads; a short row
+// (a few points at the default density) is one masked chunk — a scalar tail
+// loop would make every point its own dependent round trip.
+#ifndef PMX_SCAN_U
+#define PMX_SCAN_U 4
+#endif
+constexpr int kScanU = PMX_SCAN_U;
+// phase-1 row grouping of the per-lane search (rows per group, points per row)
+#ifndef PMX_P1_G
+#define PMX_P1_G 3
+#endif
+#ifndef PMX_P1_U
+#define PMX_P1_U 4
+#endif
+constexpr int kP1G = PMX_P1_G;
+constexpr int kP1U = PMX_P1_U;
+static_assert(9 % kP1G == 0, "phase-1 groups must tile the nine rows");
 template <typename T, int KT>
 __device__ __forceinline__ void scan_range(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                                            uint32_t a, uint32_t b, T qx, T qy, T qz, T (&kd)[KT],
                                            int32_t (&ki)[KT], uint32_t& visits) {
     visits += b - a;
-    uint32_t j = a;
-    constexpr int U = 8;
-    for (; j + U <= b; j += U) {
+    constexpr int U = kScanU;
+    for (uint32_t j = a; j < b; j += U) {
         P4<T> p[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) p[u] = gpts[j + u];
+        for (int u = 0; u < U; ++u) p[u] = gpts[j + u < b ? j + u : a];  // in-range address either way
         T d[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = gsqd(qx, qy, qz, p[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) consider<T, KT>(gidx, (int32_t)(j + u), d[u], kd, ki);
+        for (int u = 0; u < U; ++u)
+            if (j + u < b) consider<T, KT>(gidx, (int32_t)(j + u), d[u], kd, ki);
     }
-    for (; j < b; ++j) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, gpts[j]), kd, ki);
 }
 
 struct GridGeom {
@@ -145,6 +160,78 @@ __device__ __forceinline__ void cell_of_q(const GridGeom& G, const double q[3], 
         if (!(f == f)) qnan = true;
         c[a] = f < 0.0 ? 0 : (f >= (double)G.g[a] ? G.g[a] - 1 : (int)f);
     }
+}
+
+// Octant search: the 2x2x2 cells nearest to the query (its cell and, per
+// axis, the neighbour on the query's side of the cell centre: 4 rows of 2
+// cells).  Every point outside the block is at least LB = the distance to
+// the block's interior faces (>= h/2) away, so the result is final when it
+// passes the same certification as the shell search; true then.
+template <typename T, int KT>
+__device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
+                                              const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy,
+                                              T qz, const double q[3], const int c[3], T maxR2, T (&kd)[KT],
+                                              int32_t (&ki)[KT], uint32_t& visits) {
+    int b0[3], b1[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double mid = G.lo[a] + ((double)c[a] + 0.5) * G.h;
+        const int o = q[a] >= mid ? c[a] + 1 : c[a] - 1;
+        b0[a] = o < c[a] ? max(o, 0) : c[a];
+        b1[a] = o > c[a] ? min(o, G.g[a] - 1) : c[a];
+    }
+    uint32_t ra[4], rb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int y = (r & 1) ? b1[1] : b0[1], z = (r & 2) ? b1[2] : b0[2];
+        const bool ok = !((r & 1) && b1[1] == b0[1]) && !((r & 2) && b1[2] == b0[2]);  // no duplicate rows
+        const int64_t row = ((int64_t)z * G.g[1] + y) * G.g[0];
+        const uint32_t va = start[row + b0[0]];
+        const uint32_t vb = start[row + b1[0] + 1];
+        ra[r] = ok ? va : 0u;
+        rb[r] = ok ? vb : 0u;
+    }
+    constexpr int U = kP1U;
+    P4<T> p[4][U];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = ra[r] + u;
+            p[r][u] = gpts[j < rb[r] ? j : 0u];  // masked: any in-range address
+        }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = ra[r] + u;
+            if (j < rb[r]) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, p[r][u]), kd, ki);
+        }
+        visits += rb[r] - ra[r];
+        if (ra[r] + U < rb[r]) {
+            uint32_t v0 = 0;
+            scan_range<T, KT>(gpts, gidx, ra[r] + U, rb[r], qx, qy, qz, kd, ki, v0);
+        }
+    }
+    double lb = 1e300;
+    bool any = false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (b0[a] > 0) {
+            lb = fmin(lb, q[a] - (G.lo[a] + (double)b0[a] * G.h));
+            any = true;
+        }
+        if (b1[a] < G.g[a] - 1) {
+            lb = fmin(lb, (G.lo[a] + (double)(b1[a] + 1) * G.h) - q[a]);
+            any = true;
+        }
+    }
+    if (!any) return true;  // the block is the whole grid
+    if (lb > 0.0) {
+        const double lb2 = lb * lb * (1.0 - 1e-5);
+        if (((double)kd[KT - 1] < lb2 && ki[KT - 1] != kNoPos) || lb2 > (double)maxR2) return true;
+    }
+    return false;
 }
 
 // exact shell search for one query (from scratch); kd/ki must be initialised
@@ -171,8 +258,35 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
             ra[r] = ok ? va : 0u;
             rb[r] = ok ? vb : 0u;
         }
+        // The rows are scanned in groups of kP1G: the first kP1U points of
+        // every row of a group are loaded together (one round trip per group
+        // instead of one per row), longer rows finish with chunked scans.
+        constexpr int GR = kP1G, U = kP1U;
 #pragma unroll
-        for (int r = 0; r < 9; ++r) scan_range<T, KT>(gpts, gidx, ra[r], rb[r], qx, qy, qz, kd, ki, visits);
+        for (int g = 0; g < 9; g += GR) {
+            P4<T> p[GR][U];
+#pragma unroll
+            for (int rr = 0; rr < GR; ++rr)
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t j = ra[g + rr] + u;
+                    p[rr][u] = gpts[j < rb[g + rr] ? j : 0u];  // masked: any in-range address
+                }
+#pragma unroll
+            for (int rr = 0; rr < GR; ++rr) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t j = ra[g + rr] + u;
+                    if (j < rb[g + rr]) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, p[rr][u]), kd, ki);
+                }
+                visits += rb[g + rr] - ra[g + rr];
+                uint32_t rest = ra[g + rr] + U;
+                if (rest < rb[g + rr]) {
+                    uint32_t v0 = 0;
+                    scan_range<T, KT>(gpts, gidx, rest, rb[g + rr], qx, qy, qz, kd, ki, v0);
+                }
+            }
+        }
     }
     for (int R = 1;; ++R) {
         if (R >= 2) {
@@ -296,7 +410,7 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
                                                         T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                                        unsigned long long* __restrict__ visited) {
+                                                        unsigned long long* __restrict__ visited, int oct) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t visits = 0;
     if (j < N) {
@@ -313,7 +427,18 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
         int c[3];
         bool qnan;
         cell_of_q(G, q, c, qnan);
-        if (!qnan) lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, kd, ki, visits);
+        if (!qnan) {
+            bool done = false;
+            if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, kd, ki, visits);
+            if (!done) {
+#pragma unroll
+                for (int s = 0; s < KT; ++s) {  // (a k-list must not see the octant's points twice)
+                    kd[s] = (T)__builtin_huge_val();
+                    ki[s] = kNoPos;
+                }
+                lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, kd, ki, visits);
+            }
+        }
         write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i);
     }
     add_visits(visits, visited);
@@ -326,9 +451,9 @@ template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited, hipStream_t s) {
-    if (mode == 1) {
+    if (mode >= 1) {  // 1: shell search, 2: octant block first
         hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
-                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited);
+                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,

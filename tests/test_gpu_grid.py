@@ -15,13 +15,14 @@ pytestmark = pytest.mark.gpu
 # every test runs against each grid kernel: the wave-cooperative LDS tile
 # kernel (default), the same with a tiny box cap (every wave takes the
 # per-lane fallback), and the per-lane shell search alone
-MODES = {"tile": {}, "tile_fallback": {"PMX_GRID_TILE_MAX": "16"}, "lane": {"PMX_GRID_MODE": "lane"}}
+MODES = {"lane": {}, "lane_coarse": {"PMX_GRID_PPC": "32"}, "octant": {"PMX_GRID_MODE": "octant"},
+         "tile": {"PMX_GRID_MODE": "tile"}, "tile_fallback": {"PMX_GRID_MODE": "tile", "PMX_GRID_TILE_MAX": "16"}}
 
 
 @pytest.fixture(autouse=True, params=sorted(MODES))
 def grid_mode(request, monkeypatch):
-    monkeypatch.delenv("PMX_GRID_MODE", raising=False)
-    monkeypatch.delenv("PMX_GRID_TILE_MAX", raising=False)
+    for k in ("PMX_GRID_MODE", "PMX_GRID_TILE_MAX", "PMX_GRID_PPC", "PMX_GRID_LEVELS", "PMX_GRID_ADAPT"):
+        monkeypatch.delenv(k, raising=False)
     for k, v in MODES[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param
@@ -111,6 +112,36 @@ def test_tiny_reference(oracle):
         ref = random_cloud(M, seed=9)
         rd = random_cloud(300, seed=10, scale=3.0)
         check(oracle, ref, rd, np.eye(4, dtype=np.float32), min(2, M))
+
+
+def test_adaptive_levels_stay_exact(oracle, grid_mode):
+    # misaligned steps push the matcher to coarser grid levels, aligned ones
+    # back to the finest: every match in between must equal the oracle's
+    if grid_mode != "lane":
+        pytest.skip("level adaptation is exercised once, with the default kernel")
+    from libpointmatcher_amd.synth import t_gt
+
+    ref, nrm = reference_cloud(100_000)
+    rd = reading_cloud(30_000)
+    ctx = P.Context(0, np.float32)
+    ctx.set_search(1)
+    ctx.set_reference(ref, nrm)
+    ctx.set_reading(rd)
+    th = 0.5
+    Tbad = np.eye(4, dtype=np.float32)
+    Tbad[:3, :3] = [[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]]
+    Tgood = t_gt().astype(np.float32)
+    seen = []
+    for T in [Tbad, Tbad, Tbad, Tgood, Tgood, Tgood, Tbad, Tgood]:
+        ctx.match(T, knn=2)
+        ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
+        _, _, st = ctx.p2plane_system()
+        seen.append(st.visited)
+        d, i = ctx.get_matches()
+        od, oi, _ = oracle.knn(ref, oracle.transform(T, rd), k=2, method="kdtree")
+        assert np.array_equal(d, od) and np.array_equal(i, oi)
+    ctx.close()
+    assert len(set(seen)) > 2  # the level (and so the pair count) did change
 
 
 def test_grid_visits_far_fewer_pairs():
