@@ -160,7 +160,10 @@ template <typename T>
 size_t vartrim_scratch_bytes(int64_t n);
 
 // ---- reductions (pmx_reduce.hip) ----
-constexpr int kRedBlocks = 1024;
+#ifndef PMX_RED_BLOCKS
+#define PMX_RED_BLOCKS 512
+#endif
+constexpr int kRedBlocks = PMX_RED_BLOCKS;  // fixed reduction grid (deterministic sums)
 constexpr int kNVMax = 48;
 // point-to-plane result layout: upper triangle of A (NS), b (NF), then kept,
 // nonzero weights, rejected matches, rejected points

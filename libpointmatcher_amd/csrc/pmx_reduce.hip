@@ -52,6 +52,37 @@ __device__ __forceinline__ void block_store(double (&acc)[NV], double* __restric
         partials[(int64_t)blockIdx.x * NV + v] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
 }
 
+// one kept pair: F and dot in T exactly as PointToPlane.cpp:171-243, the
+// upper triangle of F F^T and F dot added in fp64
+template <typename T, int DIM, int NV>
+__device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz, const P4<T>& q, const P4<T>& n) {
+    constexpr int NF = DIM == 3 ? 6 : 3;
+    constexpr int NS = NF * (NF + 1) / 2;
+    T F[NF];
+    T dot;
+    if (DIM == 3) {
+        F[0] = py * n.z - pz * n.y;
+        F[1] = pz * n.x - px * n.z;
+        F[2] = px * n.y - py * n.x;
+        F[3] = n.x;
+        F[4] = n.y;
+        F[5] = n.z;
+        dot = ((px - q.x) * n.x + (py - q.y) * n.y) + (pz - q.z) * n.z;
+    } else {
+        F[0] = px * n.y - py * n.x;
+        F[1] = n.x;
+        F[2] = n.y;
+        dot = (px - q.x) * n.x + (py - q.y) * n.y;
+    }
+    int a = 0;
+#pragma unroll
+    for (int r = 0; r < NF; ++r) {
+#pragma unroll
+        for (int c = r; c < NF; ++c) acc[a++] += (double)(F[r] * F[c]);
+        acc[NS + r] += (double)(F[r] * dot);
+    }
+}
+
 // result layout: [0, NS) upper triangle of A row-major (r <= c), [NS, NS+NF) b,
 // then kept, nonzero weights, rejected matches, rejected points
 template <typename T, int DIM>
@@ -69,7 +100,50 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
     const WRange<T> wr = chain_resolve(chain);
     const T inf = (T)__builtin_huge_val();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 1) {
+        // k = 1: U slots per round with every load issued up front (the
+        // reduction is latency-bound: slot -> id -> gathered point / normal)
+        constexpr int U = 4;
+        for (; i0 < N; i0 += U * stride) {
+            P4<T> r[U];
+            T dv[U];
+            int32_t id[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t ii = i0 + u * stride;
+                const int64_t jj = ii < N ? ii : i0;
+                r[u] = rd[jj];
+                dv[u] = d[jj];
+                id[u] = ids[jj];
+            }
+            bool kp[U];
+            P4<T> q[U], n[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                kp[u] = i0 + u * stride < N && dv[u] != inf && chain_keep(wr, dv[u]);
+                const int32_t g = kp[u] ? id[u] : 0;  // (position 0 always exists)
+                q[u] = ref[g];
+                n[u] = nrm[g];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (i0 + u * stride >= N) continue;
+                const bool keep = chain_keep(wr, dv[u]);
+                if (keep) acc[NS + NF + 1] += 1.0;                 // (w != 0).count()
+                if (dv[u] != inf && !keep) acc[NS + NF + 2] += 1.0;  // rejected match
+                if (!kp[u]) {
+                    acc[NS + NF + 3] += 1.0;  // rejected point
+                    continue;
+                }
+                acc[NS + NF + 0] += 1.0;
+                T px, py, pz;
+                xform3(Tm, r[u], px, py, pz);
+                p2plane_add<T, DIM, NV>(acc, px, py, pz, q[u], n[u]);
+            }
+        }
+    }
+    for (int64_t i = i0; k != 1 && i < N; i += stride) {
         T px, py, pz;
         xform3(Tm, rd[i], px, py, pz);
         bool exist = false;
@@ -86,31 +160,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
             exist = true;
             acc[NS + NF + 0] += 1.0;  // kept (= sum of the 0/1 weights)
             const int32_t id = ids[e];
-            const P4<T> q = ref[id];
-            const P4<T> n = nrm[id];
-            T F[NF];
-            T dot;
-            if (DIM == 3) {
-                F[0] = py * n.z - pz * n.y;
-                F[1] = pz * n.x - px * n.z;
-                F[2] = px * n.y - py * n.x;
-                F[3] = n.x;
-                F[4] = n.y;
-                F[5] = n.z;
-                dot = ((px - q.x) * n.x + (py - q.y) * n.y) + (pz - q.z) * n.z;
-            } else {
-                F[0] = px * n.y - py * n.x;
-                F[1] = n.x;
-                F[2] = n.y;
-                dot = (px - q.x) * n.x + (py - q.y) * n.y;
-            }
-            int a = 0;
-#pragma unroll
-            for (int r = 0; r < NF; ++r) {
-#pragma unroll
-                for (int c = r; c < NF; ++c) acc[a++] += (double)(F[r] * F[c]);
-                acc[NS + r] += (double)(F[r] * dot);
-            }
+            p2plane_add<T, DIM, NV>(acc, px, py, pz, ref[id], nrm[id]);
         }
         if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
     }
