@@ -38,6 +38,8 @@
  *   PMX_E_NO_POINTS       -> ConvergenceError("ErrorMnimizer: no point to minimize")
  *   PMX_E_EMPTY_QUANTILE  -> ConvergenceError("no outlier to filter")
  *   PMX_E_BAD_PARAM       -> InvalidParameter
+ *   PMX_E_TRANSFORMATION  -> TransformationError (device loop)
+ *   PMX_E_CONVERGENCE     -> ConvergenceError (device loop checkers)
  *   PMX_E_HIP / PMX_E_RCCL / PMX_E_STATE -> std::runtime_error
  */
 #ifndef PMX_H
@@ -58,6 +60,8 @@ enum {
     PMX_E_NO_POINTS = -1,
     PMX_E_EMPTY_QUANTILE = -2,
     PMX_E_BAD_PARAM = -3,
+    PMX_E_TRANSFORMATION = -4, /* device loop: T_iter not rigid */
+    PMX_E_CONVERGENCE = -5,    /* device loop: a checker raised ConvergenceError */
     PMX_E_HIP = -10,
     PMX_E_RCCL = -11,
     PMX_E_STATE = -12,
@@ -163,6 +167,54 @@ int pmx_get_shape(const pmx_ctx* ctx, int64_t* n_local, int* knn);
 int pmx_timing_enable(pmx_ctx* ctx, int on);
 int pmx_timing_read(pmx_ctx* ctx, double* match_ms, int64_t* match_launches, double* other_ms);
 int pmx_sync(pmx_ctx* ctx);
+
+/* ------------------------------------------------- device-resident loop --- */
+/* The ICP loop body (ICP.cpp:371-430) with the step solve, the T_iter update
+ * (ICP.cpp:419) and the transformation checkers (TransformationChecker.cpp,
+ * TransformationCheckersImpl.cpp:45-225) on the device: iterations are
+ * enqueued back to back and the host synchronises once per pmx_loop_run.
+ * Requirements: a grid matcher (pmx_set_search 1/2, per-lane kernel), filters
+ * among default / Null / MaxDist / MinDist / MedianDist / TrimmedDist /
+ * VarTrimmedDist,
+ * PointToPlane (no force2D / force4DOF) or PointToPoint, checkers among
+ * Counter / Differential (smoothLength < 64) / Bound.  Otherwise pmx_loop_begin
+ * returns PMX_E_BAD_PARAM and the caller keeps the per-module calls. */
+enum { PMX_CHECK_COUNTER = 0, PMX_CHECK_DIFFERENTIAL = 1, PMX_CHECK_BOUND = 2 };
+enum { PMX_FILTER_DEFAULT = 0, PMX_FILTER_NULL = 1, PMX_FILTER_MAXDIST = 2, PMX_FILTER_MINDIST = 3,
+       PMX_FILTER_MEDIANDIST = 4, PMX_FILTER_TRIMMED = 5, PMX_FILTER_VARTRIMMED = 6 };
+typedef struct pmx_loop_cfg {
+    int knn;
+    double max_dist;
+    int n_filters;              /* 0: the empty chain's default (dist != inf) */
+    int filter_kind[8];         /* PMX_FILTER_* */
+    double filter_p[8][3];      /* maxDist / minDist / factor / ratio / (minRatio, maxRatio, lambda) */
+    int minimizer;              /* 0 PointToPlane, 1 PointToPoint */
+    int n_checkers;
+    int checker_kind[8];        /* PMX_CHECK_* */
+    double checker_p[8][3];     /* Counter: max; Differential: rot, trans, smoothLength; Bound: rot, trans */
+    int keep_trace;             /* record T_iter of every iteration (pmx_loop_trace) */
+} pmx_loop_cfg;
+typedef struct pmx_loop_status {
+    int iterations;             /* iterations completed (IterationsCount) */
+    int done;                   /* the loop has stopped */
+    int reason;                 /* 1 Counter (MaxNumIterationsReached), 2 Differential, 3 error */
+    int error;                  /* 0 or a PMX_E_* code; pmx_last_error has the reference's message */
+    int64_t point_count_touched;/* sum of the iterations' pair evaluations */
+    pmx_stats last;             /* statistics of the last iteration that reached the minimiser */
+    double T_iter[16];          /* rows x rows */
+    double cond[8][2];          /* checkers' condition variables */
+} pmx_loop_status;
+/* reset the loop: configuration, initial T_iter (rows x rows, T values;
+ * normally the identity) — the checkers' init (ICP.cpp:368-369) */
+int pmx_loop_begin(pmx_ctx* ctx, const pmx_loop_cfg* cfg, const void* T_iter0);
+/* run up to n more iterations (fewer if a checker stops the loop or an error
+ * is raised) and fill *st.  Iterations are enqueued in small batches with one
+ * batch in flight ahead of the host's check of the stop flag.  Returns 0, or
+ * the error the ICP raised (st->error, message in pmx_last_error), or a
+ * HIP / RCCL / state error. */
+int pmx_loop_run(pmx_ctx* ctx, int n, pmx_loop_status* st);
+/* T_iter after each completed iteration (keep_trace): count x rows x rows T */
+int pmx_loop_trace(pmx_ctx* ctx, int first, int count, void* out);
 
 #ifdef __cplusplus
 }

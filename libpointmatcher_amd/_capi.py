@@ -24,6 +24,7 @@ PMX_E_NO_POINTS = -1
 PMX_E_EMPTY_QUANTILE = -2
 PMX_E_BAD_PARAM = -3
 PMX_E_TRANSFORMATION = -4
+PMX_E_CONVERGENCE = -5
 PMX_E_HIP = -10
 PMX_E_RCCL = -11
 PMX_E_STATE = -12
@@ -56,6 +57,26 @@ class Stats(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+# device-resident loop (pmx_loop_*)
+FILTER_KIND = {"default": 0, "NullOutlierFilter": 1, "MaxDistOutlierFilter": 2, "MinDistOutlierFilter": 3,
+               "MedianDistOutlierFilter": 4, "TrimmedDistOutlierFilter": 5, "VarTrimmedDistOutlierFilter": 6}
+CHECK_KIND = {"CounterTransformationChecker": 0, "DifferentialTransformationChecker": 1,
+              "BoundTransformationChecker": 2}
+
+
+class LoopCfg(C.Structure):
+    _fields_ = [("knn", C.c_int), ("max_dist", C.c_double), ("n_filters", C.c_int),
+                ("filter_kind", C.c_int * 8), ("filter_p", (C.c_double * 3) * 8), ("minimizer", C.c_int),
+                ("n_checkers", C.c_int), ("checker_kind", C.c_int * 8), ("checker_p", (C.c_double * 3) * 8),
+                ("keep_trace", C.c_int)]
+
+
+class LoopStatus(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("done", C.c_int), ("reason", C.c_int), ("error", C.c_int),
+                ("point_count_touched", C.c_int64), ("last", Stats), ("T_iter", C.c_double * 16),
+                ("cond", (C.c_double * 2) * 8)]
+
+
 _lib = None
 
 EXPORTS = [
@@ -65,6 +86,7 @@ EXPORTS = [
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
+    "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace",
 ]
 
 
@@ -101,6 +123,9 @@ def lib():
         l.pmx_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_double)]
         l.pmx_sync.argtypes = [C.c_void_p]
+        l.pmx_loop_begin.argtypes = [C.c_void_p, C.POINTER(LoopCfg), C.c_void_p]
+        l.pmx_loop_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(LoopStatus)]
+        l.pmx_loop_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         _lib = l
     return _lib
 
@@ -116,7 +141,7 @@ def _ptr(a):
 def raise_for(code, msg=""):
     if code == PMX_OK:
         return
-    if code in (PMX_E_NO_POINTS, PMX_E_EMPTY_QUANTILE):
+    if code in (PMX_E_NO_POINTS, PMX_E_EMPTY_QUANTILE, PMX_E_CONVERGENCE):
         raise ConvergenceError(msg)
     if code == PMX_E_BAD_PARAM:
         raise InvalidParameter(msg)
@@ -261,3 +286,45 @@ class Context:
 
     def sync(self):
         self._chk(self._l.pmx_sync(self.h))
+
+    # --- device-resident loop
+    def loop_begin(self, knn=1, max_dist=np.inf, filters=(), minimizer="PointToPlaneErrorMinimizer",
+                   checkers=(), T0=None, keep_trace=False):
+        """filters: [(name, params...)], checkers: [(name, params...)] in chain order
+        (Counter: max; Differential: rot, trans, smoothLength; Bound: rot, trans)."""
+        cfg = LoopCfg()
+        cfg.knn = knn
+        cfg.max_dist = float(max_dist)
+        cfg.n_filters = len(filters)
+        for i, (name, *p) in enumerate(filters):
+            cfg.filter_kind[i] = FILTER_KIND[name]
+            for j, v in enumerate(p):
+                cfg.filter_p[i][j] = float(v)
+        cfg.minimizer = 0 if minimizer.startswith("PointToPlane") else 1
+        cfg.n_checkers = len(checkers)
+        for i, (name, *p) in enumerate(checkers):
+            cfg.checker_kind[i] = CHECK_KIND[name]
+            for j, v in enumerate(p):
+                cfg.checker_p[i][j] = float(v)
+        cfg.keep_trace = 1 if keep_trace else 0
+        T0 = self._arr(np.eye(self.rows) if T0 is None else T0)
+        self._loop_keep = cfg
+        self._chk(self._l.pmx_loop_begin(self.h, C.byref(cfg), _ptr(T0)))
+
+    def loop_run(self, n):
+        """Run up to n iterations; returns the status (raises the ICP's exception)."""
+        st = LoopStatus()
+        rc = self._l.pmx_loop_run(self.h, int(n), C.byref(st))
+        self.last_loop_status = st
+        self._chk(rc)
+        return st
+
+    def loop_T(self, st):
+        r = self.rows
+        return np.array(st.T_iter[:r * r], dtype=self.dtype).reshape(r, r)
+
+    def loop_trace(self, first, count):
+        r = self.rows
+        out = np.empty((count, r, r), self.dtype)
+        self._chk(self._l.pmx_loop_trace(self.h, int(first), int(count), _ptr(out)))
+        return out

@@ -168,8 +168,7 @@ int pmx_icp_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, cons
 
 int pmx_icp_iterate(pmx_icp* icp, int n, int* done) {
     return guarded(icp, [&] {
-        bool more = true;
-        for (int i = 0; i < n && more; ++i) more = BOTH(icp, icp->f->step(), icp->d->step());
+        const bool more = BOTH(icp, icp->f->iterate(n), icp->d->iterate(n));
         if (done) *done = more ? 0 : 1;
     });
 }

@@ -14,6 +14,7 @@
 //   compatibility)
 #include "pm_icp.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 
@@ -45,8 +46,12 @@ void Device::check(int rc) const {
     case PMX_E_NO_POINTS:
     case PMX_E_EMPTY_QUANTILE:
         throw ConvergenceError(msg);
+    case PMX_E_CONVERGENCE:
+        throw ConvergenceError(msg);
     case PMX_E_BAD_PARAM:
         throw InvalidParameter(msg);
+    case PMX_E_TRANSFORMATION:
+        throw TransformationError(msg);
     default:
         throw std::runtime_error("pmx error " + std::to_string(rc) + ": " + msg);
     }
@@ -145,6 +150,11 @@ struct KDTreeMatcherGPU : PM<T>::Matcher {
         m.n = n;
         return m;
     }
+    bool loopConfig(pmx_loop_cfg& cfg) const override {
+        cfg.knn = knn;
+        cfg.max_dist = (double)maxDist;
+        return true;
+    }
 };
 
 // ---- outlier filters ------------------------------------------------------
@@ -153,6 +163,10 @@ struct NullOF : PM<T>::OutlierFilter {
     explicit NullOF(const Parametrizable::Parameters&) {}
     void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
         d.check(pmx_outlier_null(d.ctx, pos));
+    }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.filter_kind[pos] = PMX_FILTER_NULL;
+        return true;
     }
 };
 template <typename T>
@@ -166,6 +180,11 @@ struct MaxDistOF : PM<T>::OutlierFilter {
     void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
         d.check(pmx_outlier_maxdist(d.ctx, pos, (double)maxDist));
     }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.filter_kind[pos] = PMX_FILTER_MAXDIST;
+        cfg.filter_p[pos][0] = (double)maxDist;
+        return true;
+    }
 };
 template <typename T>
 struct MinDistOF : PM<T>::OutlierFilter {
@@ -177,6 +196,11 @@ struct MinDistOF : PM<T>::OutlierFilter {
         : PM<T>::OutlierFilter("MinDistOutlierFilter", doc(), p), minDist(this->template get<T>("minDist")) {}
     void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
         d.check(pmx_outlier_mindist(d.ctx, pos, (double)minDist));
+    }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.filter_kind[pos] = PMX_FILTER_MINDIST;
+        cfg.filter_p[pos][0] = (double)minDist;
+        return true;
     }
 };
 template <typename T>
@@ -191,6 +215,11 @@ struct MedianDistOF : PM<T>::OutlierFilter {
     void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
         d.check(pmx_outlier_mediandist(d.ctx, pos, (double)factor));
     }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.filter_kind[pos] = PMX_FILTER_MEDIANDIST;
+        cfg.filter_p[pos][0] = (double)factor;
+        return true;
+    }
 };
 template <typename T>
 struct TrimmedDistOF : PM<T>::OutlierFilter {
@@ -202,6 +231,11 @@ struct TrimmedDistOF : PM<T>::OutlierFilter {
         : PM<T>::OutlierFilter("TrimmedDistOutlierFilter", doc(), p), ratio(this->template get<T>("ratio")) {}
     void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
         d.check(pmx_outlier_trimmed(d.ctx, pos, (double)ratio));
+    }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.filter_kind[pos] = PMX_FILTER_TRIMMED;
+        cfg.filter_p[pos][0] = (double)ratio;
+        return true;
     }
 };
 template <typename T>
@@ -224,40 +258,21 @@ struct VarTrimmedDistOF : PM<T>::OutlierFilter {
     void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
         d.check(pmx_outlier_vartrimmed(d.ctx, pos, (double)minRatio, (double)maxRatio, (double)lambda));
     }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.filter_kind[pos] = PMX_FILTER_VARTRIMMED;
+        cfg.filter_p[pos][0] = (double)minRatio;
+        cfg.filter_p[pos][1] = (double)maxRatio;
+        cfg.filter_p[pos][2] = (double)lambda;
+        return true;
+    }
 };
 
 // ---- error minimisers -----------------------------------------------------
 template <typename T>
 void build_p2plane_transform(int rows, const T* x, std::vector<T>& out) {
-    // PointToPlane.cpp:245-312
+    // PointToPlane.cpp:245-312 (shared with the device loop: pmx_dense.h)
     out.assign((size_t)rows * rows, (T)0);
-    if (rows == 4) {
-        const T z = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
-        const T ang = std::sqrt(z);
-        T axis[3];
-        if (z > (T)0) {
-            const T sq = std::sqrt(z);
-            for (int i = 0; i < 3; ++i) axis[i] = x[i] / sq;
-        } else {
-            for (int i = 0; i < 3; ++i) axis[i] = x[i];
-        }
-        T R[9];
-        dense::angle_axis(ang, axis, R);
-        for (int r = 0; r < 3; ++r) {
-            for (int c = 0; c < 3; ++c) out[r * 4 + c] = R[r * 3 + c];
-            out[r * 4 + 3] = x[3 + r];
-        }
-        out[15] = 1;
-        bool nan = false;
-        for (T v : out)
-            if (v != v) nan = true;
-        if (nan)  // degenerate: identical clouds -> NaN rotation -> identity (PointToPlane.cpp:286-292)
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) out[r * 4 + c] = r == c ? (T)1 : (T)0;
-    } else {
-        const T s = std::sin(x[0]), c = std::cos(x[0]);
-        out = {c, -s, x[1], s, c, x[2], 0, 0, 1};
-    }
+    dense::p2plane_transform(rows, x, out.data());
 }
 
 template <typename T>
@@ -296,6 +311,10 @@ struct PointToPlaneEM : PM<T>::ErrorMinimizer {
         build_p2plane_transform(rows, x, out);
         return out;
     }
+    bool loopConfig(pmx_loop_cfg& cfg) const override {
+        cfg.minimizer = 0;
+        return !force2D && !force4DOF;
+    }
 };
 
 template <typename T>
@@ -308,36 +327,19 @@ struct PointToPointEM : PM<T>::ErrorMinimizer {
         pmx_stats st;
         d.check(pmx_p2point_system(d.ctx, mp, mq, md, &st));
         this->setStats(st);
-        T m[9], U[9], S[3], V[9], R[9] = {}, Vt[9];
+        T m[9], mpT[3], mqT[3];
         for (int i = 0; i < D * D; ++i) m[i] = (T)md[i];
-        dense::jacobi_svd(m, D, U, S, V);
-        for (int r = 0; r < D; ++r)
-            for (int c = 0; c < D; ++c) Vt[r * D + c] = V[c * D + r];
-        auto mul = [&]() {
-            for (int r = 0; r < D; ++r)
-                for (int c = 0; c < D; ++c) {
-                    T s = 0;
-                    for (int k = 0; k < D; ++k) s = s + U[r * D + k] * Vt[k * D + c];
-                    R[r * D + c] = s;
-                }
-        };
-        mul();
-        const T det = D == 3 ? R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
-                                   R[2] * (R[3] * R[7] - R[4] * R[6])
-                             : R[0] * R[3] - R[1] * R[2];
-        if (det < (T)0) {
-            for (int c = 0; c < D; ++c) Vt[(D - 1) * D + c] = -Vt[(D - 1) * D + c];
-            mul();
+        for (int i = 0; i < D; ++i) {
+            mpT[i] = (T)mp[i];
+            mqT[i] = (T)mq[i];
         }
         std::vector<T> out((size_t)rows * rows, (T)0);
-        for (int r = 0; r < D; ++r) {
-            T s = 0;
-            for (int c = 0; c < D; ++c) s = s + R[r * D + c] * (T)mp[c];
-            for (int c = 0; c < D; ++c) out[r * rows + c] = R[r * D + c];
-            out[r * rows + D] = (T)mq[r] - s;
-        }
-        out[D * rows + D] = 1;
+        dense::p2point_transform(rows, m, mpT, mqT, out.data());  // (shared with the device loop)
         return out;
+    }
+    bool loopConfig(pmx_loop_cfg& cfg) const override {
+        cfg.minimizer = 1;
+        return true;
     }
 };
 
@@ -371,6 +373,11 @@ struct CounterTC : PM<T>::TransformationChecker {
             iterate = false;
             throw typename PM<T>::MaxNumIterationsReached();
         }
+    }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.checker_kind[pos] = PMX_CHECK_COUNTER;
+        cfg.checker_p[pos][0] = (double)this->limits[0];
+        return true;
     }
 };
 
@@ -439,6 +446,13 @@ struct DifferentialTC : PM<T>::TransformationChecker {
         if (cv0 != cv0) throw ConvergenceError("abs rotation norm not a number");
         if (cv1 != cv1) throw ConvergenceError("abs translation norm not a number");
     }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.checker_kind[pos] = PMX_CHECK_DIFFERENTIAL;
+        cfg.checker_p[pos][0] = (double)minDiffRotErr;
+        cfg.checker_p[pos][1] = (double)minDiffTransErr;
+        cfg.checker_p[pos][2] = (double)smoothLength;
+        return smoothLength < 64;  // the device history ring
+    }
 };
 
 template <typename T>
@@ -494,6 +508,12 @@ struct BoundTC : PM<T>::TransformationChecker {
                 << this->limits[1];
             throw ConvergenceError(oss.str());
         }
+    }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.checker_kind[pos] = PMX_CHECK_BOUND;
+        cfg.checker_p[pos][0] = (double)maxRotationNorm;
+        cfg.checker_p[pos][1] = (double)maxTranslationNorm;
+        return true;
     }
 };
 
@@ -678,6 +698,7 @@ template <typename T>
 PointMatcher<T>::ICP::ICP(int device) {
     dev.device = device;
     dev.dtype = dtype_of<T>();
+    if (const char* e = std::getenv("PMX_DEVICE_LOOP")) deviceLoop = std::strcmp(e, "0") != 0;
 }
 
 template <typename T>
@@ -754,7 +775,7 @@ template <typename T>
 typename PointMatcher<T>::TransformationParameters PointMatcher<T>::ICP::compute(
     const DataPoints& reading, const DataPoints& reference, const TransformationParameters& T_init) {
     prepare(reading, reference, T_init);
-    while (step()) {
+    while (iterate(1 << 30)) {
     }
     return finish();
 }
@@ -825,6 +846,9 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     transformationCheckers.init(T_iter_, dim, iterate_);
     iterationCount = 0;
     trace.clear();
+    loopMode_ = 0;
+    loopIters_ = 0;
+    loopTouched_ = 0;
     readingPreprocessingDuration = since<T>(t);
     prefilteredReadingPtsCount = reading.n;
     t0_ = std::chrono::steady_clock::now();
@@ -832,6 +856,76 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
 
 template <typename T>
 bool PointMatcher<T>::ICP::step() {
+    return iterate(1);
+}
+
+// every module's device form, or false (ICP.cpp:371-430 then runs through the
+// module calls)
+template <typename T>
+bool PointMatcher<T>::ICP::loopConfig(pmx_loop_cfg& cfg) const {
+    std::memset(&cfg, 0, sizeof(cfg));
+    if (!matcher->loopConfig(cfg) || !errorMinimizer->loopConfig(cfg)) return false;
+    if (outlierFilters.size() > 8 || transformationCheckers.size() > 8) return false;
+    cfg.n_filters = (int)outlierFilters.size();
+    for (size_t i = 0; i < outlierFilters.size(); ++i)
+        if (!outlierFilters[i]->loopConfig(cfg, (int)i)) return false;
+    cfg.n_checkers = (int)transformationCheckers.size();
+    for (size_t i = 0; i < transformationCheckers.size(); ++i)
+        if (!transformationCheckers[i]->loopConfig(cfg, (int)i)) return false;
+    cfg.keep_trace = keepTrace ? 1 : 0;
+    return true;
+}
+
+template <typename T>
+bool PointMatcher<T>::ICP::iterate(int n) {
+    if (!iterate_ || n <= 0) return iterate_;
+    if (loopMode_ == 0) {  // first iterations after prepare: pick the mode
+        loopMode_ = -1;
+        pmx_loop_cfg cfg;
+        if (deviceLoop && loopConfig(cfg)) {
+            const int rc = pmx_loop_begin(dev.ctx, &cfg, T_iter_.data());
+            if (rc == PMX_OK)
+                loopMode_ = 1;
+            else if (rc != PMX_E_BAD_PARAM)  // (BAD_PARAM: a configuration the loop does not take)
+                dev.check(rc);
+        }
+    }
+    if (loopMode_ < 0) {
+        for (int i = 0; i < n && iterate_; ++i) stepModules();
+        return iterate_;
+    }
+    pmx_loop_status st;
+    std::memset(&st, 0, sizeof(st));
+    const int rc = pmx_loop_run(dev.ctx, n, &st);
+    if (rc != PMX_OK && st.error == 0) dev.check(rc);  // HIP / RCCL / state failure
+    // mirror the device loop's state into the modules (what the per-module
+    // calls would have left there)
+    const int dim = rows_;
+    const int64_t fresh = st.iterations - loopIters_;
+    if (keepTrace && fresh > 0) {
+        std::vector<T> buf((size_t)fresh * dim * dim);
+        dev.check(pmx_loop_trace(dev.ctx, (int)loopIters_, (int)fresh, buf.data()));
+        for (int64_t i = 0; i < fresh; ++i)
+            trace.emplace_back(buf.begin() + i * dim * dim, buf.begin() + (i + 1) * dim * dim);
+    }
+    iterationCount += fresh;
+    loopIters_ = st.iterations;
+    matcher->visitCounter += (uint64_t)(st.point_count_touched - loopTouched_);  // MatchersImpl.cpp:98
+    loopTouched_ = st.point_count_touched;
+    if (st.last.kept > 0) errorMinimizer->setStats(st.last);
+    for (size_t i = 0; i < transformationCheckers.size(); ++i) {
+        auto& cv = transformationCheckers[i]->conditionVariables;
+        for (size_t j = 0; j < cv.size() && j < 2; ++j) cv[j] = (T)st.cond[i][j];
+    }
+    for (int i = 0; i < dim * dim; ++i) T_iter_[(size_t)i] = (T)st.T_iter[i];
+    if (st.reason == 1) maxNumIterationsReached = true;
+    if (st.done) iterate_ = false;
+    if (rc != PMX_OK) dev.check(rc);  // the exception the loop raised
+    return iterate_;
+}
+
+template <typename T>
+bool PointMatcher<T>::ICP::stepModules() {
     // one pass of the loop body, ICP.cpp:371-430
     if (!iterate_) return false;
     const int dim = rows_;

@@ -67,6 +67,9 @@ struct PointMatcher {
         uint64_t getVisitCount() const { return visitCounter; }
         virtual void init(Device& dev, const DataPoints& filteredReference) = 0;
         virtual Matches findClosests(Device& dev, const TransformationParameters& T_iter) = 0;
+        // device loop (pmx_loop_*): describe this module in cfg, or return
+        // false to keep the per-module calls (the default for any plugin)
+        virtual bool loopConfig(pmx_loop_cfg&) const { return false; }
     };
 
     // ---------------------------------------------------- OutlierFilter --
@@ -77,6 +80,7 @@ struct PointMatcher {
         // multiply this filter's weights into the device weights
         // (chain_pos 0 assigns) — OutlierFilter.cpp:90-99
         virtual void compute(Device& dev, const Matches& m, int chain_pos) = 0;
+        virtual bool loopConfig(pmx_loop_cfg&, int /*chain_pos*/) const { return false; }
     };
     struct OutlierFilters : std::vector<std::shared_ptr<OutlierFilter>> {
         void compute(Device& dev, const Matches& m);  // OutlierFilter.cpp:63-103
@@ -95,6 +99,7 @@ struct PointMatcher {
         ErrorMinimizer(const std::string& n, const ParametersDoc& d, const Parameters& p) : Parametrizable(n, d, p) {}
         virtual ~ErrorMinimizer() {}
         virtual TransformationParameters compute(Device& dev, int rows) = 0;
+        virtual bool loopConfig(pmx_loop_cfg&) const { return false; }
         T getPointUsedRatio() const { return pointUsedRatio; }
         T getWeightedPointUsedRatio() const { return weightedPointUsedRatio; }
         virtual T getOverlap() const { return weightedPointUsedRatio; }
@@ -111,6 +116,7 @@ struct PointMatcher {
         virtual ~TransformationChecker() {}
         virtual void init(const TransformationParameters& T_, int rows, bool& iterate) = 0;
         virtual void check(const TransformationParameters& T_, int rows, bool& iterate) = 0;
+        virtual bool loopConfig(pmx_loop_cfg&, int /*pos*/) const { return false; }
     };
     struct TransformationCheckers : std::vector<std::shared_ptr<TransformationChecker>> {
         void init(const TransformationParameters& T_, int rows, bool& iterate);
@@ -180,6 +186,13 @@ struct PointMatcher {
         // phases, so a caller can time the iterations alone
         void prepare(const DataPoints& reading, const DataPoints& reference, const TransformationParameters& T_init);
         bool step();                          // one iteration; false when a checker stopped
+        // up to n iterations; false when a checker stopped.  When every module
+        // has a device form (loopConfig) the iterations run as the
+        // device-resident loop (pmx_loop_*: solve, T_iter update and checkers
+        // on the GPU, no host round trip per iteration); PMX_DEVICE_LOOP=0 or
+        // deviceLoop = false keeps the per-module calls.
+        bool iterate(int n);
+        bool deviceLoop = true;
         TransformationParameters finish();    // T_refIn_refMean * T_iter * T_refMean_dataIn
 
         // statistics (Inspector::addStat names, ICP.cpp:305-307, 363-365, 432-436)
@@ -192,6 +205,10 @@ struct PointMatcher {
         bool getMaxNumIterationsReached() const { return maxNumIterationsReached; }
 
       private:
+        bool stepModules();                   // ICP.cpp:371-430 through the module calls
+        bool loopConfig(pmx_loop_cfg& cfg) const;
+        int loopMode_ = 0;                    // 0 undecided, 1 device loop, -1 module calls
+        int64_t loopIters_ = 0, loopTouched_ = 0;
         int rows_ = 0;
         bool iterate_ = false;
         TransformationParameters T_refIn_refMean_, T_refMean_dataIn_, T_iter_;

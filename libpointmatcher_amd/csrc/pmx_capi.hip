@@ -16,10 +16,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <sstream>
 #include <string>
 #include <vector>
 
 #include "../../include/pmx.h"
+#include "pmx_loop.h"
 
 using namespace pmx;
 
@@ -147,6 +149,23 @@ struct pmx_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
 
+    // device-resident loop (pmx_loop.hip)
+    LoopCtl* d_ctl = nullptr;     // control word read by every kernel in loop mode
+    void* d_gdesc = nullptr;      // GridDesc<T>[levels]
+    void* d_loop = nullptr;       // LoopState<T>
+    void* d_loop_T0 = nullptr;    // initial T_iter (upload)
+    void* d_trace = nullptr;      // T_iter per iteration (keep_trace)
+    int64_t trace_cap = 0;        // iterations
+    bool loop_on = false;         // enqueueing loop iterations
+    bool loop_begun = false;
+    pmx_loop_cfg loop_cfg{};
+    LoopCfg loop_dev{};
+    void* h_loop = nullptr;       // pinned: LoopState<T> mirror, then the per-batch stop flags
+    hipEvent_t loop_ev[2] = {nullptr, nullptr};  // end of the batches in flight
+    int64_t loop_issued = 0;      // iterations enqueued since pmx_loop_begin
+    int loop_iters = 0;           // iterations completed (last status)
+    bool loop_done = false;       // the loop has stopped (last status)
+
     // timing of the match kernel
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -177,6 +196,9 @@ int fail(pmx_ctx* c, int code, const std::string& msg) {
     } while (0)
 
 size_t tsize(const pmx_ctx* c) { return c->dtype == PMX_F64 ? 8 : 4; }
+
+// the device loop's control word while iterations are being enqueued
+const LoopCtl* loop_ctl(const pmx_ctx* c) { return c->loop_on ? c->d_ctl : nullptr; }
 
 int ensure(pmx_ctx* c, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes && *p) return PMX_OK;
@@ -352,6 +374,28 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::
         L.ppc = target;
         c->levels.push_back(L);
     }
+    // the device table of levels (the device loop picks the level on the GPU)
+    std::vector<GridDesc<T>> tab(c->levels.size());
+    for (size_t l = 0; l < c->levels.size(); ++l) {
+        const GridLevel& L = c->levels[l];
+        GridDesc<T>& D = tab[l];
+        D.gpts = (const P4<T>*)L.gpts;
+        D.gnrm = (const P4<T>*)L.gnrm;
+        D.gidx = L.gidx;
+        D.start = L.gstart;
+        for (int a = 0; a < 3; ++a) {
+            D.G.lo[a] = L.lo[a];
+            D.G.g[a] = L.dim[a];
+        }
+        D.G.h = L.h;
+        D.G.inv_h = 1.0 / L.h;
+    }
+    if (c->d_gdesc) (void)hipFree(c->d_gdesc);
+    c->d_gdesc = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_gdesc, sizeof(GridDesc<T>) * std::max<size_t>(tab.size(), 1)));
+    HIPCHK(c, hipMemcpyAsync(c->d_gdesc, tab.data(), sizeof(GridDesc<T>) * tab.size(), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     c->grid_ready = true;
     return PMX_OK;
 }
@@ -657,7 +701,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
-                             c->d_iter_err, c->stream);
+                             c->d_iter_err, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
         if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
         c->ids_grid = true;
@@ -681,13 +725,14 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
     for (int p = 0; p < passes; ++p) {
         if ((c->comm && c->nranks > 1) || c->select_split) {
             // the histogram is all-reduced between the two halves of a pass
-            launch_select_hist<T>(d, n, c->d_hist, st, p, c->stream);
+            launch_select_hist<T>(d, n, c->d_hist, st, p, loop_ctl(c), c->stream);
             if (c->comm && c->nranks > 1)
                 NCCLCHK(c, ncclAllReduce(c->d_hist, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), ncclUint32,
                                          ncclSum, c->comm, c->stream));
-            launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, c->stream);
+            launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), c->stream);
         } else {
-            launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, c->stream);
+            launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, loop_ctl(c),
+                                  c->stream);
         }
     }
     HIPCHK(c, hipGetLastError());
@@ -857,7 +902,7 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
         const size_t need = vartrim_scratch_bytes<T>(nsrc);
         if ((rc = ensure(c, &c->d_vt, &c->vt_bytes, need))) return rc;
         launch_vartrim<T>(dsrc, nsrc, points_nbr, minR, maxR, (const T*)c->d_deno, c->d_vt, c->vt_bytes, c->d_ratio,
-                          c->d_iter_err, c->stream);
+                          c->d_iter_err, loop_ctl(c), c->stream);
         HIPCHK(c, hipGetLastError());
         if ((rc = quantile_select<T>(c, d, n, 0.0, c->d_ratio, slot))) return rc;
         chain_set(c, chain_pos, kWPState, 1.0);
@@ -914,6 +959,38 @@ void after_readback(pmx_ctx* c) {
     choose_level(c, v);
 }
 
+// the point-to-plane system into the iteration block (no host sync)
+template <typename T>
+int p2plane_enqueue(pmx_ctx* c) {
+    const int NV = p2plane_nv(c->dim);
+    Mat4<T> Tm = step_mat<T>(c);
+    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const P4<T>*)match_nrm(c),
+                              (const T*)c->d_dists, c->d_ids, chain_of<T>(c), c->knn, c->N, c->dim, c->d_partials,
+                              loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
+    HIPCHK(c, hipGetLastError());
+    return allreduce_f64(c, c->d_result, NV);
+}
+
+// the point-to-point sums, means and cross-covariance (no host sync)
+template <typename T>
+int p2point_enqueue(pmx_ctx* c) {
+    Mat4<T> Tm = step_mat<T>(c);
+    const WChain<T> chain = chain_of<T>(c);
+    const GridDesc<T>* gd = (const GridDesc<T>*)c->d_gdesc;
+    launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
+                            chain, c->knn, c->N, c->d_partials, loop_ctl(c), gd, c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, loop_ctl(c), c->stream);
+    int rc = allreduce_f64(c, c->d_result, 11);
+    if (rc) return rc;
+    launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, loop_ctl(c), c->stream);
+    launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
+                            chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, loop_ctl(c), gd, c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, loop_ctl(c), c->stream);
+    HIPCHK(c, hipGetLastError());
+    return allreduce_f64(c, c->d_result + 16, 9);
+}
+
 template <typename T>
 int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     int rc = check_match(c);
@@ -922,14 +999,7 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
         return fail(c, PMX_E_BAD_PARAM, "PointToPlaneErrorMinimizer requires \"normals\" on the reference");
     const int NF = c->dim == 3 ? 6 : 3;
     const int NS = NF * (NF + 1) / 2;
-    const int NV = p2plane_nv(c->dim);
-    Mat4<T> Tm = step_mat<T>(c);
-    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c),
-                              (const P4<T>*)match_nrm(c), (const T*)c->d_dists, c->d_ids,
-                              chain_of<T>(c), c->knn, c->N, c->dim, c->d_partials, c->stream);
-    launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, c->stream);
-    HIPCHK(c, hipGetLastError());
-    if ((rc = allreduce_f64(c, c->d_result, NV))) return rc;
+    if ((rc = p2plane_enqueue<T>(c))) return rc;
     if ((rc = readback(c))) return rc;
     after_readback(c);
     const double* r = c->h_result;
@@ -953,18 +1023,7 @@ template <typename T>
 int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stats* st) {
     int rc = check_match(c);
     if (rc) return rc;
-    Mat4<T> Tm = step_mat<T>(c);
-    const WChain<T> chain = chain_of<T>(c);
-    launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
-                            chain, c->knn, c->N, c->d_partials, c->stream);
-    launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, c->stream);
-    if ((rc = allreduce_f64(c, c->d_result, 11))) return rc;
-    launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, c->stream);
-    launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
-                            chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, c->stream);
-    launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, c->stream);
-    HIPCHK(c, hipGetLastError());
-    if ((rc = allreduce_f64(c, c->d_result + 16, 9))) return rc;
+    if ((rc = p2point_enqueue<T>(c))) return rc;
     if ((rc = readback(c))) return rc;
     after_readback(c);
     const double* r = c->h_result;
@@ -1032,6 +1091,254 @@ int get_weights_impl(pmx_ctx* c, void* w) {
     HIPCHK(c, hipMemcpyAsync(hw.data(), c->d_w, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     unpermute<T>(c, hw, (T*)w, c->knn);
+    return PMX_OK;
+}
+
+// ------------------------------------------------------------ device loop --
+// pmx_loop_*: whole ICP iterations enqueued back to back (pmx_loop.hip).  The
+// host checks the stop flag once per batch of kLoopBatch iterations while the
+// next batch is already queued, so the GPU never waits for the host; after a
+// stop the queued iterations return at once (every kernel reads LoopCtl.done).
+constexpr int kLoopBatch = 4;
+struct LoopFlag {
+    int iter;
+    int done;
+};
+
+template <typename T>
+LoopFlag* loop_flags(const pmx_ctx* c) {
+    return (LoopFlag*)((char*)c->h_loop + ((sizeof(LoopState<T>) + 63) & ~(size_t)63));
+}
+
+template <typename T>
+int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
+    if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
+    if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
+    if (c->search_type == 0 || !c->grid_ready || c->grid_mode == 0)
+        return fail(c, PMX_E_BAD_PARAM, "device loop: needs the per-lane grid matcher (searchType 1 or 2)");
+    if (cfg->knn < 1 || cfg->knn > 16) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 16] on the GPU path");
+    if (!(cfg->max_dist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
+    if (cfg->n_filters < 0 || cfg->n_filters > kMaxChain)
+        return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 outlier filters");
+    for (int i = 0; i < cfg->n_filters; ++i) {
+        const int k = cfg->filter_kind[i];
+        const double* p = cfg->filter_p[i];
+        if (k < PMX_FILTER_DEFAULT || k > PMX_FILTER_VARTRIMMED || (k == PMX_FILTER_DEFAULT && i != 0))
+            return fail(c, PMX_E_BAD_PARAM, "device loop: unknown outlier filter");
+        if ((k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST) && !(p[0] >= 1e-7))
+            return fail(c, PMX_E_BAD_PARAM, "device loop: distance threshold < 1e-7");
+        if (k == PMX_FILTER_TRIMMED && !(p[0] >= 1e-7 && p[0] <= 1.0))
+            return fail(c, PMX_E_BAD_PARAM, "TrimmedDistOutlierFilter: ratio out of [1e-7, 1]");
+        if (k == PMX_FILTER_VARTRIMMED && !((T)p[0] < (T)p[1]))
+            return fail(c, PMX_E_BAD_PARAM, "VarTrimmedDistOutlierFilter: minRatio should be smaller than maxRatio");
+    }
+    if (cfg->minimizer != 0 && cfg->minimizer != 1) return fail(c, PMX_E_BAD_PARAM, "device loop: unknown minimizer");
+    if (cfg->minimizer == 0 && !c->has_normals)
+        return fail(c, PMX_E_BAD_PARAM, "PointToPlaneErrorMinimizer requires \"normals\" on the reference");
+    if (cfg->n_checkers < 0 || cfg->n_checkers > kMaxCheckers)
+        return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 transformation checkers");
+    for (int i = 0; i < cfg->n_checkers; ++i) {
+        const int k = cfg->checker_kind[i];
+        if (k < PMX_CHECK_COUNTER || k > PMX_CHECK_BOUND)
+            return fail(c, PMX_E_BAD_PARAM, "device loop: unknown transformation checker");
+        const double sl = cfg->checker_p[i][2];
+        if (k == PMX_CHECK_DIFFERENTIAL && !(sl >= 0 && sl < kLoopHist && sl == std::floor(sl)))
+            return fail(c, PMX_E_BAD_PARAM, "device loop: smoothLength must be an integer in [0, 63]");
+    }
+    if (c->levels.size() > (size_t)kMaxLevels) return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 grid levels");
+    LoopCfg d{};
+    d.rows = c->rows;
+    d.minimizer = cfg->minimizer;
+    d.n_checkers = cfg->n_checkers;
+    for (int i = 0; i < cfg->n_checkers; ++i) {
+        d.checker_kind[i] = cfg->checker_kind[i];
+        for (int j = 0; j < 3; ++j) d.checker_p[i][j] = cfg->checker_p[i][j];
+    }
+    d.adaptive = c->adaptive && !c->no_visits ? 1 : 0;
+    d.n_levels = (int)c->levels.size();
+    for (int l = 0; l < d.n_levels; ++l) d.level_ppc[l] = c->lv(l).ppc;
+    d.n_local = c->N;
+    int rc;
+    size_t cap = 0;
+    if (!c->d_loop && (rc = ensure(c, &c->d_loop, &cap, sizeof(LoopState<double>)))) return rc;
+    cap = 0;
+    if (!c->d_loop_T0 && (rc = ensure(c, &c->d_loop_T0, &cap, 16 * sizeof(double)))) return rc;
+    if (!c->h_loop) HIPCHK(c, hipHostMalloc(&c->h_loop, sizeof(LoopState<double>) + 128, hipHostMallocDefault));
+    for (hipEvent_t& e : c->loop_ev)
+        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->loop_cfg = *cfg;
+    c->loop_dev = d;
+    const int rr = c->rows * c->rows;
+    HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, T0, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
+    launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (T0 may be a stack buffer of the caller)
+    c->loop_issued = 0;
+    c->loop_iters = 0;
+    c->loop_done = false;
+    c->loop_begun = true;
+    return PMX_OK;
+}
+
+// trace room for `iters` iterations (the enqueued loop_step kernels hold the
+// old pointer: drain the stream before the old buffer goes)
+template <typename T>
+int loop_trace_room(pmx_ctx* c, int64_t iters) {
+    if (iters <= c->trace_cap && c->d_trace) return PMX_OK;
+    const size_t rb = sizeof(T) * c->rows * c->rows;
+    const int64_t cap = std::max<int64_t>({iters, 2 * c->trace_cap, 64});
+    void* nb = nullptr;
+    HIPCHK(c, hipMalloc(&nb, rb * (size_t)cap));
+    if (c->d_trace) {
+        HIPCHK(c, hipMemcpyAsync(nb, c->d_trace, rb * (size_t)c->trace_cap, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_trace);
+    }
+    c->d_trace = nb;
+    c->trace_cap = cap;
+    return PMX_OK;
+}
+
+// one ICP iteration, device-driven (transform and level from LoopCtl)
+template <typename T>
+int loop_enqueue_iteration(pmx_ctx* c) {
+    const pmx_loop_cfg& cfg = c->loop_cfg;
+    T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
+    for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
+    int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr);
+    if (rc) return rc;
+    if (cfg.n_filters == 0) {
+        if ((rc = outlier_impl<T>(c, 0, 0, 0, 0, 0))) return rc;
+    }
+    for (int i = 0; i < cfg.n_filters; ++i) {
+        const double* p = cfg.filter_p[i];
+        if ((rc = outlier_impl<T>(c, cfg.filter_kind[i], i, p[0], p[1], p[2]))) return rc;
+    }
+    if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c))) return rc;
+    launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
+                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, c->stream);
+    HIPCHK(c, hipGetLastError());
+    return PMX_OK;
+}
+
+template <typename T>
+int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
+    if (!c->loop_begun) return fail(c, PMX_E_STATE, "pmx_loop_begin must be called first");
+    if (n < 0) return fail(c, PMX_E_BAD_PARAM, "negative iteration count");
+    LoopFlag* hf = loop_flags<T>(c);
+    int rc = PMX_OK;
+    int issued = 0, slot = 0;
+    int fly[2], nfly = 0, head = 0;
+    bool stop = c->loop_done;
+    c->loop_on = true;
+    while (!stop && rc == PMX_OK) {
+        while (issued < n && nfly < 2 && rc == PMX_OK) {
+            const int b = std::min(kLoopBatch, n - issued);
+            if (c->loop_cfg.keep_trace && (rc = loop_trace_room<T>(c, c->loop_issued + b))) break;
+            for (int i = 0; i < b && rc == PMX_OK; ++i) rc = loop_enqueue_iteration<T>(c);
+            if (rc) break;
+            c->loop_issued += b;
+            issued += b;
+            hipError_t e = hipMemcpyAsync(&hf[slot], (char*)c->d_loop + offsetof(LoopState<T>, iter), sizeof(LoopFlag),
+                                          hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipEventRecord(c->loop_ev[slot], c->stream);
+            if (e != hipSuccess) {
+                rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
+                break;
+            }
+            fly[(head + nfly) % 2] = slot;
+            ++nfly;
+            slot ^= 1;
+        }
+        if (rc || nfly == 0) break;
+        const int s = fly[head];
+        head = (head + 1) % 2;
+        --nfly;
+        const hipError_t e = hipEventSynchronize(c->loop_ev[s]);
+        if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
+        if (hf[s].done) stop = true;
+    }
+    c->loop_on = false;
+    if (rc) {
+        (void)hipStreamSynchronize(c->stream);
+        return rc;
+    }
+    // the final state, the iteration block (limit, counters) and the control word
+    HIPCHK(c, hipMemcpyAsync(c->h_loop, c->d_loop, sizeof(LoopState<T>), hipMemcpyDeviceToHost, c->stream));
+    LoopCtl ctl{};
+    HIPCHK(c, hipMemcpyAsync(&ctl, c->d_ctl, sizeof(LoopCtl), hipMemcpyDeviceToHost, c->stream));
+    if ((rc = readback(c))) return rc;
+    const LoopState<T>& S = *(const LoopState<T>*)c->h_loop;
+    c->loop_iters = S.iter;
+    c->loop_done = S.done != 0;
+    c->level = ctl.level;
+    c->ids_level = S.last_level;
+    // map the device error to the reference's exception and message
+    int err = 0;
+    std::string msg;
+    if (S.err) {
+        const int e = S.err;
+        if (e == kLoopNoPoints) {
+            err = PMX_E_NO_POINTS;
+            msg = "ErrorMnimizer: no point to minimize";
+        } else if (e == PMX_E_EMPTY_QUANTILE) {
+            err = PMX_E_EMPTY_QUANTILE;
+            msg = "no outlier to filter";
+        } else if (e == kLoopNotRigid) {
+            err = PMX_E_TRANSFORMATION;
+            msg = "RigidTransformation: Error, rotation matrix is not orthogonal.";
+        } else if (e == kLoopRotNaN) {
+            err = PMX_E_CONVERGENCE;
+            msg = "abs rotation norm not a number";
+        } else if (e == kLoopTransNaN) {
+            err = PMX_E_CONVERGENCE;
+            msg = "abs translation norm not a number";
+        } else if (e == kLoopBound) {
+            err = PMX_E_CONVERGENCE;
+            // TransformationCheckersImpl.cpp:215-222 (the first bound exceeded)
+            for (int i = 0; i < c->loop_cfg.n_checkers; ++i) {
+                if (c->loop_cfg.checker_kind[i] != PMX_CHECK_BOUND) continue;
+                const T l0 = (T)c->loop_cfg.checker_p[i][0], l1 = (T)c->loop_cfg.checker_p[i][1];
+                if (S.cond[i][0] > l0 || S.cond[i][1] > l1) {
+                    std::ostringstream oss;
+                    oss << "limit out of bounds: rot: " << S.cond[i][0] << "/" << l0 << " tr: " << S.cond[i][1] << "/"
+                        << l1;
+                    msg = oss.str();
+                    break;
+                }
+            }
+        } else {
+            err = e;
+            msg = "quantile must be between 0 and 1";
+        }
+        c->err = msg;
+    }
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->iterations = S.iter;
+        st->done = S.done;
+        st->reason = S.reason;
+        st->error = err;
+        st->point_count_touched = (int64_t)S.touched;
+        fill_stats(c, &st->last, S.kept, S.nz, S.rejM, S.rejP, S.sw, host_limit(c));
+        st->last.visited = (int64_t)S.last_visited;
+        const int rr = c->rows * c->rows;
+        for (int i = 0; i < rr; ++i) st->T_iter[i] = (double)S.Titer[i];
+        for (int i = 0; i < kMaxCheckers; ++i)
+            for (int j = 0; j < 2; ++j) st->cond[i][j] = (double)S.cond[i][j];
+    }
+    return err;
+}
+
+template <typename T>
+int loop_trace_impl(pmx_ctx* c, int first, int count, void* out) {
+    if (!c->loop_begun || !c->loop_cfg.keep_trace) return fail(c, PMX_E_STATE, "no loop trace (keep_trace = 0)");
+    if (first < 0 || count < 0 || first + count > c->loop_iters)
+        return fail(c, PMX_E_BAD_PARAM, "trace range beyond the completed iterations");
+    if (count == 0) return PMX_OK;
+    const size_t rb = sizeof(T) * c->rows * c->rows;
+    HIPCHK(c, hipMemcpyAsync(out, (const char*)c->d_trace + rb * first, rb * count, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return PMX_OK;
 }
 
@@ -1120,6 +1427,9 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     c->d_ticket = c->d_hist + 2048;
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
     if (hipHostMalloc((void**)&c->h_result, kBlkBytes, hipHostMallocDefault) != hipSuccess) return bad(PMX_E_HIP);
+    // the device loop's control word (done = 0: kernels given it run normally)
+    if (hipMalloc((void**)&c->d_ctl, sizeof(LoopCtl)) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_ctl, 0, sizeof(LoopCtl));
     *out = c;
     return PMX_OK;
 }
@@ -1131,11 +1441,14 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
-                    c->d_sel_more};
+                    c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();
     if (c->h_result) (void)hipHostFree(c->h_result);
+    if (c->h_loop) (void)hipHostFree(c->h_loop);
+    for (hipEvent_t e : c->loop_ev)
+        if (e) (void)hipEventDestroy(e);
     for (auto& pr : c->ev_pending) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -1258,6 +1571,23 @@ int pmx_sync(pmx_ctx* c) {
     if (!c) return PMX_E_BAD_PARAM;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PMX_OK;
+}
+
+int pmx_loop_begin(pmx_ctx* c, const pmx_loop_cfg* cfg, const void* T0) {
+    if (!c || !cfg || !T0) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c, loop_begin_impl<float>(c, cfg, (const float*)T0), loop_begin_impl<double>(c, cfg, (const double*)T0));
+}
+
+int pmx_loop_run(pmx_ctx* c, int n, pmx_loop_status* st) {
+    if (!c) return PMX_E_BAD_PARAM;
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c, loop_run_impl<float>(c, n, st), loop_run_impl<double>(c, n, st));
+}
+
+int pmx_loop_trace(pmx_ctx* c, int first, int count, void* out) {
+    if (!c || (!out && count > 0)) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return DISPATCH(c, loop_trace_impl<float>(c, first, count, out), loop_trace_impl<double>(c, first, count, out));
 }
 
 }  // extern "C"

@@ -147,12 +147,6 @@ __device__ __forceinline__ void scan_range(const P4<T>* __restrict__ gpts, const
     }
 }
 
-struct GridGeom {
-    double lo[3];
-    double h, inv_h;
-    int g[3];
-};
-
 __device__ __forceinline__ void cell_of_q(const GridGeom& G, const double q[3], int c[3], bool& qnan) {
     qnan = false;
     for (int a = 0; a < 3; ++a) {
@@ -375,8 +369,10 @@ __device__ __forceinline__ void add_visits(uint32_t visits, unsigned long long* 
 // before any filter can raise one)
 __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long* __restrict__ vpart,
                                                               unsigned long long* __restrict__ out,
-                                                              int* __restrict__ iter_err) {
+                                                              int* __restrict__ iter_err,
+                                                              const LoopCtl* __restrict__ ctl) {
     __shared__ unsigned long long red[2][kVSlots / 64];
+    if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     unsigned long long a = vpart[(size_t)t * kVStride], b = vpart[(size_t)(kVSlots + t) * kVStride];
     vpart[(size_t)t * kVStride] = 0;  // ready for the next match
@@ -410,7 +406,18 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
                                                         T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                                        unsigned long long* __restrict__ visited, int oct) {
+                                                        unsigned long long* __restrict__ visited, int oct,
+                                                        const LoopCtl* __restrict__ ctl,
+                                                        const GridDesc<T>* __restrict__ gd) {
+    if (ctl) {  // device loop: transform and level from the device
+        if (ctl->done) return;
+        const GridDesc<T>& D = gd[ctl->level];
+        gpts = D.gpts;
+        gidx = D.gidx;
+        start = D.start;
+        G = D.G;
+        ctl_transform(ctl, Tm);
+    }
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t visits = 0;
     if (j < N) {
@@ -450,10 +457,11 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
 template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
-                      T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited, hipStream_t s) {
+                      T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
+                      const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
     if (mode >= 1) {  // 1: shell search, 2: octant block first
         hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
-                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0);
+                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ctl, gd);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -465,7 +473,8 @@ template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
-                       unsigned long long* visited, unsigned long long* vout, int* iter_err, hipStream_t s) {
+                       unsigned long long* visited, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
+                       const GridDesc<T>* gd, hipStream_t s) {
     if (N <= 0) return;
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -475,7 +484,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.h = h;
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
-    launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, s)
+    launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
+                     ctl, gd, s)
     if (knn == 1)
         PMX_KT(1);
     else if (knn <= 2)
@@ -488,17 +498,19 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
         PMX_KT(16);
 #undef PMX_KT
     if (visited && vout)
-        hipLaunchKernelGGL(counter_sum_kernel, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err);
+        hipLaunchKernelGGL(counter_sum_kernel, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl);
 }
 
 template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, const uint32_t*, const double*, double,
                                        const int*, const P4<float>*, int64_t, const uint32_t*, int64_t,
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
-                                       unsigned long long*, unsigned long long*, int*, hipStream_t);
+                                       unsigned long long*, unsigned long long*, int*, const LoopCtl*,
+                                       const GridDesc<float>*, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
-                                        unsigned long long*, unsigned long long*, int*, hipStream_t);
+                                        unsigned long long*, unsigned long long*, int*, const LoopCtl*,
+                                        const GridDesc<double>*, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

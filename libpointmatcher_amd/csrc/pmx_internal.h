@@ -59,14 +59,49 @@ int64_t match_part_elems(int64_t N, int64_t M_pad, int knn, int cu_count);
 template <typename T>
 void launch_transform(const P4<T>* in, P4<T>* out, int64_t N, const Mat4<T>& Tm, hipStream_t s);
 
+// ---- grid levels and the device-resident loop ----
+struct GridGeom {
+    double lo[3];
+    double h, inv_h;
+    int g[3];
+};
+// one grid level as the kernels see it (device table, indexed by LoopCtl::level)
+template <typename T>
+struct GridDesc {
+    const P4<T>* gpts;
+    const P4<T>* gnrm;
+    const int32_t* gidx;
+    const uint32_t* start;
+    GridGeom G;
+};
+// Per-context control word of the device-resident ICP loop (pmx_loop.hip):
+// every kernel of an enqueued iteration reads it first.  done != 0 makes the
+// kernels of the iterations enqueued past convergence return at once; T is
+// the step transform (embedded 4x4, T values) and level the grid level of
+// this iteration's match, both written by the previous iteration's step.
+struct LoopCtl {
+    int done;
+    int level;
+    int pad[2];
+    double T[16];
+};
+template <typename T>
+__device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Tm.m[i] = (T)ctl->T[i];
+}
+
 // ---- grid match (pmx_grid.hip) ----
-// mode 0 = wave-cooperative LDS tiles (default), 1 = per-lane shell search.
-// ids written are positions in gpts; launch_pos_to_index maps them back.
+// mode 0 = wave-cooperative LDS tiles, 1 = per-lane shell search (default),
+// 2 = octant block first.  ids written are positions in gpts;
+// launch_pos_to_index maps them back.  ctl / gd (device loop, modes 1-2):
+// transform and level are read on the device.
 template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
-                       unsigned long long* vpart, unsigned long long* vout, int* iter_err, hipStream_t s);
+                       unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
+                       const GridDesc<T>* gd, hipStream_t s);
 // spread pair / fallback counters of the grid kernels (bytes; zero-initialised once)
 size_t grid_counter_bytes();
 void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, int64_t n, hipStream_t s);
@@ -121,32 +156,21 @@ __device__ __forceinline__ bool chain_keep(const WRange<T>& r, T d) {
 }
 
 // ---- quantile / weights (pmx_select.hip) ----
-enum WeightOp { kWAssign = 0, kWMul = 1 };
-template <typename T>
-void launch_weights_default(const T* d, T* w, int64_t n, hipStream_t s);
-template <typename T>
-void launch_weights_const(T* w, int64_t n, int mul, hipStream_t s);
-template <typename T>
-void launch_weights_cmp(const T* d, T* w, int64_t n, T thr, int ge, int mul, hipStream_t s);
-// threshold from the select state: w = (d <= scale * state.limit)
-template <typename T>
-void launch_weights_state(const T* d, T* w, int64_t n, const SelectState* st, T scale, int mul,
-                          hipStream_t s);
-
 // one radix-select pass: histogram of digit `pass` among keys matching the
 // resolved prefix.  hist must be zero on entry (select zeroes it on exit).
 template <typename T>
 void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass,
-                        hipStream_t s);
+                        const LoopCtl* ctl, hipStream_t s);
 // resolve the digit of `pass`; pass 0 also computes count and the target
 // rank from ratio (host value, or *ratio_dev when non-null).
 template <typename T>
 void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
-                        const double* ratio_dev, int* iter_err, hipStream_t s);
+                        const double* ratio_dev, int* iter_err, const LoopCtl* ctl, hipStream_t s);
 // hist + pick in one launch (single rank; ticket: zeroed uint32, reset on exit)
 template <typename T>
 void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
-                        const double* ratio_dev, unsigned int* ticket, int* iter_err, hipStream_t s);
+                        const double* ratio_dev, unsigned int* ticket, int* iter_err, const LoopCtl* ctl,
+                        hipStream_t s);
 template <typename T>
 int select_passes();
 int select_bins(int pass, int key_bits);
@@ -155,7 +179,7 @@ int select_bins(int pass, int key_bits);
 template <typename T>
 void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRatio, const T* deno,
                     void* scratch, size_t scratch_bytes, double* ratio_dev, int* err_dev,
-                    hipStream_t s);
+                    const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 size_t vartrim_scratch_bytes(int64_t n);
 
@@ -168,21 +192,23 @@ constexpr int kNVMax = 48;
 // point-to-plane result layout: upper triangle of A (NS), b (NF), then kept,
 // nonzero weights, rejected matches, rejected points
 constexpr int p2plane_nv(int dim) { return dim == 3 ? 21 + 6 + 4 : 6 + 3 + 4; }
+// ctl / gd (device loop, may be null): early exit, step transform and the
+// grid level whose positions the ids are (ref / nrm then come from gd)
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
-                            double* partials, hipStream_t s);
-void launch_finalize(const double* partials, int nblocks, int nv, double* out, hipStream_t s);
+                            double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
+void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
                           const int32_t* ids, const WChain<T>& chain, int k, int64_t N, double* partials,
-                          hipStream_t s);
+                          const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 template <typename T>
-void launch_p2point_means(const double* sums, T* means_dev, int dim, hipStream_t s);
+void launch_p2point_means(const double* sums, T* means_dev, int dim, const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
                           const int32_t* ids, const WChain<T>& chain, int k, int64_t N, const T* means_dev,
-                          double* partials, hipStream_t s);
+                          double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 template <typename T>
 void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, hipStream_t s);
 

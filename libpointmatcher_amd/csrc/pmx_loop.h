@@ -1,0 +1,66 @@
+// pmx_loop.h — configuration and device state of the device-resident ICP
+// loop (pmx_loop.hip, driven by pmx_loop_* in pmx_capi.hip).
+#pragma once
+
+#include "pmx_internal.h"
+
+namespace pmx {
+
+constexpr int kLoopHist = 64;      // Differential checker history ring (smoothLength < 64)
+constexpr int kMaxCheckers = 8;
+constexpr int kMaxLevels = 8;
+
+enum CheckKind { kCheckCounter = 0, kCheckDifferential = 1, kCheckBound = 2 };
+// why the loop stopped
+enum LoopReason { kLoopRunning = 0, kLoopCounter = 1, kLoopDifferential = 2, kLoopError = 3 };
+// device-side error codes (mapped to pmx.h codes / messages by the host)
+enum LoopErr {
+    kLoopNoPoints = -1,   // PMX_E_NO_POINTS: "ErrorMnimizer: no point to minimize"
+    kLoopNotRigid = -4,   // PMX_E_TRANSFORMATION
+    kLoopRotNaN = -20,    // ConvergenceError("abs rotation norm not a number")
+    kLoopTransNaN = -21,  // ConvergenceError("abs translation norm not a number")
+    kLoopBound = -22,     // ConvergenceError("limit out of bounds ...")
+};
+
+struct LoopCfg {
+    int rows;       // 3 (2-D) or 4 (3-D)
+    int minimizer;  // 0 point-to-plane, 1 point-to-point
+    int n_checkers;
+    int checker_kind[kMaxCheckers];
+    double checker_p[kMaxCheckers][3];
+    // grid level adaptation (choose_level)
+    int adaptive;
+    int n_levels;
+    double level_ppc[kMaxLevels];
+    int64_t n_local;
+};
+
+template <typename T>
+struct LoopState {
+    T Titer[16];  // rows x rows
+    int iter;     // iterations completed
+    int done;
+    int err;
+    int reason;
+    T cond[kMaxCheckers][2];     // checkers' condition variables
+    T qhist[kLoopHist][4];       // Differential: quaternions (ring)
+    T thist[kLoopHist][3];       //               translations
+    int nhist;
+    T bq0[4], bt0[3], brot2d0;   // Bound: initial rotation / translation
+    double kept, nz, rejM, rejP, sw;  // last minimised iteration's ErrorElements statistics
+    unsigned long long last_visited, touched;
+    int last_level;
+    int pad;
+    long long match_count;
+    double level_cells[kMaxLevels];
+    long long level_seen[kMaxLevels];
+};
+
+template <typename T>
+void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, hipStream_t s);
+template <typename T>
+void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
+                      const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
+                      hipStream_t s);
+
+}  // namespace pmx

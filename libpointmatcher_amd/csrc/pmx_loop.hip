@@ -1,0 +1,289 @@
+// pmx_loop.hip — the device-resident ICP iteration (ICP.cpp:371-430 with the
+// host solve moved onto the GPU).
+//
+// The classic path syncs once per iteration: the host reads the normal
+// equations back, solves them, updates T_iter, runs the transformation
+// checkers and launches the next match — the GPU idles for the round trip
+// (~25-30 us at C3, 15 % of an iteration).  In loop mode the host enqueues
+// whole iterations back to back; the last kernel of each iteration is
+// loop_step_kernel (one lane) which does what the host did:
+//   * quantile / empty-match errors of the iteration (ConvergenceError),
+//   * PointToPlane: solvePossiblyUnderdetermined on the 6x6 / 3x3 system and
+//     the rigid step (PointToPlane.cpp:108-161, 245-312); PointToPoint: the
+//     SVD of the cross-covariance (PointToPoint.cpp:61-101),
+//   * T_iter = dT * T_iter (ICP.cpp:419),
+//   * the checkers in chain order: Counter, Differential, Bound
+//     (TransformationCheckersImpl.cpp:45-225), with the reference's stop /
+//     exception semantics,
+//   * the next iteration's grid level (same rule as choose_level),
+// and publishes the next step transform and level in the LoopCtl word every
+// kernel of the next iteration reads.  Once a checker stops the loop (or an
+// error is raised) the remaining enqueued iterations return at once.  The
+// same dense code (common/pmx_dense.h) runs on the host in classic mode.
+#include "pmx_internal.h"
+
+#include "common/pmx_dense.h"
+#include "pmx_loop.h"
+
+namespace pmx {
+
+using namespace pmx_dense;
+
+template <typename T>
+__device__ void loop_fail(LoopCtl* ctl, LoopState<T>* S, int code, int reason) {
+    S->err = code;
+    S->reason = reason;
+    S->done = 1;
+    ctl->done = 1;
+}
+
+template <typename T>
+__device__ void loop_publish(LoopCtl* ctl, const LoopState<T>* S, int rows) {
+    // the next step transform, embedded in 4x4 as the kernels expect
+    if (rows == 4) {
+        for (int i = 0; i < 16; ++i) ctl->T[i] = (double)S->Titer[i];
+    } else {
+        const T* m = S->Titer;
+        const double e[16] = {m[0], m[1], 0, m[2], m[3], m[4], 0, m[5], 0, 0, 1, 0, m[6], m[7], 0, m[8]};
+        for (int i = 0; i < 16; ++i) ctl->T[i] = e[i];
+    }
+}
+
+template <typename T>
+__device__ void quat_of(const T* M, int rows, bool init2d, T* q) {
+    T m3[9];
+    if (init2d) {  // TransformationCheckersImpl.cpp:107-110: 2-D init uses [R 0; 0 1]
+        for (int i = 0; i < 9; ++i) m3[i] = (i % 4 == 0) ? (T)1 : (T)0;
+        m3[0] = M[0];
+        m3[1] = M[1];
+        m3[3] = M[3];
+        m3[4] = M[4];
+    } else {
+        // topLeftCorner(3,3): in 2-D the whole homogeneous 3x3
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) m3[r * 3 + c] = M[r * rows + c];
+    }
+    quat_from_matrix(m3, q);
+}
+
+template <typename T>
+__global__ void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
+                                 const double* __restrict__ res, const int* __restrict__ iter_err,
+                                 const unsigned long long* __restrict__ visited, const T* __restrict__ means,
+                                 LoopCfg cfg, T* __restrict__ trace) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (ctl->done) return;
+    const int rows = cfg.rows, D = rows - 1;
+    // statistics of the iteration (ErrorElements, ErrorMinimizer.cpp:133-192)
+    double kept, nz, rejM, rejP, sw;
+    if (cfg.minimizer == 0) {
+        const int NF = D == 3 ? 6 : 3, o = NF * (NF + 1) / 2 + NF;
+        kept = res[o];
+        nz = res[o + 1];
+        rejM = res[o + 2];
+        rejP = res[o + 3];
+        sw = kept;  // 0/1 weights
+    } else {
+        kept = res[7];
+        nz = res[8];
+        rejM = res[9];
+        rejP = res[10];
+        sw = res[0];
+    }
+    S->last_level = ctl->level;  // the level whose positions this iteration's ids are
+    const int e = *iter_err;
+    if (e) {
+        loop_fail(ctl, S, e, kLoopError);
+        return;
+    }
+    if (nz == 0.0 || kept == 0.0) {
+        loop_fail(ctl, S, kLoopNoPoints, kLoopError);  // "ErrorMnimizer: no point to minimize"
+        return;
+    }
+    // the minimiser returned: its statistics and the matcher's visit counter
+    // (ICP.cpp:406-416, MatchersImpl.cpp:98)
+    S->kept = kept;
+    S->nz = nz;
+    S->rejM = rejM;
+    S->rejP = rejP;
+    S->sw = sw;
+    S->last_visited = visited[0];
+    S->touched += visited[0];
+    // the step transform
+    T dT[16];
+    if (cfg.minimizer == 0) {
+        const int NF = D == 3 ? 6 : 3, NS = NF * (NF + 1) / 2;
+        T A[36], b[6], x[6];
+        int a = 0;
+        for (int i = 0; i < NF; ++i)
+            for (int j = i; j < NF; ++j, ++a) A[i * NF + j] = A[j * NF + i] = (T)res[a];
+        for (int i = 0; i < NF; ++i) b[i] = (T)(-res[NS + i]);
+        solve_underdetermined(A, b, NF, x);
+        p2plane_transform(rows, x, dT);
+    } else {
+        T m[9], mp[3], mq[3];
+        for (int i = 0; i < D; ++i) {
+            mp[i] = means[i];
+            mq[i] = means[3 + i];
+            for (int j = 0; j < D; ++j) m[i * D + j] = (T)res[16 + i * 3 + j];
+        }
+        p2point_transform(rows, m, mp, mq, dT);
+    }
+    matmul(dT, S->Titer, rows, S->Titer);
+    // transformation checkers, in chain order (TransformationCheckers::check)
+    bool stop = false;
+    for (int ci = 0; ci < cfg.n_checkers; ++ci) {
+        const int kind = cfg.checker_kind[ci];
+        if (kind == kCheckCounter) {
+            S->cond[ci][0] = S->cond[ci][0] + (T)1;
+            if (S->cond[ci][0] >= (T)cfg.checker_p[ci][0]) {  // MaxNumIterationsReached: ends the loop
+                stop = true;
+                S->reason = kLoopCounter;
+                break;  // (the exception skips the remaining checkers)
+            }
+        } else if (kind == kCheckDifferential) {
+            const int sl = (int)cfg.checker_p[ci][2];
+            T q[4];
+            quat_of(S->Titer, rows, false, q);
+            const int slot = S->nhist % kLoopHist;
+            for (int i = 0; i < 4; ++i) S->qhist[slot][i] = q[i];
+            for (int r = 0; r < 3; ++r) S->thist[slot][r] = r < D ? S->Titer[r * rows + D] : (T)0;
+            ++S->nhist;
+            T cv0 = 0, cv1 = 0;
+            if (S->nhist > sl) {
+                for (int i = S->nhist - 1; i >= S->nhist - sl; --i) {
+                    const int a0 = i % kLoopHist, a1 = (i - 1) % kLoopHist;
+                    cv0 = cv0 + fabs(angular_distance(S->qhist[a0], S->qhist[a1]));
+                    T nn = 0;
+                    for (int r = 0; r < D; ++r) {
+                        const T d = S->thist[a0][r] - S->thist[a1][r];
+                        nn = nn + d * d;
+                    }
+                    cv1 = cv1 + fabs(sqrt(nn));
+                }
+                cv0 = cv0 / (T)sl;
+                cv1 = cv1 / (T)sl;
+                if (cv0 < (T)cfg.checker_p[ci][0] && cv1 < (T)cfg.checker_p[ci][1]) {
+                    stop = true;
+                    S->reason = kLoopDifferential;
+                }
+            }
+            S->cond[ci][0] = cv0;
+            S->cond[ci][1] = cv1;
+            if (cv0 != cv0 || cv1 != cv1) {
+                loop_fail(ctl, S, cv0 != cv0 ? kLoopRotNaN : kLoopTransNaN, kLoopError);
+                return;
+            }
+        } else {  // kCheckBound
+            T cv0;
+            if (rows == 4) {
+                T q[4];
+                quat_of(S->Titer, rows, false, q);
+                cv0 = angular_distance(q, S->bq0);
+            } else {
+                T v = acos(S->Titer[0]) - S->brot2d0;
+                while (v > (T)3.14159265358979323846) v -= (T)(2 * 3.14159265358979323846);
+                while (v < (T)-3.14159265358979323846) v += (T)(2 * 3.14159265358979323846);
+                cv0 = v;
+            }
+            T nn = 0;
+            for (int r = 0; r < D; ++r) {
+                const T d = S->Titer[r * rows + D] - S->bt0[r];
+                nn = nn + d * d;
+            }
+            const T cv1 = sqrt(nn);
+            S->cond[ci][0] = cv0;
+            S->cond[ci][1] = cv1;
+            if (cv0 > (T)cfg.checker_p[ci][0] || cv1 > (T)cfg.checker_p[ci][1]) {
+                loop_fail(ctl, S, kLoopBound, kLoopError);
+                return;
+            }
+        }
+    }
+    if (trace) {
+        T* t = trace + (size_t)S->iter * rows * rows;
+        for (int i = 0; i < rows * rows; ++i) t[i] = S->Titer[i];
+    }
+    ++S->iter;
+    if (stop) {
+        S->done = 1;
+        ctl->done = 1;
+        return;
+    }
+    // the next step starts with RigidTransformation::compute's check
+    // (TransformationsImpl.cpp:62-63)
+    if (fabs((T)1 - det_rot(S->Titer, rows)) > (T)0.001) {
+        loop_fail(ctl, S, kLoopNotRigid, kLoopError);
+        return;
+    }
+    // grid level of the next match (pmx_capi.hip choose_level)
+    if (cfg.adaptive && cfg.n_levels > 1 && cfg.n_local > 0) {
+        const int l = ctl->level;
+        const double cells = (double)visited[0] / ((double)cfg.n_local * cfg.level_ppc[l]);
+        ++S->match_count;
+        S->level_cells[l] = cells;
+        S->level_seen[l] = S->match_count;
+        int next = l;
+        if (cells > 32.0 && l + 1 < cfg.n_levels) {
+            next = l + 1;
+        } else if (cells < 16.0 && l > 0) {
+            const bool recent = S->level_seen[l - 1] > 0 && S->match_count - S->level_seen[l - 1] <= 3;
+            if (!(recent && S->level_cells[l - 1] > 32.0)) next = l - 1;
+        }
+        ctl->level = next;
+    }
+    loop_publish(ctl, S, rows);
+}
+
+// reset the loop state for a new ICP (checkers' init, ICP.cpp:368-369)
+template <typename T>
+__global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S, LoopCfg cfg,
+                                 const T* __restrict__ T0, int level) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int rows = cfg.rows, D = rows - 1;
+    LoopState<T> z = {};
+    *S = z;
+    for (int i = 0; i < rows * rows; ++i) S->Titer[i] = T0[i];
+    for (int ci = 0; ci < cfg.n_checkers; ++ci) {
+        if (cfg.checker_kind[ci] == kCheckDifferential) {
+            T q[4];
+            quat_of(S->Titer, rows, rows != 4, q);
+            for (int i = 0; i < 4; ++i) S->qhist[0][i] = q[i];
+            for (int r = 0; r < 3; ++r) S->thist[0][r] = r < D ? S->Titer[r * rows + D] : (T)0;
+            S->nhist = 1;
+        } else if (cfg.checker_kind[ci] == kCheckBound) {
+            if (rows == 4) {
+                quat_of(S->Titer, rows, false, S->bq0);
+            } else {
+                S->brot2d0 = acos(S->Titer[0]);
+            }
+            for (int r = 0; r < 3; ++r) S->bt0[r] = r < D ? S->Titer[r * rows + D] : (T)0;
+        }
+    }
+    ctl->done = 0;
+    ctl->level = level;
+    loop_publish(ctl, S, rows);
+}
+
+template <typename T>
+void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, hipStream_t s) {
+    hipLaunchKernelGGL(loop_init_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, cfg, T0, level);
+}
+template <typename T>
+void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
+                      const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(loop_step_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, res, iter_err, visited, means, cfg,
+                       trace);
+}
+
+template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg&, const float*, int, hipStream_t);
+template void launch_loop_init<double>(LoopCtl*, LoopState<double>*, const LoopCfg&, const double*, int,
+                                       hipStream_t);
+template void launch_loop_step<float>(LoopCtl*, LoopState<float>*, const double*, const int*,
+                                      const unsigned long long*, const float*, const LoopCfg&, float*, hipStream_t);
+template void launch_loop_step<double>(LoopCtl*, LoopState<double>*, const double*, const int*,
+                                       const unsigned long long*, const double*, const LoopCfg&, double*,
+                                       hipStream_t);
+
+}  // namespace pmx

@@ -90,10 +90,18 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                                                               const P4<T>* __restrict__ ref,
                                                               const P4<T>* __restrict__ nrm, const T* __restrict__ d,
                                                               const int32_t* __restrict__ ids, WChain<T> chain,
-                                                              int k, int64_t N, double* __restrict__ partials) {
+                                                              int k, int64_t N, double* __restrict__ partials,
+                                                              const LoopCtl* __restrict__ ctl,
+                                                              const GridDesc<T>* __restrict__ gd) {
     constexpr int NF = DIM == 3 ? 6 : 3;
     constexpr int NS = NF * (NF + 1) / 2;
     constexpr int NV = NS + NF + 4;
+    if (ctl) {  // device loop
+        if (ctl->done) return;
+        ctl_transform(ctl, Tm);
+        ref = gd[ctl->level].gpts;
+        nrm = gd[ctl->level].gnrm;
+    }
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
@@ -170,21 +178,22 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, const T* d,
                             const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim, double* partials,
-                            hipStream_t s) {
+                            const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
     if (dim == 3)
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
-                           ids, chain, k, N, partials);
+                           ids, chain, k, N, partials, ctl, gd);
     else
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
-                           ids, chain, k, N, partials);
+                           ids, chain, k, N, partials, ctl, gd);
 }
 
 // Sum the per-block partials: one block per accumulator, each thread adds a
 // fixed strided subset in order, then a fixed-shape tree — the summation
 // order never changes, so results are bitwise reproducible.
 __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ partials, int nblocks, int nv,
-                                                       double* __restrict__ out) {
+                                                       double* __restrict__ out, const LoopCtl* __restrict__ ctl) {
     __shared__ double red[4];
+    if (ctl && ctl->done) return;
     const int v = blockIdx.x;
     double s = 0.0;
     for (int b = threadIdx.x; b < nblocks; b += 256) s += partials[(int64_t)b * nv + v];
@@ -194,8 +203,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
     if (threadIdx.x == 0) out[v] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-void launch_finalize(const double* partials, int nblocks, int nv, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(nv), dim3(256), 0, s, partials, nblocks, nv, out);
+void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(nv), dim3(256), 0, s, partials, nblocks, nv, out, ctl);
 }
 
 // ------------------------------------------------------------ point-to-point --
@@ -205,8 +214,15 @@ template <typename T>
 __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
                                                             const P4<T>* __restrict__ ref, const T* __restrict__ d,
                                                             const int32_t* __restrict__ ids, WChain<T> chain, int k,
-                                                            int64_t N, double* __restrict__ partials) {
+                                                            int64_t N, double* __restrict__ partials,
+                                                            const LoopCtl* __restrict__ ctl,
+                                                            const GridDesc<T>* __restrict__ gd) {
     constexpr int NV = 11;
+    if (ctl) {  // device loop
+        if (ctl->done) return;
+        ctl_transform(ctl, Tm);
+        ref = gd[ctl->level].gpts;
+    }
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
@@ -246,15 +262,17 @@ __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restr
 
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
-                          const WChain<T>& chain, int k, int64_t N, double* partials, hipStream_t s) {
+                          const WChain<T>& chain, int k, int64_t N, double* partials, const LoopCtl* ctl,
+                          const GridDesc<T>* gd, hipStream_t s) {
     hipLaunchKernelGGL(p2point_pass1_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, chain, k, N,
-                       partials);
+                       partials, ctl, gd);
 }
 
 // means in T: w_sum_inv = 1 / w.sum(); mean = sum * w_sum_inv (PointToPoint.cpp:67-72)
 template <typename T>
-__global__ void p2point_means_kernel(const double* __restrict__ sums, T* __restrict__ means, int dim) {
-    if (threadIdx.x != 0) return;
+__global__ void p2point_means_kernel(const double* __restrict__ sums, T* __restrict__ means, int dim,
+                                     const LoopCtl* __restrict__ ctl) {
+    if (threadIdx.x != 0 || (ctl && ctl->done)) return;
     const T winv = (T)1 / (T)sums[0];
     for (int r = 0; r < 3; ++r) {
         means[r] = r < dim ? (T)sums[1 + r] * winv : (T)0;
@@ -263,8 +281,8 @@ __global__ void p2point_means_kernel(const double* __restrict__ sums, T* __restr
 }
 
 template <typename T>
-void launch_p2point_means(const double* sums, T* means_dev, int dim, hipStream_t s) {
-    hipLaunchKernelGGL(p2point_means_kernel<T>, dim3(1), dim3(64), 0, s, sums, means_dev, dim);
+void launch_p2point_means(const double* sums, T* means_dev, int dim, const LoopCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(p2point_means_kernel<T>, dim3(1), dim3(64), 0, s, sums, means_dev, dim, ctl);
 }
 
 // pass 2: m = sum (qc * w) pc^T  (PointToPoint.cpp:76-81), 3x3 (2-D uses the
@@ -274,8 +292,15 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
                                                             const P4<T>* __restrict__ ref, const T* __restrict__ d,
                                                             const int32_t* __restrict__ ids, WChain<T> chain, int k,
                                                             int64_t N, const T* __restrict__ means,
-                                                            double* __restrict__ partials) {
+                                                            double* __restrict__ partials,
+                                                            const LoopCtl* __restrict__ ctl,
+                                                            const GridDesc<T>* __restrict__ gd) {
     constexpr int NV = 9;
+    if (ctl) {  // device loop
+        if (ctl->done) return;
+        ctl_transform(ctl, Tm);
+        ref = gd[ctl->level].gpts;
+    }
     double acc[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) acc[v] = 0.0;
@@ -312,9 +337,9 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
 template <typename T>
 void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
                           const WChain<T>& chain, int k, int64_t N, const T* means_dev, double* partials,
-                          hipStream_t s) {
+                          const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
     hipLaunchKernelGGL(p2point_pass2_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, chain, k, N,
-                       means_dev, partials);
+                       means_dev, partials, ctl, gd);
 }
 
 // materialise the chain's 0/1 weights (host mirror only)
@@ -336,12 +361,14 @@ void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, h
 #define PMX_INST(T)                                                                                                  \
     template void launch_p2plane_partial<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const P4<T>*, const T*,      \
                                             const int32_t*, const WChain<T>&, int, int64_t, int, double*,           \
-                                            hipStream_t);                                                             \
+                                            const LoopCtl*, const GridDesc<T>*, hipStream_t);                        \
     template void launch_p2point_pass1<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
-                                          const WChain<T>&, int, int64_t, double*, hipStream_t);                     \
-    template void launch_p2point_means<T>(const double*, T*, int, hipStream_t);                                      \
+                                          const WChain<T>&, int, int64_t, double*, const LoopCtl*,                   \
+                                          const GridDesc<T>*, hipStream_t);                                          \
+    template void launch_p2point_means<T>(const double*, T*, int, const LoopCtl*, hipStream_t);                      \
     template void launch_p2point_pass2<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
-                                          const WChain<T>&, int, int64_t, const T*, double*, hipStream_t);           \
+                                          const WChain<T>&, int, int64_t, const T*, double*, const LoopCtl*,         \
+                                          const GridDesc<T>*, hipStream_t);                                          \
     template void launch_weights_chain<T>(const T*, T*, int64_t, const WChain<T>&, hipStream_t);
 PMX_INST(float)
 PMX_INST(double)

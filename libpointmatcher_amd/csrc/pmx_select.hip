@@ -165,8 +165,10 @@ __device__ __forceinline__ void hist_phase(const T* __restrict__ d, int64_t n, u
 template <typename T>
 __global__ __launch_bounds__(256) void select_hist_kernel(const T* __restrict__ d, int64_t n,
                                                           uint32_t* __restrict__ hist,
-                                                          const SelectState* __restrict__ st, int pass, int agg) {
+                                                          const SelectState* __restrict__ st, int pass, int agg,
+                                                          const LoopCtl* __restrict__ ctl) {
     __shared__ uint32_t lh[2048];
+    if (ctl && ctl->done) return;
     hist_phase<T>(d, n, hist, st, pass, lh, agg);
 }
 
@@ -198,9 +200,10 @@ static int64_t select_blocks(int64_t n) {
 }
 
 template <typename T>
-void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass, hipStream_t s) {
+void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass, const LoopCtl* ctl,
+                        hipStream_t s) {
     hipLaunchKernelGGL(select_hist_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
-                       pass, select_agg());
+                       pass, select_agg(), ctl);
 }
 
 // ------------------------------------------------------------------ pick --
@@ -309,10 +312,12 @@ template <typename T>
 __global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__ hist, SelectState* __restrict__ st,
                                                           int pass, double ratio_host,
                                                           const double* __restrict__ ratio_dev,
-                                                          int* __restrict__ iter_err, int last) {
+                                                          int* __restrict__ iter_err, int last,
+                                                          const LoopCtl* __restrict__ ctl) {
     __shared__ unsigned long long part[256];
     __shared__ unsigned long long s_rank;
     __shared__ int s_err;
+    if (ctl && ctl->done) return;
     pick_phase<T, false>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err);
 }
 
@@ -325,12 +330,14 @@ __global__ __launch_bounds__(256) void select_pass_kernel(const T* __restrict__ 
                                                           int pass, double ratio_host,
                                                           const double* __restrict__ ratio_dev,
                                                           int* __restrict__ iter_err, int last,
-                                                          unsigned int* __restrict__ ticket, int agg) {
+                                                          unsigned int* __restrict__ ticket, int agg,
+                                                          const LoopCtl* __restrict__ ctl) {
     __shared__ uint32_t lh[2048];
     __shared__ unsigned long long part[256];
     __shared__ unsigned long long s_rank;
     __shared__ int s_err;
     __shared__ bool s_last;
+    if (ctl && ctl->done) return;  // (uniform: no block takes a ticket)
     hist_phase<T>(d, n, hist, st, pass, lh, agg);
     __syncthreads();  // every thread's flush has returned
     if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
@@ -344,50 +351,19 @@ __global__ __launch_bounds__(256) void select_pass_kernel(const T* __restrict__ 
 
 template <typename T>
 void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio, const double* ratio_dev,
-                        int* iter_err, hipStream_t s) {
+                        int* iter_err, const LoopCtl* ctl, hipStream_t s) {
     const int last = pass == select_passes<T>() - 1;
     hipLaunchKernelGGL(select_pick_kernel<T>, dim3(1), dim3(256), 0, s, hist, st, pass, ratio, ratio_dev,
-                       iter_err, last);
+                       iter_err, last, ctl);
 }
 
 template <typename T>
 void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
-                        const double* ratio_dev, unsigned int* ticket, int* iter_err, hipStream_t s) {
+                        const double* ratio_dev, unsigned int* ticket, int* iter_err, const LoopCtl* ctl,
+                        hipStream_t s) {
     const int last = pass == select_passes<T>() - 1;
     hipLaunchKernelGGL(select_pass_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
-                       pass, ratio, ratio_dev, iter_err, last, ticket, select_agg());
-}
-
-// ---------------------------------------------------------------- weights --
-template <typename T>
-__global__ void w_default_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        w[i] = d[i] == (T)__builtin_huge_val() ? (T)0 : (T)1;
-}
-template <typename T>
-__global__ void w_const_kernel(T* __restrict__ w, int64_t n, int mul) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        w[i] = mul ? w[i] * (T)1 : (T)1;
-}
-template <typename T>
-__global__ void w_cmp_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n, T thr, int ge, int mul) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const T v = (ge ? (d[i] >= thr) : (d[i] <= thr)) ? (T)1 : (T)0;
-        w[i] = mul ? w[i] * v : v;
-    }
-}
-template <typename T>
-__global__ void w_state_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n,
-                               const SelectState* __restrict__ st, T scale, int mul) {
-    const T thr = scale * (T)st->limit;  // MedianDist: factor * median (OutlierFiltersImpl.cpp:121-122)
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const T v = d[i] <= thr ? (T)1 : (T)0;
-        w[i] = mul ? w[i] * v : v;
-    }
+                       pass, ratio, ratio_dev, iter_err, last, ticket, select_agg(), ctl);
 }
 
 static unsigned grid_for(int64_t n) {
@@ -395,24 +371,6 @@ static unsigned grid_for(int64_t n) {
     if (g < 1) g = 1;
     if (g > 4096) g = 4096;
     return (unsigned)g;
-}
-
-template <typename T>
-void launch_weights_default(const T* d, T* w, int64_t n, hipStream_t s) {
-    if (n > 0) hipLaunchKernelGGL(w_default_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, w, n);
-}
-template <typename T>
-void launch_weights_const(T* w, int64_t n, int mul, hipStream_t s) {
-    if (n > 0) hipLaunchKernelGGL(w_const_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, w, n, mul);
-}
-template <typename T>
-void launch_weights_cmp(const T* d, T* w, int64_t n, T thr, int ge, int mul, hipStream_t s) {
-    if (n > 0) hipLaunchKernelGGL(w_cmp_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, w, n, thr, ge, mul);
-}
-template <typename T>
-void launch_weights_state(const T* d, T* w, int64_t n, const SelectState* st, T scale, int mul, hipStream_t s) {
-    if (n > 0)
-        hipLaunchKernelGGL(w_state_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, w, n, st, scale, mul);
 }
 
 // ============================================================ VarTrimmed ==
@@ -437,8 +395,9 @@ size_t vartrim_scratch_bytes(int64_t n) {
 
 template <typename T>
 __global__ void vt_compact_kernel(const T* __restrict__ d, int64_t n, typename KeyOf<T>::K* __restrict__ keys,
-                                  int* __restrict__ count) {
+                                  int* __restrict__ count, const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
+    if (ctl && ctl->done) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const T v = d[i];
@@ -451,8 +410,10 @@ __global__ void vt_compact_kernel(const T* __restrict__ d, int64_t n, typename K
 
 template <typename K>
 __global__ __launch_bounds__(256) void rs_count_kernel(const K* __restrict__ keys, const int* __restrict__ count,
-                                                       int shift, int tiles, uint32_t* __restrict__ counts) {
+                                                       int shift, int tiles, uint32_t* __restrict__ counts,
+                                                       const LoopCtl* __restrict__ ctl) {
     __shared__ uint32_t lc[256];
+    if (ctl && ctl->done) return;
     lc[threadIdx.x] = 0;
     __syncthreads();
     const int64_t c = *count;
@@ -467,8 +428,9 @@ __global__ __launch_bounds__(256) void rs_count_kernel(const K* __restrict__ key
 
 // exclusive scan over 256*tiles counts (digit-major), one block of 1024
 __global__ __launch_bounds__(1024) void rs_scan_kernel(const uint32_t* __restrict__ counts, int64_t total,
-                                                       uint32_t* __restrict__ offsets) {
+                                                       uint32_t* __restrict__ offsets, const LoopCtl* __restrict__ ctl) {
     __shared__ uint32_t part[1024];
+    if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     const int64_t per = (total + 1023) / 1024;
     const int64_t lo = t * per;
@@ -495,8 +457,10 @@ __global__ __launch_bounds__(1024) void rs_scan_kernel(const uint32_t* __restric
 template <typename K>
 __global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ in, K* __restrict__ out,
                                                          const int* __restrict__ count, int shift, int tiles,
-                                                         const uint32_t* __restrict__ offsets) {
+                                                         const uint32_t* __restrict__ offsets,
+                                                         const LoopCtl* __restrict__ ctl) {
     __shared__ uint32_t run[256];
+    if (ctl && ctl->done) return;
     __shared__ uint32_t wcnt[4][256];
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -540,8 +504,10 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ i
 // running sum after adding element l of each 64-chunk)
 template <typename T>
 __global__ __launch_bounds__(64) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
-                                                       const int* __restrict__ count, T* __restrict__ cum) {
+                                                       const int* __restrict__ count, T* __restrict__ cum,
+                                                       const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
+    if (ctl && ctl->done) return;
     const int lane = threadIdx.x;
     const int64_t c = *count;
     T acc = 0;
@@ -565,9 +531,11 @@ template <typename T>
 __global__ __launch_bounds__(1024) void vt_frms_kernel(const T* __restrict__ cum, const int* __restrict__ count,
                                                        const T* __restrict__ deno, int minEl, int maxEl,
                                                        int points_nbr, double* __restrict__ ratio_dev,
-                                                       int* __restrict__ err, int* __restrict__ iter_err) {
+                                                       int* __restrict__ err, int* __restrict__ iter_err,
+                                                       const LoopCtl* __restrict__ ctl) {
     __shared__ T sv[1024];
     __shared__ int si[1024];
+    if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     const int c = *count;
     int hi = maxEl < c ? maxEl : c;  // reference reads past the filtered count (UB); build clamps
@@ -615,7 +583,7 @@ __global__ __launch_bounds__(1024) void vt_frms_kernel(const T* __restrict__ cum
 
 template <typename T>
 void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRatio, const T* deno, void* scratch,
-                    size_t scratch_bytes, double* ratio_dev, int* err_dev, hipStream_t s) {
+                    size_t scratch_bytes, double* ratio_dev, int* err_dev, const LoopCtl* ctl, hipStream_t s) {
     (void)scratch_bytes;
     using K = typename KeyOf<T>::K;
     char* p = static_cast<char*>(scratch);
@@ -635,50 +603,44 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
 
     (void)hipMemsetAsync(hdr, 0, 256, s);
     if (n > 0)
-        hipLaunchKernelGGL(vt_compact_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr);
+        hipLaunchKernelGGL(vt_compact_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl);
     const int key_bits = KeyOf<T>::bits;
     K* src = keysA;
     K* dst = keysB;
     for (int shift = 0; shift < key_bits; shift += 8) {
         hipLaunchKernelGGL(rs_count_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, hdr, shift, (int)tiles,
-                           counts);
-        hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, counts, (int64_t)256 * tiles, offsets);
+                           counts, ctl);
+        hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, counts, (int64_t)256 * tiles, offsets, ctl);
         hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, dst, hdr, shift,
-                           (int)tiles, offsets);
+                           (int)tiles, offsets, ctl);
         K* tmp = src;
         src = dst;
         dst = tmp;
     }
-    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(64), 0, s, src, hdr, cum);
+    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(64), 0, s, src, hdr, cum, ctl);
     const int minEl = (int)std::floor(minRatio * (T)points_nbr);
     const int maxEl = (int)std::floor(maxRatio * (T)points_nbr);
     hipLaunchKernelGGL(vt_frms_kernel<T>, dim3(1), dim3(1024), 0, s, cum, hdr, deno, minEl, maxEl, points_nbr,
-                       ratio_dev, hdr + 1, err_dev);
+                       ratio_dev, hdr + 1, err_dev, ctl);
 }
 
 // explicit instantiations
-template void launch_select_hist<float>(const float*, int64_t, uint32_t*, const SelectState*, int, hipStream_t);
-template void launch_select_hist<double>(const double*, int64_t, uint32_t*, const SelectState*, int, hipStream_t);
-template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, const double*, int*, hipStream_t);
-template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, hipStream_t);
+template void launch_select_hist<float>(const float*, int64_t, uint32_t*, const SelectState*, int, const LoopCtl*,
+                                        hipStream_t);
+template void launch_select_hist<double>(const double*, int64_t, uint32_t*, const SelectState*, int, const LoopCtl*,
+                                         hipStream_t);
+template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
+                                        hipStream_t);
+template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
+                                         hipStream_t);
 template void launch_select_pass<float>(const float*, int64_t, uint32_t*, SelectState*, int, double, const double*,
-                                        unsigned int*, int*, hipStream_t);
+                                        unsigned int*, int*, const LoopCtl*, hipStream_t);
 template void launch_select_pass<double>(const double*, int64_t, uint32_t*, SelectState*, int, double, const double*,
-                                         unsigned int*, int*, hipStream_t);
-template void launch_weights_default<float>(const float*, float*, int64_t, hipStream_t);
-template void launch_weights_default<double>(const double*, double*, int64_t, hipStream_t);
-template void launch_weights_const<float>(float*, int64_t, int, hipStream_t);
-template void launch_weights_const<double>(double*, int64_t, int, hipStream_t);
-template void launch_weights_cmp<float>(const float*, float*, int64_t, float, int, int, hipStream_t);
-template void launch_weights_cmp<double>(const double*, double*, int64_t, double, int, int, hipStream_t);
-template void launch_weights_state<float>(const float*, float*, int64_t, const SelectState*, float, int,
-                                          hipStream_t);
-template void launch_weights_state<double>(const double*, double*, int64_t, const SelectState*, double, int,
-                                           hipStream_t);
+                                         unsigned int*, int*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<float>(const float*, int64_t, int, float, float, const float*, void*, size_t, double*,
-                                    int*, hipStream_t);
+                                    int*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,
-                                     double*, int*, hipStream_t);
+                                     double*, int*, const LoopCtl*, hipStream_t);
 template size_t vartrim_scratch_bytes<float>(int64_t);
 template size_t vartrim_scratch_bytes<double>(int64_t);
 

@@ -119,7 +119,7 @@ logger:
 
 
 def chain_yaml(knn=1, maxdist="inf", filters=(("TrimmedDistOutlierFilter", {"ratio": 0.85}),),
-               minimizer="PointToPlaneErrorMinimizer", maxit=40, differential=None):
+               minimizer="PointToPlaneErrorMinimizer", maxit=40, differential=None, bound=None):
     if filters:
         fl = []
         for name, p in filters:
@@ -134,5 +134,8 @@ def chain_yaml(knn=1, maxdist="inf", filters=(("TrimmedDistOutlierFilter", {"rat
     if differential:
         diff = ("  - DifferentialTransformationChecker:\n" +
                 "".join(f"      {k}: {v}\n" for k, v in differential.items()))
+    if bound:
+        diff += ("  - BoundTransformationChecker:\n" +
+                 "".join(f"      {k}: {v}\n" for k, v in bound.items()))
     return CHAIN_P2PLANE.format(knn=knn, maxdist=maxdist, filters=ftxt, minimizer=minimizer, maxit=maxit,
                                 diff=diff)

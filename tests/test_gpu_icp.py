@@ -14,6 +14,14 @@ from libpointmatcher_amd.synth import reading_cloud, reference_cloud
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True, params=["loop", "modules"])
+def icp_mode(request, monkeypatch):
+    """Every chain runs twice: as the device-resident loop (the default when
+    every module has a device form) and through the per-module calls."""
+    monkeypatch.setenv("PMX_DEVICE_LOOP", "1" if request.param == "loop" else "0")
+    return request.param
+
 DIFF = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
 
 
