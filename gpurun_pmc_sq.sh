@@ -1,0 +1,9 @@
+#!/bin/bash
+# One PMC pass (SQ instruction mix and wave cycles) over a short C3 bench.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+R="$(pwd)"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_WAIT_INST_ANY SQ_INSTS_BRANCH \
+  -d "$R/gpurun_out/pmc_sq" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/pmc_sq.log" 2>&1

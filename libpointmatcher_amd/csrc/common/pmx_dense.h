@@ -21,6 +21,14 @@
 #else
 #define PMX_HD
 #endif
+// full unrolling on the device: with the sizes constant after inlining, every
+// array index becomes static and the arrays stay in VGPRs (a single lane
+// walking scratch memory is ~10x slower)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PMX_UNROLL _Pragma("unroll")
+#else
+#define PMX_UNROLL
+#endif
 
 namespace pmx_dense {
 
@@ -56,7 +64,9 @@ PMX_HD inline void vswap(T& a, T& b) {
 template <typename T>
 PMX_HD inline T dot(const T* x, const T* y, int n) {
     T s = 0;
-    for (int i = 0; i < n; ++i) s = s + x[i] * y[i];
+    PMX_UNROLL
+    for (int i = 0; i < 6; ++i)  // (n <= 6; a fixed bound unrolls on the device)
+        if (i < n) s = s + x[i] * y[i];
     return s;
 }
 
@@ -64,16 +74,28 @@ PMX_HD inline T dot(const T* x, const T* y, int n) {
 // failed decomposition, so does this
 template <typename T>
 PMX_HD void llt(const T* A, int n, T* L) {
+    PMX_UNROLL
     for (int i = 0; i < n * n; ++i) L[i] = 0;
+    PMX_UNROLL
     for (int r = 0; r < n; ++r)
-        for (int c = 0; c <= r; ++c) L[r * n + c] = A[r * n + c];
+        PMX_UNROLL
+        for (int c = 0; c < n; ++c)
+            if (c <= r) L[r * n + c] = A[r * n + c];
+    bool failed = false;  // (a flag rather than a return keeps the loop unrollable)
+    PMX_UNROLL
     for (int k = 0; k < n; ++k) {
+        if (failed) continue;
         T x = L[k * n + k];
         if (k > 0) x = x - dot(&L[k * n], &L[k * n], k);
-        if (x <= (T)0) return;
+        if (x <= (T)0) {
+            failed = true;
+            continue;
+        }
         x = sqrt(x);
         L[k * n + k] = x;
-        for (int i = k + 1; i < n; ++i) {
+        PMX_UNROLL
+        for (int i = 0; i < n; ++i) {
+            if (i <= k) continue;
             T v = L[i * n + k];
             if (k > 0) v = v - dot(&L[i * n], &L[k * n], k);
             L[i * n + k] = v / x;
@@ -82,15 +104,23 @@ PMX_HD void llt(const T* A, int n, T* L) {
 }
 template <typename T>
 PMX_HD void llt_solve(const T* L, int n, const T* b, T* x) {
+    // inner loops run over fixed bounds with a guard so that the device
+    // unroller sees constant trip counts (same operation order)
     T y[6];
+    PMX_UNROLL
     for (int i = 0; i < n; ++i) {
         T s = b[i];
-        for (int j = 0; j < i; ++j) s = s - L[i * n + j] * y[j];
+        PMX_UNROLL
+        for (int j = 0; j < n; ++j)
+            if (j < i) s = s - L[i * n + j] * y[j];
         y[i] = s / L[i * n + i];
     }
+    PMX_UNROLL
     for (int i = n - 1; i >= 0; --i) {
         T s = y[i];
-        for (int j = i + 1; j < n; ++j) s = s - L[j * n + i] * x[j];
+        PMX_UNROLL
+        for (int j = 0; j < n; ++j)
+            if (j > i) s = s - L[j * n + i] * x[j];
         x[i] = s / L[i * n + i];
     }
 }
@@ -99,16 +129,19 @@ PMX_HD void llt_solve(const T* L, int n, const T* b, T* x) {
 template <typename T>
 PMX_HD void make_householder(T* v, int stride, int m, T& tau, T& beta) {
     T tail = 0;
+    PMX_UNROLL
     for (int i = 1; i < m; ++i) tail = tail + v[i * stride] * v[i * stride];
     const T c0 = v[0];
     if (m == 1 || tail <= tiny<T>()) {
         tau = 0;
         beta = c0;
+        PMX_UNROLL
         for (int i = 1; i < m; ++i) v[i * stride] = 0;
         return;
     }
     T b = sqrt(c0 * c0 + tail);
     if (c0 >= (T)0) b = -b;
+    PMX_UNROLL
     for (int i = 1; i < m; ++i) v[i * stride] = v[i * stride] / (c0 - b);
     tau = (b - c0) / b;
     beta = b;
@@ -118,15 +151,19 @@ PMX_HD void make_householder(T* v, int stride, int m, T& tau, T& beta) {
 template <typename T>
 PMX_HD void householder_left(T* M, int n, int r0, int m, int c0, int nc, const T* ess, int es, T tau) {
     if (m == 1) {
+        PMX_UNROLL
         for (int c = 0; c < nc; ++c) M[r0 * n + c0 + c] = M[r0 * n + c0 + c] * ((T)1 - tau);
         return;
     }
     if (tau == (T)0) return;
+    PMX_UNROLL
     for (int c = 0; c < nc; ++c) {
         T t = 0;
+        PMX_UNROLL
         for (int i = 1; i < m; ++i) t = t + ess[(i - 1) * es] * M[(r0 + i) * n + c0 + c];
         t = t + M[r0 * n + c0 + c];
         M[r0 * n + c0 + c] = M[r0 * n + c0 + c] - tau * t;
+        PMX_UNROLL
         for (int i = 1; i < m; ++i) M[(r0 + i) * n + c0 + c] = M[(r0 + i) * n + c0 + c] - tau * ess[(i - 1) * es] * t;
     }
 }
@@ -137,21 +174,27 @@ struct FullPivQR {
     int n = 0;
     T qr[36];
     T hcoeffs[6];
-    int rowtr[6], coltr[6], perm[6];
+    int rowtr[6], coltr[6];
     int nonzero = 0;
     T maxpivot = 0;
 
     PMX_HD void compute(const T* A, int nn) {
         n = nn;
+        PMX_UNROLL
         for (int i = 0; i < n * n; ++i) qr[i] = A[i];
         const T precision = eps<T>() * (T)n;
         maxpivot = 0;
         nonzero = n;
         T biggest = 0;
+        bool dead = false;  // (a flag rather than a break keeps the k loop unrollable)
+        PMX_UNROLL
         for (int k = 0; k < n; ++k) {
+            if (dead) continue;
             int br = k, bc = k;
             T best = -1;
+            PMX_UNROLL
             for (int c = k; c < n; ++c)
+                PMX_UNROLL
                 for (int r = k; r < n; ++r) {
                     const T v = fabs(qr[r * n + c]);
                     if (v > best) {
@@ -163,19 +206,39 @@ struct FullPivQR {
             if (k == 0) biggest = best;
             if (best <= biggest * precision) {
                 nonzero = k;
+                PMX_UNROLL
                 for (int i = k; i < n; ++i) {
                     rowtr[i] = i;
                     coltr[i] = i;
                     hcoeffs[i] = 0;
                 }
-                break;
+                dead = true;
+                continue;
             }
             rowtr[k] = br;
             coltr[k] = bc;
-            if (k != br)
-                for (int c = k; c < n; ++c) vswap(qr[k * n + c], qr[br * n + c]);
-            if (k != bc)
-                for (int r = 0; r < n; ++r) vswap(qr[r * n + k], qr[r * n + bc]);
+            // swaps written with static indices (the compare selects the row /
+            // column) so that qr stays in registers on the device
+            PMX_UNROLL
+            for (int r2 = k + 1; r2 < n; ++r2) {
+                const bool sw = r2 == br;
+                PMX_UNROLL
+                for (int c = k; c < n; ++c) {
+                    const T a = qr[k * n + c], b = qr[r2 * n + c];
+                    qr[k * n + c] = sw ? b : a;
+                    qr[r2 * n + c] = sw ? a : b;
+                }
+            }
+            PMX_UNROLL
+            for (int c2 = k + 1; c2 < n; ++c2) {
+                const bool sw = c2 == bc;
+                PMX_UNROLL
+                for (int r = 0; r < n; ++r) {
+                    const T a = qr[r * n + k], b = qr[r * n + c2];
+                    qr[r * n + k] = sw ? b : a;
+                    qr[r * n + c2] = sw ? a : b;
+                }
+            }
             T tau, beta;
             make_householder(&qr[k * n + k], n, n - k, tau, beta);
             hcoeffs[k] = tau;
@@ -183,13 +246,18 @@ struct FullPivQR {
             if (fabs(beta) > maxpivot) maxpivot = fabs(beta);
             householder_left(qr, n, k, n - k, k + 1, n - k - 1, &qr[(k + 1) * n + k], n, tau);
         }
+    }
+    // colsPermutation (only the rank-deficient path needs it)
+    PMX_HD void permutation(int* perm) const {
         for (int i = 0; i < n; ++i) perm[i] = i;
         for (int k = 0; k < n; ++k) vswap(perm[k], perm[coltr[k]]);
     }
     PMX_HD int rank() const {
         const T thr = fabs(maxpivot) * ((T)n * eps<T>());
         int r = 0;
-        for (int i = 0; i < nonzero; ++i) r += fabs(qr[i * n + i]) > thr;
+        PMX_UNROLL
+        for (int i = 0; i < n; ++i)
+            if (i < nonzero) r += fabs(qr[i * n + i]) > thr;
         return r;
     }
     PMX_HD void matrixQ(T* Q) const {
@@ -305,13 +373,14 @@ PMX_HD int jacobi_svd(const T* A, int n, T* U, T* S, T* V) {
             nonzero = i;
             break;
         }
-        if (pos != i) {
-            vswap(S[i], S[pos]);
-            for (int r = 0; r < n; ++r) {
-                vswap(U[r * n + i], U[r * n + pos]);
-                vswap(V[r * n + i], V[r * n + pos]);
+        for (int j = i + 1; j < n; ++j)  // (static indices: see FullPivQR)
+            if (j == pos) {
+                vswap(S[i], S[j]);
+                for (int r = 0; r < n; ++r) {
+                    vswap(U[r * n + i], U[r * n + j]);
+                    vswap(V[r * n + i], V[r * n + j]);
+                }
             }
-        }
     }
     return nonzero;
 }
@@ -334,18 +403,29 @@ PMX_HD void svd_solve(const T* A, int n, const T* b, T* x) {
     }
 }
 
-// solvePossiblyUnderdeterminedLinearSystem (ErrorMinimizers/PointToPlane.cpp:108-161)
+// The full-rank branch: FullPivHouseholderQR(A).isInvertible() -> LLT solve
+// (PointToPlane.cpp:116-118, 159).  Returns false (x untouched) when A is
+// rank-deficient.
 template <typename T>
-PMX_HD void solve_underdetermined(const T* A, const T* b, int n, T* x) {
+PMX_HD bool solve_full_rank(const T* A, const T* b, int n, T* x) {
+    FullPivQR<T> qr;
+    qr.compute(A, n);
+    if (qr.rank() != n) return false;
+    T L[36];
+    llt(A, n, L);
+    llt_solve(L, n, b, x);
+    return true;
+}
+
+// The rank-deficient branch (PointToPlane.cpp:119-156): minimal-norm solution
+// of the rank-r reduced system, double JacobiSVD when that is inaccurate.
+template <typename T>
+PMX_HD void solve_rank_deficient(const T* A, const T* b, int n, T* x) {
     FullPivQR<T> qr;
     qr.compute(A, n);
     const int rank = qr.rank();
-    if (rank == n) {
-        T L[36];
-        llt(A, n, L);
-        llt_solve(L, n, b, x);
-        return;
-    }
+    int perm[6];
+    qr.permutation(perm);
     T Q[36], Q1t[36], QA[36], R1[36];
     qr.matrixQ(Q);
     for (int r = 0; r < rank; ++r)
@@ -357,7 +437,7 @@ PMX_HD void solve_underdetermined(const T* A, const T* b, int n, T* x) {
             QA[r * n + c] = s;
         }
     for (int r = 0; r < rank; ++r)
-        for (int c = 0; c < n; ++c) R1[r * n + c] = QA[r * n + qr.perm[c]];
+        for (int c = 0; c < n; ++c) R1[r * n + c] = QA[r * n + perm[c]];
     T RRt[36], Qb[6], y[6], L[36], xp[6];
     for (int i = 0; i < rank; ++i)
         for (int j = 0; j < rank; ++j) RRt[i * rank + j] = dot(&R1[i * n], &R1[j * n], n);
@@ -369,7 +449,7 @@ PMX_HD void solve_underdetermined(const T* A, const T* b, int n, T* x) {
         for (int r = 0; r < rank; ++r) s = s + ((c >= r) ? R1[r * n + c] : (T)0) * y[r];
         xp[c] = s;
     }
-    for (int i = 0; i < n; ++i) x[qr.perm[i]] = xp[i];
+    for (int i = 0; i < n; ++i) x[perm[i]] = xp[i];
     T dn = 0, bn = 0, an = 0;
     for (int r = 0; r < n; ++r) {
         const T ax = dot(&A[r * n], x, n);
@@ -386,6 +466,12 @@ PMX_HD void solve_underdetermined(const T* A, const T* b, int n, T* x) {
         svd_solve<double>(Ad, n, bd, xd);
         for (int i = 0; i < n; ++i) x[i] = (T)xd[i];
     }
+}
+
+// solvePossiblyUnderdeterminedLinearSystem (ErrorMinimizers/PointToPlane.cpp:108-161)
+template <typename T>
+PMX_HD void solve_underdetermined(const T* A, const T* b, int n, T* x) {
+    if (!solve_full_rank(A, b, n, x)) solve_rank_deficient(A, b, n, x);
 }
 
 // AngleAxis::toRotationMatrix (Eigen/src/Geometry/AngleAxis.h)

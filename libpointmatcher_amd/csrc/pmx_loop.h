@@ -54,6 +54,7 @@ struct LoopState {
     long long match_count;
     double level_cells[kMaxLevels];
     long long level_seen[kMaxLevels];
+    T xsolve[6];  // the rank-deficient solve's result (loop_solve_rank_deficient)
 };
 
 template <typename T>

@@ -66,14 +66,37 @@ __device__ void quat_of(const T* M, int rows, bool init2d, T* q) {
     quat_from_matrix(m3, q);
 }
 
-template <typename T>
-__global__ void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
+// The normal equations of the point-to-plane step as T (PointToPlane.cpp:230, 243)
+template <typename T, int NF>
+__device__ __forceinline__ void p2plane_system_of(const double* __restrict__ res, T* A, T* b) {
+    constexpr int NS = NF * (NF + 1) / 2;
+    int a = 0;
+    for (int i = 0; i < NF; ++i)
+        for (int j = i; j < NF; ++j, ++a) A[i * NF + j] = A[j * NF + i] = (T)res[a];
+    for (int i = 0; i < NF; ++i) b[i] = (T)(-res[NS + i]);
+}
+
+// Rank-deficient point-to-plane system: rare, kept out of line so that its
+// dynamically indexed work arrays do not push the hot path's into scratch.
+template <typename T, int NF>
+__device__ __noinline__ void loop_solve_rank_deficient(const double* __restrict__ res, T* __restrict__ xout) {
+    T A[36], b[6], x[6];
+    p2plane_system_of<T, NF>(res, A, b);
+    solve_rank_deficient(A, b, NF, x);
+    for (int i = 0; i < NF; ++i) xout[i] = x[i];
+}
+
+// ROWS is the homogeneous dimension (4 in 3-D, 3 in 2-D): with every size a
+// compile-time constant the dense kit's arrays live in VGPRs, not scratch
+// (a single lane walking scratch took ~75 us per iteration at C3).
+template <typename T, int ROWS>
+__global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
                                  const double* __restrict__ res, const int* __restrict__ iter_err,
                                  const unsigned long long* __restrict__ visited, const T* __restrict__ means,
                                  LoopCfg cfg, T* __restrict__ trace) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     if (ctl->done) return;
-    const int rows = cfg.rows, D = rows - 1;
+    constexpr int rows = ROWS, D = ROWS - 1;
     // statistics of the iteration (ErrorElements, ErrorMinimizer.cpp:133-192)
     double kept, nz, rejM, rejP, sw;
     if (cfg.minimizer == 0) {
@@ -112,13 +135,13 @@ __global__ void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __rest
     // the step transform
     T dT[16];
     if (cfg.minimizer == 0) {
-        const int NF = D == 3 ? 6 : 3, NS = NF * (NF + 1) / 2;
-        T A[36], b[6], x[6];
-        int a = 0;
-        for (int i = 0; i < NF; ++i)
-            for (int j = i; j < NF; ++j, ++a) A[i * NF + j] = A[j * NF + i] = (T)res[a];
-        for (int i = 0; i < NF; ++i) b[i] = (T)(-res[NS + i]);
-        solve_underdetermined(A, b, NF, x);
+        constexpr int NF = D == 3 ? 6 : 3;
+        T A[NF * NF], b[NF], x[NF];
+        p2plane_system_of<T, NF>(res, A, b);
+        if (!solve_full_rank(A, b, NF, x)) {
+            loop_solve_rank_deficient<T, NF>(res, S->xsolve);
+            for (int i = 0; i < NF; ++i) x[i] = S->xsolve[i];
+        }
         p2plane_transform(rows, x, dT);
     } else {
         T m[9], mp[3], mq[3];
@@ -273,8 +296,12 @@ template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
                       hipStream_t s) {
-    hipLaunchKernelGGL(loop_step_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, res, iter_err, visited, means, cfg,
-                       trace);
+    if (cfg.rows == 4)
+        hipLaunchKernelGGL((loop_step_kernel<T, 4>), dim3(1), dim3(64), 0, s, ctl, S, res, iter_err, visited, means,
+                           cfg, trace);
+    else
+        hipLaunchKernelGGL((loop_step_kernel<T, 3>), dim3(1), dim3(64), 0, s, ctl, S, res, iter_err, visited, means,
+                           cfg, trace);
 }
 
 template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg&, const float*, int, hipStream_t);
