@@ -87,6 +87,7 @@ struct pmx_ctx {
     std::vector<int64_t> level_seen;   // match count when it was seen (0: never)
     int64_t match_count = 0;
     bool adaptive = true;
+    bool hint_on = false;         // warm-start the grid match from the previous match (PMX_GRID_HINT=1: on)
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }
     std::vector<int32_t> slot_query;  // slot -> reading index (empty = identity)
@@ -111,6 +112,7 @@ struct pmx_ctx {
     void* d_part_d = nullptr;
     int32_t* d_part_i = nullptr;
     double Tstep[16] = {0};  // step transform (embedded 4x4, T values)
+    double Tprev[16] = {0};  // the previous match's (the grid match's warm start)
     bool have_match = false;
 
     // outlier weight chain (WChain): predicates recorded by the filter calls
@@ -675,7 +677,10 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         c->part_cap = pe;
     }
     Mat4<T> Tm = embed<T>(Titer, c->rows);
-    for (int i = 0; i < 16; ++i) c->Tstep[i] = (double)Tm.m[i];
+    for (int i = 0; i < 16; ++i) {
+        c->Tprev[i] = c->Tstep[i];  // (the previous match's: its warm start)
+        c->Tstep[i] = (double)Tm.m[i];
+    }
     const T md = (T)maxDist;
     const T maxR2 = md * md;  // libnabo squares the radius in T [ext]
     // reset the per-iteration error word and the pair / fallback counters
@@ -698,10 +703,17 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
     } else {
         if (e0) (void)hipEventRecord(e0, c->stream);
         const GridLevel& L = c->lv(c->level);
+        // warm start from the previous match of the same reading (same k):
+        // its ids are positions in the level it ran on (in loop mode the
+        // kernel takes that level from LoopCtl.hint_level)
+        Mat4<T> Tprev;
+        for (int i = 0; i < 16; ++i) Tprev.m[i] = (T)c->Tprev[i];
+        const bool hint = c->hint_on && c->have_match && c->ids_grid && c->knn == knn;
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
-                             c->d_iter_err, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+                             c->d_iter_err, hint ? &Tprev : nullptr, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc,
+                             c->stream);
         if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
         c->ids_grid = true;
@@ -1170,7 +1182,10 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     c->loop_dev = d;
     const int rr = c->rows * c->rows;
     HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, T0, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
-    launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, c->stream);
+    // warm start of the first loop match from the last classic one
+    const int hint = c->hint_on && c->have_match && c->ids_grid && c->knn == cfg->knn ? 1 : 0;
+    launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, hint, c->Tstep,
+                        c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));  // (T0 may be a stack buffer of the caller)
     c->loop_issued = 0;
@@ -1273,6 +1288,8 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
     c->loop_done = S.done != 0;
     c->level = ctl.level;
     c->ids_level = S.last_level;
+    if (S.iter > 0 || S.err)  // the last executed match's step transform (LoopCtl.T moved on)
+        for (int i = 0; i < 16; ++i) c->Tstep[i] = ctl.Tprev[i];
     // map the device error to the reference's exception and message
     int err = 0;
     std::string msg;
@@ -1388,6 +1405,9 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     }
     if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
+    // (measured on MI355X: -12 % match time at C3 with adaptive levels, but
+    // +15 % at C4 (k = 4); off until the per-query VALU cost is down)
+    if (const char* e = std::getenv("PMX_GRID_HINT")) c->hint_on = std::atoi(e) != 0;
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;

@@ -28,6 +28,33 @@ struct alignas(4 * sizeof(T)) P4 {
     T x, y, z, w;
 };
 
+// Loads through explicitly global pointers.  Pointers read from device
+// tables (the grid-level table of the device loop) are generic, and generic
+// loads compile to flat_load (which also waits on lgkmcnt, serialising with
+// LDS / scalar traffic); these helpers make every gather a global_load.
+template <typename T>
+struct Vec4Of;
+template <>
+struct Vec4Of<float> {
+    typedef float V __attribute__((ext_vector_type(4)));
+};
+template <>
+struct Vec4Of<double> {
+    typedef double V __attribute__((ext_vector_type(4)));
+};
+template <typename T>
+__device__ __forceinline__ P4<T> gld(const P4<T>* p, int64_t i) {
+    typedef typename Vec4Of<T>::V V;
+    const V v = ((const __attribute__((address_space(1))) V*)p)[i];
+    return P4<T>{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ uint32_t gld(const uint32_t* p, int64_t i) {
+    return ((const __attribute__((address_space(1))) uint32_t*)p)[i];
+}
+__device__ __forceinline__ int32_t gld(const int32_t* p, int64_t i) {
+    return ((const __attribute__((address_space(1))) int32_t*)p)[i];
+}
+
 template <typename T>
 struct Mat4 {
     T m[16];  // row-major
@@ -82,8 +109,10 @@ struct GridDesc {
 struct LoopCtl {
     int done;
     int level;
-    int pad[2];
+    int hint;  // the match output holds this reading's previous match (warm start, pmx_grid.hip)
+    int pad;
     double T[16];
+    double Tprev[16];  // the step transform of that previous match
 };
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
@@ -100,8 +129,8 @@ template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
-                       unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
-                       const GridDesc<T>* gd, hipStream_t s);
+                       unsigned long long* vpart, unsigned long long* vout, int* iter_err, const Mat4<T>* Tprev,
+                       const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 // spread pair / fallback counters of the grid kernels (bytes; zero-initialised once)
 size_t grid_counter_bytes();
 void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, int64_t n, hipStream_t s);

@@ -22,6 +22,10 @@ enum LoopErr {
     kLoopBound = -22,     // ConvergenceError("limit out of bounds ...")
 };
 
+struct Mat4d {
+    double m[16];
+};
+
 struct LoopCfg {
     int rows;       // 3 (2-D) or 4 (3-D)
     int minimizer;  // 0 point-to-plane, 1 point-to-point
@@ -58,7 +62,8 @@ struct LoopState {
 };
 
 template <typename T>
-void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, hipStream_t s);
+void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int hint,
+                      const double* Tprev, hipStream_t s);
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,

@@ -114,6 +114,9 @@ __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl
         sw = res[0];
     }
     S->last_level = ctl->level;  // the level whose positions this iteration's ids are
+    // the next match starts from this one's output and step transform
+    for (int i = 0; i < 16; ++i) ctl->Tprev[i] = ctl->T[i];
+    ctl->hint = 1;
     const int e = *iter_err;
     if (e) {
         loop_fail(ctl, S, e, kLoopError);
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl
 // reset the loop state for a new ICP (checkers' init, ICP.cpp:368-369)
 template <typename T>
 __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S, LoopCfg cfg,
-                                 const T* __restrict__ T0, int level) {
+                                 const T* __restrict__ T0, int level, int hint, Mat4d Tprev) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const int rows = cfg.rows, D = rows - 1;
     LoopState<T> z = {};
@@ -285,12 +288,17 @@ __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __rest
     }
     ctl->done = 0;
     ctl->level = level;
+    ctl->hint = hint;
+    for (int i = 0; i < 16; ++i) ctl->Tprev[i] = Tprev.m[i];
     loop_publish(ctl, S, rows);
 }
 
 template <typename T>
-void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, hipStream_t s) {
-    hipLaunchKernelGGL(loop_init_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, cfg, T0, level);
+void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int hint,
+                      const double* Tprev, hipStream_t s) {
+    Mat4d tp;
+    for (int i = 0; i < 16; ++i) tp.m[i] = Tprev[i];
+    hipLaunchKernelGGL(loop_init_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, cfg, T0, level, hint, tp);
 }
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
@@ -304,9 +312,10 @@ void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const in
                            cfg, trace);
 }
 
-template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg&, const float*, int, hipStream_t);
-template void launch_loop_init<double>(LoopCtl*, LoopState<double>*, const LoopCfg&, const double*, int,
-                                       hipStream_t);
+template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg&, const float*, int, int,
+                                      const double*, hipStream_t);
+template void launch_loop_init<double>(LoopCtl*, LoopState<double>*, const LoopCfg&, const double*, int, int,
+                                       const double*, hipStream_t);
 template void launch_loop_step<float>(LoopCtl*, LoopState<float>*, const double*, const int*,
                                       const unsigned long long*, const float*, const LoopCfg&, float*, hipStream_t);
 template void launch_loop_step<double>(LoopCtl*, LoopState<double>*, const double*, const int*,

@@ -131,8 +131,8 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
             for (int u = 0; u < U; ++u) {
                 kp[u] = i0 + u * stride < N && dv[u] != inf && chain_keep(wr, dv[u]);
                 const int32_t g = kp[u] ? id[u] : 0;  // (position 0 always exists)
-                q[u] = ref[g];
-                n[u] = nrm[g];
+                q[u] = gld(ref, g);
+                n[u] = gld(nrm, g);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
             exist = true;
             acc[NS + NF + 0] += 1.0;  // kept (= sum of the 0/1 weights)
             const int32_t id = ids[e];
-            p2plane_add<T, DIM, NV>(acc, px, py, pz, ref[id], nrm[id]);
+            p2plane_add<T, DIM, NV>(acc, px, py, pz, gld(ref, id), gld(nrm, id));
         }
         if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
     }
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restr
             }
             exist = true;
             acc[7] += 1.0;
-            const P4<T> q = ref[ids[e]];
+            const P4<T> q = gld(ref, ids[e]);
             // w = 1: p * w == p exactly
             acc[0] += 1.0;
             acc[1] += (double)px;
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
             const int64_t e = i * k + s;
             const T dv = d[e];
             if (dv == inf || !chain_keep(wr,dv)) continue;
-            const P4<T> q4 = ref[ids[e]];
+            const P4<T> q4 = gld(ref, ids[e]);
             const T q[3] = {q4.x, q4.y, q4.z};
             T pc[3], qc[3];
 #pragma unroll
