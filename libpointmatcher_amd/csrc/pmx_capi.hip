@@ -87,7 +87,10 @@ struct pmx_ctx {
     std::vector<int64_t> level_seen;   // match count when it was seen (0: never)
     int64_t match_count = 0;
     bool adaptive = true;
-    bool hint_on = false;         // warm-start the grid match from the previous match (PMX_GRID_HINT=1: on)
+    bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
+    bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
+    void* d_safe = nullptr;       // T[N]: safe radius per query
+    int64_t safe_cap = 0;
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }
     std::vector<int32_t> slot_query;  // slot -> reading index (empty = identity)
@@ -542,6 +545,9 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     if (rows != 3 && rows != 4) return fail(c, PMX_E_BAD_PARAM, "reference must have 3 (2-D) or 4 (3-D) rows");
     if (M <= 0) return fail(c, PMX_E_BAD_PARAM, "empty reference");
     if (M > (int64_t)0x7fffffff - kTile) return fail(c, PMX_E_BAD_PARAM, "reference larger than int32 ids");
+    // the grid kernels address the reference with 32-bit byte offsets
+    if ((M + kTile) * (int64_t)sizeof(P4<T>) >= ((int64_t)1 << 32))
+        return fail(c, PMX_E_BAD_PARAM, "reference larger than 4 GiB of points (268M float / 134M double)");
     const int D = rows - 1;
     const int64_t M_pad = ((M + kTile - 1) / kTile) * kTile;
     std::vector<P4<T>> h((size_t)M_pad);
@@ -662,7 +668,17 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         if ((rc = ensure(c, (void**)&c->d_ids, &capi, sizeof(int32_t) * (n > 0 ? n : 1)))) return rc;
         if ((rc = ensure(c, &c->d_w, &capw, sizeof(T) * (n > 0 ? n : 1)))) return rc;
         c->match_cap = n;
+        c->safe_valid = false;
         (void)cap;
+    }
+    if (c->reuse_on && (c->safe_cap < c->N || !c->d_safe)) {
+        if (c->d_safe) (void)hipFree(c->d_safe);
+        c->d_safe = nullptr;
+        size_t caps = 0;
+        int rc;
+        if ((rc = ensure(c, &c->d_safe, &caps, tsize(c) * (size_t)std::max<int64_t>(c->N, 1)))) return rc;
+        c->safe_cap = std::max<int64_t>(c->N, 1);
+        c->safe_valid = false;
     }
     const int64_t pe = match_part_elems<T>(c->N, c->M_pad, knn, c->cu_count);
     if (pe > c->part_cap) {
@@ -700,20 +716,26 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                         c->cu_count);
         c->visited_host = (uint64_t)c->N * (uint64_t)c->M;
         c->ids_grid = false;
+        c->safe_valid = false;
     } else {
         if (e0) (void)hipEventRecord(e0, c->stream);
         const GridLevel& L = c->lv(c->level);
         // warm start from the previous match of the same reading (same k):
         // its ids are positions in the level it ran on (in loop mode the
         // kernel takes that level from LoopCtl.hint_level)
-        Mat4<T> Tprev;
-        for (int i = 0; i < 16; ++i) Tprev.m[i] = (T)c->Tprev[i];
-        const bool hint = c->hint_on && c->have_match && c->ids_grid && c->knn == knn;
+        // temporal reuse: the output buffers hold this reading's previous
+        // match (same k, same level) with its safe radii
+        GridReuse<T> ru;
+        if (c->reuse_on && c->grid_mode >= 1) {
+            ru.mode = c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && c->ids_level == c->level ? 2 : 1;
+            ru.safe = (T*)c->d_safe;
+            for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
+        }
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
-                             c->d_iter_err, hint ? &Tprev : nullptr, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc,
-                             c->stream);
+                             c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+        c->safe_valid = ru.mode != 0;
         if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
         c->ids_grid = true;
@@ -765,10 +787,20 @@ const void* match_nrm(const pmx_ctx* c) { return c->ids_grid ? c->lv(c->ids_leve
 // beyond ~24 cells the search walked outer shells (misaligned clouds, large
 // k) and the next coarser level is cheaper; below ~5 a finer one is.  Any
 // level gives the identical exact result.
-void choose_level(pmx_ctx* c, uint64_t visited) {
+// With temporal reuse the level is judged on the full searches only (a
+// certified query evaluates its k pairs whatever the level), and kept while
+// fewer than 1/16 of the queries needed one: a level change restarts the
+// reuse chain.
+void choose_level(pmx_ctx* c, uint64_t visited, uint64_t full) {
     if (!c->adaptive || !c->ids_grid || c->levels.size() < 2 || c->N <= 0 || c->knn <= 0) return;
     const int l = c->ids_level;
-    const double cells = (double)visited / ((double)c->N * c->lv(l).ppc);
+    double q = (double)c->N, v = (double)visited;
+    if (c->safe_valid) {
+        if ((double)full * 16.0 < q) return;
+        v -= (double)c->knn * (q - (double)full);
+        q = (double)full;
+    }
+    const double cells = v / (q * c->lv(l).ppc);
     ++c->match_count;
     c->level_cells[(size_t)l] = cells;
     c->level_seen[(size_t)l] = c->match_count;
@@ -966,9 +998,10 @@ void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double 
 // after a readback: adapt the grid level of the next match
 void after_readback(pmx_ctx* c) {
     if (c->visited_host || c->no_visits) return;
-    unsigned long long v = 0;
+    unsigned long long v = 0, f = 0;
     std::memcpy(&v, (const char*)c->h_result + kBlkVisited, sizeof(v));
-    choose_level(c, v);
+    std::memcpy(&f, (const char*)c->h_result + kBlkVisited + 8, sizeof(f));
+    choose_level(c, v, f);
 }
 
 // the point-to-plane system into the iteration block (no host sync)
@@ -1167,6 +1200,8 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
         for (int j = 0; j < 3; ++j) d.checker_p[i][j] = cfg->checker_p[i][j];
     }
     d.adaptive = c->adaptive && !c->no_visits ? 1 : 0;
+    d.reuse = c->reuse_on && c->grid_mode >= 1 ? 1 : 0;
+    d.knn = cfg->knn;
     d.n_levels = (int)c->levels.size();
     for (int l = 0; l < d.n_levels; ++l) d.level_ppc[l] = c->lv(l).ppc;
     d.n_local = c->N;
@@ -1182,10 +1217,11 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     c->loop_dev = d;
     const int rr = c->rows * c->rows;
     HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, T0, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
-    // warm start of the first loop match from the last classic one
-    const int hint = c->hint_on && c->have_match && c->ids_grid && c->knn == cfg->knn ? 1 : 0;
-    launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, hint, c->Tstep,
-                        c->stream);
+    // the first loop match may reuse the last classic one
+    const int prev_level =
+        c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn ? c->ids_level : -1;
+    launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, prev_level,
+                        c->Tstep, c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));  // (T0 may be a stack buffer of the caller)
     c->loop_issued = 0;
@@ -1405,9 +1441,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     }
     if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
-    // (measured on MI355X: -12 % match time at C3 with adaptive levels, but
-    // +15 % at C4 (k = 4); off until the per-query VALU cost is down)
-    if (const char* e = std::getenv("PMX_GRID_HINT")) c->hint_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
@@ -1458,7 +1492,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (!c) return PMX_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
+    void* bufs[] = {c->d_safe, c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace};

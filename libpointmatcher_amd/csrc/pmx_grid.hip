@@ -80,7 +80,7 @@ __device__ __forceinline__ double vmin(double a, double b) { return fmin(a, b); 
 __device__ __forceinline__ bool tie_first(const int32_t* __restrict__ gidx, int32_t a, int32_t b) {
     if (b == kNoPos) return true;
     if (a == kNoPos) return false;
-    return gld(gidx, a) < gld(gidx, b);
+    return gld32(gidx, (uint32_t)a) < gld32(gidx, (uint32_t)b);
 }
 
 template <typename T, int KT>
@@ -110,6 +110,20 @@ __device__ __forceinline__ void consider(const int32_t* __restrict__ gidx, int32
     }
 }
 
+// the k-th entry of a k-list (k <= KT; static indexing keeps the list in
+// registers)
+template <typename T, int KT>
+__device__ __forceinline__ void kth(const T (&kd)[KT], const int32_t (&ki)[KT], int k, T& dk, int32_t& ik) {
+    dk = kd[0];
+    ik = ki[0];
+#pragma unroll
+    for (int s = 1; s < KT; ++s)
+        if (s == k - 1) {
+            dk = kd[s];
+            ik = ki[s];
+        }
+}
+
 // Scan one contiguous point range of gpts (per-lane search).  Latency-bound:
 // points are fetched kScanU at a time with independent loads; a short row
 // (a few points at the default density) is one masked chunk — a scalar tail
@@ -137,7 +151,7 @@ __device__ __forceinline__ void scan_range(const P4<T>* __restrict__ gpts, const
     for (uint32_t j = a; j < b; j += U) {
         P4<T> p[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) p[u] = gld(gpts, j + u < b ? j + u : a);  // in-range address either way
+        for (int u = 0; u < U; ++u) p[u] = gld32(gpts, j + u < b ? j + u : a);  // in-range address either way
         T d[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = gsqd(qx, qy, qz, p[u]);
@@ -164,7 +178,7 @@ __device__ __forceinline__ void cell_of_q(const GridGeom& G, const double q[3], 
 template <typename T, int KT>
 __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                                               const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy,
-                                              T qz, const double q[3], const int c[3], T maxR2, T (&kd)[KT],
+                                              T qz, const double q[3], const int c[3], T maxR2, int k, T (&kd)[KT],
                                               int32_t (&ki)[KT], uint32_t& visits) {
     int b0[3], b1[3];
 #pragma unroll
@@ -179,9 +193,9 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
     for (int r = 0; r < 4; ++r) {
         const int y = (r & 1) ? b1[1] : b0[1], z = (r & 2) ? b1[2] : b0[2];
         const bool ok = !((r & 1) && b1[1] == b0[1]) && !((r & 2) && b1[2] == b0[2]);  // no duplicate rows
-        const int64_t row = ((int64_t)z * G.g[1] + y) * G.g[0];
-        const uint32_t va = gld(start, row + b0[0]);
-        const uint32_t vb = gld(start, row + b1[0] + 1);
+        const uint32_t row = ((uint32_t)z * (uint32_t)G.g[1] + (uint32_t)y) * (uint32_t)G.g[0];
+        const uint32_t va = gld32(start, row + b0[0]);
+        const uint32_t vb = gld32(start, row + b1[0] + 1);
         ra[r] = ok ? va : 0u;
         rb[r] = ok ? vb : 0u;
     }
@@ -192,7 +206,7 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t j = ra[r] + u;
-            p[r][u] = gld(gpts, j < rb[r] ? j : 0u);  // masked: any in-range address
+            p[r][u] = gld32(gpts, j < rb[r] ? j : 0u);  // masked: any in-range address
         }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -223,18 +237,25 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
     if (!any) return true;  // the block is the whole grid
     if (lb > 0.0) {
         const double lb2 = lb * lb * (1.0 - 1e-5);
-        if (((double)kd[KT - 1] < lb2 && ki[KT - 1] != kNoPos) || lb2 > (double)maxR2) return true;
+        T dk;
+        int32_t ik;
+        kth(kd, ki, k, dk, ik);
+        if (((double)dk < lb2 && ik != kNoPos) || lb2 > (double)maxR2) return true;
     }
     return false;
 }
 
-// exact shell search for one query (from scratch); kd/ki must be initialised
+// Exact shell search for one query (from scratch); kd/ki must be
+// initialised.  Certified on the k-th entry of the list (entries past k, when
+// KT > k, are the next-nearest points visited).  lb_exit: the distance from
+// the query to the unvisited region at exit (1e300: the whole grid).
 template <typename T, int KT>
 __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                             const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy, T qz,
-                            const double q[3], const int c[3], T maxR2, T (&kd)[KT], int32_t (&ki)[KT],
-                            uint32_t& visits) {
+                            const double q[3], const int c[3], T maxR2, int k, T (&kd)[KT], int32_t (&ki)[KT],
+                            uint32_t& visits, double& lb_exit) {
     const double margin = 1.0 - 1e-5;
+    lb_exit = 1e300;
     {
         // phase 1: the whole 3x3x3 block (R = 0 and 1).  The nine row
         // bounds are loaded together from always-valid (clamped)
@@ -246,9 +267,9 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
             const int z = c[2] + r / 3 - 1, y = c[1] + r % 3 - 1;
             const bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
             const int zc = min(max(z, 0), G.g[2] - 1), yc = min(max(y, 0), G.g[1] - 1);
-            const int64_t row = ((int64_t)zc * G.g[1] + yc) * G.g[0];
-            const uint32_t va = gld(start, row + x0);
-            const uint32_t vb = gld(start, row + x1 + 1);
+            const uint32_t row = ((uint32_t)zc * (uint32_t)G.g[1] + (uint32_t)yc) * (uint32_t)G.g[0];
+            const uint32_t va = gld32(start, row + x0);
+            const uint32_t vb = gld32(start, row + x1 + 1);
             ra[r] = ok ? va : 0u;
             rb[r] = ok ? vb : 0u;
         }
@@ -264,7 +285,7 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const uint32_t j = ra[g + rr] + u;
-                    p[rr][u] = gld(gpts, j < rb[g + rr] ? j : 0u);  // masked: any in-range address
+                    p[rr][u] = gld32(gpts, j < rb[g + rr] ? j : 0u);  // masked: any in-range address
                 }
 #pragma unroll
             for (int rr = 0; rr < GR; ++rr) {
@@ -292,16 +313,16 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
                 const bool zface = (z == c[2] - R) || (z == c[2] + R);
                 for (int y = y0; y <= y1; ++y) {
                     const bool yface = (y == c[1] - R) || (y == c[1] + R);
-                    const int64_t row = ((int64_t)z * G.g[1] + y) * G.g[0];
+                    const uint32_t row = ((uint32_t)z * (uint32_t)G.g[1] + (uint32_t)y) * (uint32_t)G.g[0];
                     if (zface || yface) {
-                        scan_range<T, KT>(gpts, gidx, gld(start, row + x0), gld(start, row + x1 + 1), qx, qy, qz, kd, ki,
+                        scan_range<T, KT>(gpts, gidx, gld32(start, row + x0), gld32(start, row + x1 + 1), qx, qy, qz, kd, ki,
                                           visits);
                     } else {
                         if (c[0] - R >= 0)
-                            scan_range<T, KT>(gpts, gidx, gld(start, row + c[0] - R), gld(start, row + c[0] - R + 1), qx, qy,
+                            scan_range<T, KT>(gpts, gidx, gld32(start, row + c[0] - R), gld32(start, row + c[0] - R + 1), qx, qy,
                                               qz, kd, ki, visits);
                         if (c[0] + R <= G.g[0] - 1)
-                            scan_range<T, KT>(gpts, gidx, gld(start, row + c[0] + R), gld(start, row + c[0] + R + 1), qx, qy,
+                            scan_range<T, KT>(gpts, gidx, gld32(start, row + c[0] + R), gld32(start, row + c[0] + R + 1), qx, qy,
                                               qz, kd, ki, visits);
                     }
                 }
@@ -322,10 +343,14 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
                 any = true;
             }
         }
+        lb_exit = any ? lb : 1e300;
         if (!any) break;  // the whole grid has been visited
         if (lb > 0.0) {
             const double lb2 = lb * lb * margin;
-            if ((double)kd[KT - 1] < lb2 && ki[KT - 1] != kNoPos) break;
+            T dk;
+            int32_t ik;
+            kth(kd, ki, k, dk, ik);
+            if ((double)dk < lb2 && ik != kNoPos) break;
             if (lb2 > (double)maxR2) break;
         }
     }
@@ -399,109 +424,45 @@ __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long
 }
 size_t grid_counter_bytes() { return sizeof(unsigned long long) * 2 * kVSlots * kVStride; }
 
-// Warm-start search (the ICP loop matches nearly the same queries every
-// iteration).  The previous match of this query, at its previous position
-// q' = T_prev * p, found k points within sqrt(d_prev) (its k-th distance);
-// they are now within sqrt(d_prev) + |q - q'| of the query, so the k-th
-// neighbour is inside the cube of that half-side r (capped at maxDist).  When
-// the cube covers at most 2 cells per axis its (<= 4) rows are scanned and
-// the result is certified exactly as the octant search certifies its block:
-// the k-th distance below the squared distance to the nearest interior face
-// of the visited block, with the 1e-5 relative margin.  The certificate alone
-// makes the result exact — r only chooses the block — so a stale or poor
-// hint merely sends the query to the fallback.  Nothing extra is fetched:
-// d_prev is the query's own output slot, q' is recomputed from the reading
-// point already in registers.  Returns true when the k-list is final; on
-// false the caller restarts from an empty list.
-// cells the warm-start block may span along x (one contiguous range per row)
-#ifndef PMX_HINT_SPAN_X
-#define PMX_HINT_SPAN_X 2
-#endif
-constexpr int kHintSpanX = PMX_HINT_SPAN_X;
-#ifndef PMX_HINT_G
-#define PMX_HINT_G 2
-#endif
-constexpr int kHintG = PMX_HINT_G;  // rows fetched together
-static_assert(4 % kHintG == 0, "hint row groups must tile the four rows");
+// ---------------------------------------------------- temporal reuse --
+// ICP matches the same reading every iteration under a slowly changing
+// transform.  A full search of query q' (previous position) leaves two
+// facts: its k-list, whose k-th squared distance is dk', and a safe radius
+// rs' — every reference point outside the k-list is at least rs' from q'
+// (rs' = min(distance to the unvisited region at exit, distance of the
+// (k+1)-th point visited)).  At the new position q = q' + delta:
+//   the k-list points are within  a = sqrt(dk') + |delta|,
+//   every other point is beyond   b = rs' - |delta|,
+// so when a < b (with 1e-5 relative margins, far above the T rounding of
+// any distance involved) the k nearest neighbours of q are exactly the
+// previous k-list.  Their distances are recomputed in T (the same arithmetic
+// a full search uses) and re-sorted with the (distance, original index)
+// rule, so the output is bit-identical to a full search; the new safe radius
+// is b.  Queries that fail the test (moved too far, previous list
+// incomplete, grid level changed) take the full search.  Only the certificate
+// decides the result: no cached answer is ever returned unverified.
+//
+// reuse: 0 = off, 1 = store safe radii only (no usable previous match),
+//        2 = store and try the certificate (out_d/out_i/safe hold the
+//            previous match of this reading at this level, made at Tprev).
+constexpr double kReuseMargin = 1e-5;
+
+// safe radius of a full search: the unvisited region and the (k+1)-th
+// visited point (list entry k, when KT > k) bound every non-neighbour
 template <typename T, int KT>
-__device__ __forceinline__ bool hint_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
-                                            const uint32_t* __restrict__ start, const GridGeom& G, double r, int k,
-                                            T qx, T qy, T qz, const double q[3], T maxR2, T (&kd)[KT],
-                                            int32_t (&ki)[KT], uint32_t& visits) {
-    int b0[3], b1[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const double f0 = (q[a] - r - G.lo[a]) * G.inv_h, f1 = (q[a] + r - G.lo[a]) * G.inv_h;
-        b0[a] = f0 < 0.0 ? 0 : (f0 >= (double)G.g[a] ? G.g[a] - 1 : (int)f0);
-        b1[a] = f1 < 0.0 ? 0 : (f1 >= (double)G.g[a] ? G.g[a] - 1 : (int)f1);
-        if (b1[a] - b0[a] > (a == 0 ? kHintSpanX : 1)) return false;
-    }
-    uint32_t ra[4], rb[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const int y = (rr & 1) ? b1[1] : b0[1], z = (rr & 2) ? b1[2] : b0[2];
-        const bool use = !((rr & 1) && b1[1] == b0[1]) && !((rr & 2) && b1[2] == b0[2]);  // no duplicate rows
-        const int64_t row = ((int64_t)z * G.g[1] + y) * G.g[0];
-        const uint32_t va = gld(start, row + b0[0]);
-        const uint32_t vb = gld(start, row + b1[0] + 1);
-        ra[rr] = use ? va : 0u;
-        rb[rr] = use ? vb : 0u;
-    }
-    // rows in groups of kHintG: the first kP1U points of every row of a group
-    // are fetched together, longer rows finish with chunked scans
-    constexpr int U = kP1U, GR = kHintG;
-#pragma unroll
-    for (int g = 0; g < 4; g += GR) {
-        P4<T> p[GR][U];
-#pragma unroll
-        for (int rr = 0; rr < GR; ++rr)
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t j = ra[g + rr] + u;
-                p[rr][u] = gld(gpts, j < rb[g + rr] ? j : 0u);  // masked: any in-range address
-            }
-#pragma unroll
-        for (int rr = 0; rr < GR; ++rr) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t j = ra[g + rr] + u;
-                if (j < rb[g + rr]) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, p[rr][u]), kd, ki);
-            }
-            visits += rb[g + rr] - ra[g + rr];
-            if (ra[g + rr] + U < rb[g + rr]) {
-                uint32_t v0 = 0;
-                scan_range<T, KT>(gpts, gidx, ra[g + rr] + U, rb[g + rr], qx, qy, qz, kd, ki, v0);
-            }
-        }
-    }
-    // the k-th entry (static indexing keeps the list in registers)
-    T dk = kd[0];
-    int32_t ik = ki[0];
+__device__ __forceinline__ T safe_radius(const T (&kd)[KT], const int32_t (&ki)[KT], int k, double lb_exit) {
+    double r = lb_exit;
+    T dn = (T)__builtin_huge_val();
 #pragma unroll
     for (int s = 1; s < KT; ++s)
-        if (s == k - 1) {
-            dk = kd[s];
-            ik = ki[s];
-        }
-    double lb = 1e300;
-    bool any = false;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        if (b0[a] > 0) {
-            lb = fmin(lb, q[a] - (G.lo[a] + (double)b0[a] * G.h));
-            any = true;
-        }
-        if (b1[a] < G.g[a] - 1) {
-            lb = fmin(lb, (G.lo[a] + (double)(b1[a] + 1) * G.h) - q[a]);
-            any = true;
-        }
-    }
-    if (!any) return true;  // the block is the whole grid
-    if (lb > 0.0) {
-        const double lb2 = lb * lb * (1.0 - 1e-5);
-        if (((double)dk < lb2 && ik != kNoPos) || lb2 > (double)maxR2) return true;
-    }
-    return false;
+        if (s == k) dn = kd[s];
+    if (k >= KT) r = -1.0;  // (no room for the next point: never certify)
+    r = fmin(r, sqrt((double)dn));
+    T dk;
+    int32_t ik;
+    kth(kd, ki, k, dk, ik);
+    if (ik == kNoPos || !(r > 0.0)) return (T)0;
+    return (T)(r * (1.0 - 1e-6));  // (rounded down into T)
 }
 
 // one query from scratch: octant block (oct) or the shell search
@@ -510,7 +471,7 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
                                            const uint32_t* __restrict__ start, const GridGeom& G,
                                            const P4<T>* __restrict__ rd, int64_t j, const Mat4<T>& Tm, int k,
                                            T maxR2, int oct, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                           uint32_t& visits) {
+                                           T* __restrict__ safe, uint32_t& visits) {
     T qx, qy, qz;
     gxform(Tm, gld(rd, j), qx, qy, qz);
     T kd[KT];
@@ -524,19 +485,62 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
     int c[3];
     bool qnan;
     cell_of_q(G, q, c, qnan);
+    double lb_exit = -1.0;
     if (!qnan) {
         bool done = false;
-        if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, kd, ki, visits);
+        if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits);
         if (!done) {
 #pragma unroll
             for (int s = 0; s < KT; ++s) {  // (a k-list must not see the octant's points twice)
                 kd[s] = (T)__builtin_huge_val();
                 ki[s] = kNoPos;
             }
-            lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, kd, ki, visits);
+            lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit);
         }
     }
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i);
+    if (safe) safe[j] = oct ? (T)0 : safe_radius<T, KT>(kd, ki, k, lb_exit);
+}
+
+// the certificate for query j; true when the k-list was rewritten from the
+// previous one
+template <typename T, int KT>
+__device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
+                                            const P4<T>& p, T qx, T qy, T qz, const Mat4<T>& Tprev, int64_t j,
+                                            int k, T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
+                                            T* __restrict__ safe, uint32_t& visits) {
+    const T rs = safe[j];
+    const T dkp = out_d[j * k + k - 1];
+    int32_t id[KT];
+    bool ok = rs > (T)0 && dkp < (T)__builtin_huge_val();
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+        id[s] = s < k ? out_i[j * k + s] : 0;
+        ok = ok && id[s] >= 0;
+    }
+    if (!ok) return false;
+    T ox, oy, oz;
+    gxform(Tprev, p, ox, oy, oz);
+    const double ex = (double)qx - (double)ox, ey = (double)qy - (double)oy, ez = (double)qz - (double)oz;
+    const double delta = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + kReuseMargin);
+    const double a = sqrt((double)dkp) * (1.0 + kReuseMargin) + delta;
+    const double b = (double)rs * (1.0 - kReuseMargin) - delta;
+    if (!(a < b)) return false;
+    // the same k points: new distances, sorted as a full search sorts them
+    T kd[KT];
+    int32_t ki[KT];
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+        kd[s] = (T)__builtin_huge_val();
+        ki[s] = kNoPos;
+    }
+#pragma unroll
+    for (int s = 0; s < KT; ++s)
+        if (s < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx, qy, qz, gld32(gpts, (uint32_t)id[s])), id[s]);
+    visits += (uint32_t)k;
+    write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i);
+    safe[j] = (T)(b * (1.0 - 1e-6));
+    return true;
 }
 
 // ------------------------------------------------------- per-lane kernel --
@@ -547,9 +551,10 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
                                                         T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
                                                         unsigned long long* __restrict__ visited, int oct,
-                                                        int hint, Mat4<T> Tprev, const LoopCtl* __restrict__ ctl,
+                                                        int reuse, T* __restrict__ safe, Mat4<T> Tprev,
+                                                        const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd) {
-    if (ctl) {  // device loop: transform, level and warm start from the device
+    if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
         gpts = D.gpts;
@@ -557,23 +562,27 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
         start = D.start;
         G = D.G;
         ctl_transform(ctl, Tm);
-        hint = hint && ctl->hint;
-        if (hint) {
+        if (reuse) {
+            reuse = ctl->prev_level == ctl->level ? 2 : 1;
 #pragma unroll
             for (int i = 0; i < 16; ++i) Tprev.m[i] = (T)ctl->Tprev[i];
         }
     }
-
+    if (!reuse) safe = nullptr;
     uint32_t visits = 0;
-    if (!hint) {
+    if (reuse < 2) {
         const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (j < N) full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, maxR2, oct, out_d, out_i, visits);
+        if (j < N) full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, maxR2, oct, out_d, out_i, safe, visits);
         add_visits(visits, visited);
+        if (reuse) {  // every query took the full search (the counter the level choice reads)
+            const unsigned long long m = __ballot(j < N);
+            if ((threadIdx.x & 63) == 0 && visited && m) atomicAdd(vslot(visited, 1), (unsigned long long)__popcll(m));
+        }
         return;
     }
-    // Warm start.  Phase 1: every lane tries its hint block.  Phase 2: the
-    // block's misses, compacted in slot order, run the full search with
-    // consecutive lanes — a miss no longer makes its whole wave pay for both.
+    // Phase 1: every lane tries the certificate.  Phase 2: the block's misses,
+    // compacted in slot order, run the full search on consecutive lanes (a
+    // miss does not make its whole wave pay for both paths).
     __shared__ int miss[256];
     __shared__ int wave_cnt[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -581,32 +590,9 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
     bool missed = false;
     if (j < N) {
         const P4<T> p = gld(rd, j);
-        // the previous k-th distance of this query (read before write_out
-        // overwrites it)
-        const T dprev = out_d[j * k + k - 1];
         T qx, qy, qz;
         gxform(Tm, p, qx, qy, qz);
-        T kd[KT];
-        int32_t ki[KT];
-#pragma unroll
-        for (int s = 0; s < KT; ++s) {
-            kd[s] = (T)__builtin_huge_val();
-            ki[s] = kNoPos;
-        }
-        const double q[3] = {(double)qx, (double)qy, (double)qz};
-        bool done = false;
-        if (dprev < (T)__builtin_huge_val() && q[0] == q[0] && q[1] == q[1] && q[2] == q[2]) {
-            T ox, oy, oz;
-            gxform(Tprev, p, ox, oy, oz);
-            const double ex = q[0] - (double)ox, ey = q[1] - (double)oy, ez = q[2] - (double)oz;
-            double r = (sqrt((double)dprev) + sqrt(ex * ex + ey * ey + ez * ez)) * (1.0 + 1e-4);
-            r = fmin(r, sqrt((double)maxR2) * (1.0 + 2e-5));
-            done = hint_search<T, KT>(gpts, gidx, start, G, r, k, qx, qy, qz, q, maxR2, kd, ki, visits);
-        }
-        if (done)
-            write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i);
-        else
-            missed = true;
+        missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, maxR2, out_d, out_i, safe, visits);
     }
     const unsigned long long m = __ballot(missed);
     if (lane == 0) wave_cnt[wave] = __popcll(m);
@@ -622,10 +608,10 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
     __syncthreads();
     if ((int)threadIdx.x < total) {
         const int64_t j2 = (int64_t)blockIdx.x * blockDim.x + miss[threadIdx.x];
-        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, maxR2, oct, out_d, out_i, visits);
+        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, maxR2, oct, out_d, out_i, safe, visits);
     }
     add_visits(visits, visited);
-    // queries whose warm start fell back (the "fallback" counter)
+    // queries that took the full search (the "fallback" counter)
     if (threadIdx.x == 0 && visited && total) atomicAdd(vslot(visited, 1), (unsigned long long)total);
 }
 
@@ -636,11 +622,11 @@ template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
-                      const Mat4<T>* Tprev, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
+                      const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
     if (mode >= 1) {  // 1: shell search, 2: octant block first
         hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
-                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, Tprev ? 1 : 0,
-                           Tprev ? *Tprev : Tm, ctl, gd);
+                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe,
+                           ru.Tprev, ctl, gd);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -653,7 +639,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
-                       const Mat4<T>* Tprev, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
+                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
     if (N <= 0) return;
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -664,14 +650,16 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     Tprev, ctl, gd, s)
-    if (knn == 1)
+                     ru, ctl, gd, s)
+    // with reuse the list keeps room for the (k+1)-th point (the safe radius)
+    const int kl = ru.mode && mode >= 1 && knn < 16 ? knn + 1 : knn;
+    if (kl == 1)
         PMX_KT(1);
-    else if (knn <= 2)
+    else if (kl <= 2)
         PMX_KT(2);
-    else if (knn <= 4)
+    else if (kl <= 4)
         PMX_KT(4);
-    else if (knn <= 8)
+    else if (kl <= 8)
         PMX_KT(8);
     else
         PMX_KT(16);
@@ -683,12 +671,12 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
 template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, const uint32_t*, const double*, double,
                                        const int*, const P4<float>*, int64_t, const uint32_t*, int64_t,
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
-                                       unsigned long long*, unsigned long long*, int*, const Mat4<float>*,
+                                       unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
-                                        unsigned long long*, unsigned long long*, int*, const Mat4<double>*,
+                                        unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices

@@ -48,6 +48,22 @@ __device__ __forceinline__ P4<T> gld(const P4<T>* p, int64_t i) {
     const V v = ((const __attribute__((address_space(1))) V*)p)[i];
     return P4<T>{v.x, v.y, v.z, v.w};
 }
+// 32-bit element index: the byte offset stays 32-bit, so the load is
+// `global_load v, v_off, s[base]` (no 64-bit address arithmetic per lane).
+// Callers guarantee count * sizeof(element) < 4 GiB (pmx_set_reference
+// checks the reference; the grid arrays are sized from it).
+template <typename T>
+__device__ __forceinline__ P4<T> gld32(const P4<T>* p, uint32_t i) {
+    typedef typename Vec4Of<T>::V V;
+    const uint32_t off = i * (uint32_t)sizeof(P4<T>);
+    const V v = *(const __attribute__((address_space(1))) V*)((const __attribute__((address_space(1))) char*)p + off);
+    return P4<T>{v.x, v.y, v.z, v.w};
+}
+template <typename E>
+__device__ __forceinline__ E gld32(const E* p, uint32_t i) {
+    const uint32_t off = i * (uint32_t)sizeof(E);
+    return *(const __attribute__((address_space(1))) E*)((const __attribute__((address_space(1))) char*)p + off);
+}
 __device__ __forceinline__ uint32_t gld(const uint32_t* p, int64_t i) {
     return ((const __attribute__((address_space(1))) uint32_t*)p)[i];
 }
@@ -109,10 +125,18 @@ struct GridDesc {
 struct LoopCtl {
     int done;
     int level;
-    int hint;  // the match output holds this reading's previous match (warm start, pmx_grid.hip)
+    int prev_level;  // level of the match the output buffers hold (-1: none; temporal reuse, pmx_grid.hip)
     int pad;
     double T[16];
     double Tprev[16];  // the step transform of that previous match
+};
+// temporal reuse of the grid match (pmx_grid.hip): mode 0 off, 1 store the
+// safe radii, 2 store and certify from the previous match made at Tprev
+template <typename T>
+struct GridReuse {
+    int mode = 0;
+    T* safe = nullptr;
+    Mat4<T> Tprev{};
 };
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
@@ -129,7 +153,7 @@ template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
-                       unsigned long long* vpart, unsigned long long* vout, int* iter_err, const Mat4<T>* Tprev,
+                       unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 // spread pair / fallback counters of the grid kernels (bytes; zero-initialised once)
 size_t grid_counter_bytes();

@@ -37,6 +37,8 @@ struct LoopCfg {
     int n_levels;
     double level_ppc[kMaxLevels];
     int64_t n_local;
+    int reuse;  // the grid match's temporal reuse is on (level choice on full searches only)
+    int knn;
 };
 
 template <typename T>
@@ -62,7 +64,7 @@ struct LoopState {
 };
 
 template <typename T>
-void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int hint,
+void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int prev_level,
                       const double* Tprev, hipStream_t s);
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,

@@ -114,9 +114,9 @@ __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl
         sw = res[0];
     }
     S->last_level = ctl->level;  // the level whose positions this iteration's ids are
-    // the next match starts from this one's output and step transform
+    // the next match may reuse this one's output (pmx_grid.hip temporal reuse)
     for (int i = 0; i < 16; ++i) ctl->Tprev[i] = ctl->T[i];
-    ctl->hint = 1;
+    ctl->prev_level = ctl->level;
     const int e = *iter_err;
     if (e) {
         loop_fail(ctl, S, e, kLoopError);
@@ -243,9 +243,19 @@ __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl
         return;
     }
     // grid level of the next match (pmx_capi.hip choose_level)
-    if (cfg.adaptive && cfg.n_levels > 1 && cfg.n_local > 0) {
+    // (with reuse: judged on the full searches only, kept while fewer than
+    // 1/16 of the queries needed one — the rule of choose_level)
+    double q = (double)cfg.n_local, v = (double)visited[0];
+    bool adapt = cfg.adaptive && cfg.n_levels > 1 && cfg.n_local > 0;
+    if (adapt && cfg.reuse) {
+        const double full = (double)visited[1];
+        adapt = full * 16.0 >= q;
+        v -= (double)cfg.knn * (q - full);
+        q = full;
+    }
+    if (adapt) {
         const int l = ctl->level;
-        const double cells = (double)visited[0] / ((double)cfg.n_local * cfg.level_ppc[l]);
+        const double cells = v / (q * cfg.level_ppc[l]);
         ++S->match_count;
         S->level_cells[l] = cells;
         S->level_seen[l] = S->match_count;
@@ -264,7 +274,7 @@ __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl
 // reset the loop state for a new ICP (checkers' init, ICP.cpp:368-369)
 template <typename T>
 __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S, LoopCfg cfg,
-                                 const T* __restrict__ T0, int level, int hint, Mat4d Tprev) {
+                                 const T* __restrict__ T0, int level, int prev_level, Mat4d Tprev) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const int rows = cfg.rows, D = rows - 1;
     LoopState<T> z = {};
@@ -288,17 +298,17 @@ __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __rest
     }
     ctl->done = 0;
     ctl->level = level;
-    ctl->hint = hint;
+    ctl->prev_level = prev_level;
     for (int i = 0; i < 16; ++i) ctl->Tprev[i] = Tprev.m[i];
     loop_publish(ctl, S, rows);
 }
 
 template <typename T>
-void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int hint,
+void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int prev_level,
                       const double* Tprev, hipStream_t s) {
     Mat4d tp;
     for (int i = 0; i < 16; ++i) tp.m[i] = Tprev[i];
-    hipLaunchKernelGGL(loop_init_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, cfg, T0, level, hint, tp);
+    hipLaunchKernelGGL(loop_init_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, cfg, T0, level, prev_level, tp);
 }
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,

@@ -31,13 +31,13 @@ def run_mode(monkeypatch, mode, yaml, rd, ref, nrm, dtype):
     return T, icp.stats(), icp.trace()
 
 
-@pytest.mark.parametrize("hint", ["0", "1"])
+@pytest.mark.parametrize("reuse", ["0", "1"])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("minimizer", ["PointToPlaneErrorMinimizer", "PointToPointErrorMinimizer"])
-def test_loop_equals_modules(monkeypatch, oracle, dtype, minimizer, hint):
-    # hint=1: the grid match warm-starts from the previous iteration's output
+def test_loop_equals_modules(monkeypatch, oracle, dtype, minimizer, reuse):
+    # reuse=1: the grid match may certify the previous iteration's k-lists
     # (LoopCtl.Tprev in loop mode, the host's previous step in module mode)
-    monkeypatch.setenv("PMX_GRID_HINT", hint)
+    monkeypatch.setenv("PMX_GRID_REUSE", reuse)
     ref, nrm = reference_cloud(50000, dtype)
     rd = reading_cloud(40000, dtype)
     yaml = chain_yaml(minimizer=minimizer, maxit=25, differential=DIFF)
