@@ -216,6 +216,27 @@ int pmx_loop_run(pmx_ctx* ctx, int n, pmx_loop_status* st);
 /* T_iter after each completed iteration (keep_trace): count x rows x rows T */
 int pmx_loop_trace(pmx_ctx* ctx, int first, int count, void* out);
 
+/* ------------------------------------------------------ data filters --- */
+/* SurfaceNormalDataPointsFilter::inPlaceFilter
+ * (DataPointsFilters/SurfaceNormal.cpp:80-290) on the GPU: the self k-NN of
+ * the cloud on the exact grid matcher (the filter's KDTreeMatcher with
+ * ALLOW_SELF_MATCH, :158-162), then one kernel for the per-point statistics.
+ * Standalone (a temporary context on `device`); pmx_last_error(NULL) has the
+ * message of a failed call.
+ *   feat: rows x n point-major T (dtype PMX_F32 / PMX_F64), rows = D + 1
+ *   knn in [1, 16], maxDist: neighbour radius (+inf = none)
+ *   outputs (point-major T, each may be NULL): normals D x n, densities n,
+ *   eig_values D x n (ascending), eig_vectors D*D x n (serializeEigVec,
+ *   row-major; column j = eigenvector of eig_values[j], largest component
+ *   positive), matched_ids knn x n (reference indices as T, -1 = none),
+ *   mean_dists n; degenerate (may be NULL): points whose C failed the rank test.
+ *   flags: PMX_SN_SMOOTH = smoothNormals (sequential in point order, as the
+ *   reference; needs normals). */
+enum { PMX_SN_SMOOTH = 1 };
+int pmx_surface_normals(int device, int dtype, const void* feat, int rows, int64_t n, int knn, double maxDist,
+                        unsigned flags, void* normals, void* densities, void* eig_values, void* eig_vectors,
+                        void* matched_ids, void* mean_dists, int64_t* degenerate);
+
 #ifdef __cplusplus
 }
 #endif

@@ -86,7 +86,7 @@ EXPORTS = [
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
-    "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace",
+    "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_surface_normals",
 ]
 
 
@@ -126,12 +126,44 @@ def lib():
         l.pmx_loop_begin.argtypes = [C.c_void_p, C.POINTER(LoopCfg), C.c_void_p]
         l.pmx_loop_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(LoopStatus)]
         l.pmx_loop_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        l.pmx_surface_normals.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_double,
+                                          C.c_uint] + [C.c_void_p] * 6 + [C.POINTER(C.c_int64)]
         _lib = l
     return _lib
 
 
 def device_count():
     return lib().pmx_device_count()
+
+
+PMX_SN_SMOOTH = 1
+
+
+def surface_normals(points, knn=5, max_dist=np.inf, smooth=False, device=0):
+    """SurfaceNormalDataPointsFilter (DataPointsFilters/SurfaceNormal.cpp:80-290) on
+    the GPU (pmx_surface_normals).  points: (n, rows) float32/float64 with the
+    homogeneous row last.  Returns a dict of point-major arrays: normals (n, D),
+    densities (n,), eig_values (n, D), eig_vectors (n, D*D), matched_ids (n, knn),
+    mean_dists (n,), and the degenerate count."""
+    pts = np.ascontiguousarray(points)
+    if pts.dtype not in (np.float32, np.float64):
+        pts = pts.astype(np.float32)
+    n, rows = pts.shape
+    D = rows - 1
+    dt = pts.dtype
+    out = {"normals": np.empty((n, D), dt), "densities": np.empty(n, dt), "eig_values": np.empty((n, D), dt),
+           "eig_vectors": np.empty((n, D * D), dt), "matched_ids": np.empty((n, knn), dt),
+           "mean_dists": np.empty(n, dt)}
+    deg = C.c_int64(0)
+    l = lib()
+    rc = l.pmx_surface_normals(int(device), PMX_F64 if dt == np.float64 else PMX_F32, _ptr(pts), rows, n, int(knn),
+                               float(max_dist), PMX_SN_SMOOTH if smooth else 0, _ptr(out["normals"]),
+                               _ptr(out["densities"]), _ptr(out["eig_values"]), _ptr(out["eig_vectors"]),
+                               _ptr(out["matched_ids"]), _ptr(out["mean_dists"]), C.byref(deg))
+    if rc != PMX_OK:
+        raise_for(rc, l.pmx_last_error(None).decode())
+    out["degenerate"] = deg.value
+    return out
 
 
 def _ptr(a):

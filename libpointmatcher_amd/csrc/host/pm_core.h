@@ -201,6 +201,20 @@ struct DataPoints {
         }
         throw InvalidElement("DataPoints::getDescriptorViewByName(): descriptor " + name + " not found");
     }
+    // allocateDescriptors + the view assignment of a data filter: overwrite an
+    // existing label of the same span, else append (PointMatcher.h:281-296)
+    void setDescriptor(const std::string& name, int span, const T* data) {
+        int off = 0;
+        for (auto& l : descriptorLabels) {
+            if (l.text == name && l.span == span) {
+                for (int64_t i = 0; i < n; ++i)
+                    for (int r = 0; r < span; ++r) descriptors[i * descDim + off + r] = data[i * span + r];
+                return;
+            }
+            off += l.span;
+        }
+        addDescriptor(name, span, data);
+    }
     void addDescriptor(const std::string& name, int span, const T* data) {
         std::vector<T> nd((size_t)(descDim + span) * n);
         for (int64_t i = 0; i < n; ++i) {

@@ -524,6 +524,83 @@ struct IdentityDPF : PM<T>::DataPointsFilter {
     void inPlaceFilter(DataPoints<T>&) override {}
 };
 
+// SurfaceNormalDataPointsFilter (DataPointsFilters/SurfaceNormal.cpp:50-290,
+// parameters SurfaceNormal.h:64-80): the self k-NN and the per-point
+// statistics on the GPU (pmx_surface_normals, pmx_normals.hip); descriptors
+// in the reference's label order.  epsilon > 0 is accepted: the search is
+// exact, which any approximation bound admits.
+template <typename T>
+struct SurfaceNormalDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("knn", "number of nearest neighbors to consider, including the point itself", "5", "3",
+                     "2147483647", &P::Comp<unsigned>),
+                PDoc("maxDist", "maximum distance to consider for neighbors", "inf", "0", "inf", &P::Comp<T>),
+                PDoc("epsilon", "approximation to use for the nearest-neighbor search", "0", "0", "inf", &P::Comp<T>),
+                PDoc("keepNormals", "whether the normals should be added as descriptors to the resulting cloud", "1"),
+                PDoc("keepDensities", "whether the point densities should be added as descriptors to the resulting cloud",
+                     "0"),
+                PDoc("keepEigenValues", "whether the eigen values should be added as descriptors to the resulting cloud",
+                     "0"),
+                PDoc("keepEigenVectors",
+                     "whether the eigen vectors should be added as descriptors to the resulting cloud", "0"),
+                PDoc("keepMatchedIds",
+                     "whether the identifiers of matches points should be added as descriptors to the resulting cloud",
+                     "0"),
+                PDoc("keepMeanDist", "whether the distance to the nearest neighbor mean should be added as descriptors "
+                                     "to the resulting cloud",
+                     "0"),
+                PDoc("sortEigen", "whether the eigenvalues and eigenvectors should be sorted (ascending) based on the "
+                                  "eigenvalues",
+                     "0"),
+                PDoc("smoothNormals", "whether the normal vector should be average with the nearest neighbors", "0")};
+    }
+    unsigned knn;
+    T maxDist, epsilon;
+    bool keepNormals, keepDensities, keepEigenValues, keepEigenVectors, keepMatchedIds, keepMeanDist, sortEigen,
+        smoothNormals;
+    explicit SurfaceNormalDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter("SurfaceNormalDataPointsFilter", doc(), p),
+          knn(this->template get<unsigned>("knn")),
+          maxDist(this->template get<T>("maxDist")),
+          epsilon(this->template get<T>("epsilon")),
+          keepNormals(this->template get<bool>("keepNormals")),
+          keepDensities(this->template get<bool>("keepDensities")),
+          keepEigenValues(this->template get<bool>("keepEigenValues")),
+          keepEigenVectors(this->template get<bool>("keepEigenVectors")),
+          keepMatchedIds(this->template get<bool>("keepMatchedIds")),
+          keepMeanDist(this->template get<bool>("keepMeanDist")),
+          sortEigen(this->template get<bool>("sortEigen")),
+          smoothNormals(this->template get<bool>("smoothNormals")) {}
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        const int D = cloud.rows - 1;
+        const int64_t n = cloud.n;
+        // (eigenpairs are always returned in ascending order: sortEigen's
+        // order, and the order computeNormal's choice does not depend on)
+        std::vector<T> nrm, dens, eva, eve, ids, md;
+        if (keepNormals || smoothNormals) nrm.resize((size_t)(n * D));
+        if (keepDensities) dens.resize((size_t)n);
+        if (keepEigenValues) eva.resize((size_t)(n * D));
+        if (keepEigenVectors) eve.resize((size_t)(n * D * D));
+        if (keepMatchedIds) ids.resize((size_t)(n * knn));
+        if (keepMeanDist) md.resize((size_t)n);
+        auto ptr = [](std::vector<T>& v) { return v.empty() ? nullptr : (void*)v.data(); };
+        int64_t degenerate = 0;
+        const int rc = pmx_surface_normals(this->device, dtype_of<T>(), cloud.features.data(), cloud.rows, n,
+                                           (int)std::min<unsigned>(knn, 1u << 30), (double)maxDist,
+                                           smoothNormals ? PMX_SN_SMOOTH : 0u, ptr(nrm), ptr(dens), ptr(eva), ptr(eve),
+                                           ptr(ids), ptr(md), &degenerate);
+        if (rc == PMX_E_BAD_PARAM) throw InvalidParameter(pmx_last_error(nullptr));
+        if (rc) throw std::runtime_error(std::string("SurfaceNormalDataPointsFilter: ") + pmx_last_error(nullptr));
+        if (keepNormals) cloud.setDescriptor("normals", D, nrm.data());
+        if (keepDensities) cloud.setDescriptor("densities", 1, dens.data());
+        if (keepEigenValues) cloud.setDescriptor("eigValues", D, eva.data());
+        if (keepEigenVectors) cloud.setDescriptor("eigVectors", D * D, eve.data());
+        if (keepMatchedIds) cloud.setDescriptor("matchedIds", (int)knn, ids.data());
+        if (keepMeanDist) cloud.setDescriptor("meanDists", 1, md.data());
+    }
+};
+
 // Reference data filters that are outside the hot path:
 // registered with the reference's parameter docs so chain files validate
 // exactly as in the reference (bounds, unused parameters, module types), but
@@ -558,15 +635,6 @@ void register_unsupported_filters(Registrar<typename PM<T>::DataPointsFilter>& R
          PDoc("averageExistingDescriptors", "keep and average existing descriptors", "1"),
          PDoc("keepNormals", "add normals as descriptors", "1"), PDoc("keepDensities", "add densities", "0"),
          PDoc("keepEigenValues", "add eigen values", "0"), PDoc("keepEigenVectors", "add eigen vectors", "0")});
-    add("SurfaceNormalDataPointsFilter",
-        {PDoc("knn", "number of nearest neighbors to consider, including the point itself", "5", "3", "2147483647",
-              &P::Comp<unsigned>),
-         PDoc("maxDist", "maximum distance to consider for neighbors", "inf", "0", "inf", &P::Comp<T>),
-         PDoc("epsilon", "approximation to use for the nearest-neighbor search", "0", "0", "inf", &P::Comp<T>),
-         PDoc("keepNormals", "add normals", "1"), PDoc("keepDensities", "add densities", "0"),
-         PDoc("keepEigenValues", "add eigen values", "0"), PDoc("keepEigenVectors", "add eigen vectors", "0"),
-         PDoc("keepMatchedIds", "add matched ids", "0"), PDoc("keepMeanDist", "add mean distance", "0"),
-         PDoc("sortEigen", "sort eigenvalues", "0"), PDoc("smoothNormals", "average normals", "0")});
     add("MaxDistDataPointsFilter",
         {PDoc("dim", "dimension on which the filter will be applied. x=0, y=1, z=2, radius=-1", "-1", "-1", "2",
               &P::Comp<int>),
@@ -639,6 +707,8 @@ PointMatcher<T>::PointMatcher() {
                                        [](const Ps& p) { return std::make_shared<BoundTC<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("IdentityDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<IdentityDPF<T>>(p); }, false);
+    DataPointsFilterRegistrar.reg("SurfaceNormalDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<SurfaceNormalDPF<T>>(p); }, true);
     register_unsupported_filters<T>(DataPointsFilterRegistrar);
     InspectorRegistrar.reg("NullInspector", [](const Ps& p) {
         return std::make_shared<NoOp<Inspector>>("NullInspector", Parametrizable::ParametersDoc(), p);
@@ -796,6 +866,8 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     const int dim = referenceIn.rows;
     if (dim != 3 && dim != 4) throw std::runtime_error("clouds must be 2-D or 3-D (3 or 4 homogeneous rows)");
     DataPoints reference(referenceIn);
+    for (auto& f : referenceDataPointsFilters) f->device = dev.device;
+    for (auto& f : readingDataPointsFilters) f->device = dev.device;
     referenceDataPointsFilters.init();
     referenceDataPointsFilters.apply(reference);
     const int64_t M = reference.n;

@@ -131,6 +131,7 @@ struct PointMatcher {
         virtual ~DataPointsFilter() {}
         virtual void init() {}
         virtual void inPlaceFilter(DataPoints& cloud) = 0;
+        int device = 0;  // HIP device of the ICP that applies the filter (GPU filters)
     };
     struct DataPointsFilters : std::vector<std::shared_ptr<DataPointsFilter>> {
         void init() {

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -180,6 +181,8 @@ struct pmx_ctx {
 };
 
 namespace {
+
+thread_local std::string g_err;  // message of a failed standalone call (pmx_last_error(NULL))
 
 int fail(pmx_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -1395,6 +1398,110 @@ int loop_trace_impl(pmx_ctx* c, int first, int count, void* out) {
     return PMX_OK;
 }
 
+// SurfaceNormalDataPointsFilter (DataPointsFilters/SurfaceNormal.cpp:80-290):
+// self-match on a temporary context, the statistics kernel, and the
+// smoothNormals pass on the host (the reference smooths in place, point by
+// point: later points see the already smoothed normals of earlier ones,
+// :256-283 — a sequential dependency kept as is).
+template <typename T>
+int surface_normals_impl(int device, const T* feat, int rows, int64_t n, int knn, double maxDist, unsigned flags,
+                         T* o_nrm, T* o_dens, T* o_eval, T* o_evec, T* o_ids, T* o_mdist, int64_t* degenerate) {
+    if (rows != 3 && rows != 4) {
+        g_err = "SurfaceNormalDataPointsFilter: clouds must be 2-D or 3-D (3 or 4 homogeneous rows)";
+        return PMX_E_BAD_PARAM;
+    }
+    if (knn < 1 || knn > 16) {
+        g_err = "SurfaceNormalDataPointsFilter: knn must be in [1, 16] on the GPU path";
+        return PMX_E_BAD_PARAM;
+    }
+    if (degenerate) *degenerate = 0;
+    if (n <= 0) return PMX_OK;
+    pmx_ctx* c = nullptr;
+    int rc = pmx_ctx_create(device, sizeof(T) == 8 ? PMX_F64 : PMX_F32, &c);
+    if (rc) {
+        g_err = "SurfaceNormalDataPointsFilter: no HIP device";
+        return rc;
+    }
+    struct Guard {
+        pmx_ctx* c;
+        ~Guard() { pmx_ctx_destroy(c); }
+    } guard{c};
+    auto err = [&](int r) {
+        g_err = c->err;
+        return r;
+    };
+    c->reuse_on = false;
+    c->search_type = 1;
+    if (c->grid_mode == 0) c->grid_mode = 1;
+    const int D = rows - 1;
+    std::vector<T> I((size_t)rows * rows, (T)0);
+    for (int i = 0; i < rows; ++i) I[(size_t)i * rows + i] = 1;
+    if ((rc = set_reference_impl<T>(c, feat, rows, n, nullptr))) return err(rc);
+    if ((rc = set_reading_impl<T>(c, feat, rows, n, I.data()))) return err(rc);
+    if ((rc = match_impl<T>(c, I.data(), knn, maxDist, nullptr))) return err(rc);
+    const int64_t per = D + 1 + D + D * D + 1;  // normals, density, eigen values, eigen vectors, mean distance
+    T* d_out = nullptr;
+    unsigned long long* d_deg = nullptr;
+    HIPCHK(c, hipMalloc((void**)&d_out, sizeof(T) * (size_t)(n * per)));
+    std::unique_ptr<void, void (*)(void*)> free_out(d_out, [](void* p) { (void)hipFree(p); });
+    HIPCHK(c, hipMalloc((void**)&d_deg, sizeof(unsigned long long)));
+    std::unique_ptr<void, void (*)(void*)> free_deg(d_deg, [](void* p) { (void)hipFree(p); });
+    HIPCHK(c, hipMemsetAsync(d_deg, 0, sizeof(unsigned long long), c->stream));
+    T* d_nrm = d_out;
+    T* d_dens = d_nrm + n * D;
+    T* d_eval = d_dens + n;
+    T* d_evec = d_eval + n * D;
+    T* d_md = d_evec + n * D * D;
+    const GridLevel& L = c->lv(c->ids_level);
+    launch_surface_normals<T>((const P4<T>*)c->d_rd, (const P4<T>*)L.gpts, c->d_ids, (const T*)c->d_dists, n, knn, D,
+                              d_nrm, d_dens, d_eval, d_evec, d_md, d_deg, c->stream);
+    HIPCHK(c, hipGetLastError());
+    std::vector<T> h((size_t)(n * per));
+    unsigned long long deg = 0;
+    HIPCHK(c, hipMemcpyAsync(h.data(), d_out, sizeof(T) * h.size(), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&deg, d_deg, sizeof(deg), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // slot order -> point order
+    auto take = [&](int64_t off, int span, T* dst) {
+        if (!dst) return;
+        std::vector<T> src(h.begin() + off, h.begin() + off + n * span);
+        unpermute<T>(c, src, dst, span);
+    };
+    const bool smooth = (flags & PMX_SN_SMOOTH) && o_nrm;
+    take(0, D, o_nrm);
+    take(n * D, 1, o_dens);
+    take(n * (D + 1), D, o_eval);
+    take(n * (2 * D + 1), D * D, o_evec);
+    take(n * (2 * D + 1 + D * D), 1, o_mdist);
+    if (o_ids || smooth) {
+        std::vector<T> dd((size_t)(n * knn));
+        std::vector<int32_t> ii((size_t)(n * knn));
+        if ((rc = get_matches_impl<T>(c, dd.data(), ii.data()))) return err(rc);
+        if (o_ids)  // matches.ids.cast<T>() (SurfaceNormal.cpp:250-253)
+            for (size_t e = 0; e < ii.size(); ++e) o_ids[e] = (T)ii[e];
+        if (smooth) {  // SurfaceNormal.cpp:256-283, in place, point order
+            const T inf = std::numeric_limits<T>::infinity();
+            for (int64_t i = 0; i < n; ++i) {
+                T cur[3] = {0, 0, 0}, mean[3] = {0, 0, 0};
+                for (int r = 0; r < D; ++r) cur[r] = o_nrm[i * D + r];
+                int cnt = 0;
+                for (int j = 0; j < knn; ++j) {
+                    if (dd[(size_t)(i * knn + j)] == inf) continue;
+                    const int64_t ref = ii[(size_t)(i * knn + j)];
+                    const T* nb = o_nrm + ref * D;
+                    T dot = 0;
+                    for (int r = 0; r < D; ++r) dot = dot + cur[r] * nb[r];
+                    for (int r = 0; r < D; ++r) mean[r] = dot > (T)0 ? mean[r] + nb[r] : mean[r] - nb[r];
+                    ++cnt;
+                }
+                for (int r = 0; r < D; ++r) o_nrm[i * D + r] = mean[r] / (T)cnt;
+            }
+        }
+    }
+    if (degenerate) *degenerate = (int64_t)deg;
+    return PMX_OK;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1408,7 +1515,7 @@ int pmx_device_count(void) {
     return n;
 }
 
-const char* pmx_last_error(const pmx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* pmx_last_error(const pmx_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (!out) return PMX_E_BAD_PARAM;
@@ -1642,6 +1749,26 @@ int pmx_loop_run(pmx_ctx* c, int n, pmx_loop_status* st) {
 int pmx_loop_trace(pmx_ctx* c, int first, int count, void* out) {
     if (!c || (!out && count > 0)) return fail(c, PMX_E_BAD_PARAM, "null argument");
     return DISPATCH(c, loop_trace_impl<float>(c, first, count, out), loop_trace_impl<double>(c, first, count, out));
+}
+
+int pmx_surface_normals(int device, int dtype, const void* feat, int rows, int64_t n, int knn, double maxDist,
+                        unsigned flags, void* normals, void* densities, void* eig_values, void* eig_vectors,
+                        void* matched_ids, void* mean_dists, int64_t* degenerate) {
+    if (!feat && n > 0) {
+        g_err = "null cloud";
+        return PMX_E_BAD_PARAM;
+    }
+    if (dtype == PMX_F32)
+        return surface_normals_impl<float>(device, (const float*)feat, rows, n, knn, maxDist, flags, (float*)normals,
+                                           (float*)densities, (float*)eig_values, (float*)eig_vectors,
+                                           (float*)matched_ids, (float*)mean_dists, degenerate);
+    if (dtype == PMX_F64)
+        return surface_normals_impl<double>(device, (const double*)feat, rows, n, knn, maxDist, flags,
+                                            (double*)normals, (double*)densities, (double*)eig_values,
+                                            (double*)eig_vectors, (double*)matched_ids, (double*)mean_dists,
+                                            degenerate);
+    g_err = "dtype must be PMX_F32 or PMX_F64";
+    return PMX_E_BAD_PARAM;
 }
 
 }  // extern "C"

@@ -155,6 +155,11 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
+// SurfaceNormalDataPointsFilter statistics over a self-match (pmx_normals.hip)
+template <typename T>
+void launch_surface_normals(const P4<T>* pts, const P4<T>* gpts, const int32_t* ids, const T* dists, int64_t N,
+                            int k, int D, T* o_nrm, T* o_dens, T* o_eval, T* o_evec, T* o_mdist,
+                            unsigned long long* degenerate, hipStream_t s);
 // spread pair / fallback counters of the grid kernels (bytes; zero-initialised once)
 size_t grid_counter_bytes();
 void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, int64_t n, hipStream_t s);

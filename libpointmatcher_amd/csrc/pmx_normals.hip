@@ -1,0 +1,264 @@
+// pmx_normals.hip — SurfaceNormalDataPointsFilter on the device
+// (DataPointsFilters/SurfaceNormal.cpp:80-290, utils/utils.h:101-156).
+//
+// The k nearest neighbours of every point in its own cloud (the filter's
+// KDTreeMatcher with ALLOW_SELF_MATCH, SurfaceNormal.cpp:158-162,
+// MatchersImpl.cpp:98) come from the exact grid matcher; this kernel does the
+// per-point statistics, one lane per point:
+//   mean of the valid neighbours and the centred set NN in T
+//                                                  (SurfaceNormal.cpp:170-181)
+//   C = NN NN^T in T, sequential over the neighbours (:183)
+//   the rank test C.fullPivHouseholderQr().rank() + 1 >= D (:188), with the
+//     restated FullPivHouseholderQR of common/pmx_dense.h
+//   eigenvalues / eigenvectors of C (:190-205), normal = eigenvector of the
+//     smallest eigenvalue (computeNormal, utils.h:141-156), clamped to [-1, 1]
+//   density = |NN| / (4/3 pi max_j |NN_j|^3) (computeDensity, utils.h:118-133)
+//   mean distance |p - mean| (:238-247); degenerate points: zero eigen
+//     pairs, density 0, mean distance SIZE_MAX (:213-216, 232-236).
+//
+// Eigen decomposition.  The reference runs the general Eigen::EigenSolver on
+// the symmetric C [ext]; its eigenvalue order and eigenvector signs are
+// implementation-defined (only sortEigen fixes the order).  Here the
+// symmetric C is diagonalised by cyclic Jacobi rotations in double (to
+// double precision), the pairs are sorted by ascending eigenvalue and every
+// eigenvector is signed so that its largest-magnitude component is positive.
+// Parity is therefore defined on the eigenvalues and on the eigenvectors /
+// normals up to sign (the point-to-plane minimiser is invariant to a normal's
+// sign); the CPU oracle (oracle/pmo_impl.inc) uses the same convention.
+//
+// Bound: a gather of k neighbour points per lane (16 B each, L2-resident:
+// neighbours of neighbouring slots overlap) and ~60 + 40 k FLOP: latency /
+// gather bound, like the reductions.
+#include "pmx_internal.h"
+
+#include "common/pmx_dense.h"
+
+namespace pmx {
+
+// cyclic Jacobi eigen-decomposition of a symmetric D x D matrix (double):
+// eigenvalues ascending in w, eigenvectors in the columns of V
+template <int D>
+__device__ __forceinline__ void sym_eigen(double (&a)[D][D], double (&w)[D], double (&V)[D][D]) {
+    double fro = 0.0;
+#pragma unroll
+    for (int r = 0; r < D; ++r)
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+            fro += a[r][c] * a[r][c];
+            V[r][c] = r == c ? 1.0 : 0.0;
+        }
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = 0.0;
+#pragma unroll
+        for (int p = 0; p < D; ++p)
+#pragma unroll
+            for (int q = p + 1; q < D; ++q) off += a[p][q] * a[p][q];
+        if (!(off > 1e-36 * fro)) break;
+#pragma unroll
+        for (int p = 0; p < D; ++p)
+#pragma unroll
+            for (int q = p + 1; q < D; ++q) {
+                if (a[p][q] == 0.0) continue;
+                const double theta = (a[q][q] - a[p][p]) / (2.0 * a[p][q]);
+                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+                    const double arp = a[r][p], arq = a[r][q];
+                    a[r][p] = c * arp - s * arq;
+                    a[r][q] = s * arp + c * arq;
+                }
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+                    const double apr = a[p][r], aqr = a[q][r];
+                    a[p][r] = c * apr - s * aqr;
+                    a[q][r] = s * apr + c * aqr;
+                }
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+                    const double vrp = V[r][p], vrq = V[r][q];
+                    V[r][p] = c * vrp - s * vrq;
+                    V[r][q] = s * vrp + c * vrq;
+                }
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) w[i] = a[i][i];
+    // ascending (selection by pairwise swaps with static indices)
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int j = i + 1; j < D; ++j) {
+            const bool sw = w[j] < w[i];
+            const double wi = w[i], wj = w[j];
+            w[i] = sw ? wj : wi;
+            w[j] = sw ? wi : wj;
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const double vi = V[r][i], vj = V[r][j];
+                V[r][i] = sw ? vj : vi;
+                V[r][j] = sw ? vi : vj;
+            }
+        }
+    // sign: the largest-magnitude component positive (the first on ties)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        double big = V[0][j];
+#pragma unroll
+        for (int r = 1; r < D; ++r)
+            if (fabs(V[r][j]) > fabs(big)) big = V[r][j];
+        if (big < 0.0)
+#pragma unroll
+            for (int r = 0; r < D; ++r) V[r][j] = -V[r][j];
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T coord(const P4<T>& p, int r) {
+    return r == 0 ? p.x : (r == 1 ? p.y : p.z);
+}
+
+// one point per lane, slot order (the reading order of the self-match);
+// neighbours are grid positions of gpts
+template <typename T, int D>
+__global__ __launch_bounds__(256) void surface_normals_kernel(
+    const P4<T>* __restrict__ pts, const P4<T>* __restrict__ gpts, const int32_t* __restrict__ ids,
+    const T* __restrict__ dists, int64_t N, int k, T* __restrict__ o_nrm, T* __restrict__ o_dens,
+    T* __restrict__ o_eval, T* __restrict__ o_evec, T* __restrict__ o_mdist,
+    unsigned long long* __restrict__ degenerate) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool degen = false;
+    if (s < N) {
+        const T inf = (T)__builtin_huge_val();
+        // mean of the valid neighbours (d.rowwise().sum() / realKnn)
+        T sum[D];
+#pragma unroll
+        for (int r = 0; r < D; ++r) sum[r] = 0;
+        int real = 0;
+        for (int j = 0; j < k; ++j) {
+            if (dists[s * k + j] == inf) continue;
+            const P4<T> p = gld32(gpts, (uint32_t)ids[s * k + j]);
+#pragma unroll
+            for (int r = 0; r < D; ++r) sum[r] = sum[r] + coord(p, r);
+            ++real;
+        }
+        T mean[D];
+#pragma unroll
+        for (int r = 0; r < D; ++r) mean[r] = sum[r] / (T)real;
+        // C = NN NN^T and the largest |NN_j|
+        T C[D * D];
+#pragma unroll
+        for (int i = 0; i < D * D; ++i) C[i] = 0;
+        T maxn = 0;
+        for (int j = 0; j < k; ++j) {
+            if (dists[s * k + j] == inf) continue;
+            const P4<T> p = gld32(gpts, (uint32_t)ids[s * k + j]);
+            T nn[D];
+            T n2 = 0;
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                nn[r] = coord(p, r) - mean[r];
+                n2 = n2 + nn[r] * nn[r];
+            }
+#pragma unroll
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int b = 0; b < D; ++b) C[a * D + b] = C[a * D + b] + nn[a] * nn[b];
+            const T nrm = sqrt(n2);
+            maxn = nrm > maxn ? nrm : maxn;
+        }
+        // rank test (SurfaceNormal.cpp:188)
+        pmx_dense::FullPivQR<T> qr;
+        qr.compute(C, D);
+        degen = !(qr.rank() + 1 >= D);
+        T ev[D], evec[D][D];
+        if (!degen) {
+            double a[D][D], w[D], V[D][D];
+#pragma unroll
+            for (int r = 0; r < D; ++r)
+#pragma unroll
+                for (int c = 0; c < D; ++c) a[r][c] = (double)C[r * D + c];
+            sym_eigen<D>(a, w, V);
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                ev[r] = (T)w[r];
+#pragma unroll
+                for (int c = 0; c < D; ++c) evec[r][c] = (T)V[r][c];
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                ev[r] = 0;
+#pragma unroll
+                for (int c = 0; c < D; ++c) evec[r][c] = 0;
+            }
+        }
+        if (o_nrm) {
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                T v = evec[r][0];  // the smallest eigenvalue's vector
+                v = v < (T)-1 ? (T)-1 : (v > (T)1 ? (T)1 : v);
+                o_nrm[s * D + r] = v;
+            }
+        }
+        if (o_dens) {
+            T dens = 0;
+            if (!degen) {
+                const T volume = (T)((4.0 / 3.0) * 3.14159265358979323846 * pow((double)maxn, 3.0));
+                dens = (T)real / volume;
+            }
+            o_dens[s] = dens;
+        }
+        if (o_eval) {
+#pragma unroll
+            for (int r = 0; r < D; ++r) o_eval[s * D + r] = ev[r];
+        }
+        if (o_evec) {  // serializeEigVec: row-major (utils.h:101-114)
+#pragma unroll
+            for (int r = 0; r < D; ++r)
+#pragma unroll
+                for (int c = 0; c < D; ++c) o_evec[s * D * D + r * D + c] = evec[r][c];
+        }
+        if (o_mdist) {
+            T md;
+            if (degen) {
+                md = (T)18446744073709551615.0;  // std::numeric_limits<std::size_t>::max()
+            } else {
+                const P4<T> p = pts[s];
+                T n2 = 0;
+#pragma unroll
+                for (int r = 0; r < D; ++r) {
+                    const T d = coord(p, r) - mean[r];
+                    n2 = n2 + d * d;
+                }
+                md = sqrt(n2);
+            }
+            o_mdist[s] = md;
+        }
+    }
+    const unsigned long long m = __ballot(degen);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(degenerate, (unsigned long long)__popcll(m));
+}
+
+template <typename T>
+void launch_surface_normals(const P4<T>* pts, const P4<T>* gpts, const int32_t* ids, const T* dists, int64_t N,
+                            int k, int D, T* o_nrm, T* o_dens, T* o_eval, T* o_evec, T* o_mdist,
+                            unsigned long long* degenerate, hipStream_t s) {
+    if (N <= 0) return;
+    const dim3 grid((unsigned)((N + 255) / 256));
+    if (D == 3)
+        hipLaunchKernelGGL((surface_normals_kernel<T, 3>), grid, dim3(256), 0, s, pts, gpts, ids, dists, N, k, o_nrm,
+                           o_dens, o_eval, o_evec, o_mdist, degenerate);
+    else
+        hipLaunchKernelGGL((surface_normals_kernel<T, 2>), grid, dim3(256), 0, s, pts, gpts, ids, dists, N, k, o_nrm,
+                           o_dens, o_eval, o_evec, o_mdist, degenerate);
+}
+
+template void launch_surface_normals<float>(const P4<float>*, const P4<float>*, const int32_t*, const float*,
+                                            int64_t, int, int, float*, float*, float*, float*, float*,
+                                            unsigned long long*, hipStream_t);
+template void launch_surface_normals<double>(const P4<double>*, const P4<double>*, const int32_t*, const double*,
+                                             int64_t, int, int, double*, double*, double*, double*, double*,
+                                             unsigned long long*, hipStream_t);
+
+}  // namespace pmx

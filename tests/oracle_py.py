@@ -209,3 +209,25 @@ def icp(cfg, reading, reference, normals=None, T_init=None, trace=False):
     if trace:
         tr = tr[: st.iterations]
     return rc, T_out, st, tr
+
+
+def surface_normals(pts, k=5, max_dist=np.inf, threads=8, smooth=False):
+    """SurfaceNormalDataPointsFilter restated (oracle/pmo_impl.inc).  pts: (n, rows).
+    Returns a dict of point-major arrays and the degenerate count."""
+    dt = pts.dtype
+    pts = np.ascontiguousarray(pts)
+    n, rows = pts.shape
+    D = rows - 1
+    out = {"normals": np.empty((n, D), dt), "densities": np.empty(n, dt), "eig_values": np.empty((n, D), dt),
+           "eig_vectors": np.empty((n, D * D), dt), "matched_ids": np.empty((n, k), dt),
+           "mean_dists": np.empty(n, dt)}
+    deg = C.c_int64(0)
+    f = getattr(lib(), "pmo_surface_normals_" + _sfx(dt))
+    f.restype = C.c_int
+    ct = C.c_float if dt == np.float32 else C.c_double
+    rc = f(_p(pts), C.c_int(rows), C.c_int64(n), C.c_int(k), ct(max_dist), C.c_int(threads), C.c_int(int(smooth)),
+           _p(out["normals"]), _p(out["densities"]), _p(out["eig_values"]), _p(out["eig_vectors"]),
+           _p(out["matched_ids"]), _p(out["mean_dists"]), C.byref(deg))
+    assert rc == OK, rc
+    out["degenerate"] = deg.value
+    return out

@@ -192,3 +192,70 @@ def test_float_accumulation_gap_is_small(oracle, golden):
         assert rc == 0
         out.append(T)
     assert np.linalg.norm(out[0] - out[1]) < 1e-4
+
+
+# ------------------------------------------------------------ surface normals --
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_surface_normals_oracle_vs_numpy(oracle, dtype):
+    # SurfaceNormalDataPointsFilter restated (DataPointsFilters/SurfaceNormal.cpp:80-290)
+    # against an independent numpy computation on the same neighbourhoods:
+    # eigenvalues (numpy eigh), normals up to sign, density and mean distance
+    # formulas (utils/utils.h:118-133, SurfaceNormal.cpp:238-247)
+    from scipy.spatial import cKDTree
+
+    rng = np.random.default_rng(3)
+    xy = rng.uniform(-1, 1, (3000, 2))
+    z = 0.3 * xy[:, 0] - 0.2 * xy[:, 1] + rng.normal(0, 0.01, 3000)
+    pts = hom(np.column_stack([xy, z]), dtype)
+    k = 8
+    out = oracle.surface_normals(pts, k=k)
+    assert out["degenerate"] == 0
+    p = pts[:, :3].astype(np.float64)
+    _, idx = cKDTree(p).query(p, k=k)
+    assert np.array_equal(np.sort(idx, axis=1), np.sort(out["matched_ids"].astype(np.int64), axis=1))
+    nb = p[idx]
+    mean = nb.mean(axis=1)
+    c = nb - mean[:, None, :]
+    w, v = np.linalg.eigh(np.einsum("nki,nkj->nij", c, c))
+    tol = 2e-4 if dtype == np.float32 else 1e-10
+    scale = np.abs(w).max(axis=1, keepdims=True)
+    assert np.max(np.abs(out["eig_values"] - w) / scale) < tol
+    assert np.min(np.abs(np.sum(out["normals"] * v[:, :, 0], axis=1))) > 1 - tol
+    # eigenvector columns (serializeEigVec row-major) up to sign, sign convention
+    ev = out["eig_vectors"].reshape(-1, 3, 3)
+    for j in range(3):
+        col = ev[:, :, j]
+        assert np.min(np.abs(np.sum(col * v[:, :, j], axis=1))) > 1 - 10 * tol
+        big = col[np.arange(len(col)), np.argmax(np.abs(col), axis=1)]
+        assert np.all(big > 0)
+    maxn = np.linalg.norm(c, axis=2).max(axis=1)
+    np.testing.assert_allclose(out["densities"], k / (4.0 / 3.0 * np.pi * maxn ** 3), rtol=10 * tol)
+    np.testing.assert_allclose(out["mean_dists"], np.linalg.norm(p - mean, axis=1), rtol=10 * tol,
+                               atol=10 * tol * np.abs(p).max())
+
+
+def test_surface_normals_oracle_degenerate_and_smoothing(oracle):
+    # collinear points: C has rank 1 < D - 1 -> zero eigen pairs, density 0,
+    # mean distance SIZE_MAX (SurfaceNormal.cpp:208-236)
+    t = np.linspace(0, 1, 50)
+    line = hom(np.column_stack([t, 2 * t, -t]), np.float32)
+    out = oracle.surface_normals(line, k=5)
+    assert out["degenerate"] == 50
+    assert np.all(out["normals"] == 0) and np.all(out["eig_values"] == 0) and np.all(out["densities"] == 0)
+    assert np.all(out["mean_dists"] == np.float32(18446744073709551615.0))
+    # smoothNormals: sequential in place over the points (SurfaceNormal.cpp:256-283)
+    rng = np.random.default_rng(5)
+    pts = hom(rng.normal(size=(400, 3)) * [1, 1, 0.05], np.float32)
+    raw = oracle.surface_normals(pts, k=6)
+    sm = oracle.surface_normals(pts, k=6, smooth=True)
+    n = raw["normals"].copy()
+    ids = raw["matched_ids"].astype(np.int64)
+    for i in range(len(n)):
+        cur = n[i].copy()
+        acc = np.zeros(3, np.float32)
+        for j in ids[i]:
+            nb = n[j]
+            d = np.float32(np.float32(cur[0] * nb[0]) + np.float32(cur[1] * nb[1])) + np.float32(cur[2] * nb[2])
+            acc = acc + nb if d > 0 else acc - nb
+        n[i] = acc / np.float32(len(ids[i]))
+    np.testing.assert_allclose(sm["normals"], n, rtol=1e-6, atol=1e-7)
