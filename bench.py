@@ -13,6 +13,8 @@ histograms and the normal equations over RCCL.
 
 Timing: W untimed iterations, then exactly K iterations between a barrier +
 device synchronisation on both sides; the max over ranks is reported.  The
+defaults (K = 40, W = 0) time one whole ICP of 40 iterations from the initial
+pose — the same work the CPU baseline times.  The
 clouds are resident in HBM before the timed region.  The match kernel's
 device time is measured with HIP events on the context stream (pmx_timing_*).
 The CPU baseline (rank 0, N = 1 only) is the oracle's libnabo-style kd-tree
@@ -78,12 +80,14 @@ def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # default: one whole ICP of 40 iterations from the initial pose, as the
+    # CPU baseline runs it (SURVEY.md §8(d) timing runs)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--matcher", default="grid", choices=["brute", "grid"],
                     help="KDTreeMatcher searchType 0 (brute force) or 1 (spatial grid)")
-    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-iters", type=int, default=40)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist", action="store_true",
@@ -130,7 +134,16 @@ def main():
         icp.comm_init(bytes(t.tolist()), world, rank)
 
     icp.prepare(reading, reference, normals if minimizer.startswith("PointToPlane") else None)
-    icp.iterate(args.warmup)
+    # the first iteration's match is a cold search at the initial pose (no
+    # previous k-lists to certify): timed on its own and reported beside the
+    # steady-state average
+    cold_launch_ms = None
+    if args.warmup > 0:
+        icp.timing(True)
+        icp.iterate(1)
+        cold_ms, cold_n = icp.timing_read()
+        cold_launch_ms = cold_ms / max(cold_n, 1)
+        icp.iterate(args.warmup - 1)
     icp.timing(True)
 
     def barrier():
@@ -170,6 +183,18 @@ def main():
         alg_bytes_extra = 0
     alg_bytes += alg_bytes_extra
     achieved_gbs = alg_bytes / avg_match_s / 1e9
+    # HBM traffic of the match kernel from the committed PMC passes of this
+    # exact command (profiles/r01/pmc_c3_traffic.json: rocprofv3 FETCH_SIZE x2
+    # (gfx950 correction) + WRITE_SIZE, per launch); null for other configs
+    traffic, traffic_src = None, None
+    if args.config == "c3" and args.matcher == "grid" and world == 1:
+        try:
+            with open(os.path.join(ROOT, "profiles", "r01", "pmc_c3_traffic.json")) as f:
+                kk = json.load(f)["kernels"]
+            traffic = next(v["hbm_bytes"] for k, v in kk.items() if "grid_lane_kernel" in k)
+            traffic_src = "profiles/r01/pmc_c3_traffic.json"
+        except (OSError, KeyError, StopIteration, ValueError):
+            pass
     peak_tf = FP32_VALU_TFLOPS if esz == 4 else FP64_VALU_TFLOPS
     metric = "ICP iterations/sec + matched-pairs/sec, 1M→1M pts, k=1, point-to-plane"
     try:
@@ -197,9 +222,15 @@ def main():
         "icp_iterations_per_s": args.steps / elapsed,
         "kept_pairs_last_iter": st.kept,
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                      "kernel": "match (k-NN + fused transform)", "avg_launch_ms": avg_match_s * 1e3,
-                     "algorithmic_bytes_per_launch": alg_bytes},
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "cold_launch_ms": cold_launch_ms,
+                     "note": "steady-state launches certify most k-lists from the previous iteration "
+                             "(exact temporal reuse, DESIGN.md §5); with --warmup 0 (default) the timed steps are "
+                             "the whole 40-iteration ICP from the initial pose, cold first iterations included; "
+                             "cold_launch_ms (warmup > 0) is the first iteration's full search"},
         "compute_roofline": {"bound": "valu", "achieved": flops / avg_match_s / 1e12, "peak": peak_tf,
                              "unit": "TFLOP/s", "frac": flops / avg_match_s / 1e12 / peak_tf,
                              "pairs_evaluated_per_launch": pairs_eval,

@@ -83,6 +83,7 @@ struct pmx_ctx {
     std::vector<GridLevel> levels;
     std::vector<double> level_ppc{2.0, 4.0, 8.0, 16.0, 32.0, 64.0};
     int level = 0;      // level of the next grid match
+    double first_ppc = 16.0;  // level of a new reading's first (cold) match (PMX_GRID_FIRST_PPC)
     int ids_level = 0;  // level whose positions the current match ids are
     std::vector<double> level_cells;   // last cells-per-query seen at each level
     std::vector<int64_t> level_seen;   // match count when it was seen (0: never)
@@ -632,6 +633,17 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     c->N = N;
     c->N_total = N;
     c->N_max = N;
+    // A new reading's first match has no previous match to adapt the level
+    // from, and the initial pose is usually the worst aligned: a coarse level
+    // walks few shells where the finest walks dozens (measured on MI355X, C3).
+    // Any level answers exactly.
+    if (c->adaptive && !c->levels.empty()) {
+        int best = 0;
+        for (int l = 0; l < (int)c->levels.size(); ++l)
+            if (std::fabs(std::log(c->lv(l).ppc / c->first_ppc)) < std::fabs(std::log(c->lv(best).ppc / c->first_ppc)))
+                best = l;
+        c->level = best;
+    }
     if (c->comm && c->nranks > 1) {
         // global reading size and the largest shard (padding of all-gathers)
         double* tmp = c->d_result;
@@ -1549,6 +1561,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
@@ -1563,6 +1576,16 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bad(PMX_E_HIP);
+    static bool preloaded = false;  // (once per process; modules are per process)
+    if (!preloaded) {
+        preload_match();
+        preload_grid();
+        preload_select();
+        preload_reduce();
+        preload_loop();
+        preload_normals();
+        preloaded = true;
+    }
     // One small "iteration block" holds everything the host reads back per
     // iteration, so a single D2H copy returns it (see kBlk*):
     //   [0, 1024)     reduction results (128 doubles)

@@ -170,6 +170,17 @@ __device__ __forceinline__ void cell_of_q(const GridGeom& G, const double q[3], 
     }
 }
 
+// distance from coordinate v to the slab of cell c along axis a (0 inside)
+__device__ __forceinline__ double axis_gap(const GridGeom& G, int a, int c, double v) {
+    const double lo = G.lo[a] + (double)c * G.h, hi = lo + G.h;
+    return v < lo ? lo - v : (v > hi ? v - hi : 0.0);
+}
+// x cell of a coordinate, clamped to the grid
+__device__ __forceinline__ int cell_x(const GridGeom& G, double v) {
+    const double f = (v - G.lo[0]) * G.inv_h;
+    return f < 0.0 ? 0 : (f >= (double)G.g[0] ? G.g[0] - 1 : (int)f);
+}
+
 // Octant search: the 2x2x2 cells nearest to the query (its cell and, per
 // axis, the neighbour on the query's side of the cell centre: 4 rows of 2
 // cells).  Every point outside the block is at least LB = the distance to
@@ -305,25 +316,58 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
     }
     for (int R = 1;; ++R) {
         if (R >= 2) {
-            // walk the shell at Chebyshev radius R
+            // walk the shell at Chebyshev radius R.  Rows (and the x-range of
+            // a face row) whose cells are all farther than the current k-th
+            // (k+1-th) distance are skipped: every point there has d > d_k, so it can
+            // neither enter the list nor tie (1e-5 relative margin on the
+            // gap, far above the T rounding of d and the host's cell
+            // assignment; one extra cell each side of an x-range for the
+            // latter).  The certificate below is unchanged: skipped cells hold
+            // no candidate.
             const int y0 = max(c[1] - R, 0), y1 = min(c[1] + R, G.g[1] - 1);
             const int z0 = max(c[2] - R, 0), z1 = min(c[2] + R, G.g[2] - 1);
             const int x0 = max(c[0] - R, 0), x1 = min(c[0] + R, G.g[0] - 1);
             for (int z = z0; z <= z1; ++z) {
+                // (pruned against list entry k + 1 when the list has room for
+                // it: the safe radius of the temporal reuse takes that entry
+                // as a bound on every non-neighbour, so no cell holding a
+                // point closer than it may be skipped)
+                T dkT;
+                int32_t ikT;
+                kth(kd, ki, k < KT ? k + 1 : k, dkT, ikT);
+                const double lim = ikT == kNoPos ? 1e300 : (double)dkT / margin;
+                const double gz = axis_gap(G, 2, z, q[2]), gz2 = gz * gz;
+                if (gz2 > lim) continue;
                 const bool zface = (z == c[2] - R) || (z == c[2] + R);
                 for (int y = y0; y <= y1; ++y) {
+                    const double gy = axis_gap(G, 1, y, q[1]), g2 = gz2 + gy * gy;
+                    if (g2 > lim) continue;
                     const bool yface = (y == c[1] - R) || (y == c[1] + R);
                     const uint32_t row = ((uint32_t)z * (uint32_t)G.g[1] + (uint32_t)y) * (uint32_t)G.g[0];
                     if (zface || yface) {
-                        scan_range<T, KT>(gpts, gidx, gld32(start, row + x0), gld32(start, row + x1 + 1), qx, qy, qz, kd, ki,
-                                          visits);
+                        int xa = x0, xb = x1;
+                        if (lim < 1e300) {
+                            const double rem = sqrt(lim - g2);
+                            xa = max(x0, cell_x(G, q[0] - rem) - 1);
+                            xb = min(x1, cell_x(G, q[0] + rem) + 1);
+                        }
+                        if (xa <= xb)
+                            scan_range<T, KT>(gpts, gidx, gld32(start, row + xa), gld32(start, row + xb + 1), qx, qy,
+                                              qz, kd, ki, visits);
                     } else {
-                        if (c[0] - R >= 0)
-                            scan_range<T, KT>(gpts, gidx, gld32(start, row + c[0] - R), gld32(start, row + c[0] - R + 1), qx, qy,
-                                              qz, kd, ki, visits);
-                        if (c[0] + R <= G.g[0] - 1)
-                            scan_range<T, KT>(gpts, gidx, gld32(start, row + c[0] + R), gld32(start, row + c[0] + R + 1), qx, qy,
-                                              qz, kd, ki, visits);
+                        const int xl = c[0] - R, xr = c[0] + R;
+                        if (xl >= 0) {
+                            const double gx = axis_gap(G, 0, xl, q[0]);
+                            if (g2 + gx * gx <= lim)
+                                scan_range<T, KT>(gpts, gidx, gld32(start, row + xl), gld32(start, row + xl + 1), qx,
+                                                  qy, qz, kd, ki, visits);
+                        }
+                        if (xr <= G.g[0] - 1) {
+                            const double gx = axis_gap(G, 0, xr, q[0]);
+                            if (g2 + gx * gx <= lim)
+                                scan_range<T, KT>(gpts, gidx, gld32(start, row + xr), gld32(start, row + xr + 1), qx,
+                                                  qy, qz, kd, ki, visits);
+                        }
                     }
                 }
             }
@@ -693,6 +737,16 @@ void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, 
     int64_t g = (n + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(pos_to_index_kernel, dim3((unsigned)g), dim3(256), 0, s, pos, gidx, out, n);
+}
+
+
+// Load this translation unit's code object now (pmx_ctx_create): HIP loads a
+// module at the first launch of any of its kernels, and that host-side stall
+// (milliseconds for the large grid module) would otherwise land inside the
+// first ICP iteration.
+void preload_grid() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1>));
 }
 
 }  // namespace pmx

@@ -155,6 +155,13 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
+// code-object preloads (one per translation unit, called by pmx_ctx_create)
+void preload_match();
+void preload_grid();
+void preload_select();
+void preload_reduce();
+void preload_loop();
+void preload_normals();
 // SurfaceNormalDataPointsFilter statistics over a self-match (pmx_normals.hip)
 template <typename T>
 void launch_surface_normals(const P4<T>* pts, const P4<T>* gpts, const int32_t* ids, const T* dists, int64_t N,

@@ -332,4 +332,14 @@ template void launch_loop_step<double>(LoopCtl*, LoopState<double>*, const doubl
                                        const unsigned long long*, const double*, const LoopCfg&, double*,
                                        hipStream_t);
 
+
+// Load this translation unit's code object now (pmx_ctx_create): HIP loads a
+// module at the first launch of any of its kernels, and that host-side stall
+// (milliseconds for the large grid module) would otherwise land inside the
+// first ICP iteration.
+void preload_loop() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&loop_step_kernel<float, 4>));
+}
+
 }  // namespace pmx

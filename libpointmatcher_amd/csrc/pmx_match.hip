@@ -471,4 +471,14 @@ template void launch_transform<float>(const P4<float>*, P4<float>*, int64_t, con
 template void launch_transform<double>(const P4<double>*, P4<double>*, int64_t, const Mat4<double>&,
                                        hipStream_t);
 
+
+// Load this translation unit's code object now (pmx_ctx_create): HIP loads a
+// module at the first launch of any of its kernels, and that host-side stall
+// (milliseconds for the large grid module) would otherwise land inside the
+// first ICP iteration.
+void preload_match() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&transform_kernel<float>));
+}
+
 }  // namespace pmx

@@ -261,4 +261,14 @@ template void launch_surface_normals<double>(const P4<double>*, const P4<double>
                                              int64_t, int, int, double*, double*, double*, double*, double*,
                                              unsigned long long*, hipStream_t);
 
+
+// Load this translation unit's code object now (pmx_ctx_create): HIP loads a
+// module at the first launch of any of its kernels, and that host-side stall
+// (milliseconds for the large grid module) would otherwise land inside the
+// first ICP iteration.
+void preload_normals() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&surface_normals_kernel<float, 3>));
+}
+
 }  // namespace pmx

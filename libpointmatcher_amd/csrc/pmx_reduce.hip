@@ -374,4 +374,14 @@ PMX_INST(float)
 PMX_INST(double)
 #undef PMX_INST
 
+
+// Load this translation unit's code object now (pmx_ctx_create): HIP loads a
+// module at the first launch of any of its kernels, and that host-side stall
+// (milliseconds for the large grid module) would otherwise land inside the
+// first ICP iteration.
+void preload_reduce() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&finalize_kernel));
+}
+
 }  // namespace pmx

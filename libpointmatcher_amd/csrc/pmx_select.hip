@@ -644,4 +644,14 @@ template void launch_vartrim<double>(const double*, int64_t, int, double, double
 template size_t vartrim_scratch_bytes<float>(int64_t);
 template size_t vartrim_scratch_bytes<double>(int64_t);
 
+
+// Load this translation unit's code object now (pmx_ctx_create): HIP loads a
+// module at the first launch of any of its kernels, and that host-side stall
+// (milliseconds for the large grid module) would otherwise land inside the
+// first ICP iteration.
+void preload_select() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&select_pass_kernel<float>));
+}
+
 }  // namespace pmx
