@@ -2,7 +2,7 @@
 # A/B session: grid + loop GPU tests, then the C3/C4/C5 bench with and without
 # an environment knob ($AB_ENV, e.g. "PMX_GRID_HINT=0"), then a kernel trace.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/bin/bash
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/cold
 for p in 2 4 8 16 32 64; do
   echo "== $(date +%T) ppc $p" >> gpurun_out/steps.log

@@ -2,7 +2,7 @@
 # Round bench session: the default bench line (C3 + CPU baseline), the other
 # configs' lines, and the kernel-trace summary of the default command.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

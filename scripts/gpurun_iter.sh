@@ -3,7 +3,7 @@
 # kernel-trace of the C3 bench.  Each GPU step has its own time limit; the
 # chain stops at the first failure.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

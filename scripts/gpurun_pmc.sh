@@ -3,7 +3,7 @@
 # rocprofv3 --pmc passes (TCC budget: FETCH_SIZE 3 counters, WRITE_SIZE 2),
 # plus the kernel-trace summary of the same command.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

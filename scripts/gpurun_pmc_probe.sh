@@ -2,7 +2,7 @@
 # One SQ PMC pass of perf_probe.py per environment variant.
 #   gpurun_pmc_probe.sh "NAME:ENV=V,ENV=V" ...
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out/pmcp
 export TMPDIR=/tmp

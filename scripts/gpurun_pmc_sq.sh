@@ -1,7 +1,7 @@
 #!/bin/bash
 # One PMC pass (SQ instruction mix and wave cycles) over a short C3 bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # perf_probe.py under environment variants (no profiler).  Usage:
 #   gpurun_probe.sh "NAME:ENV=V,ENV=V" ...   (PROBE_ARGS overrides the probe args)
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/probe
 PROBE_ARGS=${PROBE_ARGS:-"1000000 1000000 1 5 aligned"}
 for spec in "$@"; do

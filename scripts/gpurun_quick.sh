@@ -1,7 +1,7 @@
 #!/bin/bash
 # Short GPU session: parity tests, then C3 (tile and per-lane grid kernels) and C4 benches.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { echo "== $(date +%T) $*" >> gpurun_out/steps.log; }

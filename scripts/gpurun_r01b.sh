@@ -3,7 +3,7 @@
 # HBM traffic PMC passes (FETCH_SIZE and WRITE_SIZE in separate passes).
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -3,7 +3,7 @@
 # C2/C4/C5 bench lines, rocprofv3 kernel-trace summary of the C3 bench.
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

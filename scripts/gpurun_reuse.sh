@@ -2,7 +2,7 @@
 # Validation of the grid match's temporal reuse: grid + loop + icp GPU tests,
 # probe and bench with reuse on / off, and a kernel trace of the C3 bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out/probe
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # One GPU session: parity tests, benches, rocprof kernel-trace summary.
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { echo "== $(date +%T) $*" >> gpurun_out/steps.log; }

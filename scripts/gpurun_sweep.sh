@@ -1,7 +1,7 @@
 #!/bin/bash
 # Parameter sweep of the grid matcher on C3 (bench lines only); stops at the first failure.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/sweep
 step() { echo "== $(date +%T) $*" >> gpurun_out/steps.log; }
 CFG=${SWEEP_CONFIG:-c3}

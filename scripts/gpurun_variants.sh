@@ -2,7 +2,7 @@
 # Kernel traces of the match probe under environment variants (one rocprofv3
 # --kernel-trace run each).  Usage: gpurun_variants.sh "NAME:ENV=V,ENV=V" ...
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
 mkdir -p gpurun_out/var
 export TMPDIR=/tmp
