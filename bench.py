@@ -133,18 +133,10 @@ def main():
         tdist.broadcast(t, src=0)
         icp.comm_init(bytes(t.tolist()), world, rank)
 
-    icp.prepare(reading, reference, normals if minimizer.startswith("PointToPlane") else None)
-    # the first iteration's match is a cold search at the initial pose (no
-    # previous k-lists to certify): timed on its own and reported beside the
-    # steady-state average
-    cold_launch_ms = None
+    nrm_in = normals if minimizer.startswith("PointToPlane") else None
+    icp.prepare(reading, reference, nrm_in)
     if args.warmup > 0:
-        icp.timing(True)
-        icp.iterate(1)
-        cold_ms, cold_n = icp.timing_read()
-        cold_launch_ms = cold_ms / max(cold_n, 1)
-        icp.iterate(args.warmup - 1)
-    icp.timing(True)
+        icp.iterate(args.warmup)
 
     def barrier():
         if dist:
@@ -156,8 +148,26 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    match_ms, launches = icp.timing_read()
     st = icp.stats()
+    # Roofline pass: the same ICP again (prepare resets the pose and the
+    # match history), now with HIP events around every match launch on the
+    # context stream.  The events are kept out of the timed region above: each
+    # record is a marker packet that adds ~6 us of idle GPU time per record
+    # pair to the iteration (measured in the kernel trace).  The first
+    # iteration's match is a cold search at the initial pose (no previous
+    # k-lists to certify): with --warmup > 0 it is timed on its own.
+    icp.prepare(reading, reference, nrm_in)
+    cold_launch_ms = None
+    if args.warmup > 0:
+        icp.timing(True)
+        icp.iterate(1)
+        cold_ms, cold_n = icp.timing_read()
+        cold_launch_ms = cold_ms / max(cold_n, 1)
+        icp.iterate(args.warmup - 1)
+    icp.timing(True)
+    icp.iterate(args.steps)
+    match_ms, launches = icp.timing_read()
+    icp.timing(False)
     if dist:
         import torch
 

@@ -215,6 +215,12 @@ int pmx_loop_begin(pmx_ctx* ctx, const pmx_loop_cfg* cfg, const void* T_iter0);
 int pmx_loop_run(pmx_ctx* ctx, int n, pmx_loop_status* st);
 /* T_iter after each completed iteration (keep_trace): count x rows x rows T */
 int pmx_loop_trace(pmx_ctx* ctx, int first, int count, void* out);
+/* Quantile window statistics of the device loop (no reference counterpart;
+ * diagnostics): iterations whose TrimmedDist / MedianDist quantile (chain
+ * position 0) was resolved inside the match's key window, and iterations
+ * that ran the radix passes instead.  Both results are exact; counts
+ * accumulate over the loops of this context since the last pmx_loop_begin. */
+int pmx_loop_select_stats(pmx_ctx* ctx, uint64_t* window_hits, uint64_t* window_misses);
 
 /* ------------------------------------------------------ data filters --- */
 /* SurfaceNormalDataPointsFilter::inPlaceFilter

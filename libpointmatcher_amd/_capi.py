@@ -86,7 +86,7 @@ EXPORTS = [
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
-    "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_surface_normals",
+    "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_surface_normals",
 ]
 
 
@@ -126,6 +126,7 @@ def lib():
         l.pmx_loop_begin.argtypes = [C.c_void_p, C.POINTER(LoopCfg), C.c_void_p]
         l.pmx_loop_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(LoopStatus)]
         l.pmx_loop_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        l.pmx_loop_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         l.pmx_surface_normals.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_double,
                                           C.c_uint] + [C.c_void_p] * 6 + [C.POINTER(C.c_int64)]
         _lib = l
@@ -350,6 +351,12 @@ class Context:
         self.last_loop_status = st
         self._chk(rc)
         return st
+
+    def loop_select_stats(self):
+        """(window hits, radix fallbacks) of the fused quantile window (pmx_spec.h)."""
+        h, m = C.c_uint64(), C.c_uint64()
+        self._chk(self._l.pmx_loop_select_stats(self.h, C.byref(h), C.byref(m)))
+        return h.value, m.value
 
     def loop_T(self, st):
         r = self.rows

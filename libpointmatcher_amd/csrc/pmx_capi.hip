@@ -7,6 +7,7 @@
 // pmx_p2plane_system / pmx_p2point_system, when the ~400-byte system is
 // copied back for the host solve (PointToPlane.cpp:108-161).
 #include "pmx_internal.h"
+#include "pmx_spec.h"
 
 #include <rccl/rccl.h>
 
@@ -164,6 +165,14 @@ struct pmx_ctx {
     void* d_trace = nullptr;      // T_iter per iteration (keep_trace)
     int64_t trace_cap = 0;        // iterations
     bool loop_on = false;         // enqueueing loop iterations
+    // quantile window fused into the grid match (pmx_spec.h): device loop,
+    // single rank, quantile filter at chain position 0 (PMX_SPEC_SELECT=0: off)
+    SpecSel* d_spec = nullptr;
+    void* d_spec_keys = nullptr;
+    bool spec_allowed = true;
+    bool spec_on = false;
+    SpecSel spec_init{};  // (host staging of the reset)
+    SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;
     pmx_loop_cfg loop_cfg{};
     LoopCfg loop_dev{};
@@ -749,7 +758,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
-                             c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+                             c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->spec_now(), c->d_sel,
+                             c->stream);
         c->safe_valid = ru.mode != 0;
         if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
@@ -768,7 +778,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
 
 // ----------------------------------------------------------------- outliers --
 template <typename T>
-int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const double* ratio_dev, SelectState* st) {
+int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const double* ratio_dev, SelectState* st,
+                    SpecSel* spec = nullptr) {
     // (no state reset: pass 0 starts a fresh select)
     const int passes = select_passes<T>();
     for (int p = 0; p < passes; ++p) {
@@ -781,7 +792,7 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
             launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), c->stream);
         } else {
             launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, loop_ctl(c),
-                                  c->stream);
+                                  spec, c->stream);
         }
     }
     HIPCHK(c, hipGetLastError());
@@ -904,13 +915,15 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
         break;
     }
     case 4: {  // MedianDist: limit = factor * quantile(0.5)
-        if ((rc = quantile_select<T>(c, d, n, 0.5, nullptr, slot))) return rc;
+        if ((rc = quantile_select<T>(c, d, n, 0.5, nullptr, slot, chain_pos == 0 ? c->spec_now() : nullptr)))
+            return rc;
         chain_set(c, chain_pos, kWPState, (double)(T)p0);
         break;
     }
     case 5: {  // TrimmedDist: limit = quantile(ratio)
         if (!(p0 >= 1e-7 && p0 <= 1.0)) return fail(c, PMX_E_BAD_PARAM, "TrimmedDistOutlierFilter: ratio out of [1e-7, 1]");
-        if ((rc = quantile_select<T>(c, d, n, p0, nullptr, slot))) return rc;
+        if ((rc = quantile_select<T>(c, d, n, p0, nullptr, slot, chain_pos == 0 ? c->spec_now() : nullptr)))
+            return rc;
         chain_set(c, chain_pos, kWPState, 1.0);
         break;
     }
@@ -1237,6 +1250,22 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
         c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn ? c->ids_level : -1;
     launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, prev_level,
                         c->Tstep, c->stream);
+    // quantile window: a fresh window each loop (the first iteration runs the
+    // radix passes, which centre the window for the next)
+    const int k0 = cfg->n_filters > 0 ? cfg->filter_kind[0] : -1;
+    c->spec_on = c->spec_allowed && !(c->comm && c->nranks > 1) && !c->select_split && !c->no_visits &&
+                 (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
+    if (c->spec_on) {
+        if (!c->d_spec) {
+            HIPCHK(c, hipMalloc((void**)&c->d_spec, sizeof(SpecSel)));
+            HIPCHK(c, hipMalloc(&c->d_spec_keys, sizeof(unsigned long long) * kSpecCap));
+        }
+        SpecSel init{};
+        init.keys = c->d_spec_keys;
+        init.ratio = (double)(T)(k0 == PMX_FILTER_TRIMMED ? cfg->filter_p[0][0] : 0.5);
+        c->spec_init = init;
+        HIPCHK(c, hipMemcpyAsync(c->d_spec, &c->spec_init, sizeof(SpecSel), hipMemcpyHostToDevice, c->stream));
+    }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));  // (T0 may be a stack buffer of the caller)
     c->loop_issued = 0;
@@ -1545,6 +1574,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_TILE_MAX")) c->tile_max = (uint32_t)std::max(0, std::atoi(e));
     c->no_visits = std::getenv("PMX_NO_VISITS") != nullptr;
     c->select_split = std::getenv("PMX_SELECT_SPLIT") != nullptr;
+    if (const char* e = std::getenv("PMX_SPEC_SELECT")) c->spec_allowed = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
     if (const char* e = std::getenv("PMX_GRID_LEVELS")) {
@@ -1625,7 +1655,8 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     void* bufs[] = {c->d_safe, c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
-                    c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace};
+                    c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace,
+                    c->d_spec, c->d_spec_keys};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();
@@ -1772,6 +1803,19 @@ int pmx_loop_run(pmx_ctx* c, int n, pmx_loop_status* st) {
 int pmx_loop_trace(pmx_ctx* c, int first, int count, void* out) {
     if (!c || (!out && count > 0)) return fail(c, PMX_E_BAD_PARAM, "null argument");
     return DISPATCH(c, loop_trace_impl<float>(c, first, count, out), loop_trace_impl<double>(c, first, count, out));
+}
+
+int pmx_loop_select_stats(pmx_ctx* c, uint64_t* window_hits, uint64_t* window_misses) {
+    if (!c || !window_hits || !window_misses) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    *window_hits = 0;
+    *window_misses = 0;
+    if (!c->d_spec) return PMX_OK;
+    SpecSel h{};
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(&h, c->d_spec, sizeof(SpecSel), hipMemcpyDeviceToHost));
+    *window_hits = h.n_hit;
+    *window_misses = h.n_miss;
+    return PMX_OK;
 }
 
 int pmx_surface_normals(int device, int dtype, const void* feat, int rows, int64_t n, int knn, double maxDist,

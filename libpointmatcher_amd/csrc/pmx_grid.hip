@@ -43,6 +43,7 @@
 // per-lane search from LDS (broadcast reads) and measures 0.187 ms at C3: a
 // candidate for QPT > 1 and for very dense references.
 #include "pmx_internal.h"
+#include "pmx_spec.h"
 
 namespace pmx {
 
@@ -402,7 +403,7 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
 
 template <typename T, int KT>
 __device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&kd)[KT], const int32_t (&ki)[KT],
-                                          T* __restrict__ out_d, int32_t* __restrict__ out_i) {
+                                          T* __restrict__ out_d, int32_t* __restrict__ out_i, SpecAcc<T>& sa) {
 #pragma unroll
     for (int s = 0; s < KT; ++s) {  // static indexing keeps kd/ki in registers
         if (s < k) {
@@ -414,8 +415,17 @@ __device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&k
             }
             out_d[j * k + s] = d;
             out_i[j * k + s] = id;
+            if (sa.on) spec_acc<T>(sa, d);
         }
     }
+}
+
+template <typename T, int KT>
+__device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&kd)[KT], const int32_t (&ki)[KT],
+                                          T* __restrict__ out_d, int32_t* __restrict__ out_i) {
+    SpecAcc<T> none;
+    none.on = false;
+    write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, none);
 }
 
 // Pair / fallback counters.  One device-scope atomic per wave on a single
@@ -435,38 +445,49 @@ __device__ __forceinline__ void add_visits(uint32_t visits, unsigned long long* 
 }
 
 // (also clears the iteration's error word: it runs first after the match,
-// before any filter can raise one)
+// before any filter can raise one).  With a quantile window (pmx_spec.h) it
+// also resolves the iteration's quantile from the window when it can.
+template <typename T>
 __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long* __restrict__ vpart,
                                                               unsigned long long* __restrict__ out,
                                                               int* __restrict__ iter_err,
-                                                              const LoopCtl* __restrict__ ctl) {
-    __shared__ unsigned long long red[2][kVSlots / 64];
+                                                              const LoopCtl* __restrict__ ctl,
+                                                              SpecSel* __restrict__ spec,
+                                                              SelectState* __restrict__ st) {
+    __shared__ unsigned long long red[4][kVSlots / 64];
+    __shared__ uint32_t lh[2048];
+    __shared__ unsigned long long part[kVSlots];
+    __shared__ unsigned long long bc[2];
     if (ctl && ctl->done) return;
     const int t = threadIdx.x;
-    unsigned long long a = vpart[(size_t)t * kVStride], b = vpart[(size_t)(kVSlots + t) * kVStride];
-    vpart[(size_t)t * kVStride] = 0;  // ready for the next match
-    vpart[(size_t)(kVSlots + t) * kVStride] = 0;
+    unsigned long long v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        v[c] = vpart[(size_t)(c * kVSlots + t) * kVStride];
+        vpart[(size_t)(c * kVSlots + t) * kVStride] = 0;  // ready for the next match
+    }
     for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_xor(a, off);
-        b += __shfl_xor(b, off);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] += __shfl_xor(v[c], off);
     }
     if ((t & 63) == 0) {
-        red[0][t >> 6] = a;
-        red[1][t >> 6] = b;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[c][t >> 6] = v[c];
     }
     __syncthreads();
+    unsigned long long sum[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        for (int w = 0; w < kVSlots / 64; ++w) sum[c] += red[c][w];
     if (t == 0) {
-        unsigned long long sa = 0, sb = 0;
-        for (int w = 0; w < kVSlots / 64; ++w) {
-            sa += red[0][w];
-            sb += red[1][w];
-        }
-        out[0] = sa;
-        out[1] = sb;
+        out[0] = sum[0];
+        out[1] = sum[1];
         if (iter_err) *iter_err = 0;
     }
+    if (spec) spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], lh, part, bc);
 }
-size_t grid_counter_bytes() { return sizeof(unsigned long long) * 2 * kVSlots * kVStride; }
+// counters: 0 pairs, 1 full-search fallbacks, 2 finite distances, 3 below the quantile window
+size_t grid_counter_bytes() { return sizeof(unsigned long long) * 4 * kVSlots * kVStride; }
 
 // ---------------------------------------------------- temporal reuse --
 // ICP matches the same reading every iteration under a slowly changing
@@ -515,7 +536,7 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
                                            const uint32_t* __restrict__ start, const GridGeom& G,
                                            const P4<T>* __restrict__ rd, int64_t j, const Mat4<T>& Tm, int k,
                                            T maxR2, int oct, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                           T* __restrict__ safe, uint32_t& visits) {
+                                           T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa) {
     T qx, qy, qz;
     gxform(Tm, gld(rd, j), qx, qy, qz);
     T kd[KT];
@@ -542,7 +563,7 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
             lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit);
         }
     }
-    write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i);
+    write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
     if (safe) safe[j] = oct ? (T)0 : safe_radius<T, KT>(kd, ki, k, lb_exit);
 }
 
@@ -552,7 +573,7 @@ template <typename T, int KT>
 __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                                             const P4<T>& p, T qx, T qy, T qz, const Mat4<T>& Tprev, int64_t j,
                                             int k, T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                            T* __restrict__ safe, uint32_t& visits) {
+                                            T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa) {
     const T rs = safe[j];
     const T dkp = out_d[j * k + k - 1];
     int32_t id[KT];
@@ -582,7 +603,7 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
     for (int s = 0; s < KT; ++s)
         if (s < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx, qy, qz, gld32(gpts, (uint32_t)id[s])), id[s]);
     visits += (uint32_t)k;
-    write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i);
+    write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
     safe[j] = (T)(b * (1.0 - 1e-6));
     return true;
 }
@@ -597,7 +618,8 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
                                                         unsigned long long* __restrict__ visited, int oct,
                                                         int reuse, T* __restrict__ safe, Mat4<T> Tprev,
                                                         const LoopCtl* __restrict__ ctl,
-                                                        const GridDesc<T>* __restrict__ gd) {
+                                                        const GridDesc<T>* __restrict__ gd,
+                                                        SpecSel* __restrict__ spec) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -614,14 +636,19 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
     }
     if (!reuse) safe = nullptr;
     uint32_t visits = 0;
+    // quantile window (pmx_spec.h): every written distance is classified
+    SpecAcc<T> sa;
+    spec_acc_init<T>(sa, spec);
     if (reuse < 2) {
         const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (j < N) full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, maxR2, oct, out_d, out_i, safe, visits);
+        if (j < N)
+            full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, maxR2, oct, out_d, out_i, safe, visits, sa);
         add_visits(visits, visited);
         if (reuse) {  // every query took the full search (the counter the level choice reads)
             const unsigned long long m = __ballot(j < N);
             if ((threadIdx.x & 63) == 0 && visited && m) atomicAdd(vslot(visited, 1), (unsigned long long)__popcll(m));
         }
+        if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
         return;
     }
     // Phase 1: every lane tries the certificate.  Phase 2: the block's misses,
@@ -636,7 +663,7 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
         const P4<T> p = gld(rd, j);
         T qx, qy, qz;
         gxform(Tm, p, qx, qy, qz);
-        missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, maxR2, out_d, out_i, safe, visits);
+        missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, maxR2, out_d, out_i, safe, visits, sa);
     }
     const unsigned long long m = __ballot(missed);
     if (lane == 0) wave_cnt[wave] = __popcll(m);
@@ -652,11 +679,12 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
     __syncthreads();
     if ((int)threadIdx.x < total) {
         const int64_t j2 = (int64_t)blockIdx.x * blockDim.x + miss[threadIdx.x];
-        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, maxR2, oct, out_d, out_i, safe, visits);
+        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, maxR2, oct, out_d, out_i, safe, visits, sa);
     }
     add_visits(visits, visited);
     // queries that took the full search (the "fallback" counter)
     if (threadIdx.x == 0 && visited && total) atomicAdd(vslot(visited, 1), (unsigned long long)total);
+    if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
 }
 
 // ------------------------------------------------------------ tile kernel --
@@ -666,11 +694,12 @@ template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
-                      const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
+                      const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
+                      hipStream_t s) {
     if (mode >= 1) {  // 1: shell search, 2: octant block first
         hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
                            start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe,
-                           ru.Tprev, ctl, gd);
+                           ru.Tprev, ctl, gd, spec);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -683,8 +712,10 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
-                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
+                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
+                       SelectState* spec_st, hipStream_t s) {
     if (N <= 0) return;
+    if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
         G.lo[a] = lo[a];
@@ -694,7 +725,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, s)
+                     ru, ctl, gd, spec, s)
     // with reuse the list keeps room for the (k+1)-th point (the safe radius)
     const int kl = ru.mode && mode >= 1 && knn < 16 ? knn + 1 : knn;
     if (kl == 1)
@@ -709,19 +740,20 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
         PMX_KT(16);
 #undef PMX_KT
     if (visited && vout)
-        hipLaunchKernelGGL(counter_sum_kernel, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl);
+        hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
+                           spec_st);
 }
 
 template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, const uint32_t*, const double*, double,
                                        const int*, const P4<float>*, int64_t, const uint32_t*, int64_t,
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
-                                       const LoopCtl*, const GridDesc<float>*, hipStream_t);
+                                       const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
-                                        const LoopCtl*, const GridDesc<double>*, hipStream_t);
+                                        const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

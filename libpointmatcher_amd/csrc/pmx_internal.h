@@ -102,6 +102,9 @@ int64_t match_part_elems(int64_t N, int64_t M_pad, int knn, int cu_count);
 template <typename T>
 void launch_transform(const P4<T>* in, P4<T>* out, int64_t N, const Mat4<T>& Tm, hipStream_t s);
 
+// quantile window fused into the grid match (pmx_spec.h); null = off
+struct SpecSel;
+
 // ---- grid levels and the device-resident loop ----
 struct GridGeom {
     double lo[3];
@@ -154,7 +157,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
-                       const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
+                       const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
+                       hipStream_t s);
 // code-object preloads (one per translation unit, called by pmx_ctx_create)
 void preload_match();
 void preload_grid();
@@ -233,9 +237,11 @@ void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
                         const double* ratio_dev, int* iter_err, const LoopCtl* ctl, hipStream_t s);
 // hist + pick in one launch (single rank; ticket: zeroed uint32, reset on exit)
 template <typename T>
+// spec (may be null): the pass is skipped when the window resolved the
+// quantile; the last pass re-centres the window on the limit it finds
 void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
                         const double* ratio_dev, unsigned int* ticket, int* iter_err, const LoopCtl* ctl,
-                        hipStream_t s);
+                        SpecSel* spec, hipStream_t s);
 template <typename T>
 int select_passes();
 int select_bins(int pass, int key_bits);

@@ -19,31 +19,13 @@
 // in T (one wave, bit-identical to the CPU), the FRMS curve and a first-index
 // argmin, then the same radix select with the optimised ratio.
 #include "pmx_internal.h"
+#include "pmx_spec.h"
 
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
 namespace pmx {
-
-template <typename T>
-struct KeyOf;
-template <>
-struct KeyOf<float> {
-    using K = uint32_t;
-    static constexpr int bits = 32;
-    static __device__ __forceinline__ K key(float v) { return __float_as_uint(v); }
-    static __device__ __forceinline__ float val(K k) { return __uint_as_float(k); }
-    static constexpr K inf_key = 0x7F800000u;
-};
-template <>
-struct KeyOf<double> {
-    using K = unsigned long long;
-    static constexpr int bits = 64;
-    static __device__ __forceinline__ K key(double v) { return (K)__double_as_longlong(v); }
-    static __device__ __forceinline__ double val(K k) { return __longlong_as_double((long long)k); }
-    static constexpr K inf_key = 0x7FF0000000000000ull;
-};
 
 // digit layout: 11-bit digits from the top, the last one(s) 10-bit
 // f32: [31:21] [20:10] [9:0]          f64: [63:53] [52:42] [41:31] [30:20] [19:10] [9:0]
@@ -230,7 +212,7 @@ template <typename T, bool kCoherent>
 __device__ __forceinline__ void pick_phase(uint32_t* __restrict__ hist, SelectState* __restrict__ st, int pass,
                                            double ratio_host, const double* __restrict__ ratio_dev,
                                            int* __restrict__ iter_err, int last, unsigned long long* part,
-                                           unsigned long long& s_rank, int& s_err) {
+                                           unsigned long long& s_rank, int& s_err, SpecSel* __restrict__ spec) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     int shift, bits;
@@ -297,7 +279,12 @@ __device__ __forceinline__ void pick_phase(uint32_t* __restrict__ hist, SelectSt
                     const K prefix = ((K)st->prefix << bits) | digit;
                     st->prefix = (unsigned long long)prefix;
                     st->rank = rank - cum;
-                    if (last) st->limit = (double)KO::val(prefix);
+                    if (last) {
+                        st->limit = (double)KO::val(prefix);
+                        // next iteration's quantile window, centred here; the
+                        // keys sharing this pass's prefix span 2^bits key units
+                        if (spec) spec_update<T>(spec, prefix, (double)part[255] / (double)nb);
+                    }
                     break;
                 }
                 cum += c;
@@ -318,7 +305,7 @@ __global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__
     __shared__ unsigned long long s_rank;
     __shared__ int s_err;
     if (ctl && ctl->done) return;
-    pick_phase<T, false>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err);
+    pick_phase<T, false>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err, nullptr);
 }
 
 // One radix-select pass in one launch (single rank): every block builds and
@@ -331,13 +318,15 @@ __global__ __launch_bounds__(256) void select_pass_kernel(const T* __restrict__ 
                                                           const double* __restrict__ ratio_dev,
                                                           int* __restrict__ iter_err, int last,
                                                           unsigned int* __restrict__ ticket, int agg,
-                                                          const LoopCtl* __restrict__ ctl) {
+                                                          const LoopCtl* __restrict__ ctl,
+                                                          SpecSel* __restrict__ spec) {
     __shared__ uint32_t lh[2048];
     __shared__ unsigned long long part[256];
     __shared__ unsigned long long s_rank;
     __shared__ int s_err;
     __shared__ bool s_last;
     if (ctl && ctl->done) return;  // (uniform: no block takes a ticket)
+    if (spec && spec->hit) return;  // the quantile window resolved it (pmx_spec.h)
     hist_phase<T>(d, n, hist, st, pass, lh, agg);
     __syncthreads();  // every thread's flush has returned
     if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
@@ -345,7 +334,7 @@ __global__ __launch_bounds__(256) void select_pass_kernel(const T* __restrict__ 
     if (!s_last) return;
     // the last block: every other block's flush was performed before its
     // ticket; the bins are read with device-scope atomics (pick_phase)
-    pick_phase<T, true>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err);
+    pick_phase<T, true>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err, spec);
     if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -360,10 +349,10 @@ void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
 template <typename T>
 void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
                         const double* ratio_dev, unsigned int* ticket, int* iter_err, const LoopCtl* ctl,
-                        hipStream_t s) {
+                        SpecSel* spec, hipStream_t s) {
     const int last = pass == select_passes<T>() - 1;
     hipLaunchKernelGGL(select_pass_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
-                       pass, ratio, ratio_dev, iter_err, last, ticket, select_agg(), ctl);
+                       pass, ratio, ratio_dev, iter_err, last, ticket, select_agg(), ctl, spec);
 }
 
 static unsigned grid_for(int64_t n) {
@@ -634,9 +623,9 @@ template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, co
 template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
                                          hipStream_t);
 template void launch_select_pass<float>(const float*, int64_t, uint32_t*, SelectState*, int, double, const double*,
-                                        unsigned int*, int*, const LoopCtl*, hipStream_t);
+                                        unsigned int*, int*, const LoopCtl*, SpecSel*, hipStream_t);
 template void launch_select_pass<double>(const double*, int64_t, uint32_t*, SelectState*, int, double, const double*,
-                                         unsigned int*, int*, const LoopCtl*, hipStream_t);
+                                         unsigned int*, int*, const LoopCtl*, SpecSel*, hipStream_t);
 template void launch_vartrim<float>(const float*, int64_t, int, float, float, const float*, void*, size_t, double*,
                                     int*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,

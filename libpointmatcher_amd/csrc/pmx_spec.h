@@ -1,0 +1,251 @@
+// pmx_spec.h — windowed quantile select fused into the grid match.
+//
+// TrimmedDist / MedianDist need one order statistic of the k*N match
+// distances per iteration (Matches::getDistsQuantile, Matches.cpp:60-87).
+// The radix select of pmx_select.hip finds it exactly in three dependent
+// passes over the distances (f32).  Across ICP iterations the quantile moves
+// little, so the match kernel itself classifies every distance it writes
+// against a key window [lo, hi] around the previous iteration's limit:
+//
+//   fin    = number of finite distances          (Matches.cpp:71)
+//   below  = number of finite keys  <  lo
+//   keys[] = the keys inside [lo, hi]             (appended, capacity cap)
+//
+// The target rank r = (size_t)((T)fin * ratio) (clamped; ratio == 1 -> the
+// maximum) is in the window iff below <= r < below + n_keys, and then the
+// limit is exactly the (r - below)-th smallest appended key: the select runs
+// over a few thousand keys inside counter_sum_kernel (pmx_grid.hip), which
+// follows the match anyway.  Nothing is approximated: when the window misses
+// (rank outside, overflow, first iteration, any error condition) `hit` stays
+// 0 and the regular radix passes run and produce the limit, exactly as
+// without the window.  Either way the next window is centred on the resolved
+// limit, its half-width from the last movement of the limit and capped by the
+// observed key density so the expected append count stays below cap/2.
+//
+// Used by the device-resident loop only, single rank, chain position 0.
+#pragma once
+
+#include "pmx_internal.h"
+
+namespace pmx {
+
+template <typename T>
+struct KeyOf;
+template <>
+struct KeyOf<float> {
+    using K = uint32_t;
+    static constexpr int bits = 32;
+    static __device__ __forceinline__ K key(float v) { return __float_as_uint(v); }
+    static __device__ __forceinline__ float val(K k) { return __uint_as_float(k); }
+    static constexpr K inf_key = 0x7F800000u;
+};
+template <>
+struct KeyOf<double> {
+    using K = unsigned long long;
+    static constexpr int bits = 64;
+    static __device__ __forceinline__ K key(double v) { return (K)__double_as_longlong(v); }
+    static __device__ __forceinline__ double val(K k) { return __longlong_as_double((long long)k); }
+    static constexpr K inf_key = 0x7FF0000000000000ull;
+};
+
+constexpr unsigned kSpecCap = 16384;  // appended keys per iteration
+
+struct SpecSel {
+    unsigned long long lo, hi;  // key window (inclusive); valid != 0
+    unsigned long long prev;    // last resolved limit key
+    double ratio;               // quantile ratio (T value)
+    void* keys;                 // K[kSpecCap]
+    unsigned int n_keys;        // appended by the match (may exceed the capacity)
+    int valid;                  // lo / hi describe a window
+    int have_prev;              // prev holds a limit
+    int hit;                    // this iteration's limit came from the window
+    unsigned long long n_hit, n_miss;  // statistics (host-readable)
+};
+
+// ---- match side: classify every distance the match writes ----
+template <typename T>
+struct SpecAcc {
+    using K = typename KeyOf<T>::K;
+    K lo, hi;
+    K* keys;
+    unsigned int* n_keys;
+    uint32_t fin, below;
+    bool on;
+};
+// off when there is no window (no spec, or the radix passes resolve this
+// iteration): the match then classifies nothing
+template <typename T>
+__device__ __forceinline__ void spec_acc_init(SpecAcc<T>& a, SpecSel* sp) {
+    using K = typename KeyOf<T>::K;
+    a.on = sp && sp->valid;  // (uniform)
+    a.fin = 0;
+    a.below = 0;
+    a.lo = 0;
+    a.hi = 0;
+    a.keys = nullptr;
+    a.n_keys = nullptr;
+    if (!a.on) return;
+    a.lo = (K)sp->lo;
+    a.hi = (K)sp->hi;
+    a.keys = (K*)sp->keys;
+    a.n_keys = &sp->n_keys;
+}
+template <typename T>
+__device__ __forceinline__ void spec_acc(SpecAcc<T>& a, T d) {
+    using KO = KeyOf<T>;
+    using K = typename KO::K;
+    const K k = KO::key(d);
+    if (k < KO::inf_key) {  // (+inf and NaN excluded; distances are >= +0)
+        a.fin += 1;
+        if (k < a.lo) {
+            a.below += 1;
+        } else if (k <= a.hi) {  // rare: a few thousand of k*N
+            const unsigned pos = atomicAdd(a.n_keys, 1u);
+            if (pos < kSpecCap) a.keys[pos] = k;
+        }
+    }
+}
+// wave sums into the spread counters (all lanes of the wave call it)
+template <typename T>
+__device__ __forceinline__ void spec_acc_flush(const SpecAcc<T>& a, unsigned long long* c_fin,
+                                               unsigned long long* c_below) {
+    uint32_t f = a.fin, b = a.below;
+    for (int off = 32; off > 0; off >>= 1) {
+        f += __shfl_xor(f, off);
+        b += __shfl_xor(b, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (f) atomicAdd(c_fin, (unsigned long long)f);
+        if (b) atomicAdd(c_below, (unsigned long long)b);
+    }
+}
+
+// ---- next window, centred on the resolved limit key kl ----
+// density: keys per key unit around the limit (observed)
+template <typename T>
+__device__ __forceinline__ void spec_update(SpecSel* sp, typename KeyOf<T>::K kl, double density) {
+    using KO = KeyOf<T>;
+    using K = typename KO::K;
+    const double move = sp->have_prev ? (double)(kl > (K)sp->prev ? kl - (K)sp->prev : (K)sp->prev - kl) : 0.0;
+    double hw = 3.0 * move + 64.0;
+    const double dens = density > 1e-30 ? density : 1e-30;
+    // expected appends <= cap / 8: every append is an atomic on one counter
+    // inside the match kernel, so the window is kept small
+    const double cap_hw = (double)(kSpecCap / 16) / dens;
+    if (hw > cap_hw) hw = cap_hw;
+    if (hw > 1.0e15) hw = 1.0e15;
+    if (hw < 1.0) hw = 1.0;
+    const K h = (K)hw;
+    const K lo = kl > h ? kl - h : (K)0;
+    const K hi = (KO::inf_key - 1 - kl) > h ? kl + h : KO::inf_key - 1;
+    sp->lo = lo;
+    sp->hi = hi;
+    sp->prev = kl;
+    sp->have_prev = 1;
+    sp->valid = 1;
+}
+
+// ---- counter side: resolve the limit from the window (one block) ----
+// fin / below: the match's counters.  Writes st (as the radix select's last
+// pass would) and sp->hit; resets the append counter.  Block of kThreads.
+template <typename T, int kThreads>
+__device__ __forceinline__ void spec_pick(SpecSel* __restrict__ sp, SelectState* __restrict__ st,
+                                          unsigned long long fin, unsigned long long below, uint32_t* lh,
+                                          unsigned long long* part, unsigned long long* bc) {
+    using KO = KeyOf<T>;
+    using K = typename KO::K;
+    const int t = threadIdx.x;
+    const unsigned nk_raw = sp->n_keys;
+    const unsigned nk = nk_raw < kSpecCap ? nk_raw : kSpecCap;
+    const K lo = (K)sp->lo, hi = (K)sp->hi;
+    const K* keys = (const K*)sp->keys;
+    // target rank (Matches.cpp:83-86 via pick_phase's rule)
+    bool ok = sp->valid && nk_raw <= kSpecCap && fin > 0;
+    const T q = (T)sp->ratio;
+    unsigned long long rank = 0;
+    if (ok) {
+        if (!(q >= (T)0 && q <= (T)1)) {
+            ok = false;
+        } else if (q == (T)1) {
+            rank = fin - 1;
+        } else {
+            rank = (unsigned long long)((T)fin * q);
+            if (rank >= fin) rank = fin - 1;
+        }
+    }
+    ok = ok && rank >= below && rank < below + nk;
+    __syncthreads();
+    if (!ok) {
+        if (t == 0) {
+            sp->hit = 0;
+            sp->n_miss += 1;
+            sp->n_keys = 0;
+        }
+        return;
+    }
+    unsigned long long r = rank - below;
+    // radix select over offsets (key - lo) < 2^nb, 11-bit digits from the top
+    const unsigned long long w = (unsigned long long)(hi - lo);
+    const int nb = w == 0 ? 1 : 64 - __builtin_clzll(w);
+    unsigned long long prefix = 0;  // resolved high bits of the offset
+    int done_bits = 0;
+    while (done_bits < nb) {  // uniform
+        const int bits = (nb - done_bits) < 11 ? (nb - done_bits) : 11;
+        const int shift = nb - done_bits - bits;
+        const int nbins = 1 << bits;
+        for (int i = t; i < 2048; i += kThreads) lh[i] = 0;
+        __syncthreads();
+        for (unsigned i = t; i < nk; i += kThreads) {
+            const unsigned long long off = (unsigned long long)(keys[i] - lo);
+            if (done_bits == 0 || (off >> (shift + bits)) == prefix)
+                atomicAdd(&lh[(off >> shift) & (unsigned long long)(nbins - 1)], 1u);
+        }
+        __syncthreads();
+        // each thread owns 2048 / kThreads consecutive bins
+        constexpr int per = 2048 / kThreads;
+        unsigned long long mine = 0;
+        for (int j = 0; j < per; ++j) mine += lh[t * per + j];
+        part[t] = mine;
+        __syncthreads();
+        for (int off = 1; off < kThreads; off <<= 1) {
+            const unsigned long long v = t >= off ? part[t - off] : 0ull;
+            __syncthreads();
+            part[t] += v;
+            __syncthreads();
+        }
+        const unsigned long long excl = t > 0 ? part[t - 1] : 0ull;
+        if (r >= excl && r < part[t]) {
+            unsigned long long cum = excl;
+            for (int j = 0; j < per; ++j) {
+                const unsigned long long c = lh[t * per + j];
+                if (r < cum + c) {
+                    bc[0] = (unsigned long long)(t * per + j);
+                    bc[1] = r - cum;
+                    break;
+                }
+                cum += c;
+            }
+        }
+        __syncthreads();
+        prefix = (prefix << bits) | bc[0];
+        r = bc[1];
+        done_bits += bits;
+        __syncthreads();
+    }
+    if (t == 0) {
+        const K kl = lo + (K)prefix;
+        st->err = 0;
+        st->count = fin;
+        st->prefix = (unsigned long long)kl;
+        st->rank = 0;
+        st->ratio = (double)q;
+        st->limit = (double)KO::val(kl);
+        sp->hit = 1;
+        sp->n_hit += 1;
+        sp->n_keys = 0;
+        const double width = (double)(hi - lo) + 1.0;
+        spec_update<T>(sp, kl, (double)nk / width);
+    }
+}
+
+}  // namespace pmx

@@ -169,3 +169,33 @@ def test_loop_rejects_brute_force():
     with pytest.raises(_capi.InvalidParameter):
         ctx.loop_begin(knn=1, checkers=[("CounterTransformationChecker", 3)])
     ctx.close()
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("filt", [("TrimmedDistOutlierFilter", 0.85), ("MedianDistOutlierFilter", 3.0),
+                                  ("TrimmedDistOutlierFilter", 1.0)])
+def test_quantile_window_is_exact(monkeypatch, dtype, filt):
+    """The quantile resolved inside the match's key window (pmx_spec.h) is the
+    radix select's: with and without the window the whole loop is bit-identical
+    (the limit feeds the weights, the system and every later iteration) and the
+    window resolves most converged iterations.  (Oracle parity of the loop with
+    the window on, the default: test_loop_equals_modules / _filter_chains.)"""
+    ref, nrm = reference_cloud(60000, dtype)
+    rd = reading_cloud(50000, dtype)
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("PMX_SPEC_SELECT", on)
+        ctx = _capi.Context(0, dtype)
+        ctx.set_reference(ref, nrm)
+        ctx.set_reading(rd)
+        ctx.loop_begin(knn=1, filters=[filt], checkers=[("CounterTransformationChecker", 30)], keep_trace=True)
+        st = ctx.loop_run(30)
+        out[on] = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept, st.iterations)
+        ctx.close()
+    tr1, (hits, misses), kept1, it1 = out["1"]
+    tr0, (h0, m0), kept0, it0 = out["0"]
+    assert it1 == it0 == 30
+    assert h0 == 0 and m0 == 0
+    assert hits + misses == 30 and hits >= 15, (hits, misses)
+    assert kept1 == kept0
+    assert np.array_equal(tr1, tr0)
