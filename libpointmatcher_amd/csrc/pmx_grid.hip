@@ -448,17 +448,13 @@ __device__ __forceinline__ void add_visits(uint32_t visits, unsigned long long* 
 // before any filter can raise one).  With a quantile window (pmx_spec.h) it
 // also resolves the iteration's quantile from the window when it can.
 template <typename T>
-__global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long* __restrict__ vpart,
-                                                              unsigned long long* __restrict__ out,
-                                                              int* __restrict__ iter_err,
-                                                              const LoopCtl* __restrict__ ctl,
-                                                              SpecSel* __restrict__ spec,
-                                                              SelectState* __restrict__ st) {
+__device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ vpart,
+                                              unsigned long long* __restrict__ out, int* __restrict__ iter_err,
+                                              SpecSel* __restrict__ spec, SelectState* __restrict__ st) {
     __shared__ unsigned long long red[4][kVSlots / 64];
     __shared__ uint32_t lh[2048];
     __shared__ unsigned long long part[kVSlots];
     __shared__ unsigned long long bc[2];
-    if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     unsigned long long v[4];
 #pragma unroll
@@ -486,6 +482,18 @@ __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long
     }
     if (spec) spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], lh, part, bc);
 }
+
+template <typename T>
+__global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long* __restrict__ vpart,
+                                                              unsigned long long* __restrict__ out,
+                                                              int* __restrict__ iter_err,
+                                                              const LoopCtl* __restrict__ ctl,
+                                                              SpecSel* __restrict__ spec,
+                                                              SelectState* __restrict__ st) {
+    if (ctl && ctl->done) return;
+    counter_phase<T>(vpart, out, iter_err, spec, st);
+}
+
 // counters: 0 pairs, 1 full-search fallbacks, 2 finite distances, 3 below the quantile window
 size_t grid_counter_bytes() { return sizeof(unsigned long long) * 4 * kVSlots * kVStride; }
 
