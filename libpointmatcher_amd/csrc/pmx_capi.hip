@@ -759,9 +759,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->spec_now(), c->d_sel,
-                             c->stream);
+                             e1, c->stream);  // (e1 recorded after the match kernel, before the counter sum)
         c->safe_valid = ru.mode != 0;
-        if (e1) (void)hipEventRecord(e1, c->stream);
         c->visited_host = 0;
         c->ids_grid = true;
         c->ids_level = c->level;

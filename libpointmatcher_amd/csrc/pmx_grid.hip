@@ -721,7 +721,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                       SelectState* spec_st, hipStream_t s) {
+                       SelectState* spec_st, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
@@ -747,6 +747,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     else
         PMX_KT(16);
 #undef PMX_KT
+    if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel alone)
     if (visited && vout)
         hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
                            spec_st);
@@ -756,12 +757,14 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const int*, const P4<float>*, int64_t, const uint32_t*, int64_t,
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
-                                       const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*, hipStream_t);
+                                       const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*, hipEvent_t,
+                                       hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
-                                        const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*, hipStream_t);
+                                        const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
+                                        hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

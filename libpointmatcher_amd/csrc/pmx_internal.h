@@ -158,7 +158,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       hipStream_t s);
+                       hipEvent_t ev_end, hipStream_t s);
 // code-object preloads (one per translation unit, called by pmx_ctx_create)
 void preload_match();
 void preload_grid();
