@@ -19,7 +19,7 @@ from . import _capi
 from ._capi import ConvergenceError, InvalidParameter, TransformationError
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "lib", "libpmx_icp.so")
+LIB = os.path.join(HERE, "lib", os.environ.get("PMX_LIB_VARIANT", ""), "libpmx_icp.so")  # (variant: _capi.py)
 
 
 class InvalidElement(RuntimeError):
