@@ -263,6 +263,14 @@ __device__ __forceinline__ void pick_phase(uint32_t* __restrict__ hist, SelectSt
             }
         }
         s_rank = st->rank;
+        // key density around the quantile for the next window (pmx_spec.h):
+        // the finest bucket of this select still holding >= 64 keys (the
+        // last pass's 2^10-key bucket holds ~1 key for f64)
+        if (spec) {
+            const unsigned long long cnt = part[255];
+            if (pass == 0) spec->dens = -1.0;
+            if (cnt >= 64) spec->dens = (double)cnt / ldexp(1.0, shift + bits);
+        }
     }
     __syncthreads();
     if (s_err == 0) {
@@ -281,9 +289,10 @@ __device__ __forceinline__ void pick_phase(uint32_t* __restrict__ hist, SelectSt
                     st->rank = rank - cum;
                     if (last) {
                         st->limit = (double)KO::val(prefix);
-                        // next iteration's quantile window, centred here; the
-                        // keys sharing this pass's prefix span 2^bits key units
-                        if (spec) spec_update<T>(spec, prefix, (double)part[255] / (double)nb);
+                        // next iteration's quantile window, centred here
+                        if (spec)
+                            spec_update<T>(spec, prefix,
+                                           spec->dens > 0.0 ? spec->dens : (double)(part[255] + 1) / (double)nb);
                     }
                     break;
                 }

@@ -60,6 +60,7 @@ struct SpecSel {
     int have_prev;              // prev holds a limit
     int hit;                    // this iteration's limit came from the window
     unsigned long long n_hit, n_miss;  // statistics (host-readable)
+    double dens;                // key density estimate of the last radix select (keys per key unit)
 };
 
 // ---- match side: classify every distance the match writes ----

@@ -171,15 +171,18 @@ def test_loop_rejects_brute_force():
     ctx.close()
 
 
+@pytest.mark.parametrize("knn,max_dist", [(1, np.inf), (3, np.inf), (1, 0.05)])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 @pytest.mark.parametrize("filt", [("TrimmedDistOutlierFilter", 0.85), ("MedianDistOutlierFilter", 3.0),
                                   ("TrimmedDistOutlierFilter", 1.0)])
-def test_quantile_window_is_exact(monkeypatch, dtype, filt):
+def test_quantile_window_is_exact(monkeypatch, dtype, filt, knn, max_dist):
     """The quantile resolved inside the match's key window (pmx_spec.h) is the
     radix select's: with and without the window the whole loop is bit-identical
     (the limit feeds the weights, the system and every later iteration) and the
-    window resolves most converged iterations.  (Oracle parity of the loop with
-    the window on, the default: test_loop_equals_modules / _filter_chains.)"""
+    window resolves most converged iterations — also with k > 1 and with
+    radius-limited matches (infinite distances excluded from the count).
+    (Oracle parity of the loop with the window on, the default:
+    test_loop_equals_modules / _filter_chains.)"""
     ref, nrm = reference_cloud(60000, dtype)
     rd = reading_cloud(50000, dtype)
     out = {}
@@ -188,7 +191,8 @@ def test_quantile_window_is_exact(monkeypatch, dtype, filt):
         ctx = _capi.Context(0, dtype)
         ctx.set_reference(ref, nrm)
         ctx.set_reading(rd)
-        ctx.loop_begin(knn=1, filters=[filt], checkers=[("CounterTransformationChecker", 30)], keep_trace=True)
+        ctx.loop_begin(knn=knn, max_dist=max_dist, filters=[filt], checkers=[("CounterTransformationChecker", 30)],
+                       keep_trace=True)
         st = ctx.loop_run(30)
         out[on] = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept, st.iterations)
         ctx.close()
