@@ -106,7 +106,17 @@ def main():
         import torch
         import torch.distributed as tdist
 
-        tdist.init_process_group("gloo", init_method="env://")  # control plane only
+        # (gloo prints its connection banner on fd 1: keep stdout for the one
+        # JSON line by pointing fd 1 at stderr while the group is created)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            tdist.init_process_group("gloo", init_method="env://")  # control plane only
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     from libpointmatcher_amd import _capi
     from libpointmatcher_amd.icp import ICP
     from libpointmatcher_amd.synth import reading_cloud, reference_cloud
