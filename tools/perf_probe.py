@@ -1,6 +1,6 @@
 """Device-time probe of the per-iteration kernels (development tool).
 
-python tests/perf_probe.py N M k iters [f64] [brute]
+python tools/perf_probe.py N M k iters [f64] [brute]
 """
 import os
 import sys

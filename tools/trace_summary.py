@@ -1,6 +1,6 @@
 """Summarise rocprofv3 kernel traces (development tool).
 
-python tests/trace_summary.py gpurun_out/var/*/   -> per kernel-name position in the last
+python tools/trace_summary.py gpurun_out/var/*/   -> per kernel-name position in the last
 iteration: duration (us), plus the mean over the last `--last` occurrences.
 """
 import csv
