@@ -9,7 +9,9 @@
 //                                 ErrorMinimizers/PointToPlane.h:61-90, PointToPoint.h
 //   Counter / Differential / Bound TransformationChecker
 //                                 TransformationCheckersImpl.h:60-130
-//   IdentityDataPointsFilter, NullInspector, NullLogger (+ no-op stand-ins for
+//   Identity / SurfaceNormal / MaxDist / MinDist DataPointsFilter
+//                                 DataPointsFilters/{SurfaceNormal,MaxDist,MinDist}.h
+//   NullInspector, NullLogger (+ no-op stand-ins for
 //   the VTK/Performance inspectors and FileLogger, accepted for config
 //   compatibility)
 #include "pm_icp.h"
@@ -601,6 +603,61 @@ struct SurfaceNormalDPF : PM<T>::DataPointsFilter {
     }
 };
 
+// MaxDist / MinDist data filters (DataPointsFilters/MaxDist.cpp:55-96,
+// MinDist.cpp:55-96, parameters MaxDist.h:57-61, MinDist.h:57-61): keep the
+// points whose coordinate `dim` (or Euclidean norm when dim == -1, against
+// |limit|) is strictly below (Max) / strictly above (Min) the limit,
+// stable compaction of features and descriptors; dim >= D throws.  Host code,
+// once per compute and outside the ICP loop, as in the reference.
+template <typename T, bool kMax>
+struct DistDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static const char* pname() { return kMax ? "maxDist" : "minDist"; }
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("dim", "dimension on which the filter will be applied. x=0, y=1, z=2, radius=-1", "-1", "-1", "2",
+                     &P::Comp<int>),
+                PDoc(pname(), kMax ? "maximum distance authorized" : "minimum value authorized", "1", "-inf", "inf",
+                     &P::Comp<T>)};
+    }
+    const int dim;
+    const T limit;
+    explicit DistDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter(kMax ? "MaxDistDataPointsFilter" : "MinDistDataPointsFilter", doc(), p),
+          dim(this->template get<int>("dim")),
+          limit(this->template get<T>(pname())) {}
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        const int D = cloud.rows - 1;
+        if (dim >= D)
+            throw InvalidParameter(this->className + ": Error, filtering on dimension number " + std::to_string(dim) +
+                                   ", larger than authorized axis id " + std::to_string(D - 1));
+        const T absLimit = std::abs(limit);
+        int64_t j = 0;
+        for (int64_t i = 0; i < cloud.n; ++i) {
+            const T* f = &cloud.features[(size_t)i * cloud.rows];
+            bool keep;
+            if (dim == -1) {
+                T s = 0;
+                for (int r = 0; r < D; ++r) s += f[r] * f[r];
+                const T norm = std::sqrt(s);
+                keep = kMax ? (norm < absLimit) : (norm > absLimit);
+            } else {
+                keep = kMax ? (f[dim] < limit) : (f[dim] > limit);
+            }
+            if (!keep) continue;
+            if (j != i) {
+                std::copy(f, f + cloud.rows, &cloud.features[(size_t)j * cloud.rows]);
+                std::copy(&cloud.descriptors[(size_t)i * cloud.descDim],
+                          &cloud.descriptors[(size_t)i * cloud.descDim] + cloud.descDim,
+                          &cloud.descriptors[(size_t)j * cloud.descDim]);
+            }
+            ++j;
+        }
+        cloud.n = j;
+        cloud.features.resize((size_t)j * cloud.rows);
+        cloud.descriptors.resize((size_t)j * cloud.descDim);
+    }
+};
+
 // Reference data filters that are outside the hot path:
 // registered with the reference's parameter docs so chain files validate
 // exactly as in the reference (bounds, unused parameters, module types), but
@@ -635,14 +692,6 @@ void register_unsupported_filters(Registrar<typename PM<T>::DataPointsFilter>& R
          PDoc("averageExistingDescriptors", "keep and average existing descriptors", "1"),
          PDoc("keepNormals", "add normals as descriptors", "1"), PDoc("keepDensities", "add densities", "0"),
          PDoc("keepEigenValues", "add eigen values", "0"), PDoc("keepEigenVectors", "add eigen vectors", "0")});
-    add("MaxDistDataPointsFilter",
-        {PDoc("dim", "dimension on which the filter will be applied. x=0, y=1, z=2, radius=-1", "-1", "-1", "2",
-              &P::Comp<int>),
-         PDoc("maxDist", "maximum distance authorized", "1", "-inf", "inf", &P::Comp<T>)});
-    add("MinDistDataPointsFilter",
-        {PDoc("dim", "dimension on which the filter will be applied. x=0, y=1, z=2, radius=-1", "-1", "-1", "2",
-              &P::Comp<int>),
-         PDoc("minDist", "minimum value authorized", "1", "-inf", "inf", &P::Comp<T>)});
 }
 
 // no-op stand-in accepting a reference module's parameters (reads them all so
@@ -709,6 +758,10 @@ PointMatcher<T>::PointMatcher() {
                                   [](const Ps& p) { return std::make_shared<IdentityDPF<T>>(p); }, false);
     DataPointsFilterRegistrar.reg("SurfaceNormalDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<SurfaceNormalDPF<T>>(p); }, true);
+    DataPointsFilterRegistrar.reg("MaxDistDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<DistDPF<T, true>>(p); }, true);
+    DataPointsFilterRegistrar.reg("MinDistDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<DistDPF<T, false>>(p); }, true);
     register_unsupported_filters<T>(DataPointsFilterRegistrar);
     InspectorRegistrar.reg("NullInspector", [](const Ps& p) {
         return std::make_shared<NoOp<Inspector>>("NullInspector", Parametrizable::ParametersDoc(), p);

@@ -1,0 +1,96 @@
+"""MaxDist / MinDist DataPointsFilter as reading filters of the ICP chain
+(DataPointsFilters/MaxDist.cpp:55-96, MinDist.cpp:55-96).
+
+The reference's own tests (utest/ui/DataFilters.cpp:107-180) add each filter to
+the reading chain with dim 0 / 1 / -1 and check the validT2d / validT3d known
+answers, dim 2 throwing on the 2-D clouds and dim 3 rejected at construction.
+Here the same, plus an exact check of the filtering itself: the chain with the
+filter gives the bit-identical transform of the chain without it run on the
+reading pre-filtered by the reference's rule in numpy (strict < / >, the
+Euclidean norm against |limit| for dim -1).
+"""
+import numpy as np
+import pytest
+
+from helpers import chain_yaml, hom, validate2d, validate3d
+from libpointmatcher_amd.icp import ICP
+
+DIFF = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
+
+
+def with_reading_filter(yaml, name, params):
+    body = "".join(f"      {k}: {v}\n" for k, v in params.items())
+    return f"readingDataPointsFilters:\n  - {name}:\n{body}" + yaml
+
+
+def keep_rule(pts, kind, dim, limit):
+    if dim == -1:
+        v, lim = np.sqrt((pts.astype(pts.dtype) ** 2).sum(axis=1)), abs(limit)
+    else:
+        v, lim = pts[:, dim], limit
+    return v < lim if kind == "Max" else v > lim
+
+
+def test_dim_out_of_range_rejected_at_construction():
+    # DataFilters.cpp:143-145: dim 3 is outside the parameter bounds [-1, 2]
+    icp = ICP(np.float32)
+    with pytest.raises(Exception):
+        icp.load_yaml(with_reading_filter(chain_yaml(), "MaxDistDataPointsFilter", {"dim": 3, "maxDist": 6.0}))
+    with pytest.raises(Exception):
+        icp.load_yaml(with_reading_filter(chain_yaml(), "MinDistDataPointsFilter", {"dim": -2, "minDist": 0.05}))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,limit", [("Max", 6.0), ("Min", 0.05)])
+@pytest.mark.parametrize("dim", [0, 1, 2, -1])
+def test_reference_ui_cases_3d(golden, kind, limit, dim):
+    # DataFilters.cpp:107-180, validate3dTransformation (point-to-plane, car clouds)
+    g, kat = golden
+    name = f"{kind}DistDataPointsFilter"
+    icp = ICP(np.float32)
+    icp.load_yaml(with_reading_filter(chain_yaml(differential=DIFF), name,
+                                      {"dim": dim, f"{kind.lower()}Dist": limit}))
+    T = icp.compute(hom(g["car401"], np.float32), hom(g["car400"], np.float32), g["car400_normals"])
+    ok, dt, da = validate3d(T, np.array(kat["validT3d"]), kat["tol3d"])
+    assert ok, (dt, da)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,limit", [("Max", 6.0), ("Min", 0.05)])
+@pytest.mark.parametrize("dim", [0, 1, 2, -1])
+def test_reference_ui_cases_2d(golden, kind, limit, dim):
+    # validate2dTransformation (point-to-point, box clouds); dim 2 throws on 2-D
+    g, kat = golden
+    name = f"{kind}DistDataPointsFilter"
+    icp = ICP(np.float32)
+    icp.load_yaml(with_reading_filter(chain_yaml(minimizer="PointToPointErrorMinimizer", differential=DIFF), name,
+                                      {"dim": dim, f"{kind.lower()}Dist": limit}))
+    if dim == 2:
+        with pytest.raises(Exception):
+            icp.compute(hom(g["box2"], np.float32), hom(g["box1"], np.float32), None)
+        return
+    T = icp.compute(hom(g["box2"], np.float32), hom(g["box1"], np.float32), None)
+    ok, dt, da = validate2d(T, np.array(kat["validT2d"]), kat["tol2d"])
+    assert ok, (dt, da)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("kind,dim,limit", [("Max", 0, 2.0), ("Max", -1, -20.0), ("Min", 1, -3.0),
+                                            ("Min", -1, 3.0), ("Max", 2, 10.0)])
+def test_filter_equals_prefiltered_reading(golden, dtype, kind, dim, limit):
+    g, _ = golden
+    rd = g["car401"].astype(dtype)
+    ref = g["car400"].astype(dtype)
+    nrm = g["car400_normals"].astype(dtype)
+    keep = keep_rule(rd, kind, dim, dtype(limit))
+    assert 0 < keep.sum() <= rd.shape[0]
+    base = chain_yaml(differential=DIFF)
+    a = ICP(dtype)
+    a.load_yaml(with_reading_filter(base, f"{kind}DistDataPointsFilter", {"dim": dim, f"{kind.lower()}Dist": limit}))
+    Ta = a.compute(hom(rd, dtype), hom(ref, dtype), nrm)
+    b = ICP(dtype)
+    b.load_yaml(base)
+    Tb = b.compute(hom(rd[keep], dtype), hom(ref, dtype), nrm)
+    assert np.array_equal(Ta, Tb)
+    assert a.stats().iterations == b.stats().iterations
