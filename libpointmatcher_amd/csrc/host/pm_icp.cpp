@@ -9,8 +9,8 @@
 //                                 ErrorMinimizers/PointToPlane.h:61-90, PointToPoint.h
 //   Counter / Differential / Bound TransformationChecker
 //                                 TransformationCheckersImpl.h:60-130
-//   Identity / SurfaceNormal / MaxDist / MinDist DataPointsFilter
-//                                 DataPointsFilters/{SurfaceNormal,MaxDist,MinDist}.h
+//   Identity / SurfaceNormal / MaxDist / MinDist / RandomSampling / FixStepSampling
+//   DataPointsFilter              DataPointsFilters/{SurfaceNormal,MaxDist,MinDist,RandomSampling,FixStepSampling}.h
 //   NullInspector, NullLogger (+ no-op stand-ins for
 //   the VTK/Performance inspectors and FileLogger, accepted for config
 //   compatibility)
@@ -603,6 +603,27 @@ struct SurfaceNormalDPF : PM<T>::DataPointsFilter {
     }
 };
 
+// Stable in-place compaction of a cloud's points (features and descriptors),
+// keep(f) called once per point in index order — DataPoints::setColFrom +
+// conservativeResize of the reference's subsampling filters.
+template <typename T, typename Keep>
+void compact_points(DataPoints<T>& cloud, Keep keep) {
+    int64_t j = 0;
+    for (int64_t i = 0; i < cloud.n; ++i) {
+        const T* f = &cloud.features[(size_t)i * cloud.rows];
+        if (!keep(f)) continue;
+        if (j != i) {
+            std::copy(f, f + cloud.rows, &cloud.features[(size_t)j * cloud.rows]);
+            const T* d = &cloud.descriptors[(size_t)i * cloud.descDim];
+            std::copy(d, d + cloud.descDim, &cloud.descriptors[(size_t)j * cloud.descDim]);
+        }
+        ++j;
+    }
+    cloud.n = j;
+    cloud.features.resize((size_t)j * cloud.rows);
+    cloud.descriptors.resize((size_t)j * cloud.descDim);
+}
+
 // MaxDist / MinDist data filters (DataPointsFilters/MaxDist.cpp:55-96,
 // MinDist.cpp:55-96, parameters MaxDist.h:57-61, MinDist.h:57-61): keep the
 // points whose coordinate `dim` (or Euclidean norm when dim == -1, against
@@ -631,30 +652,78 @@ struct DistDPF : PM<T>::DataPointsFilter {
             throw InvalidParameter(this->className + ": Error, filtering on dimension number " + std::to_string(dim) +
                                    ", larger than authorized axis id " + std::to_string(D - 1));
         const T absLimit = std::abs(limit);
-        int64_t j = 0;
-        for (int64_t i = 0; i < cloud.n; ++i) {
-            const T* f = &cloud.features[(size_t)i * cloud.rows];
-            bool keep;
+        compact_points(cloud, [&](const T* f) {
             if (dim == -1) {
                 T s = 0;
                 for (int r = 0; r < D; ++r) s += f[r] * f[r];
                 const T norm = std::sqrt(s);
-                keep = kMax ? (norm < absLimit) : (norm > absLimit);
-            } else {
-                keep = kMax ? (f[dim] < limit) : (f[dim] > limit);
+                return kMax ? (norm < absLimit) : (norm > absLimit);
             }
-            if (!keep) continue;
-            if (j != i) {
-                std::copy(f, f + cloud.rows, &cloud.features[(size_t)j * cloud.rows]);
-                std::copy(&cloud.descriptors[(size_t)i * cloud.descDim],
-                          &cloud.descriptors[(size_t)i * cloud.descDim] + cloud.descDim,
-                          &cloud.descriptors[(size_t)j * cloud.descDim]);
-            }
-            ++j;
-        }
-        cloud.n = j;
-        cloud.features.resize((size_t)j * cloud.rows);
-        cloud.descriptors.resize((size_t)j * cloud.descDim);
+            return kMax ? (f[dim] < limit) : (f[dim] > limit);
+        });
+    }
+};
+
+// RandomSamplingDataPointsFilter (DataPointsFilters/RandomSampling.cpp:55-74,
+// RandomSampling.h:59-62): keep point i when (float)std::rand() /
+// (float)RAND_MAX < prob, one draw per point in order — the same C library
+// generator and state as the reference, so the kept set is identical for the
+// same srand seed.
+template <typename T>
+struct RandomSamplingDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("prob", "probability to keep a point, one over decimation factor ", "0.75", "0", "1",
+                     &P::Comp<T>)};
+    }
+    const double prob;
+    explicit RandomSamplingDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter("RandomSamplingDataPointsFilter", doc(), p), prob(this->template get<double>("prob")) {}
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        compact_points(cloud, [&](const T*) {
+            const float r = (float)std::rand() / (float)RAND_MAX;
+            return r < prob;
+        });
+    }
+};
+
+// FixStepSamplingDataPointsFilter (DataPointsFilters/FixStepSampling.cpp:37-93,
+// FixStepSampling.h:57-72): keep every step-th point from a random phase
+// rand() % step; step starts at startStep (reset by init) and is multiplied by
+// stepMult after each application, clamped at endStep.
+template <typename T>
+struct FixStepSamplingDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("startStep", "initial number of point to skip (initial decimation factor)", "10", "1",
+                     "2147483647", &P::Comp<unsigned>),
+                PDoc("endStep", "maximal or minimal number of points to skip (final decimation factor)", "10", "1",
+                     "2147483647", &P::Comp<unsigned>),
+                PDoc("stepMult", "multiplication factor to compute the new decimation factor for each iteration", "1",
+                     "0.0000001", "inf", &P::Comp<double>)};
+    }
+    const unsigned startStep, endStep;
+    const double stepMult;
+    double step;
+    explicit FixStepSamplingDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter("FixStepSamplingDataPointsFilter", doc(), p),
+          startStep(this->template get<unsigned>("startStep")),
+          endStep(this->template get<unsigned>("endStep")),
+          stepMult(this->template get<double>("stepMult")),
+          step(startStep) {}
+    void init() override { step = startStep; }
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        const int iStep((int)step);
+        const int64_t phase = std::rand() % iStep;
+        int64_t i = -1;
+        compact_points(cloud, [&](const T*) {
+            ++i;
+            return i >= phase && (i - phase) % iStep == 0;
+        });
+        const double deltaStep(startStep * stepMult - startStep);
+        step *= stepMult;
+        if (deltaStep < 0 && step < endStep) step = endStep;
+        if (deltaStep > 0 && step > endStep) step = endStep;
     }
 };
 
@@ -682,8 +751,6 @@ void register_unsupported_filters(Registrar<typename PM<T>::DataPointsFilter>& R
     auto add = [&](const std::string& name, Parametrizable::ParametersDoc d) {
         R.reg(name, [name, d](const Ps& p) { return std::make_shared<UnsupportedDPF<T>>(name, d, p); }, true);
     };
-    add("RandomSamplingDataPointsFilter",
-        {PDoc("prob", "probability to keep a point, one over decimation factor ", "0.75", "0", "1", &P::Comp<T>)});
     add("SamplingSurfaceNormalDataPointsFilter",
         {PDoc("ratio", "ratio of points to keep with random subsampling", "0.5", "0.0000001", "1.0", &P::Comp<T>),
          PDoc("knn", "how many points are used to compute the normals", "7", "3", "2147483647", &P::Comp<unsigned>),
@@ -758,6 +825,10 @@ PointMatcher<T>::PointMatcher() {
                                   [](const Ps& p) { return std::make_shared<IdentityDPF<T>>(p); }, false);
     DataPointsFilterRegistrar.reg("SurfaceNormalDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<SurfaceNormalDPF<T>>(p); }, true);
+    DataPointsFilterRegistrar.reg("RandomSamplingDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<RandomSamplingDPF<T>>(p); }, true);
+    DataPointsFilterRegistrar.reg("FixStepSamplingDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<FixStepSamplingDPF<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("MaxDistDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<DistDPF<T, true>>(p); }, true);
     DataPointsFilterRegistrar.reg("MinDistDataPointsFilter",

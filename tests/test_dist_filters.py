@@ -1,4 +1,4 @@
-"""MaxDist / MinDist DataPointsFilter as reading filters of the ICP chain
+"""MaxDist / MinDist / RandomSampling / FixStepSampling DataPointsFilter as reading filters of the ICP chain
 (DataPointsFilters/MaxDist.cpp:55-96, MinDist.cpp:55-96).
 
 The reference's own tests (utest/ui/DataFilters.cpp:107-180) add each filter to
@@ -94,3 +94,85 @@ def test_filter_equals_prefiltered_reading(golden, dtype, kind, dim, limit):
     Tb = b.compute(hom(rd[keep], dtype), hom(ref, dtype), nrm)
     assert np.array_equal(Ta, Tb)
     assert a.stats().iterations == b.stats().iterations
+
+
+# ---- RandomSampling / FixStepSampling (RandomSampling.cpp:55-74,
+# FixStepSampling.cpp:63-93): both draw from the C library's rand(), as the
+# reference; the expected kept set is replayed here from the same libc state
+# (srand(seed) in this process, which the filter shares).
+LIBC = None
+
+
+def libc():
+    global LIBC
+    if LIBC is None:
+        import ctypes
+        LIBC = ctypes.CDLL(None)
+        LIBC.rand.restype = ctypes.c_int
+    return LIBC
+
+
+RAND_MAX = 2147483647  # glibc
+
+
+def random_keep(n, prob, seed):
+    c = libc()
+    c.srand(seed)
+    r = np.array([c.rand() for _ in range(n)], dtype=np.float32) / np.float32(RAND_MAX)
+    return r.astype(np.float64) < prob
+
+
+def fixstep_keep(n, step, seed):
+    c = libc()
+    c.srand(seed)
+    phase = c.rand() % step
+    keep = np.zeros(n, bool)
+    keep[phase::step] = True
+    return keep
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prob", [0.80, 0.85, 0.90, 0.95])
+def test_random_sampling_reference_cases(golden, prob):
+    # DataFilters.cpp:362-376: validate2dTransformation / validate3dTransformation
+    g, kat = golden
+    for rd, ref, nrm, mini, val, V, tol in [
+            (g["box2"], g["box1"], None, "PointToPointErrorMinimizer", validate2d, kat["validT2d"], kat["tol2d"]),
+            (g["car401"], g["car400"], g["car400_normals"], "PointToPlaneErrorMinimizer", validate3d,
+             kat["validT3d"], kat["tol3d"])]:
+        icp = ICP(np.float32)
+        icp.load_yaml(with_reading_filter(chain_yaml(minimizer=mini, differential=DIFF),
+                                          "RandomSamplingDataPointsFilter", {"prob": prob}))
+        T = icp.compute(hom(rd, np.float32), hom(ref, np.float32), nrm)
+        ok, dt, da = val(T, np.array(V), tol)
+        assert ok, (dt, da)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,param,value,keepfn", [
+    ("RandomSamplingDataPointsFilter", "prob", 0.5, random_keep),
+    ("FixStepSamplingDataPointsFilter", "startStep", 3, fixstep_keep),
+    ("FixStepSamplingDataPointsFilter", "startStep", 1, fixstep_keep)])
+@pytest.mark.parametrize("seed", [1, 12345])
+def test_sampling_equals_prefiltered_reading(golden, name, param, value, keepfn, seed):
+    g, _ = golden
+    rd, ref, nrm = g["car401"], g["car400"], g["car400_normals"]
+    keep = keepfn(rd.shape[0], value, seed)
+    base = chain_yaml(differential=DIFF)
+    b = ICP(np.float32)
+    b.load_yaml(base)
+    Tb = b.compute(hom(rd[keep], np.float32), hom(ref, np.float32), nrm)
+    a = ICP(np.float32)
+    a.load_yaml(with_reading_filter(base, name, {param: value, **({"endStep": value} if "FixStep" in name else {})}))
+    libc().srand(seed)
+    Ta = a.compute(hom(rd, np.float32), hom(ref, np.float32), nrm)
+    assert np.array_equal(Ta, Tb)
+    assert a.stats().iterations == b.stats().iterations
+
+
+@pytest.mark.parametrize("name,param,value", [("FixStepSamplingDataPointsFilter", "startStep", 0),
+                                              ("RandomSamplingDataPointsFilter", "prob", 1.5)])
+def test_sampling_bad_params(name, param, value):
+    icp = ICP(np.float32)
+    with pytest.raises(Exception):
+        icp.load_yaml(with_reading_filter(chain_yaml(), name, {param: value}))
