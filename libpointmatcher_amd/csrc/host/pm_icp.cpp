@@ -9,8 +9,8 @@
 //                                 ErrorMinimizers/PointToPlane.h:61-90, PointToPoint.h
 //   Counter / Differential / Bound TransformationChecker
 //                                 TransformationCheckersImpl.h:60-130
-//   Identity / SurfaceNormal / MaxDist / MinDist / RandomSampling / FixStepSampling
-//   DataPointsFilter              DataPointsFilters/{SurfaceNormal,MaxDist,MinDist,RandomSampling,FixStepSampling}.h
+//   Identity / SurfaceNormal / MaxDist / MinDist / RandomSampling / FixStepSampling /
+//   BoundingBox DataPointsFilter  DataPointsFilters/{SurfaceNormal,MaxDist,MinDist,RandomSampling,FixStepSampling,BoundingBox}.h
 //   NullInspector, NullLogger (+ no-op stand-ins for
 //   the VTK/Performance inspectors and FileLogger, accepted for config
 //   compatibility)
@@ -687,6 +687,51 @@ struct RandomSamplingDPF : PM<T>::DataPointsFilter {
     }
 };
 
+// BoundingBoxDataPointsFilter (DataPointsFilters/BoundingBox.cpp:76-108,
+// BoundingBox.h:57-67): open box (strict < / >) on x, y and z (z ignored for
+// 2-D clouds); removeInside keeps the points outside the box, else inside.
+template <typename T>
+struct BoundingBoxDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("xMin", "minimum value on x-axis defining one side of the bounding box", "-1", "-inf", "inf",
+                     &P::Comp<T>),
+                PDoc("xMax", "maximum value on x-axis defining one side of the bounding box", "1", "-inf", "inf",
+                     &P::Comp<T>),
+                PDoc("yMin", "minimum value on y-axis defining one side of the bounding box", "-1", "-inf", "inf",
+                     &P::Comp<T>),
+                PDoc("yMax", "maximum value on y-axis defining one side of the bounding box", "1", "-inf", "inf",
+                     &P::Comp<T>),
+                PDoc("zMin", "minimum value on z-axis defining one side of the bounding box", "-1", "-inf", "inf",
+                     &P::Comp<T>),
+                PDoc("zMax", "maximum value on z-axis defining one side of the bounding box", "1", "-inf", "inf",
+                     &P::Comp<T>),
+                PDoc("removeInside",
+                     "If set to true (1), remove points inside the bounding box; else (0), remove points outside the "
+                     "bounding box",
+                     "1", "0", "1", &P::Comp<bool>)};
+    }
+    const T xMin, xMax, yMin, yMax, zMin, zMax;
+    const bool removeInside;
+    explicit BoundingBoxDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter("BoundingBoxDataPointsFilter", doc(), p),
+          xMin(this->template get<T>("xMin")),
+          xMax(this->template get<T>("xMax")),
+          yMin(this->template get<T>("yMin")),
+          yMax(this->template get<T>("yMax")),
+          zMin(this->template get<T>("zMin")),
+          zMax(this->template get<T>("zMax")),
+          removeInside(this->template get<bool>("removeInside")) {}
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        const bool flat = cloud.rows == 3;
+        compact_points(cloud, [&](const T* f) {
+            const bool in = f[0] > xMin && f[0] < xMax && f[1] > yMin && f[1] < yMax &&
+                            ((f[2] > zMin && f[2] < zMax) || flat);
+            return removeInside ? !in : in;
+        });
+    }
+};
+
 // FixStepSamplingDataPointsFilter (DataPointsFilters/FixStepSampling.cpp:37-93,
 // FixStepSampling.h:57-72): keep every step-th point from a random phase
 // rand() % step; step starts at startStep (reset by init) and is multiplied by
@@ -827,6 +872,8 @@ PointMatcher<T>::PointMatcher() {
                                   [](const Ps& p) { return std::make_shared<SurfaceNormalDPF<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("RandomSamplingDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<RandomSamplingDPF<T>>(p); }, true);
+    DataPointsFilterRegistrar.reg("BoundingBoxDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<BoundingBoxDPF<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("FixStepSamplingDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<FixStepSamplingDPF<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("MaxDistDataPointsFilter",

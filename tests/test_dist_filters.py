@@ -176,3 +176,38 @@ def test_sampling_bad_params(name, param, value):
     icp = ICP(np.float32)
     with pytest.raises(Exception):
         icp.load_yaml(with_reading_filter(chain_yaml(), name, {param: value}))
+
+
+# ---- BoundingBox (BoundingBox.cpp:76-108): open box, z ignored on 2-D clouds
+@pytest.mark.gpu
+@pytest.mark.parametrize("remove_inside", [0, 1])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_bounding_box_equals_prefiltered_reading(golden, remove_inside, dtype):
+    g, _ = golden
+    rd, ref, nrm = g["car401"].astype(dtype), g["car400"].astype(dtype), g["car400_normals"].astype(dtype)
+    box = dict(xMin=-10.0, xMax=8.0, yMin=-6.0, yMax=12.0, zMin=-1.0, zMax=2.5)
+    b_ = {k: dtype(v) for k, v in box.items()}
+    inside = ((rd[:, 0] > b_["xMin"]) & (rd[:, 0] < b_["xMax"]) & (rd[:, 1] > b_["yMin"]) & (rd[:, 1] < b_["yMax"]) &
+              (rd[:, 2] > b_["zMin"]) & (rd[:, 2] < b_["zMax"]))
+    keep = ~inside if remove_inside else inside
+    assert 0 < keep.sum() < rd.shape[0]
+    base = chain_yaml(differential=DIFF)
+    a = ICP(dtype)
+    a.load_yaml(with_reading_filter(base, "BoundingBoxDataPointsFilter", {**box, "removeInside": remove_inside}))
+    Ta = a.compute(hom(rd, dtype), hom(ref, dtype), nrm)
+    b = ICP(dtype)
+    b.load_yaml(base)
+    Tb = b.compute(hom(rd[keep], dtype), hom(ref, dtype), nrm)
+    assert np.array_equal(Ta, Tb)
+
+
+@pytest.mark.gpu
+def test_bounding_box_2d_ignores_z(golden):
+    g, kat = golden
+    icp = ICP(np.float32)
+    icp.load_yaml(with_reading_filter(chain_yaml(minimizer="PointToPointErrorMinimizer", differential=DIFF),
+                                      "BoundingBoxDataPointsFilter",
+                                      dict(xMin=-100, xMax=100, yMin=-100, yMax=100, zMin=5, zMax=6, removeInside=0)))
+    T = icp.compute(hom(g["box2"], np.float32), hom(g["box1"], np.float32), None)
+    ok, dt, da = validate2d(T, np.array(kat["validT2d"]), kat["tol2d"])
+    assert ok, (dt, da)
