@@ -46,35 +46,80 @@ FP32_VALU_TFLOPS = 157.3   # MI355X FP32 vector peak (spec)
 FP64_VALU_TFLOPS = 78.6
 
 
-def chain_yaml(knn, filters, minimizer, search_type, maxit):
+def chain_yaml(knn, filters, minimizer, search_type, maxit, differential=None):
     lines = ["matcher:", "  KDTreeMatcher:", f"    knn: {knn}", "    epsilon: 0", f"    searchType: {search_type}",
              "outlierFilters:"]
     for name, p in filters:
         lines.append(f"  - {name}:")
         lines += [f"      {k}: {v}" for k, v in p.items()]
     lines += ["errorMinimizer:", f"  {minimizer}", "transformationCheckers:", "  - CounterTransformationChecker:",
-              f"      maxIterationCount: {maxit}", "inspector:", "  NullInspector", "logger:", "  NullLogger"]
+              f"      maxIterationCount: {maxit}"]
+    if differential:
+        lines.append("  - DifferentialTransformationChecker:")
+        lines += [f"      {k}: {v}" for k, v in differential.items()]
+    lines += ["inspector:", "  NullInspector", "logger:", "  NullLogger"]
     return "\n".join(lines) + "\n"
 
 
-def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer, iters, threads):
+# parity runs: Counter 40 + Differential, equal iteration counts required
+PARITY_DIFF = {"minDiffRotErr": 0.001, "minDiffTransErr": 0.01, "smoothLength": 4}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer, iters, threads, one_thread_iters):
+    """The oracle (C restatement of the reference CPU path: libnabo-style
+    kd-tree, nth_element quantile, -O3) on the same inputs, timed on this host.
+    Runs the parity chain (Counter + Differential) with all cores, the same
+    chain with T-precision accumulation of the minimiser sums (the reference's
+    Eigen arithmetic), and a bounded 1-thread sample (the reference's default:
+    no OpenMP, CMakeLists.txt:160)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
 
-    cfg = O.make_cfg(knn=knn, filters=tuple(filters), minimizer=minimizer, counter_max=iters, threads=threads,
-                     method="kdtree")
-    t0 = time.perf_counter()
-    rc, T, st, _ = O.icp(cfg, reading, reference, normals=normals if minimizer.startswith("PointToPlane") else None)
-    wall = time.perf_counter() - t0
-    if rc != 0:
-        return None
-    loop = st.loop_seconds
+    nrm = normals if minimizer.startswith("PointToPlane") else None
     n = reading.shape[0]
-    return {"value": n * knn * st.iterations / loop, "unit": "matched-pairs/s", "cores": threads,
-            "kind": "port", "iters_per_s": st.iterations / loop,
-            "sample": f"{cfg_name} inputs ({n}->{reference.shape[0]}), {st.iterations} ICP iterations, "
-                      f"kd-tree (libnabo-style, exact) oracle restatement of the reference CPU path, "
-                      f"{threads} thread(s), loop {loop:.2f} s (setup+loop {wall:.2f} s)"}
+    out = {}
+
+    def run(th, maxit, diff, acc):
+        cfg = O.make_cfg(knn=knn, filters=tuple(filters), minimizer=minimizer, counter_max=maxit, threads=th,
+                         method="kdtree", differential=diff, acc_mode=acc)
+        t0 = time.perf_counter()
+        rc, T, st, _ = O.icp(cfg, reading, reference, normals=nrm)
+        return rc, T, st, time.perf_counter() - t0
+
+    rc, T, st, wall = run(threads, iters, PARITY_DIFF, 0)
+    if rc != 0:
+        return None, None
+    loop = st.loop_seconds
+    out = {"value": n * knn * st.iterations / loop, "unit": "matched-pairs/s", "cores": threads,
+           "kind": "port", "iters_per_s": st.iterations / loop,
+           "host_cpu": cpu_model(), "host_nproc": os.cpu_count(),
+           "sample": f"{cfg_name} inputs ({n}->{reference.shape[0]}), the parity chain (Counter {iters} + "
+                     f"Differential 0.001/0.01/4: {st.iterations} ICP iterations), oracle restatement of the "
+                     f"reference CPU path (libnabo-style kd-tree, incremental box bound, nth_element quantile, "
+                     f"gcc -O3), {threads} threads, loop {loop:.2f} s (setup+loop {wall:.2f} s)"}
+    ref_run = {"T": T, "iterations": int(st.iterations), "kept": int(st.kept)}
+    rc1, T1, st1, _ = run(1, one_thread_iters, None, 0)
+    if rc1 == 0:
+        out["single_thread"] = {"value": n * knn * st1.iterations / st1.loop_seconds, "unit": "matched-pairs/s",
+                                "cores": 1, "iters_per_s": st1.iterations / st1.loop_seconds,
+                                "sample": f"first {st1.iterations} ICP iterations, 1 thread, "
+                                          f"loop {st1.loop_seconds:.2f} s"}
+    rcT, TT, stT, _ = run(threads, iters, PARITY_DIFF, 1)
+    if rcT == 0:
+        ref_run["T_accT"] = TT
+        ref_run["iterations_accT"] = int(stT.iterations)
+    return out, ref_run
 
 
 def main():
@@ -89,6 +134,8 @@ def main():
                     help="KDTreeMatcher searchType 0 (brute force) or 1 (spatial grid)")
     ap.add_argument("--cpu-iters", type=int, default=40)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-one-thread-iters", type=int, default=2,
+                    help="ICP iterations of the bounded single-thread CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist", action="store_true",
                     help="use the torchrun/RCCL multi-rank path even at world size 1 (rehearsal on one GPU)")
@@ -144,7 +191,11 @@ def main():
         icp.comm_init(bytes(t.tolist()), world, rank)
 
     nrm_in = normals if minimizer.startswith("PointToPlane") else None
+    # setup (reported separately): reference upload + grid
+    # build (Matcher::init), reading upload + slot order, ICP.cpp:265-347
+    t_s = time.perf_counter()
     icp.prepare(reading, reference, nrm_in)
+    setup_s = time.perf_counter() - t_s
     if args.warmup > 0:
         icp.iterate(args.warmup)
 
@@ -208,12 +259,16 @@ def main():
     # (gfx950 correction) + WRITE_SIZE, per launch); null for other configs
     traffic, traffic_src = None, None
     if args.config == "c3" and args.matcher == "grid" and world == 1:
+        # the PMC passes of this exact driver command (tools/pmc_phases.py:
+        # FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE per launch, averaged
+        # over the launches of the timed steps)
+        src = os.path.join("profiles", "r02", "pmc_c3_driver.json")
         try:
-            with open(os.path.join(ROOT, "profiles", "r01", "pmc_c3_traffic.json")) as f:
-                kk = json.load(f)["kernels"]
-            traffic = next(v["hbm_bytes"] for k, v in kk.items() if "grid_lane_kernel" in k)
-            traffic_src = "profiles/r01/pmc_c3_traffic.json"
-        except (OSError, KeyError, StopIteration, ValueError):
+            with open(os.path.join(ROOT, src)) as f:
+                pm = json.load(f)
+            traffic = pm["match"]["timed"]["hbm_bytes_per_launch"]
+            traffic_src = src
+        except (OSError, KeyError, TypeError, ValueError):
             pass
     peak_tf = FP32_VALU_TFLOPS if esz == 4 else FP64_VALU_TFLOPS
     metric = "ICP iterations/sec + matched-pairs/sec, 1M→1M pts, k=1, point-to-plane"
@@ -259,10 +314,36 @@ def main():
     if args.matcher == "grid":
         result["compute_roofline"]["note"] = ("grid search: FLOP counts only the pairs actually evaluated; the kernel "
                                               "is gather-latency-bound, neither VALU- nor HBM-bandwidth-bound")
+    result["setup_ms"] = setup_s * 1e3
+    result["setup_note"] = ("ICP::compute setup before the first iteration: reference filters + mean + centring, "
+                            "Matcher::init (reference upload, grid build), reading upload and slot order")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        cb = cpu_baseline(args.config, reading, reference, normals, knn, filters, minimizer, args.cpu_iters, threads)
+        # GPU side of the parity check: the whole ICP with the parity chain
+        icp.load_yaml(chain_yaml(knn, filters, minimizer, search_type, args.cpu_iters, PARITY_DIFF))
+        T_gpu = icp.compute(reading, reference, nrm_in)
+        sg = icp.stats()
+        cb, ref_run = cpu_baseline(args.config, reading, reference, normals, knn, filters, minimizer,
+                                   args.cpu_iters, threads, args.cpu_one_thread_iters)
         result["cpu_baseline"] = cb
+        if ref_run is not None:
+            tol = 1e-5 if esz == 4 else 1e-12
+            frob = float(np.linalg.norm(np.asarray(T_gpu, np.float64) - np.asarray(ref_run["T"], np.float64)))
+            par = {"frob": frob, "tolerance": tol, "pass": bool(frob <= tol and sg.iterations == ref_run["iterations"]),
+                   "iterations_gpu": int(sg.iterations), "iterations_cpu": ref_run["iterations"],
+                   "iterations_equal": int(sg.iterations) == ref_run["iterations"],
+                   "kept_gpu": int(sg.kept), "kept_cpu": ref_run["kept"], "kept_equal": int(sg.kept) == ref_run["kept"],
+                   "chain": f"same as the workload + DifferentialTransformationChecker {PARITY_DIFF}, "
+                            f"Counter {args.cpu_iters}, identical inputs, same process"}
+            if "T_accT" in ref_run:
+                TT = np.asarray(ref_run["T_accT"], np.float64)
+                par["accumulation_gap"] = {
+                    "frob_cpu_f64sums_vs_cpu_Tsums": float(np.linalg.norm(np.asarray(ref_run["T"], np.float64) - TT)),
+                    "frob_gpu_vs_cpu_Tsums": float(np.linalg.norm(np.asarray(T_gpu, np.float64) - TT)),
+                    "iterations_Tsums": ref_run["iterations_accT"],
+                    "note": "GPU and oracle sum the normal equations in fp64 from T products; the reference sums "
+                            "in T (Eigen GEMM): this is the size of that deliberate difference at this config"}
+            result["parity"] = par
     else:
         result["cpu_baseline"] = None
     if rank == 0:

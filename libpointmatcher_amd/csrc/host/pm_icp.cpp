@@ -685,6 +685,7 @@ struct RandomSamplingDPF : PM<T>::DataPointsFilter {
             return r < prob;
         });
     }
+    bool usesRandState() const override { return true; }
 };
 
 // BoundingBoxDataPointsFilter (DataPointsFilters/BoundingBox.cpp:76-108,
@@ -770,6 +771,7 @@ struct FixStepSamplingDPF : PM<T>::DataPointsFilter {
         if (deltaStep < 0 && step < endStep) step = endStep;
         if (deltaStep > 0 && step > endStep) step = endStep;
     }
+    bool usesRandState() const override { return true; }
 };
 
 // Reference data filters that are outside the hot path:
@@ -956,11 +958,13 @@ void PointMatcher<T>::ICP::cleanup() {
 
 template <typename T>
 void PointMatcher<T>::ICP::setDefault() {
-    // ICP.cpp:99-113.  RandomSampling and SamplingSurfaceNormal (the default
-    // reading / reference data filters) are outside the GPU path: the
-    // reference cloud must carry "normals" (SURVEY.md §8(f) row 1).
+    // ICP.cpp:99-113: RandomSampling (prob 0.75) on the reading,
+    // SamplingSurfaceNormal on the reference, TrimmedDist, KDTreeMatcher,
+    // PointToPlane, Counter + Differential, NullInspector.
     cleanup();
     const PointMatcher& pm = PointMatcher::get();
+    readingDataPointsFilters.push_back(pm.DataPointsFilterRegistrar.create("RandomSamplingDataPointsFilter"));
+    referenceDataPointsFilters.push_back(pm.DataPointsFilterRegistrar.create("SamplingSurfaceNormalDataPointsFilter"));
     outlierFilters.push_back(pm.OutlierFilterRegistrar.create("TrimmedDistOutlierFilter"));
     matcher = pm.MatcherRegistrar.create("KDTreeMatcher");
     errorMinimizer = pm.ErrorMinimizerRegistrar.create("PointToPlaneErrorMinimizer");
@@ -1036,6 +1040,12 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     auto t = std::chrono::steady_clock::now();
     const int dim = referenceIn.rows;
     if (dim != 3 && dim != 4) throw std::runtime_error("clouds must be 2-D or 3-D (3 or 4 homogeneous rows)");
+    if (dev.nranks > 1)  // (every rank filters its own reading shard)
+        for (const DataPointsFilters* chain : {&readingDataPointsFilters, &referenceDataPointsFilters})
+            for (const auto& f : *chain)
+                if (f->usesRandState())
+                    throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
+                                             "the reading shards of a multi-rank ICP");
     DataPoints reference(referenceIn);
     for (auto& f : referenceDataPointsFilters) f->device = dev.device;
     for (auto& f : readingDataPointsFilters) f->device = dev.device;

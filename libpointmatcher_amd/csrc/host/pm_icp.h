@@ -131,6 +131,11 @@ struct PointMatcher {
         virtual ~DataPointsFilter() {}
         virtual void init() {}
         virtual void inPlaceFilter(DataPoints& cloud) = 0;
+        // true when the result depends on the process's C library rand()
+        // state (RandomSampling, FixStepSampling): such a filter cannot run
+        // on the shards of a multi-rank ICP (each rank would draw from its own
+        // state and restart its counting at the shard's first point)
+        virtual bool usesRandState() const { return false; }
         int device = 0;  // HIP device of the ICP that applies the filter (GPU filters)
     };
     struct DataPointsFilters : std::vector<std::shared_ptr<DataPointsFilter>> {

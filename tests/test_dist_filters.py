@@ -149,6 +149,24 @@ def test_random_sampling_reference_cases(golden, prob):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("step", [1, 2, 3])
+def test_fixstep_sampling_reference_cases(golden, step):
+    # DataFilters.cpp:378-392: startStep 1, 2, 3 with the default endStep (10)
+    # and stepMult (1), validate2dTransformation / validate3dTransformation
+    g, kat = golden
+    for rd, ref, nrm, mini, val, V, tol in [
+            (g["box2"], g["box1"], None, "PointToPointErrorMinimizer", validate2d, kat["validT2d"], kat["tol2d"]),
+            (g["car401"], g["car400"], g["car400_normals"], "PointToPlaneErrorMinimizer", validate3d,
+             kat["validT3d"], kat["tol3d"])]:
+        icp = ICP(np.float32)
+        icp.load_yaml(with_reading_filter(chain_yaml(minimizer=mini, differential=DIFF),
+                                          "FixStepSamplingDataPointsFilter", {"startStep": step}))
+        T = icp.compute(hom(rd, np.float32), hom(ref, np.float32), nrm)
+        ok, dt, da = val(T, np.array(V), tol)
+        assert ok, (step, dt, da)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,param,value,keepfn", [
     ("RandomSamplingDataPointsFilter", "prob", 0.5, random_keep),
     ("FixStepSamplingDataPointsFilter", "startStep", 3, fixstep_keep),

@@ -1,0 +1,77 @@
+"""Parity at the BASELINE.json benchmark sizes (configs 3, 4 and 5).
+
+GPU whole-ICP (the device-resident loop behind the host chain, the product
+default) against the CPU oracle on identical inputs, in the same process.
+Bar (north_star): final transform within 1e-5 (float) / 1e-12 (double)
+Frobenius norm, with equal iteration counts, and the same number of kept
+pairs in the last iteration (integer, exact).
+
+  C3  1M -> 1M float, k=1, TrimmedDist 0.85, PointToPlane
+      (Counter 40 + Differential 0.001/0.01/4: the parity chain of SURVEY §8(d))
+  C4  1M -> 1M float, k=4, MaxDist 0.05, PointToPlane (one GPU; the 8-GPU run
+      shards the reading, tests/test_gpu_multirank.py covers the sharded path)
+  C5  10M -> 1M double, k=1, empty chain, PointToPoint — Counter 5 (the
+      oracle's 10M-query kd-tree search takes seconds per iteration)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import chain_yaml
+from libpointmatcher_amd.icp import ICP
+from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+
+pytestmark = pytest.mark.gpu
+
+DIFF = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def parity(oracle, rd, ref, nrm, dtype, knn, filters, minimizer, maxit, differential):
+    icp = ICP(dtype)
+    icp.load_yaml(chain_yaml(knn=knn, filters=filters, minimizer=minimizer, maxit=maxit,
+                             differential=differential))
+    Tg = icp.compute(rd, ref, nrm)
+    sg = icp.stats()
+    icp.close()
+    cfg = oracle.make_cfg(knn=knn, filters=tuple(filters), minimizer=minimizer, counter_max=maxit,
+                          differential=differential, threads=THREADS)
+    rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm)
+    assert rc == 0
+    return Tg, sg, To, so
+
+
+def test_c3_full_size(oracle):
+    ref, nrm = reference_cloud(1_000_000, np.float32)
+    rd = reading_cloud(1_000_000, np.float32)
+    Tg, sg, To, so = parity(oracle, rd, ref, nrm, np.float32, 1, [("TrimmedDistOutlierFilter", {"ratio": 0.85})],
+                            "PointToPlaneErrorMinimizer", 40, DIFF)
+    frob = np.linalg.norm(Tg.astype(np.float64) - To.astype(np.float64))
+    print(f"C3: iterations {sg.iterations}/{so.iterations}, kept {sg.kept}/{so.kept}, |dT|_F = {frob:.3g}")
+    assert sg.iterations == so.iterations
+    assert sg.kept == so.kept
+    assert frob <= 1e-5
+
+
+def test_c4_full_size_one_gpu(oracle):
+    ref, nrm = reference_cloud(1_000_000, np.float32)
+    rd = reading_cloud(1_000_000, np.float32)
+    Tg, sg, To, so = parity(oracle, rd, ref, nrm, np.float32, 4, [("MaxDistOutlierFilter", {"maxDist": 0.05})],
+                            "PointToPlaneErrorMinimizer", 20, DIFF)
+    frob = np.linalg.norm(Tg.astype(np.float64) - To.astype(np.float64))
+    print(f"C4: iterations {sg.iterations}/{so.iterations}, kept {sg.kept}/{so.kept}, |dT|_F = {frob:.3g}")
+    assert sg.iterations == so.iterations
+    assert sg.kept == so.kept
+    assert frob <= 1e-5
+
+
+def test_c5_full_size_one_gpu(oracle):
+    ref, _ = reference_cloud(1_000_000, np.float64)
+    rd = reading_cloud(10_000_000, np.float64)
+    Tg, sg, To, so = parity(oracle, rd, ref, None, np.float64, 1, [], "PointToPointErrorMinimizer", 5, None)
+    frob = np.linalg.norm(Tg - To)
+    print(f"C5: iterations {sg.iterations}/{so.iterations}, kept {sg.kept}/{so.kept}, |dT|_F = {frob:.3g}")
+    assert sg.iterations == so.iterations == 5
+    assert sg.kept == so.kept
+    assert frob <= 1e-12
