@@ -79,16 +79,16 @@ def cpu_model():
 def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer, iters, threads, one_thread_iters):
     """The oracle (C restatement of the reference CPU path: libnabo-style
     kd-tree, nth_element quantile, -O3) on the same inputs, timed on this host.
-    Runs the parity chain (Counter + Differential) with all cores, the same
-    chain with T-precision accumulation of the minimiser sums (the reference's
-    Eigen arithmetic), and a bounded 1-thread sample (the reference's default:
-    no OpenMP, CMakeLists.txt:160)."""
+    Runs (all cores): the timing chain (Counter `iters`, the workload's chain),
+    the parity chain (+ Differential), and the timing chain with T-precision
+    accumulation of the minimiser sums (the reference's Eigen arithmetic);
+    then a bounded 1-thread sample (the reference's default: no OpenMP,
+    CMakeLists.txt:160)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
 
     nrm = normals if minimizer.startswith("PointToPlane") else None
     n = reading.shape[0]
-    out = {}
 
     def run(th, maxit, diff, acc):
         cfg = O.make_cfg(knn=knn, filters=tuple(filters), minimizer=minimizer, counter_max=maxit, threads=th,
@@ -97,29 +97,39 @@ def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer,
         rc, T, st, _ = O.icp(cfg, reading, reference, normals=nrm)
         return rc, T, st, time.perf_counter() - t0
 
-    rc, T, st, wall = run(threads, iters, PARITY_DIFF, 0)
+    rc, T, st, wall = run(threads, iters, None, 0)
     if rc != 0:
         return None, None
     loop = st.loop_seconds
     out = {"value": n * knn * st.iterations / loop, "unit": "matched-pairs/s", "cores": threads,
            "kind": "port", "iters_per_s": st.iterations / loop,
            "host_cpu": cpu_model(), "host_nproc": os.cpu_count(),
-           "sample": f"{cfg_name} inputs ({n}->{reference.shape[0]}), the parity chain (Counter {iters} + "
-                     f"Differential 0.001/0.01/4: {st.iterations} ICP iterations), oracle restatement of the "
-                     f"reference CPU path (libnabo-style kd-tree, incremental box bound, nth_element quantile, "
-                     f"gcc -O3), {threads} threads, loop {loop:.2f} s (setup+loop {wall:.2f} s)"}
-    ref_run = {"T": T, "iterations": int(st.iterations), "kept": int(st.kept)}
+           "sample": f"{cfg_name} inputs ({n}->{reference.shape[0]}), the whole timing chain ({st.iterations} ICP "
+                     f"iterations from the initial pose), oracle restatement of the reference CPU path "
+                     f"(libnabo-style kd-tree with the incremental box bound, nth_element quantile, gcc -O3), "
+                     f"{threads} threads, loop {loop:.2f} s (setup+loop {wall:.2f} s)"}
+    runs = {"counter": {"T": T, "iterations": int(st.iterations), "kept": int(st.kept)}}
+    rcd, Td, std, _ = run(threads, iters, PARITY_DIFF, 0)
+    if rcd == 0:
+        runs["differential"] = {"T": Td, "iterations": int(std.iterations), "kept": int(std.kept)}
+    rcT, TT, stT, _ = run(threads, iters, None, 1)
+    if rcT == 0:
+        runs["counter_Tsums"] = {"T": TT, "iterations": int(stT.iterations), "kept": int(stT.kept)}
     rc1, T1, st1, _ = run(1, one_thread_iters, None, 0)
     if rc1 == 0:
         out["single_thread"] = {"value": n * knn * st1.iterations / st1.loop_seconds, "unit": "matched-pairs/s",
                                 "cores": 1, "iters_per_s": st1.iterations / st1.loop_seconds,
-                                "sample": f"first {st1.iterations} ICP iterations, 1 thread, "
-                                          f"loop {st1.loop_seconds:.2f} s"}
-    rcT, TT, stT, _ = run(threads, iters, PARITY_DIFF, 1)
-    if rcT == 0:
-        ref_run["T_accT"] = TT
-        ref_run["iterations_accT"] = int(stT.iterations)
-    return out, ref_run
+                                "sample": f"first {st1.iterations} ICP iterations (the cold, most expensive ones), "
+                                          f"1 thread, loop {st1.loop_seconds:.2f} s"}
+    return out, runs
+
+
+def parity_entry(Tg, sg, ref, tol, chain):
+    frob = float(np.linalg.norm(np.asarray(Tg, np.float64) - np.asarray(ref["T"], np.float64)))
+    return {"frob": frob, "tolerance": tol,
+            "pass": bool(frob <= tol and int(sg.iterations) == ref["iterations"] and int(sg.kept) == ref["kept"]),
+            "iterations_gpu": int(sg.iterations), "iterations_cpu": ref["iterations"],
+            "kept_gpu": int(sg.kept), "kept_cpu": ref["kept"], "chain": chain}
 
 
 def main():
@@ -319,30 +329,31 @@ def main():
                             "Matcher::init (reference upload, grid build), reading upload and slot order")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        # GPU side of the parity check: the whole ICP with the parity chain
-        icp.load_yaml(chain_yaml(knn, filters, minimizer, search_type, args.cpu_iters, PARITY_DIFF))
-        T_gpu = icp.compute(reading, reference, nrm_in)
-        sg = icp.stats()
-        cb, ref_run = cpu_baseline(args.config, reading, reference, normals, knn, filters, minimizer,
-                                   args.cpu_iters, threads, args.cpu_one_thread_iters)
+        # GPU side of the parity checks: whole ICPs from the initial pose
+        # with the timing chain and with the parity chain (same inputs)
+        gpu = {}
+        for name, diff in (("counter", None), ("differential", PARITY_DIFF)):
+            icp.load_yaml(chain_yaml(knn, filters, minimizer, search_type, args.cpu_iters, diff))
+            gpu[name] = (icp.compute(reading, reference, nrm_in), icp.stats())
+        cb, runs = cpu_baseline(args.config, reading, reference, normals, knn, filters, minimizer,
+                                args.cpu_iters, threads, args.cpu_one_thread_iters)
         result["cpu_baseline"] = cb
-        if ref_run is not None:
+        if runs is not None:
             tol = 1e-5 if esz == 4 else 1e-12
-            frob = float(np.linalg.norm(np.asarray(T_gpu, np.float64) - np.asarray(ref_run["T"], np.float64)))
-            par = {"frob": frob, "tolerance": tol, "pass": bool(frob <= tol and sg.iterations == ref_run["iterations"]),
-                   "iterations_gpu": int(sg.iterations), "iterations_cpu": ref_run["iterations"],
-                   "iterations_equal": int(sg.iterations) == ref_run["iterations"],
-                   "kept_gpu": int(sg.kept), "kept_cpu": ref_run["kept"], "kept_equal": int(sg.kept) == ref_run["kept"],
-                   "chain": f"same as the workload + DifferentialTransformationChecker {PARITY_DIFF}, "
-                            f"Counter {args.cpu_iters}, identical inputs, same process"}
-            if "T_accT" in ref_run:
-                TT = np.asarray(ref_run["T_accT"], np.float64)
+            par = {"counter": parity_entry(*gpu["counter"], runs["counter"], tol,
+                                           f"the workload's chain, Counter {args.cpu_iters}")}
+            if "differential" in runs:
+                par["differential"] = parity_entry(*gpu["differential"], runs["differential"], tol,
+                                                   f"+ DifferentialTransformationChecker {PARITY_DIFF}")
+            par["pass"] = all(v["pass"] for v in par.values() if isinstance(v, dict))
+            if "counter_Tsums" in runs:
+                TT = np.asarray(runs["counter_Tsums"]["T"], np.float64)
                 par["accumulation_gap"] = {
-                    "frob_cpu_f64sums_vs_cpu_Tsums": float(np.linalg.norm(np.asarray(ref_run["T"], np.float64) - TT)),
-                    "frob_gpu_vs_cpu_Tsums": float(np.linalg.norm(np.asarray(T_gpu, np.float64) - TT)),
-                    "iterations_Tsums": ref_run["iterations_accT"],
+                    "frob_cpu_f64sums_vs_cpu_Tsums": float(np.linalg.norm(np.asarray(runs["counter"]["T"],
+                                                                                     np.float64) - TT)),
+                    "frob_gpu_vs_cpu_Tsums": float(np.linalg.norm(np.asarray(gpu["counter"][0], np.float64) - TT)),
                     "note": "GPU and oracle sum the normal equations in fp64 from T products; the reference sums "
-                            "in T (Eigen GEMM): this is the size of that deliberate difference at this config"}
+                            "in T (Eigen GEMM): the size of that deliberate difference here (Counter chain)"}
             result["parity"] = par
     else:
         result["cpu_baseline"] = None
