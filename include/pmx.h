@@ -97,10 +97,28 @@ const char* pmx_version(void);
 /* RCCL unique id (128 bytes) generated on rank 0 and broadcast by the
  * launcher; every rank then calls pmx_comm_init.  With a communicator set,
  * pmx_set_reading takes the rank's shard of the reading cloud and every
- * reduction (quantile histograms, normal equations) is all-reduced on the
- * context stream over RCCL/xGMI. */
+ * exchange step (quantile histograms or window segments, VarTrimmed's
+ * distances, the normal equations) is a collective on the context stream
+ * over RCCL/xGMI — issued whenever a communicator exists, also at nranks 1.
+ * (The reference is single-process: these have no reference counterpart;
+ * the sharded results equal the single-process ones) */
 int pmx_comm_unique_id(void* out128);
 int pmx_comm_init(pmx_ctx* ctx, const void* uid128, int nranks, int rank);
+/* Host-staged collectives: the caller's transport (MPI, gloo, a test
+ * harness) instead of RCCL.  The library copies the device buffer to pinned
+ * host memory, synchronises its stream, calls the callback and copies the
+ * result back.  allreduce: in place over `count` elements of `type`
+ * (PMX_COLL_*) with `op`; allgather: `bytes` from every rank into recv, in
+ * rank order.  A callback returns 0 on success.  Exclusive with
+ * pmx_comm_init; call before pmx_set_reading. */
+enum { PMX_COLL_F64 = 0, PMX_COLL_U32 = 1, PMX_COLL_U64 = 2 };
+enum { PMX_COLL_SUM = 0, PMX_COLL_MAX = 1 };
+typedef int (*pmx_allreduce_fn)(void* user, void* buf, int64_t count, int type, int op);
+typedef int (*pmx_allgather_fn)(void* user, const void* send, void* recv, int64_t bytes);
+int pmx_comm_init_host(pmx_ctx* ctx, int nranks, int rank, pmx_allreduce_fn allreduce, pmx_allgather_fn allgather,
+                       void* user);
+/* kind: 0 none, 1 RCCL, 2 host callbacks */
+int pmx_comm_size(const pmx_ctx* ctx, int* nranks, int* rank, int* kind);
 
 /* ------------------------------------------------------------ clouds --- */
 /* feat: rows x M column-major (point-major) T array, rows = D + 1 with the

@@ -19,6 +19,8 @@
 
 #include <stdint.h>
 
+#include "pmx.h" /* pmx_allreduce_fn / pmx_allgather_fn */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -58,6 +60,10 @@ int pmx_icp_set_default(pmx_icp* icp);
 int pmx_icp_load_yaml(pmx_icp* icp, const char* yaml_text);
 /* multi-GPU: call before the first compute; uid from pmx_comm_unique_id */
 int pmx_icp_comm_init(pmx_icp* icp, const void* uid128, int nranks, int rank);
+/* multi-rank over the caller's host collectives (pmx_comm_init_host in pmx.h):
+ * every rank passes its shard of the reading to compute/prepare */
+int pmx_icp_comm_init_host(pmx_icp* icp, int nranks, int rank, pmx_allreduce_fn allreduce, pmx_allgather_fn allgather,
+                           void* user);
 int pmx_icp_keep_trace(pmx_icp* icp, int on);
 
 /* ICP::compute (ICP.cpp:265-449): T_out = transform of reading into reference */

@@ -77,11 +77,72 @@ class LoopStatus(C.Structure):
                 ("cond", (C.c_double * 2) * 8)]
 
 
+# host-staged collectives (pmx_comm_init_host)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+COLL_F64, COLL_U32, COLL_U64 = 0, 1, 2
+COLL_SUM, COLL_MAX = 0, 1
+_COLL_CT = {COLL_F64: C.c_double, COLL_U32: C.c_uint32, COLL_U64: C.c_uint64}
+
+
+class HostComm:
+    """A transport for pmx_comm_init_host: allreduce(np_array, op) reduces the
+    array in place over the ranks ("sum" / "max"), allgather(np_uint8_array)
+    returns the nranks concatenated blocks.  The ctypes callbacks stay alive
+    with this object (keep it referenced for the life of the context)."""
+
+    def __init__(self, nranks, rank, allreduce, allgather):
+        self.nranks, self.rank = nranks, rank
+        self.errors = []
+
+        def _ar(user, buf, count, typ, op):
+            try:
+                a = np.ctypeslib.as_array(C.cast(buf, C.POINTER(_COLL_CT[typ])), shape=(count,))
+                allreduce(a, "max" if op == COLL_MAX else "sum")
+                return 0
+            except Exception as e:  # (an exception must not cross the C frame)
+                self.errors.append(repr(e))
+                return 1
+
+        def _ag(user, send, recv, nbytes):
+            try:
+                a = np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(nbytes,))
+                out = np.ctypeslib.as_array(C.cast(recv, C.POINTER(C.c_uint8)), shape=(nbytes * nranks,))
+                out[:] = allgather(a.copy())
+                return 0
+            except Exception as e:
+                self.errors.append(repr(e))
+                return 1
+
+        self.ar = ALLREDUCE_FN(_ar)
+        self.ag = ALLGATHER_FN(_ag)
+
+
+def gloo_host_comm():
+    """HostComm over the default torch.distributed process group (gloo on the
+    CPU): the multi-rank test path on one GPU.  Integers travel as int64."""
+    import torch
+    import torch.distributed as dist
+
+    def allreduce(a, op):
+        t = torch.from_numpy(a.astype(np.float64) if a.dtype == np.float64 else a.astype(np.int64))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        a[:] = t.numpy().astype(a.dtype)
+
+    def allgather(a):
+        t = torch.from_numpy(a)
+        outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(outs, t)
+        return torch.cat(outs).numpy()
+
+    return HostComm(dist.get_world_size(), dist.get_rank(), allreduce, allgather)
+
+
 _lib = None
 
 EXPORTS = [
     "pmx_ctx_create", "pmx_ctx_destroy", "pmx_last_error", "pmx_device_count", "pmx_version",
-    "pmx_comm_unique_id", "pmx_comm_init", "pmx_set_reference", "pmx_set_reading", "pmx_set_search", "pmx_match",
+    "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_set_reference", "pmx_set_reading", "pmx_set_search", "pmx_match",
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
@@ -103,6 +164,8 @@ def lib():
         l.pmx_ctx_destroy.argtypes = [C.c_void_p]
         l.pmx_comm_unique_id.argtypes = [C.c_void_p]
         l.pmx_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        l.pmx_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, ALLGATHER_FN, C.c_void_p]
+        l.pmx_comm_size.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         l.pmx_set_reference.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
         l.pmx_set_reading.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
         l.pmx_set_search.argtypes = [C.c_void_p, C.c_int]
@@ -228,6 +291,15 @@ class Context:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = (C.c_char * 128).from_buffer_copy(uid)
         self._chk(self._l.pmx_comm_init(self.h, buf, nranks, rank))
+
+    def comm_init_host(self, comm: HostComm):
+        self._comm = comm  # (the callbacks must outlive the context)
+        self._chk(self._l.pmx_comm_init_host(self.h, comm.nranks, comm.rank, comm.ar, comm.ag, None))
+
+    def comm_size(self):
+        n, r, k = C.c_int(), C.c_int(), C.c_int()
+        self._chk(self._l.pmx_comm_size(self.h, C.byref(n), C.byref(r), C.byref(k)))
+        return n.value, r.value, k.value
 
     # --- clouds
     def set_reference(self, feat, normals=None):

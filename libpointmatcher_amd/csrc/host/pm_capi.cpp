@@ -154,6 +154,21 @@ int pmx_icp_comm_init(pmx_icp* icp, const void* uid, int nranks, int rank) {
     });
 }
 
+int pmx_icp_comm_init_host(pmx_icp* icp, int nranks, int rank, pmx_allreduce_fn allreduce, pmx_allgather_fn allgather,
+                           void* user) {
+    return guarded(icp, [&] {
+        Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
+        if (dev.ctx) throw std::runtime_error("pmx_icp_comm_init_host must precede the first compute");
+        if (!allreduce || !allgather || nranks < 1 || rank < 0 || rank >= nranks)
+            throw InvalidParameter("pmx_icp_comm_init_host: bad arguments");
+        dev.nranks = nranks;
+        dev.rank = rank;
+        dev.host_ar = allreduce;
+        dev.host_ag = allgather;
+        dev.host_user = user;
+    });
+}
+
 int pmx_icp_keep_trace(pmx_icp* icp, int on) {
     return guarded(icp, [&] { BOTH(icp, icp->f->keepTrace = on != 0, icp->d->keepTrace = on != 0); });
 }

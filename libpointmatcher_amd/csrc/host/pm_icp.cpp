@@ -35,7 +35,9 @@ void Device::ensure() {
         throw std::runtime_error("pmx_ctx_create failed (" + std::to_string(rc) + "): no usable HIP device " +
                                  std::to_string(device) + " (" + std::to_string(pmx_device_count()) + " visible)");
     }
-    if (nranks > 1) {
+    if (host_ar) {
+        check(pmx_comm_init_host(ctx, nranks, rank, host_ar, host_ag, host_user));
+    } else if (!uid.empty()) {  // (a communicator issues its collectives at any nranks, also 1)
         if (uid.size() != 128) throw std::runtime_error("multi-rank ICP needs a 128-byte RCCL unique id");
         check(pmx_comm_init(ctx, uid.data(), nranks, rank));
     }
@@ -1040,7 +1042,7 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     auto t = std::chrono::steady_clock::now();
     const int dim = referenceIn.rows;
     if (dim != 3 && dim != 4) throw std::runtime_error("clouds must be 2-D or 3-D (3 or 4 homogeneous rows)");
-    if (dev.nranks > 1)  // (every rank filters its own reading shard)
+    if (dev.sharded())  // (every rank filters its own reading shard)
         for (const DataPointsFilters* chain : {&readingDataPointsFilters, &referenceDataPointsFilters})
             for (const auto& f : *chain)
                 if (f->usesRandState())

@@ -31,7 +31,12 @@ struct Device {
     int dtype = PMX_F32;
     int nranks = 1;
     int rank = 0;
-    std::vector<unsigned char> uid;  // RCCL unique id when nranks > 1
+    std::vector<unsigned char> uid;  // RCCL unique id of a sharded ICP (pmx_comm_init)
+    // or the caller's host collectives (pmx_comm_init_host)
+    pmx_allreduce_fn host_ar = nullptr;
+    pmx_allgather_fn host_ag = nullptr;
+    void* host_user = nullptr;
+    bool sharded() const { return !uid.empty() || host_ar != nullptr; }
     ~Device();
     void ensure();
     void check(int rc) const;  // PMX_E_* -> reference exception types

@@ -96,7 +96,19 @@ struct pmx_ctx {
     int64_t safe_cap = 0;
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }
-    std::vector<int32_t> slot_query;  // slot -> reading index (empty = identity)
+    std::vector<int32_t> slot_query;  // host copy of d_order (host mirrors only; filled on demand)
+    int32_t* d_order = nullptr;       // slot -> reading index (has_order; else identity)
+    size_t order_bytes = 0;
+    bool has_order = false;
+    // once-per-compute setup on the device (pmx_setup.hip)
+    SetupScratch setup;
+    int64_t setup_n = 0, setup_cells = 0;
+    void* d_raw = nullptr;            // upload staging of a caller's cloud
+    size_t raw_bytes = 0;
+    void* d_bbox = nullptr;
+    size_t bbox_bytes = 0;
+    void* d_occ = nullptr;            // occupancy bitmap + counter
+    size_t occ_bytes = 0;
     uint32_t* d_waves = nullptr;      // tile-kernel wave table: first slot of each wave (+ N)
     int64_t n_waves = 0;
     bool ids_grid = false;            // last match wrote grid positions
@@ -153,9 +165,18 @@ struct pmx_ctx {
     void* d_means = nullptr;
     double* h_result = nullptr;  // pinned
 
-    // multi-GPU
+    // multi-GPU: the collectives of a sharded ICP (coll_*).  RCCL over
+    // xGMI (pmx_comm_init), or caller-provided host collectives
+    // (pmx_comm_init_host: device buffers staged through pinned memory).
+    // Once either is set up every exchange step is issued, whatever nranks.
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    pmx_allreduce_fn host_ar = nullptr;
+    pmx_allgather_fn host_ag = nullptr;
+    void* host_user = nullptr;
+    void* h_stage = nullptr;      // pinned staging of the host collectives
+    size_t h_stage_cap = 0;
+    unsigned long long* d_specx = nullptr;  // quantile window exchange: own segment, then nranks gathered
 
     // device-resident loop (pmx_loop.hip)
     LoopCtl* d_ctl = nullptr;     // control word read by every kernel in loop mode
@@ -249,16 +270,70 @@ Mat4<T> step_mat(const pmx_ctx* c) {
     return m;
 }
 
-template <typename T>
-int ncclType() {
-    return sizeof(T) == 8 ? (int)ncclFloat64 : (int)ncclFloat32;
-}
+// ------------------------------------------------------------- collectives --
+// A sharded ICP (reading split over ranks) exchanges, per
+// iteration: the radix-select histograms (or the quantile window segments),
+// VarTrimmed's distances, and the packed fp64 system.  All of them go through
+// these two calls, on the context stream.
+bool sharded(const pmx_ctx* c) { return c->comm != nullptr || c->host_ar != nullptr; }
 
-int allreduce_f64(pmx_ctx* c, double* buf, size_t n) {
-    if (!c->comm || c->nranks == 1) return PMX_OK;
-    NCCLCHK(c, ncclAllReduce(buf, buf, n, ncclFloat64, ncclSum, c->comm, c->stream));
+size_t coll_size(int type) { return type == PMX_COLL_U32 ? 4 : 8; }
+
+int stage_room(pmx_ctx* c, size_t bytes) {
+    if (c->h_stage_cap >= bytes && c->h_stage) return PMX_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (a pending copy may still read the old stage)
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->h_stage_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 1 << 16);
+    HIPCHK(c, hipHostMalloc(&c->h_stage, cap, hipHostMallocDefault));
+    c->h_stage_cap = cap;
     return PMX_OK;
 }
+
+// in-place all-reduce of `count` elements of device memory
+int coll_allreduce(pmx_ctx* c, void* dbuf, int64_t count, int type, int op) {
+    if (!sharded(c) || count <= 0) return PMX_OK;
+    if (c->comm) {
+        const ncclDataType_t dt = type == PMX_COLL_U32 ? ncclUint32 : type == PMX_COLL_U64 ? ncclUint64 : ncclFloat64;
+        NCCLCHK(c, ncclAllReduce(dbuf, dbuf, (size_t)count, dt, op == PMX_COLL_MAX ? ncclMax : ncclSum, c->comm,
+                                 c->stream));
+        return PMX_OK;
+    }
+    const size_t bytes = (size_t)count * coll_size(type);
+    int rc = stage_room(c, bytes);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_stage, dbuf, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = c->host_ar(c->host_user, c->h_stage, count, type, op)) != 0)
+        return fail(c, PMX_E_RCCL, "host all-reduce callback failed (" + std::to_string(rc) + ")");
+    HIPCHK(c, hipMemcpyAsync(dbuf, c->h_stage, bytes, hipMemcpyHostToDevice, c->stream));
+    return PMX_OK;
+}
+
+// all-gather `bytes` per rank: recv holds nranks blocks in rank order
+int coll_allgather(pmx_ctx* c, const void* dsend, void* drecv, size_t bytes) {
+    if (!sharded(c)) {
+        if (drecv != dsend) HIPCHK(c, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, c->stream));
+        return PMX_OK;
+    }
+    if (c->comm) {
+        NCCLCHK(c, ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, c->stream));
+        return PMX_OK;
+    }
+    const size_t total = bytes * (size_t)(c->nranks + 1);
+    int rc = stage_room(c, total);
+    if (rc) return rc;
+    char* send = (char*)c->h_stage + bytes * (size_t)c->nranks;
+    HIPCHK(c, hipMemcpyAsync(send, dsend, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = c->host_ag(c->host_user, send, c->h_stage, (int64_t)bytes)) != 0)
+        return fail(c, PMX_E_RCCL, "host all-gather callback failed (" + std::to_string(rc) + ")");
+    HIPCHK(c, hipMemcpyAsync(drecv, c->h_stage, bytes * (size_t)c->nranks, hipMemcpyHostToDevice, c->stream));
+    return PMX_OK;
+}
+
+int allreduce_f64(pmx_ctx* c, double* buf, size_t n) { return coll_allreduce(c, buf, (int64_t)n, PMX_COLL_F64, PMX_COLL_SUM); }
 
 void resolve_events(pmx_ctx* c) {
     for (auto& pr : c->ev_pending) {
@@ -288,62 +363,96 @@ hipEvent_t get_event(pmx_ctx* c) {
 // Uniform grid of the (centred) reference for the exact shell search.  The
 // cell size targets ~4 points per occupied cell: the occupied-cell count at
 // two trial sizes gives the data's local dimension (surface ~2, volume ~3),
-// from which the size for the target density follows.  Points are counting-
-// sorted by cell (x fastest) so every x-row of cells is one contiguous range.
+// from which the size for the target density follows.  Points are sorted by
+// cell (x fastest, index order inside a cell) so every x-row of cells is one
+// contiguous range.  The sizing runs on the host from three device counts;
+// the build itself is pmx_setup.hip.
 constexpr int64_t kMaxCells = (int64_t)1 << 26;
 
-struct GridShape {
-    double lo[3], h;
-    int g[3];
-    int64_t cells() const { return (int64_t)g[0] * g[1] * g[2]; }
-};
-
-static GridShape grid_shape(const double lo[3], const double ext[3], double h) {
-    GridShape s;
+SetupShape grid_shape(const double lo[3], const double ext[3], double h) {
+    SetupShape s;
     for (int a = 0; a < 3; ++a) {
         s.lo[a] = lo[a];
         const double gg = std::floor(ext[a] / h) + 1.0;
         s.g[a] = gg > 1e9 ? 1000000000 : (int)gg;
     }
     s.h = h;
+    s.cells = (int64_t)s.g[0] * s.g[1] * s.g[2];
     return s;
 }
 
-template <typename T>
-static int64_t cell_of(const GridShape& s, const P4<T>& p) {
-    const double q[3] = {(double)p.x, (double)p.y, (double)p.z};
-    int64_t ci[3];
-    for (int a = 0; a < 3; ++a) {
-        double f = std::floor((q[a] - s.lo[a]) / s.h);
-        if (f < 0) f = 0;
-        if (f > s.g[a] - 1) f = s.g[a] - 1;
-        ci[a] = (int64_t)f;
+// setup scratch for n points and grids of up to max_cells cells
+int setup_room(pmx_ctx* c, int64_t n, int64_t max_cells) {
+    n = std::max<int64_t>(n, 1);
+    SetupScratch& sc = c->setup;
+    if (c->setup_n < n) {
+        for (void* p : {(void*)sc.keys64, (void*)sc.keys64_out, (void*)sc.idx, (void*)sc.idx_out})
+            if (p) (void)hipFree(p);
+        sc.keys64 = sc.keys64_out = nullptr;
+        sc.idx = sc.idx_out = nullptr;
+        c->setup_n = 0;
+        HIPCHK(c, hipMalloc((void**)&sc.keys64, sizeof(unsigned long long) * n));
+        HIPCHK(c, hipMalloc((void**)&sc.keys64_out, sizeof(unsigned long long) * n));
+        HIPCHK(c, hipMalloc((void**)&sc.idx, sizeof(int32_t) * n));
+        HIPCHK(c, hipMalloc((void**)&sc.idx_out, sizeof(int32_t) * n));
+        sc.keys32 = (uint32_t*)sc.keys64;
+        sc.keys32_out = (uint32_t*)sc.keys64_out;
+        c->setup_n = n;
     }
-    return (ci[2] * s.g[1] + ci[1]) * s.g[0] + ci[0];
+    if (c->setup_cells < max_cells) {
+        if (sc.counts) (void)hipFree(sc.counts);
+        sc.counts = nullptr;
+        c->setup_cells = 0;
+        HIPCHK(c, hipMalloc((void**)&sc.counts, sizeof(uint32_t) * (size_t)(max_cells + 1)));
+        c->setup_cells = max_cells;
+    }
+    const size_t tb = setup_temp_bytes(c->setup_n, c->setup_cells);
+    if (sc.temp_bytes < tb) {
+        if (sc.temp) (void)hipFree(sc.temp);
+        sc.temp = nullptr;
+        sc.temp_bytes = 0;
+        HIPCHK(c, hipMalloc(&sc.temp, tb));
+        sc.temp_bytes = tb;
+    }
+    return PMX_OK;
 }
 
-template <typename T>
-static bool finite_pt(const P4<T>& p) {
-    return std::isfinite((double)p.x) && std::isfinite((double)p.y) && std::isfinite((double)p.z);
+void setup_release(pmx_ctx* c) {
+    SetupScratch& sc = c->setup;
+    for (void* p : {(void*)sc.keys64, (void*)sc.keys64_out, (void*)sc.idx, (void*)sc.idx_out, (void*)sc.counts,
+                    sc.temp})
+        if (p) (void)hipFree(p);
+    c->setup = SetupScratch{};
+    c->setup_n = c->setup_cells = 0;
 }
 
-template <typename T>
-int build_level(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::vector<P4<T>>& nrm,
-                const double lo[3], const double ext[3], double maxe, int64_t valid, double h, GridLevel& out);
+// host staging of one upload (the caller's cloud, pageable) into the raw buffer
+int upload_raw(pmx_ctx* c, const void* src, size_t bytes) {
+    int rc = ensure(c, &c->d_raw, &c->raw_bytes, std::max<size_t>(bytes, 16));
+    if (rc) return rc;
+    if (bytes) HIPCHK(c, hipMemcpyAsync(c->d_raw, src, bytes, hipMemcpyHostToDevice, c->stream));
+    return PMX_OK;
+}
 
+// the grid levels over the resident reference d_ref (M points) and d_nrm
 template <typename T>
-int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::vector<P4<T>>& nrm) {
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-    int64_t valid = 0;
-    for (int64_t j = 0; j < M; ++j) {
-        if (!finite_pt(pts[j])) continue;  // inf / NaN points can never be a neighbour
-        const double q[3] = {(double)pts[j].x, (double)pts[j].y, (double)pts[j].z};
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = std::min(lo[a], q[a]);
-            hi[a] = std::max(hi[a], q[a]);
-        }
-        ++valid;
-    }
+int build_grid(pmx_ctx* c, int64_t M) {
+    const P4<T>* pts = (const P4<T>*)c->d_ref;
+    const P4<T>* nrm = (const P4<T>*)c->d_nrm;
+    // bounding box of the finite points (inf / NaN points can never be a neighbour)
+    double* sb = nullptr;  // bbox partials, then 8 doubles of result
+    size_t sbc = 0;
+    int rc = ensure(c, (void**)&c->d_bbox, &c->bbox_bytes, bbox_scratch_bytes() + 16 * sizeof(double));
+    if (rc) return rc;
+    sb = (double*)c->d_bbox;
+    (void)sbc;
+    double* bb_out = sb + bbox_scratch_bytes() / sizeof(double);
+    launch_bbox<T>(pts, M, sb, bb_out, c->stream);
+    double bb[7];
+    HIPCHK(c, hipMemcpyAsync(bb, bb_out, sizeof(bb), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double lo[3] = {bb[0], bb[1], bb[2]}, hi[3] = {bb[3], bb[4], bb[5]};
+    const int64_t valid = (int64_t)bb[6];
     if (valid == 0)
         for (int a = 0; a < 3; ++a) lo[a] = hi[a] = 0;
     double ext[3], maxe = 0;
@@ -352,24 +461,33 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::
         maxe = std::max(maxe, ext[a]);
     }
     if (!(maxe > 0)) maxe = 1;
-    auto occupied = [&](double h) -> int64_t {
-        GridShape s = grid_shape(lo, ext, h);
-        if (s.cells() > ((int64_t)1 << 28)) return -1;
-        std::vector<uint8_t> bm((size_t)s.cells(), 0);
-        int64_t occ = 0;
-        for (int64_t j = 0; j < M; ++j) {
-            if (!finite_pt(pts[j])) continue;
-            uint8_t& b = bm[(size_t)cell_of(s, pts[j])];
-            occ += b == 0;
-            b = 1;
-        }
-        return occ;
+    // distinct occupied cells at a trial size (device bitmap)
+    auto occupied = [&](double h, int64_t& occ) -> int {
+        const SetupShape s = grid_shape(lo, ext, h);
+        occ = -1;
+        if (s.cells > ((int64_t)1 << 28)) return PMX_OK;
+        // bitmap, then the 8-byte counter on its own aligned line (a 64-bit
+        // atomic must be naturally aligned)
+        const size_t words = (size_t)((s.cells + 31) / 32);
+        const size_t cnt_off = (sizeof(uint32_t) * words + 255) & ~(size_t)255;
+        int r = ensure(c, &c->d_occ, &c->occ_bytes, cnt_off + 256);
+        if (r) return r;
+        unsigned long long* cnt = (unsigned long long*)((char*)c->d_occ + cnt_off);
+        HIPCHK(c, hipMemsetAsync(c->d_occ, 0, cnt_off + 8, c->stream));
+        launch_occupancy<T>(pts, M, s, (uint32_t*)c->d_occ, cnt, c->stream);
+        unsigned long long v = 0;
+        HIPCHK(c, hipMemcpyAsync(&v, cnt, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        occ = (int64_t)v;
+        return PMX_OK;
     };
     double dim = 3.0, ppc1 = 1.0, h1 = maxe / 128.0;
     if (valid > 0) {
         const double h0 = maxe / 64.0;
-        const int64_t o0 = std::max<int64_t>(1, occupied(h0));
-        const int64_t o1 = std::max<int64_t>(1, occupied(h1));
+        int64_t o0 = 0, o1 = 0;
+        if ((rc = occupied(h0, o0)) || (rc = occupied(h1, o1))) return rc;
+        o0 = std::max<int64_t>(1, o0);
+        o1 = std::max<int64_t>(1, o1);
         dim = std::log2((double)o1 / (double)o0);
         dim = std::min(3.0, std::max(1.0, dim));
         ppc1 = (double)valid / (double)o1;
@@ -380,16 +498,43 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::
     c->match_count = 0;
     c->level_cells.assign(c->level_ppc.size(), 0.0);
     c->level_seen.assign(c->level_ppc.size(), 0);
+    // the level shapes: cell size h (clamped to the 2^26-cell budget)
+    std::vector<SetupShape> shapes;
+    int64_t max_cells = 1;
     for (double target : c->level_ppc) {
-        GridLevel L;
-        int rc = build_level<T>(c, pts, M, nrm, lo, ext, maxe, valid, valid > 0 ? h1 * std::pow(target / ppc1, 1.0 / dim)
-                                                                            : maxe / 64.0,
-                                L);
-        if (rc) {
-            L.release();
-            return rc;
+        double h = valid > 0 ? h1 * std::pow(target / ppc1, 1.0 / dim) : maxe / 64.0;
+        h = std::max(h, maxe / 4096.0);
+        SetupShape s = grid_shape(lo, ext, h);
+        while (s.cells > kMaxCells) {
+            h *= 1.25;
+            s = grid_shape(lo, ext, h);
         }
-        L.ppc = target;
+        shapes.push_back(s);
+        max_cells = std::max(max_cells, s.cells);
+    }
+    if ((rc = setup_room(c, M, max_cells))) return rc;
+    const int64_t np = std::max<int64_t>(valid, 1);
+    for (size_t l = 0; l < shapes.size(); ++l) {
+        const SetupShape& s = shapes[l];
+        GridLevel L;
+        auto bad = [&](int r) {
+            L.release();
+            return r;
+        };
+        if (hipMalloc(&L.gpts, sizeof(P4<T>) * np) != hipSuccess ||
+            hipMalloc((void**)&L.gidx, sizeof(int32_t) * np) != hipSuccess ||
+            hipMalloc((void**)&L.gstart, sizeof(uint32_t) * (size_t)(s.cells + 1)) != hipSuccess ||
+            (nrm && hipMalloc(&L.gnrm, sizeof(P4<T>) * np) != hipSuccess))
+            return bad(fail(c, PMX_E_HIP, "grid level allocation failed"));
+        const int r = build_level_device<T>(pts, M, nrm, s, valid, c->setup, (P4<T>*)L.gpts, (P4<T>*)L.gnrm, L.gidx,
+                                            L.gstart, c->stream);
+        if (r) return bad(fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")"));
+        for (int a = 0; a < 3; ++a) {
+            L.lo[a] = s.lo[a];
+            L.dim[a] = s.g[a];
+        }
+        L.h = s.h;
+        L.ppc = c->level_ppc[l];
         c->levels.push_back(L);
     }
     // the device table of levels (the device loop picks the level on the GPU)
@@ -418,138 +563,52 @@ int build_grid(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::
     return PMX_OK;
 }
 
-// one level of the grid: cell size h (clamped to the 2^26-cell budget)
-template <typename T>
-int build_level(pmx_ctx* c, const std::vector<P4<T>>& pts, int64_t M, const std::vector<P4<T>>& nrm,
-                const double lo[3], const double ext[3], double maxe, int64_t valid, double h, GridLevel& out) {
-    h = std::max(h, maxe / 4096.0);
-    GridShape s = grid_shape(lo, ext, h);
-    while (s.cells() > kMaxCells) {
-        h *= 1.25;
-        s = grid_shape(lo, ext, h);
-    }
-    const int64_t C = s.cells();
-    std::vector<uint32_t> start((size_t)C + 1, 0);
-    std::vector<int64_t> cellid((size_t)M, -1);
-    for (int64_t j = 0; j < M; ++j)
-        if (finite_pt(pts[j])) {
-            cellid[j] = cell_of(s, pts[j]);
-            start[(size_t)cellid[j] + 1]++;
-        }
-    for (int64_t i = 0; i < C; ++i) start[i + 1] += start[i];
-    std::vector<uint32_t> fill(start.begin(), start.end() - 1);
-    std::vector<P4<T>> gp((size_t)std::max<int64_t>(valid, 1));
-    std::vector<int32_t> gi((size_t)std::max<int64_t>(valid, 1));
-    for (int64_t j = 0; j < M; ++j) {  // stable: index order inside a cell
-        if (cellid[j] < 0) continue;
-        const uint32_t p = fill[(size_t)cellid[j]]++;
-        gp[p] = pts[j];
-        gi[p] = (int32_t)j;
-    }
-    HIPCHK(c, hipMalloc(&out.gpts, sizeof(P4<T>) * gp.size()));
-    HIPCHK(c, hipMalloc((void**)&out.gidx, sizeof(int32_t) * gi.size()));
-    HIPCHK(c, hipMalloc((void**)&out.gstart, sizeof(uint32_t) * start.size()));
-    HIPCHK(c, hipMemcpyAsync(out.gpts, gp.data(), sizeof(P4<T>) * gp.size(), hipMemcpyHostToDevice, c->stream));
-    std::vector<P4<T>> gn;
-    if (!nrm.empty()) {
-        gn.resize(gp.size());
-        for (int64_t p = 0; p < valid; ++p) gn[(size_t)p] = nrm[(size_t)gi[(size_t)p]];
-        HIPCHK(c, hipMalloc(&out.gnrm, sizeof(P4<T>) * gn.size()));
-        HIPCHK(c, hipMemcpyAsync(out.gnrm, gn.data(), sizeof(P4<T>) * gn.size(), hipMemcpyHostToDevice, c->stream));
-    }
-    HIPCHK(c, hipMemcpyAsync(out.gidx, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(out.gstart, start.data(), sizeof(uint32_t) * start.size(), hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    for (int a = 0; a < 3; ++a) {
-        out.lo[a] = s.lo[a];
-        out.dim[a] = s.g[a];
-    }
-    out.h = s.h;
-    return PMX_OK;
-}
-
-// 21-bit Morton spread (bit i -> bit 3i)
-static inline uint64_t spread3(uint64_t v) {
-    v &= 0x1fffffull;
-    v = (v | v << 32) & 0x1f00000000ffffull;
-    v = (v | v << 16) & 0x1f0000ff0000ffull;
-    v = (v | v << 8) & 0x100f00f00f00f00full;
-    v = (v | v << 4) & 0x10c30c30c30c30c3ull;
-    v = (v | v << 2) & 0x1249249249249249ull;
-    return v;
-}
-
 // Slot order of the reading: Morton order of the cell of the initially
 // transformed point, so the 64 queries of a wave form a compact cluster
 // (small shared LDS box in the tile kernel) and result writes are coalesced.
 // Performance only: every kernel is order-independent up to fp64 summation
-// order, and the mirrors undo the permutation.
+// order, and the mirrors undo the permutation.  Built on the device
+// (pmx_setup.hip): the slot -> query order stays there (d_order) and is
+// copied to the host only for a host mirror.
 //
-// Waves of the tile kernel: a wave takes up to 64 consecutive slots but never
-// crosses the boundary of an aligned Morton block of 2^L cells per side, so
-// its queries never straddle two distant regions (a straddling wave would
-// share one huge LDS box).  L is the smallest level whose wave count stays
-// within `fill` (default 1.25, PMX_GRID_WAVE_FILL) of ceil(N / 64).
-template <typename T>
-std::vector<int32_t> build_order(const pmx_ctx* c, const std::vector<P4<T>>& raw, int64_t N, const Mat4<T>& M0,
-                                 std::vector<uint32_t>& waves) {
-    std::vector<int32_t> order;
-    waves.clear();
-    if (!c->grid_ready || N <= 0) return order;
-    if (std::getenv("PMX_GRID_NOORDER")) return order;  // tuning knob: identity slot order
-    GridShape s;  // Morton order over the finest level's cells
-    for (int a = 0; a < 3; ++a) {
-        s.lo[a] = c->lv(0).lo[a];
-        s.g[a] = c->lv(0).dim[a];
-    }
-    s.h = c->lv(0).h;
-    const bool morton = s.g[0] <= (1 << 21) && s.g[1] <= (1 << 21) && s.g[2] <= (1 << 21);
-    std::vector<std::pair<uint64_t, int32_t>> key((size_t)N);
-    for (int64_t i = 0; i < N; ++i) {
-        const P4<T>& p = raw[i];
-        P4<double> q;
-        q.x = ((double)M0.m[0] * p.x + (double)M0.m[1] * p.y) + (double)M0.m[2] * p.z + (double)M0.m[3] * p.w;
-        q.y = ((double)M0.m[4] * p.x + (double)M0.m[5] * p.y) + (double)M0.m[6] * p.z + (double)M0.m[7] * p.w;
-        q.z = ((double)M0.m[8] * p.x + (double)M0.m[9] * p.y) + (double)M0.m[10] * p.z + (double)M0.m[11] * p.w;
-        q.w = 1;
-        uint64_t k = ~0ull;
-        if (finite_pt(q)) {
-            const int64_t cell = cell_of(s, q);
-            if (morton) {
-                const int64_t cx = cell % s.g[0], cy = (cell / s.g[0]) % s.g[1], cz = cell / ((int64_t)s.g[0] * s.g[1]);
-                k = spread3((uint64_t)cx) | (spread3((uint64_t)cy) << 1) | (spread3((uint64_t)cz) << 2);
-            } else {
-                k = (uint64_t)cell;
-            }
+// Waves of the tile kernel (PMX_GRID_MODE=tile only): a wave takes up to 64
+// consecutive slots but never crosses the boundary of an aligned Morton
+// block of 2^L cells per side, so its queries never straddle two distant
+// regions (a straddling wave would share one huge LDS box).  L is the
+// smallest level whose wave count stays within `fill` (default 1.25,
+// PMX_GRID_WAVE_FILL) of ceil(N / 64).
+std::vector<uint32_t> tile_waves(const std::vector<unsigned long long>& key, int64_t N) {
+    std::vector<uint32_t> waves;
+    double fill = 1.25;
+    if (const char* e = std::getenv("PMX_GRID_WAVE_FILL")) fill = std::max(1.0, std::atof(e));
+    const int64_t full = (N + 63) / 64;
+    auto cut = [&](int L, std::vector<uint32_t>* out) -> int64_t {
+        int64_t W = 0;
+        for (int64_t i = 0; i < N;) {
+            const uint64_t blk = L >= 21 ? 0 : key[(size_t)i] >> (3 * L);
+            int64_t j = i + 1;
+            while (j < N && j - i < 64 && (L >= 21 ? 0 : key[(size_t)j] >> (3 * L)) == blk) ++j;
+            if (out) out->push_back((uint32_t)i);
+            ++W;
+            i = j;
         }
-        key[(size_t)i] = {k, (int32_t)i};
-    }
-    std::sort(key.begin(), key.end());
-    order.resize((size_t)N);
-    for (int64_t i = 0; i < N; ++i) order[(size_t)i] = key[(size_t)i].second;
-    if (morton) {
-        double fill = 1.25;
-        if (const char* e = std::getenv("PMX_GRID_WAVE_FILL")) fill = std::max(1.0, std::atof(e));
-        const int64_t full = (N + 63) / 64;
-        auto cut = [&](int L, std::vector<uint32_t>* out) -> int64_t {
-            int64_t W = 0;
-            for (int64_t i = 0; i < N;) {
-                const uint64_t blk = L >= 21 ? 0 : key[(size_t)i].first >> (3 * L);
-                int64_t j = i + 1;
-                while (j < N && j - i < 64 && (L >= 21 ? 0 : key[(size_t)j].first >> (3 * L)) == blk) ++j;
-                if (out) out->push_back((uint32_t)i);
-                ++W;
-                i = j;
-            }
-            return W;
-        };
-        int L = 0;
-        while (L < 21 && (double)cut(L, nullptr) > fill * (double)full) ++L;
-        cut(L, &waves);
-        waves.push_back((uint32_t)N);
-    }
-    return order;
+        return W;
+    };
+    int L = 0;
+    while (L < 21 && (double)cut(L, nullptr) > fill * (double)full) ++L;
+    cut(L, &waves);
+    waves.push_back((uint32_t)N);
+    return waves;
+}
+
+// the host copy of the slot order (host mirrors only)
+int host_order(pmx_ctx* c) {
+    if (!c->has_order || (int64_t)c->slot_query.size() == c->N) return PMX_OK;
+    c->slot_query.resize((size_t)c->N);
+    HIPCHK(c, hipMemcpyAsync(c->slot_query.data(), c->d_order, sizeof(int32_t) * c->N, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
 }
 
 // ------------------------------------------------------------------ clouds --
@@ -563,31 +622,22 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
         return fail(c, PMX_E_BAD_PARAM, "reference larger than 4 GiB of points (268M float / 134M double)");
     const int D = rows - 1;
     const int64_t M_pad = ((M + kTile - 1) / kTile) * kTile;
-    std::vector<P4<T>> h((size_t)M_pad);
-    const T inf = std::numeric_limits<T>::infinity();
-    for (int64_t j = 0; j < M; ++j) {
-        const T* p = feat + j * rows;
-        h[j] = (D == 3) ? P4<T>{p[0], p[1], p[2], p[3]} : P4<T>{p[0], p[1], (T)0, p[2]};
-    }
-    for (int64_t j = M; j < M_pad; ++j) h[j] = P4<T>{inf, inf, inf, (T)1};
+    int rc;
     if (c->d_ref) (void)hipFree(c->d_ref);
     c->d_ref = nullptr;
     HIPCHK(c, hipMalloc(&c->d_ref, sizeof(P4<T>) * M_pad));
-    HIPCHK(c, hipMemcpyAsync(c->d_ref, h.data(), sizeof(P4<T>) * M_pad, hipMemcpyHostToDevice, c->stream));
+    if ((rc = upload_raw(c, feat, sizeof(T) * (size_t)rows * M))) return rc;
+    launch_pack_p4<T>((const T*)c->d_raw, rows, M, M_pad, (P4<T>*)c->d_ref, c->stream);
     if (c->d_nrm) (void)hipFree(c->d_nrm);
     c->d_nrm = nullptr;
     c->has_normals = normals != nullptr;
-    std::vector<P4<T>> hn;
     if (normals) {
-        hn.resize((size_t)M);
-        for (int64_t j = 0; j < M; ++j) {
-            const T* n = normals + j * D;
-            hn[j] = (D == 3) ? P4<T>{n[0], n[1], n[2], (T)0} : P4<T>{n[0], n[1], (T)0, (T)0};
-        }
         HIPCHK(c, hipMalloc(&c->d_nrm, sizeof(P4<T>) * M));
-        HIPCHK(c, hipMemcpyAsync(c->d_nrm, hn.data(), sizeof(P4<T>) * M, hipMemcpyHostToDevice, c->stream));
+        // (the raw buffer is reused: the copy is ordered after the pack on the stream)
+        if ((rc = upload_raw(c, normals, sizeof(T) * (size_t)D * M))) return rc;
+        launch_pack_nrm<T>((const T*)c->d_raw, D, M, (P4<T>*)c->d_nrm, c->stream);
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipGetLastError());
     c->rows = rows;
     c->dim = D;
     c->M = M;
@@ -596,7 +646,7 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     c->grid_ready = false;
     // a resident reading keeps its slot order (any permutation is correct;
     // it was only chosen for the previous grid's locality)
-    return build_grid<T>(c, h, M, hn);
+    return build_grid<T>(c, M);
 }
 
 template <typename T>
@@ -604,41 +654,68 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     if (c->rows == 0) return fail(c, PMX_E_STATE, "pmx_set_reference must be called first");
     if (rows != c->rows) return fail(c, PMX_E_BAD_PARAM, "reading and reference dimensions differ");
     if (N < 0) return fail(c, PMX_E_BAD_PARAM, "negative reading size");
-    const int D = rows - 1;
-    std::vector<P4<T>> h((size_t)(N > 0 ? N : 1));
-    for (int64_t i = 0; i < N; ++i) {
-        const T* p = feat + i * rows;
-        h[i] = (D == 3) ? P4<T>{p[0], p[1], p[2], p[3]} : P4<T>{p[0], p[1], (T)0, p[2]};
-    }
-    Mat4<T> M0 = embed<T>(T0, rows);
-    std::vector<uint32_t> waves;
-    c->slot_query = build_order<T>(c, h, N, M0, waves);
-    if (!c->slot_query.empty()) {
-        std::vector<P4<T>> hs((size_t)N);
-        for (int64_t s = 0; s < N; ++s) hs[(size_t)s] = h[(size_t)c->slot_query[(size_t)s]];
-        h.swap(hs);
-    }
+    if (N > (int64_t)0x7fffffff) return fail(c, PMX_E_BAD_PARAM, "reading larger than int32 slots");
+    const Mat4<T> M0 = embed<T>(T0, rows);
+    int rc;
+    const int64_t n1 = std::max<int64_t>(N, 1);
+    // raw P4 reading (pack), then the slot order, then T_refMean_dataIn
+    void* d_p4 = nullptr;
+    HIPCHK(c, hipMalloc(&d_p4, sizeof(P4<T>) * n1));
+    std::unique_ptr<void, void (*)(void*)> free_p4(d_p4, [](void* p) { (void)hipFree(p); });
+    if ((rc = upload_raw(c, feat, sizeof(T) * (size_t)rows * N))) return rc;
+    launch_pack_p4<T>((const T*)c->d_raw, rows, N, N, (P4<T>*)d_p4, c->stream);
+    if (c->d_rd) (void)hipFree(c->d_rd);
+    c->d_rd = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_rd, sizeof(P4<T>) * n1));
     if (c->d_waves) (void)hipFree(c->d_waves);
     c->d_waves = nullptr;
     c->n_waves = 0;
-    if (!waves.empty()) {
-        HIPCHK(c, hipMalloc((void**)&c->d_waves, sizeof(uint32_t) * waves.size()));
-        HIPCHK(c, hipMemcpyAsync(c->d_waves, waves.data(), sizeof(uint32_t) * waves.size(), hipMemcpyHostToDevice,
+    c->slot_query.clear();
+    c->has_order = false;
+    const bool order = c->grid_ready && N > 0 && !std::getenv("PMX_GRID_NOORDER");  // (knob: identity slot order)
+    if (order) {
+        // Morton order over the finest level's cells
+        const GridLevel& L0 = c->lv(0);
+        SetupShape s;
+        for (int a = 0; a < 3; ++a) {
+            s.lo[a] = L0.lo[a];
+            s.g[a] = L0.dim[a];
+        }
+        s.h = L0.h;
+        s.cells = (int64_t)s.g[0] * s.g[1] * s.g[2];
+        const bool morton = s.g[0] <= (1 << 21) && s.g[1] <= (1 << 21) && s.g[2] <= (1 << 21);
+        if ((rc = setup_room(c, N, std::max<int64_t>(c->setup_cells, 1)))) return rc;
+        void* d_sorted = nullptr;
+        HIPCHK(c, hipMalloc(&d_sorted, sizeof(P4<T>) * n1));
+        std::unique_ptr<void, void (*)(void*)> free_sorted(d_sorted, [](void* p) { (void)hipFree(p); });
+        const int r = reading_order_device<T>((const P4<T>*)d_p4, N, M0, s, morton, c->setup, (P4<T>*)d_sorted,
+                                              c->stream);
+        if (r) return fail(c, PMX_E_HIP, "reading order failed (" + std::to_string(r) + ")");
+        size_t cap = c->order_bytes;
+        if ((rc = ensure(c, (void**)&c->d_order, &cap, sizeof(int32_t) * n1))) return rc;
+        c->order_bytes = cap;
+        HIPCHK(c, hipMemcpyAsync(c->d_order, c->setup.idx_out, sizeof(int32_t) * N, hipMemcpyDeviceToDevice,
                                  c->stream));
-        c->n_waves = (int64_t)waves.size() - 1;
-    }
-    void* d_raw = nullptr;
-    HIPCHK(c, hipMalloc(&d_raw, sizeof(P4<T>) * (N > 0 ? N : 1)));
-    if (c->d_rd) (void)hipFree(c->d_rd);
-    c->d_rd = nullptr;
-    HIPCHK(c, hipMalloc(&c->d_rd, sizeof(P4<T>) * (N > 0 ? N : 1)));
-    if (N > 0) {
-        HIPCHK(c, hipMemcpyAsync(d_raw, h.data(), sizeof(P4<T>) * N, hipMemcpyHostToDevice, c->stream));
-        launch_transform<T>((const P4<T>*)d_raw, (P4<T>*)c->d_rd, N, M0, c->stream);
+        c->has_order = true;
+        launch_transform<T>((const P4<T>*)d_sorted, (P4<T>*)c->d_rd, N, M0, c->stream);
+        if (morton && c->grid_mode == 0) {  // the tile kernel's wave table (host, from the sorted keys)
+            std::vector<unsigned long long> keys((size_t)N);
+            HIPCHK(c, hipMemcpyAsync(keys.data(), c->setup.keys64_out, sizeof(unsigned long long) * N,
+                                     hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            const std::vector<uint32_t> waves = tile_waves(keys, N);
+            HIPCHK(c, hipMalloc((void**)&c->d_waves, sizeof(uint32_t) * waves.size()));
+            HIPCHK(c, hipMemcpyAsync(c->d_waves, waves.data(), sizeof(uint32_t) * waves.size(),
+                                     hipMemcpyHostToDevice, c->stream));
+            c->n_waves = (int64_t)waves.size() - 1;
+        }
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // (d_sorted is freed on return)
+    } else if (N > 0) {
+        launch_transform<T>((const P4<T>*)d_p4, (P4<T>*)c->d_rd, N, M0, c->stream);
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    (void)hipFree(d_raw);
     c->N = N;
     c->N_total = N;
     c->N_max = N;
@@ -653,14 +730,14 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
                 best = l;
         c->level = best;
     }
-    if (c->comm && c->nranks > 1) {
+    if (sharded(c)) {
         // global reading size and the largest shard (padding of all-gathers)
         double* tmp = c->d_result;
-        double hv[2] = {(double)N, 0.0};
-        HIPCHK(c, hipMemcpyAsync(tmp, hv, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        NCCLCHK(c, ncclAllReduce(tmp, tmp, 1, ncclFloat64, ncclSum, c->comm, c->stream));
-        HIPCHK(c, hipMemcpyAsync(tmp + 1, hv, sizeof(double), hipMemcpyHostToDevice, c->stream));
-        NCCLCHK(c, ncclAllReduce(tmp + 1, tmp + 1, 1, ncclFloat64, ncclMax, c->comm, c->stream));
+        double hv[2] = {(double)N, (double)N};
+        HIPCHK(c, hipMemcpyAsync(tmp, hv, 2 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        int rc2 = coll_allreduce(c, tmp, 1, PMX_COLL_F64, PMX_COLL_SUM);
+        if (rc2 == PMX_OK) rc2 = coll_allreduce(c, tmp + 1, 1, PMX_COLL_F64, PMX_COLL_MAX);
+        if (rc2) return rc2;
         HIPCHK(c, hipMemcpyAsync(hv, tmp, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->N_total = (int64_t)hv[0];
@@ -755,11 +832,22 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             ru.safe = (T*)c->d_safe;
             for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
         }
+        // several ranks: the counter sum packs this rank's window segment,
+        // the segments are all-gathered and every rank picks from the union
+        SpecSel* spec = c->spec_now();
+        unsigned long long* xseg = spec && sharded(c) ? c->d_specx : nullptr;
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
-                             c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->spec_now(), c->d_sel,
+                             c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              e1, c->stream);  // (e1 recorded after the match kernel, before the counter sum)
+        if (xseg) {
+            if (c->N <= 0)  // (no match kernel ran: an empty segment)
+                HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
+            int rc = coll_allgather(c, xseg, xseg + kSpecXStride, kSpecXStride * sizeof(unsigned long long));
+            if (rc) return rc;
+            launch_spec_pick<T>(xseg + kSpecXStride, c->nranks, spec, c->d_sel, loop_ctl(c), c->stream);
+        }
         c->safe_valid = ru.mode != 0;
         c->visited_host = 0;
         c->ids_grid = true;
@@ -782,13 +870,12 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
     // (no state reset: pass 0 starts a fresh select)
     const int passes = select_passes<T>();
     for (int p = 0; p < passes; ++p) {
-        if ((c->comm && c->nranks > 1) || c->select_split) {
+        if (sharded(c) || c->select_split) {
             // the histogram is all-reduced between the two halves of a pass
-            launch_select_hist<T>(d, n, c->d_hist, st, p, loop_ctl(c), c->stream);
-            if (c->comm && c->nranks > 1)
-                NCCLCHK(c, ncclAllReduce(c->d_hist, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), ncclUint32,
-                                         ncclSum, c->comm, c->stream));
-            launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), c->stream);
+            launch_select_hist<T>(d, n, c->d_hist, st, p, loop_ctl(c), spec, c->stream);
+            int rc = coll_allreduce(c, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), PMX_COLL_U32, PMX_COLL_SUM);
+            if (rc) return rc;
+            launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
         } else {
             launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, loop_ctl(c),
                                   spec, c->stream);
@@ -843,16 +930,19 @@ void choose_level(pmx_ctx* c, uint64_t visited, uint64_t full) {
 
 // slot-major device array -> query-major host array (the reference's order)
 template <typename V>
-void unpermute(const pmx_ctx* c, const std::vector<V>& src, V* dst, int k) {
+int unpermute(pmx_ctx* c, const std::vector<V>& src, V* dst, int k) {
     const int64_t N = c->N;
-    if (c->slot_query.empty()) {
+    if (!c->has_order) {
         std::memcpy(dst, src.data(), sizeof(V) * (size_t)(N * k));
-        return;
+        return PMX_OK;
     }
+    const int rc = host_order(c);
+    if (rc) return rc;
     for (int64_t s = 0; s < N; ++s) {
         const int64_t qi = c->slot_query[(size_t)s];
         for (int j = 0; j < k; ++j) dst[qi * k + j] = src[(size_t)(s * k + j)];
     }
+    return PMX_OK;
 }
 
 // record predicate `pos` of the weight chain (position 0 starts a new chain)
@@ -931,7 +1021,7 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
         if (!(minR < maxR)) return fail(c, PMX_E_BAD_PARAM, "VarTrimmedDistOutlierFilter: minRatio should be smaller than maxRatio");
         const T* dsrc = d;
         int64_t nsrc = n;
-        if (c->comm && c->nranks > 1) {
+        if (sharded(c)) {
             const int64_t per = c->N_max * c->knn;
             const size_t need = sizeof(T) * (size_t)per * (c->nranks + 1);
             if ((rc = ensure(c, &c->d_gather, &c->gather_bytes, need))) return rc;
@@ -943,7 +1033,7 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
                 HIPCHK(c, hipMemcpyAsync(send + n, inf.data(), sizeof(T) * (per - n), hipMemcpyHostToDevice, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
             }
-            NCCLCHK(c, ncclAllGather(send, c->d_gather, (size_t)per, (ncclDataType_t)ncclType<T>(), c->comm, c->stream));
+            if ((rc = coll_allgather(c, send, c->d_gather, sizeof(T) * (size_t)per))) return rc;
             dsrc = (const T*)c->d_gather;
             nsrc = per * c->nranks;
         }
@@ -1143,8 +1233,8 @@ int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
     const hipError_t e = hipStreamSynchronize(c->stream);
     if (d_map) (void)hipFree(d_map);
     HIPCHK(c, e);
-    if (dists) unpermute<T>(c, hd, (T*)dists, c->knn);
-    if (ids) unpermute<int32_t>(c, hi, ids, c->knn);
+    if (dists && (rc = unpermute<T>(c, hd, (T*)dists, c->knn))) return rc;
+    if (ids && (rc = unpermute<int32_t>(c, hi, ids, c->knn))) return rc;
     return PMX_OK;
 }
 
@@ -1162,7 +1252,7 @@ int get_weights_impl(pmx_ctx* c, void* w) {
     std::vector<T> hw((size_t)n);
     HIPCHK(c, hipMemcpyAsync(hw.data(), c->d_w, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    unpermute<T>(c, hw, (T*)w, c->knn);
+    if ((rc = unpermute<T>(c, hw, (T*)w, c->knn))) return rc;
     return PMX_OK;
 }
 
@@ -1252,13 +1342,15 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     // quantile window: a fresh window each loop (the first iteration runs the
     // radix passes, which centre the window for the next)
     const int k0 = cfg->n_filters > 0 ? cfg->filter_kind[0] : -1;
-    c->spec_on = c->spec_allowed && !(c->comm && c->nranks > 1) && !c->select_split && !c->no_visits &&
+    c->spec_on = c->spec_allowed && !c->no_visits &&
                  (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
     if (c->spec_on) {
         if (!c->d_spec) {
             HIPCHK(c, hipMalloc((void**)&c->d_spec, sizeof(SpecSel)));
             HIPCHK(c, hipMalloc(&c->d_spec_keys, sizeof(unsigned long long) * kSpecCap));
         }
+        if (sharded(c) && !c->d_specx)
+            HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * (c->nranks + 1)));
         SpecSel init{};
         init.keys = c->d_spec_keys;
         init.ratio = (double)(T)(k0 == PMX_FILTER_TRIMMED ? cfg->filter_p[0][0] : 0.5);
@@ -1505,9 +1597,10 @@ int surface_normals_impl(int device, const T* feat, int rows, int64_t n, int knn
     auto take = [&](int64_t off, int span, T* dst) {
         if (!dst) return;
         std::vector<T> src(h.begin() + off, h.begin() + off + n * span);
-        unpermute<T>(c, src, dst, span);
+        (void)unpermute<T>(c, src, dst, span);  // (host_order below has run)
     };
     const bool smooth = (flags & PMX_SN_SMOOTH) && o_nrm;
+    if ((rc = host_order(c))) return err(rc);
     take(0, D, o_nrm);
     take(n * D, 1, o_dens);
     take(n * (D + 1), D, o_eval);
@@ -1613,6 +1706,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
         preload_reduce();
         preload_loop();
         preload_normals();
+        preload_setup();
         preloaded = true;
     }
     // One small "iteration block" holds everything the host reads back per
@@ -1655,10 +1749,11 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace,
-                    c->d_spec, c->d_spec_keys};
+                    c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();
+    setup_release(c);
     if (c->h_result) (void)hipHostFree(c->h_result);
     if (c->h_loop) (void)hipHostFree(c->h_loop);
     for (hipEvent_t e : c->loop_ev)
@@ -1669,6 +1764,8 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     }
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->d_specx) (void)hipFree(c->d_specx);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PMX_OK;
@@ -1688,9 +1785,31 @@ int pmx_comm_init(pmx_ctx* c, const void* uid128, int nranks, int rank) {
     HIPCHK(c, hipSetDevice(c->device));
     ncclUniqueId id;
     std::memcpy(&id, uid128, sizeof(id));
+    if (sharded(c)) return fail(c, PMX_E_STATE, "the context already has a communicator");
     NCCLCHK(c, ncclCommInitRank(&c->comm, nranks, id, rank));
     c->nranks = nranks;
     c->rank = rank;
+    return PMX_OK;
+}
+
+int pmx_comm_init_host(pmx_ctx* c, int nranks, int rank, pmx_allreduce_fn allreduce, pmx_allgather_fn allgather,
+                       void* user) {
+    if (!c || !allreduce || !allgather || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(c, PMX_E_BAD_PARAM, "bad comm args");
+    if (sharded(c)) return fail(c, PMX_E_STATE, "the context already has a communicator");
+    c->host_ar = allreduce;
+    c->host_ag = allgather;
+    c->host_user = user;
+    c->nranks = nranks;
+    c->rank = rank;
+    return PMX_OK;
+}
+
+int pmx_comm_size(const pmx_ctx* c, int* nranks, int* rank, int* kind) {
+    if (!c) return PMX_E_BAD_PARAM;
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    if (kind) *kind = c->comm ? 1 : c->host_ar ? 2 : 0;
     return PMX_OK;
 }
 

@@ -446,11 +446,14 @@ __device__ __forceinline__ void add_visits(uint32_t visits, unsigned long long* 
 
 // (also clears the iteration's error word: it runs first after the match,
 // before any filter can raise one).  With a quantile window (pmx_spec.h) it
-// also resolves the iteration's quantile from the window when it can.
+// also resolves the iteration's quantile from the window when it can — or,
+// with several ranks (xseg != null), packs this rank's window segment for the
+// exchange and leaves the pick to spec_pick_kernel.
 template <typename T>
 __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ vpart,
                                               unsigned long long* __restrict__ out, int* __restrict__ iter_err,
-                                              SpecSel* __restrict__ spec, SelectState* __restrict__ st) {
+                                              SpecSel* __restrict__ spec, SelectState* __restrict__ st,
+                                              unsigned long long* __restrict__ xseg) {
     __shared__ unsigned long long red[4][kVSlots / 64];
     __shared__ uint32_t lh[2048];
     __shared__ unsigned long long part[kVSlots];
@@ -480,7 +483,27 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
         out[1] = sum[1];
         if (iter_err) *iter_err = 0;
     }
-    if (spec) spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], lh, part, bc);
+    if (!spec) return;
+    if (xseg) {  // several ranks: this rank's segment [fin, below, n, keys...]
+        using K = typename KeyOf<T>::K;
+        const unsigned nk = spec->n_keys;
+        const unsigned nc = nk < kSpecXCap ? nk : kSpecXCap;
+        const K* keys = (const K*)spec->keys;
+        if (t == 0) {
+            xseg[0] = sum[2];
+            xseg[1] = sum[3];
+            xseg[2] = spec->valid ? nk : 0ull;
+        }
+        for (unsigned i = t; i < nc; i += kVSlots) xseg[kSpecXHdr + i] = (unsigned long long)keys[i];
+        __syncthreads();  // (every lane read n_keys before it is reset)
+        if (t == 0) spec->n_keys = 0;
+        return;
+    }
+    SpecKeys<T> src;
+    src.local = (const typename KeyOf<T>::K*)spec->keys;
+    const unsigned nk_raw = spec->n_keys;
+    src.n_local = nk_raw < kSpecCap ? nk_raw : kSpecCap;
+    spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part, bc);
 }
 
 template <typename T>
@@ -489,10 +512,49 @@ __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long
                                                               int* __restrict__ iter_err,
                                                               const LoopCtl* __restrict__ ctl,
                                                               SpecSel* __restrict__ spec,
-                                                              SelectState* __restrict__ st) {
+                                                              SelectState* __restrict__ st,
+                                                              unsigned long long* __restrict__ xseg) {
     if (ctl && ctl->done) return;
-    counter_phase<T>(vpart, out, iter_err, spec, st);
+    counter_phase<T>(vpart, out, iter_err, spec, st, xseg);
 }
+
+// Several ranks: resolve the quantile from the all-gathered window segments
+// (pmx_spec.h).  Every rank runs it on the same segments and writes the same
+// limit; a miss leaves the radix passes (with their histogram all-reduce) to
+// resolve it.
+template <typename T>
+__global__ __launch_bounds__(kVSlots) void spec_pick_kernel(const unsigned long long* __restrict__ segs, int nseg,
+                                                            SpecSel* __restrict__ spec,
+                                                            SelectState* __restrict__ st,
+                                                            const LoopCtl* __restrict__ ctl) {
+    __shared__ uint32_t lh[2048];
+    __shared__ unsigned long long part[kVSlots];
+    __shared__ unsigned long long bc[2];
+    if (ctl && ctl->done) return;
+    unsigned long long fin = 0, below = 0, nk = 0;
+    bool overflow = false;
+    for (int s = 0; s < nseg; ++s) {  // (uniform; a handful of segments)
+        const unsigned long long* g = segs + (size_t)s * kSpecXStride;
+        fin += g[0];
+        below += g[1];
+        nk += g[2];
+        overflow = overflow || g[2] > kSpecXCap;
+    }
+    SpecKeys<T> src;
+    src.segs = segs;
+    src.nseg = nseg;
+    spec_pick<T, kVSlots>(spec, st, fin, below, nk, overflow, src, lh, part, bc);
+}
+
+template <typename T>
+void launch_spec_pick(const unsigned long long* segs, int nseg, SpecSel* spec, SelectState* st, const LoopCtl* ctl,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(spec_pick_kernel<T>, dim3(1), dim3(kVSlots), 0, s, segs, nseg, spec, st, ctl);
+}
+template void launch_spec_pick<float>(const unsigned long long*, int, SpecSel*, SelectState*, const LoopCtl*,
+                                      hipStream_t);
+template void launch_spec_pick<double>(const unsigned long long*, int, SpecSel*, SelectState*, const LoopCtl*,
+                                       hipStream_t);
 
 // counters: 0 pairs, 1 full-search fallbacks, 2 finite distances, 3 below the quantile window
 size_t grid_counter_bytes() { return sizeof(unsigned long long) * 4 * kVSlots * kVStride; }
@@ -721,7 +783,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                       SelectState* spec_st, hipEvent_t ev_end, hipStream_t s) {
+                       SelectState* spec_st, unsigned long long* xseg, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
@@ -750,21 +812,21 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel alone)
     if (visited && vout)
         hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
-                           spec_st);
+                           spec_st, xseg);
 }
 
 template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, const uint32_t*, const double*, double,
                                        const int*, const P4<float>*, int64_t, const uint32_t*, int64_t,
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
-                                       const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*, hipEvent_t,
-                                       hipStream_t);
+                                       const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
+                                       unsigned long long*, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        hipEvent_t, hipStream_t);
+                                        unsigned long long*, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

@@ -158,8 +158,53 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       hipEvent_t ev_end, hipStream_t s);
+                       unsigned long long* xseg, hipEvent_t ev_end, hipStream_t s);
+// several ranks: the quantile window's pick over the all-gathered segments
+// (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum
+template <typename T>
+void launch_spec_pick(const unsigned long long* segs, int nseg, SpecSel* spec, SelectState* st, const LoopCtl* ctl,
+                      hipStream_t s);
+// ---- once-per-compute setup on the device (pmx_setup.hip) ----
+// a uniform grid shape as the host sizes it (cells = g0 * g1 * g2)
+struct SetupShape {
+    double lo[3];
+    double h;
+    int g[3];
+    int64_t cells;
+};
+// scratch of the setup sorts (keys32 / keys32_out alias keys64 / keys64_out)
+struct SetupScratch {
+    unsigned long long* keys64 = nullptr;
+    unsigned long long* keys64_out = nullptr;
+    uint32_t* keys32 = nullptr;
+    uint32_t* keys32_out = nullptr;
+    int32_t* idx = nullptr;
+    int32_t* idx_out = nullptr;
+    uint32_t* counts = nullptr;  // cells + 1
+    void* temp = nullptr;        // hipcub temporary storage
+    size_t temp_bytes = 0;
+};
+template <typename T>
+void launch_pack_p4(const T* raw, int rows, int64_t n, int64_t n_pad, P4<T>* out, hipStream_t s);
+template <typename T>
+void launch_pack_nrm(const T* raw, int D, int64_t n, P4<T>* out, hipStream_t s);
+template <typename T>
+void launch_bbox(const P4<T>* p, int64_t n, double* scratch, double* out, hipStream_t s);
+size_t bbox_scratch_bytes();
+template <typename T>
+void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, uint32_t* bits, unsigned long long* count,
+                      hipStream_t st);
+template <typename T>
+int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const SetupShape& s, int64_t valid,
+                       const SetupScratch& sc, P4<T>* gp, P4<T>* gn, int32_t* gi, uint32_t* gstart, hipStream_t st);
+template <typename T>
+int reading_order_device(const P4<T>* raw, int64_t n, const Mat4<T>& M0, const SetupShape& s, bool morton,
+                         const SetupScratch& sc, P4<T>* sorted, hipStream_t st);
+size_t setup_temp_bytes(int64_t n, int64_t max_cells);
+void launch_unpermute(const void* src, const int32_t* order, int64_t n, int span, size_t esz, void* dst,
+                      hipStream_t s);
 // code-object preloads (one per translation unit, called by pmx_ctx_create)
+void preload_setup();
 void preload_match();
 void preload_grid();
 void preload_select();
@@ -229,12 +274,14 @@ __device__ __forceinline__ bool chain_keep(const WRange<T>& r, T d) {
 // resolved prefix.  hist must be zero on entry (select zeroes it on exit).
 template <typename T>
 void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass,
-                        const LoopCtl* ctl, hipStream_t s);
+                        const LoopCtl* ctl, const SpecSel* spec, hipStream_t s);
 // resolve the digit of `pass`; pass 0 also computes count and the target
 // rank from ratio (host value, or *ratio_dev when non-null).
+// spec (may be null): skipped when the window resolved the quantile; the
+// last pass re-centres the window
 template <typename T>
 void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
-                        const double* ratio_dev, int* iter_err, const LoopCtl* ctl, hipStream_t s);
+                        const double* ratio_dev, int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s);
 // hist + pick in one launch (single rank; ticket: zeroed uint32, reset on exit)
 template <typename T>
 // spec (may be null): the pass is skipped when the window resolved the

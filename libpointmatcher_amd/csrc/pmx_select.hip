@@ -148,9 +148,11 @@ template <typename T>
 __global__ __launch_bounds__(256) void select_hist_kernel(const T* __restrict__ d, int64_t n,
                                                           uint32_t* __restrict__ hist,
                                                           const SelectState* __restrict__ st, int pass, int agg,
-                                                          const LoopCtl* __restrict__ ctl) {
+                                                          const LoopCtl* __restrict__ ctl,
+                                                          const SpecSel* __restrict__ spec) {
     __shared__ uint32_t lh[2048];
     if (ctl && ctl->done) return;
+    if (spec && spec->hit) return;  // the quantile window resolved it (pmx_spec.h)
     hist_phase<T>(d, n, hist, st, pass, lh, agg);
 }
 
@@ -183,9 +185,9 @@ static int64_t select_blocks(int64_t n) {
 
 template <typename T>
 void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass, const LoopCtl* ctl,
-                        hipStream_t s) {
+                        const SpecSel* spec, hipStream_t s) {
     hipLaunchKernelGGL(select_hist_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
-                       pass, select_agg(), ctl);
+                       pass, select_agg(), ctl, spec);
 }
 
 // ------------------------------------------------------------------ pick --
@@ -309,12 +311,14 @@ __global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__
                                                           int pass, double ratio_host,
                                                           const double* __restrict__ ratio_dev,
                                                           int* __restrict__ iter_err, int last,
-                                                          const LoopCtl* __restrict__ ctl) {
+                                                          const LoopCtl* __restrict__ ctl,
+                                                          SpecSel* __restrict__ spec) {
     __shared__ unsigned long long part[256];
     __shared__ unsigned long long s_rank;
     __shared__ int s_err;
     if (ctl && ctl->done) return;
-    pick_phase<T, false>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err, nullptr);
+    if (spec && spec->hit) return;  // the quantile window resolved it (pmx_spec.h)
+    pick_phase<T, false>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err, spec);
 }
 
 // One radix-select pass in one launch (single rank): every block builds and
@@ -349,10 +353,10 @@ __global__ __launch_bounds__(256) void select_pass_kernel(const T* __restrict__ 
 
 template <typename T>
 void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio, const double* ratio_dev,
-                        int* iter_err, const LoopCtl* ctl, hipStream_t s) {
+                        int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s) {
     const int last = pass == select_passes<T>() - 1;
     hipLaunchKernelGGL(select_pick_kernel<T>, dim3(1), dim3(256), 0, s, hist, st, pass, ratio, ratio_dev,
-                       iter_err, last, ctl);
+                       iter_err, last, ctl, spec);
 }
 
 template <typename T>
@@ -624,13 +628,13 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
 
 // explicit instantiations
 template void launch_select_hist<float>(const float*, int64_t, uint32_t*, const SelectState*, int, const LoopCtl*,
-                                        hipStream_t);
+                                        const SpecSel*, hipStream_t);
 template void launch_select_hist<double>(const double*, int64_t, uint32_t*, const SelectState*, int, const LoopCtl*,
-                                         hipStream_t);
+                                         const SpecSel*, hipStream_t);
 template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
-                                        hipStream_t);
+                                        SpecSel*, hipStream_t);
 template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
-                                         hipStream_t);
+                                         SpecSel*, hipStream_t);
 template void launch_select_pass<float>(const float*, int64_t, uint32_t*, SelectState*, int, double, const double*,
                                         unsigned int*, int*, const LoopCtl*, SpecSel*, hipStream_t);
 template void launch_select_pass<double>(const double*, int64_t, uint32_t*, SelectState*, int, double, const double*,

@@ -22,7 +22,8 @@
 // limit, its half-width from the last movement of the limit and capped by the
 // observed key density so the expected append count stays below cap/2.
 //
-// Used by the device-resident loop only, single rank, chain position 0.
+// Used by the device-resident loop, chain position 0.  With several ranks the
+// counters and window keys are exchanged first (SpecKeys segments below).
 #pragma once
 
 #include "pmx_internal.h"
@@ -146,22 +147,53 @@ __device__ __forceinline__ void spec_update(SpecSel* sp, typename KeyOf<T>::K kl
     sp->valid = 1;
 }
 
+// ---- several ranks: the window's keys are exchanged ----
+// Every rank packs its counters and window keys into one segment
+//   [fin, below, n_keys, key_0 .. key_{n-1}]   (unsigned long long each)
+// after its match; the segments are all-gathered (pmx_capi.hip) and every
+// rank resolves the same limit from the union (spec_pick over nseg
+// segments).  A rank that appended more than kSpecXCap keys makes the window
+// miss on every rank (its segment carries the true count).
+constexpr unsigned kSpecXCap = 4096;
+constexpr unsigned kSpecXHdr = 3;
+constexpr unsigned kSpecXStride = kSpecXHdr + kSpecXCap;  // unsigned long longs per segment
+
+// the keys a pick runs over: one local append buffer, or nseg exchanged segments
+template <typename T>
+struct SpecKeys {
+    using K = typename KeyOf<T>::K;
+    const K* local = nullptr;                    // single rank: K[n_local]
+    unsigned n_local = 0;
+    const unsigned long long* segs = nullptr;    // several ranks: nseg * kSpecXStride
+    int nseg = 0;
+    __device__ __forceinline__ int count() const { return segs ? nseg : 1; }
+    __device__ __forceinline__ unsigned n(int s) const {
+        if (!segs) return n_local;
+        const unsigned long long c = segs[(size_t)s * kSpecXStride + 2];
+        return c < kSpecXCap ? (unsigned)c : kSpecXCap;
+    }
+    __device__ __forceinline__ K key(int s, unsigned i) const {
+        return segs ? (K)segs[(size_t)s * kSpecXStride + kSpecXHdr + i] : local[i];
+    }
+};
+
 // ---- counter side: resolve the limit from the window (one block) ----
-// fin / below: the match's counters.  Writes st (as the radix select's last
-// pass would) and sp->hit; resets the append counter.  Block of kThreads.
+// fin / below: the match's counters (global), nk_raw: keys appended inside
+// the window (global; more than the buffers hold means a miss), keys: where
+// they are.  Writes st (as the radix select's last pass would) and sp->hit;
+// resets the append counter.  Block of kThreads.
 template <typename T, int kThreads>
 __device__ __forceinline__ void spec_pick(SpecSel* __restrict__ sp, SelectState* __restrict__ st,
-                                          unsigned long long fin, unsigned long long below, uint32_t* lh,
-                                          unsigned long long* part, unsigned long long* bc) {
+                                          unsigned long long fin, unsigned long long below,
+                                          unsigned long long nk_raw, bool overflow, const SpecKeys<T>& src,
+                                          uint32_t* lh, unsigned long long* part, unsigned long long* bc) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     const int t = threadIdx.x;
-    const unsigned nk_raw = sp->n_keys;
-    const unsigned nk = nk_raw < kSpecCap ? nk_raw : kSpecCap;
+    const unsigned long long nk = nk_raw;
     const K lo = (K)sp->lo, hi = (K)sp->hi;
-    const K* keys = (const K*)sp->keys;
     // target rank (Matches.cpp:83-86 via pick_phase's rule)
-    bool ok = sp->valid && nk_raw <= kSpecCap && fin > 0;
+    bool ok = sp->valid && !overflow && fin > 0;
     const T q = (T)sp->ratio;
     unsigned long long rank = 0;
     if (ok) {
@@ -196,10 +228,13 @@ __device__ __forceinline__ void spec_pick(SpecSel* __restrict__ sp, SelectState*
         const int nbins = 1 << bits;
         for (int i = t; i < 2048; i += kThreads) lh[i] = 0;
         __syncthreads();
-        for (unsigned i = t; i < nk; i += kThreads) {
-            const unsigned long long off = (unsigned long long)(keys[i] - lo);
-            if (done_bits == 0 || (off >> (shift + bits)) == prefix)
-                atomicAdd(&lh[(off >> shift) & (unsigned long long)(nbins - 1)], 1u);
+        for (int s = 0; s < src.count(); ++s) {
+            const unsigned ns = src.n(s);
+            for (unsigned i = t; i < ns; i += kThreads) {
+                const unsigned long long off = (unsigned long long)(src.key(s, i) - lo);
+                if (done_bits == 0 || (off >> (shift + bits)) == prefix)
+                    atomicAdd(&lh[(off >> shift) & (unsigned long long)(nbins - 1)], 1u);
+            }
         }
         __syncthreads();
         // each thread owns 2048 / kThreads consecutive bins

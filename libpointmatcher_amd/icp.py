@@ -66,6 +66,8 @@ def lib():
         l.pmx_icp_set_default.argtypes = [C.c_void_p]
         l.pmx_icp_load_yaml.argtypes = [C.c_void_p, C.c_char_p]
         l.pmx_icp_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        l.pmx_icp_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, _capi.ALLREDUCE_FN, _capi.ALLGATHER_FN,
+                                             C.c_void_p]
         l.pmx_icp_keep_trace.argtypes = [C.c_void_p, C.c_int]
         l.pmx_icp_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int64,
                                       C.c_void_p, C.c_void_p, C.c_void_p]
@@ -124,6 +126,11 @@ class ICP:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = (C.c_char * 128).from_buffer_copy(uid)
         self._chk(self._l.pmx_icp_comm_init(self.h, buf, nranks, rank))
+
+    def comm_init_host(self, comm):
+        """Multi-rank over a _capi.HostComm (e.g. _capi.gloo_host_comm())."""
+        self._comm = comm  # (the callbacks must outlive the ICP object)
+        self._chk(self._l.pmx_icp_comm_init_host(self.h, comm.nranks, comm.rank, comm.ar, comm.ag, None))
 
     def keep_trace(self, on=True):
         self._chk(self._l.pmx_icp_keep_trace(self.h, 1 if on else 0))

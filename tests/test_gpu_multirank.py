@@ -1,0 +1,254 @@
+"""The product's multi-rank path, executed: two ranks on the one MI355X.
+
+Each rank is its own process with its own pmx_ctx on device 0 and the
+reading's contiguous shard.  RCCL cannot put two ranks on one
+GPU, so the ranks exchange over the host-staged collectives of the C ABI
+(pmx_comm_init_host) with torch.distributed gloo as the transport: the same
+library code, kernels and exchange steps as the RCCL path — only the
+transport under coll_allreduce / coll_allgather differs.  The RCCL transport
+itself is exercised at one rank (a communicator issues every collective at
+any nranks) by test_rccl_one_rank_is_bit_identical.
+
+Bars (against the single-process oracle on the WHOLE reading):
+  * the TrimmedDist limit (radix select with histogram all-reduce) bit-equal;
+  * the point-to-plane system equal to fp64 reassociation (1e-12 relative);
+  * VarTrimmedDist (distance all-gather) kept count exact;
+  * whole ICPs through the host chain (device loop, quantile window exchanged
+    as all-gathered segments): final T within 1e-5 (f32) / 1e-12 (f64) with
+    equal iteration counts and kept pairs, every rank the same T;
+  * the sharded window resolves quantiles (hits > 0) and equals the radix
+    path (PMX_SPEC_SELECT=0) bit for bit.
+Reference semantics: OutlierFilter.cpp:63-103, Matches.cpp:60-87,
+OutlierFiltersImpl.cpp:132-223, PointToPlane.cpp:171-243, ICP.cpp:317-449.
+"""
+import multiprocessing as mp
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(__file__))
+from helpers import chain_yaml  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+DIFF = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
+TOL = {"float32": 1e-5, "float64": 1e-12}
+N_RD, N_REF = 60000, 50000
+VT = dict(minRatio=0.05, maxRatio=0.99, **{"lambda": 2.35})
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def shard_range(n, world, rank):
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def _clouds(dtype):
+    from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+
+    ref, nrm = reference_cloud(N_REF, dtype)
+    return reading_cloud(N_RD, dtype), ref, nrm
+
+
+P2PLANE, P2POINT = "PointToPlaneErrorMinimizer", "PointToPointErrorMinimizer"
+# whole-ICP cases: (tag, outlier filters, minimizer, Counter max, Differential, reference normals)
+ICP_RUNS = [
+    ("trim", (("TrimmedDistOutlierFilter", {"ratio": 0.85}),), P2PLANE, 30, DIFF, True),
+    ("vt", (("VarTrimmedDistOutlierFilter", VT),), P2PLANE, 20, DIFF, True),
+    ("med", (("MedianDistOutlierFilter", {"factor": 3.0}), ("MaxDistOutlierFilter", {"maxDist": 0.5})), P2PLANE,
+     20, None, True),
+    ("p2pt", (), P2POINT, 10, None, False),
+]
+
+
+def _worker(rank, world, port, outdir, env):
+    os.environ.update(env)
+    # torch first: its bundled HIP runtime is then the one libpmx binds to (bench.py)
+    import torch  # noqa: F401
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from libpointmatcher_amd import _capi
+        from libpointmatcher_amd.icp import ICP
+
+        comm = _capi.gloo_host_comm()
+        res = {}
+        for dn in ("float32", "float64"):
+            dtype = np.dtype(dn)
+            rd, ref, nrm = _clouds(dtype)
+            lo, hi = shard_range(rd.shape[0], world, rank)
+            shard = np.ascontiguousarray(rd[lo:hi])
+            I = np.eye(4, dtype=dtype)
+            # per-module calls through the C ABI
+            ctx = _capi.Context(0, dtype)
+            ctx.comm_init_host(comm)
+            assert ctx.comm_size() == (world, rank, 2)
+            ctx.set_reference(ref, nrm)
+            ctx.set_reading(shard)
+            ctx.match(I, knn=1)
+            ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
+            A, b, st = ctx.p2plane_system()
+            res[f"{dn}_trim"] = np.concatenate([A.ravel(), b, [st.limit, st.kept, st.n_total]])
+            ctx.match(I, knn=1)
+            ctx.outlier("VarTrimmedDistOutlierFilter", 0, **VT)
+            A, b, st = ctx.p2plane_system()
+            res[f"{dn}_vt"] = np.concatenate([A.ravel(), b, [st.limit, st.kept]])
+            # the device loop on the context: quantile window exchanged as segments
+            ctx.set_reading(shard)
+            ctx.loop_begin(filters=[("TrimmedDistOutlierFilter", 0.85)], checkers=[("CounterTransformationChecker", 25)])
+            ls = ctx.loop_run(25)
+            hits, misses = ctx.loop_select_stats()
+            res[f"{dn}_loop"] = np.concatenate([np.asarray(ls.T_iter[:16]), [ls.iterations, ls.last.kept, hits,
+                                                                              misses]])
+            ctx.close()
+            # whole ICPs through the host chain (pmx_icp_comm_init_host)
+            for tag, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
+                icp = ICP(dtype)
+                icp.comm_init_host(comm)
+                icp.load_yaml(chain_yaml(filters=filters, minimizer=minimizer, maxit=maxit, differential=diff))
+                T = icp.compute(shard, ref, nrm if with_n else None)
+                s = icp.stats()
+                res[f"{dn}_icp_{tag}"] = np.concatenate([T.astype(np.float64).ravel(), [s.iterations, s.kept]])
+                icp.close()
+        assert not comm.errors, comm.errors
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_two_ranks(tmp, env):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(i, 2, port, str(tmp), env)) for i in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(540)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert codes == [0, 0], codes
+    return [dict(np.load(tmp / f"rank{i}.npz")) for i in range(2)]
+
+
+@pytest.fixture(scope="module")
+def two_ranks(tmp_path_factory):
+    return _run_two_ranks(tmp_path_factory.mktemp("mr_gpu"), {})
+
+
+@pytest.fixture(scope="module")
+def two_ranks_radix(tmp_path_factory):
+    # the same runs with the quantile window off: every limit from the radix
+    # passes with their histogram all-reduce
+    return _run_two_ranks(tmp_path_factory.mktemp("mr_gpu_radix"), {"PMX_SPEC_SELECT": "0"})
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dn", ["float32", "float64"])
+def test_sharded_modules_vs_oracle(two_ranks, oracle, dn):
+    r = two_ranks
+    dtype = np.dtype(dn)
+    rd, ref, nrm = _clouds(dtype)
+    for key in (f"{dn}_trim", f"{dn}_vt"):
+        np.testing.assert_array_equal(r[0][key], r[1][key])  # every rank holds the same system and limit
+    d, ids, _ = oracle.knn(ref, rd, k=1)
+    # TrimmedDist: the global quantile, bit-equal
+    rc, q = oracle.quantile(d, 0.85)
+    assert rc == 0
+    got = r[0][f"{dn}_trim"]
+    assert dtype.type(got[-3]) == q
+    rc, w = oracle.outlier_chain([("TrimmedDistOutlierFilter", {"ratio": 0.85})], d)
+    rc, A, b, st = oracle.p2plane_system(rd, ref, nrm, d, ids, w)
+    assert int(got[-2]) == st.kept and int(got[-1]) == N_RD
+    full = np.concatenate([A.ravel(), b])
+    np.testing.assert_allclose(got[:42], full, rtol=1e-12, atol=1e-12 * np.abs(full).max())
+    # VarTrimmedDist: the distances all-gathered, the same optimised ratio
+    rc, w = oracle.outlier_chain([("VarTrimmedDistOutlierFilter", VT)], d)
+    assert rc == 0
+    assert int(r[0][f"{dn}_vt"][-1]) == int((w != 0).sum())
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dn", ["float32", "float64"])
+def test_sharded_icp_vs_oracle(two_ranks, oracle, dn):
+    r = two_ranks
+    dtype = np.dtype(dn)
+    rd, ref, nrm = _clouds(dtype)
+    from test_gpu_configs import THREADS
+
+    for tag, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
+        a, b2 = r[0][f"{dn}_icp_{tag}"], r[1][f"{dn}_icp_{tag}"]
+        np.testing.assert_array_equal(a, b2)  # every rank ends with the same transform
+        cfg = oracle.make_cfg(filters=filters, minimizer=minimizer, counter_max=maxit, differential=diff,
+                              threads=THREADS)
+        rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm if with_n else None)
+        assert rc == 0
+        T = a[:16].reshape(4, 4)
+        frob = np.linalg.norm(T - To.astype(np.float64))
+        print(f"{dn} {tag}: iterations {int(a[16])}/{so.iterations} kept {int(a[17])}/{so.kept} |dT|={frob:.3g}")
+        assert int(a[16]) == so.iterations
+        assert int(a[17]) == so.kept
+        assert frob <= TOL[dn]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dn", ["float32", "float64"])
+def test_sharded_window_equals_radix(two_ranks, two_ranks_radix, dn):
+    w, x = two_ranks[0][f"{dn}_loop"], two_ranks_radix[0][f"{dn}_loop"]
+    np.testing.assert_array_equal(two_ranks[0][f"{dn}_loop"], two_ranks[1][f"{dn}_loop"])
+    assert w[18] > 0, "the exchanged window never resolved a quantile"
+    assert x[18] == 0
+    np.testing.assert_array_equal(w[:18], x[:18])  # T_iter, iterations, kept: bit-identical
+    for k in [k for k in two_ranks[0] if "_icp_" in k]:
+        np.testing.assert_array_equal(two_ranks[0][k], two_ranks_radix[0][k])
+
+
+@pytest.mark.parametrize("dn", ["float32", "float64"])
+def test_rccl_one_rank_is_bit_identical(oracle, dn):
+    """A communicator issues every collective (RCCL all-reduce / all-gather of
+    the histograms, window segments, distances and systems) even at one rank;
+    the result must equal the unsharded run bit for bit."""
+    from libpointmatcher_amd import _capi
+
+    dtype = np.dtype(dn)
+    rd, ref, nrm = _clouds(dtype)
+    out = []
+    for comm in ("none", "rccl", "host"):
+        ctx = _capi.Context(0, dtype)
+        if comm == "rccl":
+            ctx.comm_init(_capi.Context.unique_id(), 1, 0)
+            assert ctx.comm_size() == (1, 0, 1)
+        elif comm == "host":
+            hc = _capi.HostComm(1, 0, lambda a, op: None, lambda a: a)
+            ctx.comm_init_host(hc)
+        ctx.set_reference(ref, nrm)
+        ctx.set_reading(rd)
+        ctx.match(np.eye(4, dtype=dtype), knn=1)
+        ctx.outlier("VarTrimmedDistOutlierFilter", 0, **VT)
+        A, b, st = ctx.p2plane_system()
+        ctx.loop_begin(filters=[("TrimmedDistOutlierFilter", 0.85)], checkers=[("CounterTransformationChecker", 20)])
+        ls = ctx.loop_run(20)
+        hits, _ = ctx.loop_select_stats()
+        out.append((A, b, st.kept, np.asarray(ls.T_iter[:16]), ls.last.kept, hits))
+        ctx.close()
+    for o in out[1:]:
+        np.testing.assert_array_equal(o[0], out[0][0])
+        np.testing.assert_array_equal(o[1], out[0][1])
+        assert o[2] == out[0][2] and o[4] == out[0][4]
+        np.testing.assert_array_equal(o[3], out[0][3])
+        assert o[5] > 0
