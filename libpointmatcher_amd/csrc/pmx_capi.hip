@@ -40,7 +40,7 @@ static_assert(kBlkIterErr + sizeof(int) <= kBlkRatio, "iteration block layout");
 // one resolution of the uniform grid over the reference (pmx_grid.hip)
 struct GridLevel {
     void* gpts = nullptr;        // P4<T>[valid] sorted by cell (x fastest)
-    void* gnrm = nullptr;        // normals in the same order
+    void* gpn = nullptr;         // point / normal records in the same order (point-to-plane gathers)
     int32_t* gidx = nullptr;     // original reference index of each position
     uint32_t* gstart = nullptr;  // first position of each cell, + end
     double lo[3] = {0, 0, 0};
@@ -48,9 +48,9 @@ struct GridLevel {
     int dim[3] = {1, 1, 1};
     double ppc = 0.0;
     void release() {
-        for (void* b : {gpts, gnrm, (void*)gidx, (void*)gstart})
+        for (void* b : {gpts, gpn, (void*)gidx, (void*)gstart})
             if (b) (void)hipFree(b);
-        gpts = gnrm = nullptr;
+        gpts = gpn = nullptr;
         gidx = nullptr;
         gstart = nullptr;
     }
@@ -147,6 +147,9 @@ struct pmx_ctx {
     int* d_iter_err = nullptr;
     uint32_t* d_hist = nullptr;
     unsigned int* d_ticket = nullptr;  // inside the d_hist allocation
+    void* d_selx = nullptr;            // select_all_kernel's arrivals / publications / per-pass bins
+    int64_t selx_grid = 0;             // its block count of the last launch (0: zeroed)
+    bool select_all = true;            // one launch for all radix passes (PMX_SELECT_ALL=0: one per pass)
     double* d_ratio = nullptr;
 
     // VarTrimmed scratch + cached pow table
@@ -192,6 +195,7 @@ struct pmx_ctx {
     void* d_spec_keys = nullptr;
     bool spec_allowed = true;
     bool spec_on = false;
+    bool fuse_final = true;       // loop: the minimiser's last finalize inside the step kernel (PMX_FUSE_FINAL=0: off)
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;
@@ -524,9 +528,9 @@ int build_grid(pmx_ctx* c, int64_t M) {
         if (hipMalloc(&L.gpts, sizeof(P4<T>) * np) != hipSuccess ||
             hipMalloc((void**)&L.gidx, sizeof(int32_t) * np) != hipSuccess ||
             hipMalloc((void**)&L.gstart, sizeof(uint32_t) * (size_t)(s.cells + 1)) != hipSuccess ||
-            (nrm && hipMalloc(&L.gnrm, sizeof(P4<T>) * np) != hipSuccess))
+            (nrm && hipMalloc(&L.gpn, 2 * sizeof(P4<T>) * np) != hipSuccess))
             return bad(fail(c, PMX_E_HIP, "grid level allocation failed"));
-        const int r = build_level_device<T>(pts, M, nrm, s, valid, c->setup, (P4<T>*)L.gpts, (P4<T>*)L.gnrm, L.gidx,
+        const int r = build_level_device<T>(pts, M, nrm, s, valid, c->setup, (P4<T>*)L.gpts, (P4<T>*)L.gpn, L.gidx,
                                             L.gstart, c->stream);
         if (r) return bad(fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")"));
         for (int a = 0; a < 3; ++a) {
@@ -543,7 +547,7 @@ int build_grid(pmx_ctx* c, int64_t M) {
         const GridLevel& L = c->levels[l];
         GridDesc<T>& D = tab[l];
         D.gpts = (const P4<T>*)L.gpts;
-        D.gnrm = (const P4<T>*)L.gnrm;
+        D.gpn = (const P4<T>*)L.gpn;
         D.gidx = L.gidx;
         D.start = L.gstart;
         for (int a = 0; a < 3; ++a) {
@@ -876,6 +880,15 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
             int rc = coll_allreduce(c, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), PMX_COLL_U32, PMX_COLL_SUM);
             if (rc) return rc;
             launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
+        } else if (c->select_all) {
+            // every pass in one launch (a no-op launch when the window resolved it)
+            const int64_t g = select_all_blocks(n);
+            if (g != c->selx_grid) {  // (the arrival generations assume a fixed block count)
+                HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
+                c->selx_grid = g;
+            }
+            launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
+            break;
         } else {
             launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, loop_ctl(c),
                                   spec, c->stream);
@@ -892,7 +905,13 @@ int check_match(pmx_ctx* c) {
 
 // the reference layout the current match ids index
 const void* match_ref(const pmx_ctx* c) { return c->ids_grid ? c->lv(c->ids_level).gpts : c->d_ref; }
-const void* match_nrm(const pmx_ctx* c) { return c->ids_grid ? c->lv(c->ids_level).gnrm : c->d_nrm; }
+// the point-to-plane gather: a grid level's interleaved records (stride 2)
+// or the reference and its normals (stride 1)
+const void* match_pn(const pmx_ctx* c) { return c->ids_grid ? c->lv(c->ids_level).gpn : c->d_ref; }
+const void* match_nrm(const pmx_ctx* c) {
+    return c->ids_grid ? (const void*)((const char*)c->lv(c->ids_level).gpn + (c->dtype == PMX_F64 ? 32 : 16)) : c->d_nrm;
+}
+int match_rs(const pmx_ctx* c) { return c->ids_grid ? 2 : 1; }
 
 // Adaptive grid level for the next match, from the pairs this match
 // evaluated per query and per point-per-cell (~ occupied cells visited):
@@ -1121,22 +1140,31 @@ void after_readback(pmx_ctx* c) {
     choose_level(c, v, f);
 }
 
-// the point-to-plane system into the iteration block (no host sync)
+// the point-to-plane system into the iteration block (no host sync);
+// *fuse_nv != 0 on entry: leave the finalize to the loop step (single rank),
+// which gets the value count back in *fuse_nv
 template <typename T>
-int p2plane_enqueue(pmx_ctx* c) {
+int p2plane_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
     const int NV = p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
-    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const P4<T>*)match_nrm(c),
-                              (const T*)c->d_dists, c->d_ids, chain_of<T>(c), c->knn, c->N, c->dim, c->d_partials,
+    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
+                              match_rs(c), (const T*)c->d_dists, c->d_ids, chain_of<T>(c), c->knn, c->N, c->dim, c->d_partials,
                               loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+    if (fuse_nv && *fuse_nv && !sharded(c)) {
+        *fuse_nv = NV;
+        HIPCHK(c, hipGetLastError());
+        return PMX_OK;
+    }
+    if (fuse_nv) *fuse_nv = 0;
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result, NV);
 }
 
-// the point-to-point sums, means and cross-covariance (no host sync)
+// the point-to-point sums, means and cross-covariance (no host sync);
+// fuse_nv: as p2plane_enqueue (the second pass's finalize)
 template <typename T>
-int p2point_enqueue(pmx_ctx* c) {
+int p2point_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
     Mat4<T> Tm = step_mat<T>(c);
     const WChain<T> chain = chain_of<T>(c);
     const GridDesc<T>* gd = (const GridDesc<T>*)c->d_gdesc;
@@ -1148,6 +1176,12 @@ int p2point_enqueue(pmx_ctx* c) {
     launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, loop_ctl(c), c->stream);
     launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
                             chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, loop_ctl(c), gd, c->stream);
+    if (fuse_nv && *fuse_nv && !sharded(c)) {
+        *fuse_nv = 9;
+        HIPCHK(c, hipGetLastError());
+        return PMX_OK;
+    }
+    if (fuse_nv) *fuse_nv = 0;
     launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result + 16, 9);
@@ -1170,6 +1204,7 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     // 0/1 weights: sum of kept weights == kept count
     fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 0], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
+    if (ierr == kSelTimeout) return fail(c, PMX_E_HIP, "radix select: device wait timed out");
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[o + 1] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
     if (r[o + 0] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
@@ -1192,6 +1227,7 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
     const int ierr = host_iter_err(c);
     fill_stats(c, st, r[7], r[8], r[9], r[10], r[0], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
+    if (ierr == kSelTimeout) return fail(c, PMX_E_HIP, "radix select: device wait timed out");
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[8] == 0.0 || r[7] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
     T means[6];
@@ -1271,6 +1307,7 @@ template <typename T>
 LoopFlag* loop_flags(const pmx_ctx* c) {
     return (LoopFlag*)((char*)c->h_loop + ((sizeof(LoopState<T>) + 63) & ~(size_t)63));
 }
+
 
 template <typename T>
 int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
@@ -1400,9 +1437,12 @@ int loop_enqueue_iteration(pmx_ctx* c) {
         const double* p = cfg.filter_p[i];
         if ((rc = outlier_impl<T>(c, cfg.filter_kind[i], i, p[0], p[1], p[2]))) return rc;
     }
-    if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c))) return rc;
+    int fuse = c->fuse_final ? 1 : 0;  // (the last finalize into the step kernel; 0 back when not fused)
+    if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c, &fuse) : p2point_enqueue<T>(c, &fuse))) return rc;
+    double* fused_out = cfg.minimizer == 0 ? c->d_result : c->d_result + 16;
     launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
-                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, c->stream);
+                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr,
+                        fuse ? c->d_partials : nullptr, kRedBlocks, fuse, fused_out, c->stream);
     HIPCHK(c, hipGetLastError());
     return PMX_OK;
 }
@@ -1472,6 +1512,9 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
         } else if (e == PMX_E_EMPTY_QUANTILE) {
             err = PMX_E_EMPTY_QUANTILE;
             msg = "no outlier to filter";
+        } else if (e == kSelTimeout) {
+            err = PMX_E_HIP;
+            msg = "radix select: a block waited too long for the pass before (device timeout)";
         } else if (e == kLoopNotRigid) {
             err = PMX_E_TRANSFORMATION;
             msg = "RigidTransformation: Error, rotation matrix is not orthogonal.";
@@ -1667,6 +1710,8 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     c->no_visits = std::getenv("PMX_NO_VISITS") != nullptr;
     c->select_split = std::getenv("PMX_SELECT_SPLIT") != nullptr;
     if (const char* e = std::getenv("PMX_SPEC_SELECT")) c->spec_allowed = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_FUSE_FINAL")) c->fuse_final = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_SELECT_ALL")) c->select_all = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
     if (const char* e = std::getenv("PMX_GRID_LEVELS")) {
@@ -1732,6 +1777,8 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (hipMalloc((void**)&c->d_hist, (2048 + 64) * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_hist, 0, (2048 + 64) * sizeof(uint32_t));
     c->d_ticket = c->d_hist + 2048;
+    if (hipMalloc(&c->d_selx, selx_bytes()) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_selx, 0, selx_bytes());
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
     if (hipHostMalloc((void**)&c->h_result, kBlkBytes, hipHostMallocDefault) != hipSuccess) return bad(PMX_E_HIP);
     // the device loop's control word (done = 0: kernels given it run normally)
@@ -1749,7 +1796,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace,
-                    c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ};
+                    c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();

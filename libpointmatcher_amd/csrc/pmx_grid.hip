@@ -503,7 +503,7 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
     src.local = (const typename KeyOf<T>::K*)spec->keys;
     const unsigned nk_raw = spec->n_keys;
     src.n_local = nk_raw < kSpecCap ? nk_raw : kSpecCap;
-    spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part, bc);
+    (void)spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part, bc);
 }
 
 template <typename T>

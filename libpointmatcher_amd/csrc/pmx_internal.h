@@ -115,7 +115,7 @@ struct GridGeom {
 template <typename T>
 struct GridDesc {
     const P4<T>* gpts;
-    const P4<T>* gnrm;
+    const P4<T>* gpn;  // point, normal interleaved (2 P4 per position; null without normals)
     const int32_t* gidx;
     const uint32_t* start;
     GridGeom G;
@@ -196,7 +196,7 @@ void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, uint32_t* 
                       hipStream_t st);
 template <typename T>
 int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const SetupShape& s, int64_t valid,
-                       const SetupScratch& sc, P4<T>* gp, P4<T>* gn, int32_t* gi, uint32_t* gstart, hipStream_t st);
+                       const SetupScratch& sc, P4<T>* gp, P4<T>* gpn, int32_t* gi, uint32_t* gstart, hipStream_t st);
 template <typename T>
 int reading_order_device(const P4<T>* raw, int64_t n, const Mat4<T>& M0, const SetupShape& s, bool morton,
                          const SetupScratch& sc, P4<T>* sorted, hipStream_t st);
@@ -291,6 +291,15 @@ void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, 
                         SpecSel* spec, hipStream_t s);
 template <typename T>
 int select_passes();
+// every pass in one launch (single rank; pmx_select.hip select_all_kernel):
+// selx = selx_bytes() of zeroed device memory per context, re-zeroed whenever
+// the launch's block count changes (select_all_blocks)
+size_t selx_bytes();
+int64_t select_all_blocks(int64_t n);
+constexpr int kSelTimeout = -30;  // iteration error: a select_all wait timed out
+template <typename T>
+void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
+                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s);
 int select_bins(int pass, int key_bits);
 
 // VarTrimmed pieces
@@ -312,8 +321,10 @@ constexpr int kNVMax = 48;
 constexpr int p2plane_nv(int dim) { return dim == 3 ? 21 + 6 + 4 : 6 + 3 + 4; }
 // ctl / gd (device loop, may be null): early exit, step transform and the
 // grid level whose positions the ids are (ref / nrm then come from gd)
+// rs: index stride of ref / nrm (1: separate arrays; 2: a grid level's
+// interleaved point / normal records, ref = gpn, nrm = gpn + 1)
 template <typename T>
-void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm,
+void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s);

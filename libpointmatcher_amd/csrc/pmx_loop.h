@@ -66,9 +66,11 @@ struct LoopState {
 template <typename T>
 void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int prev_level,
                       const double* Tprev, hipStream_t s);
+// partials (may be null): the minimiser's last finalize fused into the step
+// (nblocks x nv block partials, summed into res_out in finalize's order)
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
-                      hipStream_t s);
+                      const double* partials, int nblocks, int nv, double* res_out, hipStream_t s);
 
 }  // namespace pmx

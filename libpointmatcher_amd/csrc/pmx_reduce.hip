@@ -88,7 +88,8 @@ __device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz,
 template <typename T, int DIM>
 __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
                                                               const P4<T>* __restrict__ ref,
-                                                              const P4<T>* __restrict__ nrm, const T* __restrict__ d,
+                                                              const P4<T>* __restrict__ nrm, int rs,
+                                                              const T* __restrict__ d,
                                                               const int32_t* __restrict__ ids, WChain<T> chain,
                                                               int k, int64_t N, double* __restrict__ partials,
                                                               const LoopCtl* __restrict__ ctl,
@@ -99,8 +100,9 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
     if (ctl) {  // device loop
         if (ctl->done) return;
         ctl_transform(ctl, Tm);
-        ref = gd[ctl->level].gpts;
-        nrm = gd[ctl->level].gnrm;
+        ref = gd[ctl->level].gpn;
+        nrm = ref + 1;
+        rs = 2;
     }
     double acc[NV];
 #pragma unroll
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 kp[u] = i0 + u * stride < N && dv[u] != inf && chain_keep(wr, dv[u]);
-                const int32_t g = kp[u] ? id[u] : 0;  // (position 0 always exists)
+                const int64_t g = (int64_t)(kp[u] ? id[u] : 0) * rs;  // (position 0 always exists)
                 q[u] = gld(ref, g);
                 n[u] = gld(nrm, g);
             }
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
             exist = true;
             acc[NS + NF + 0] += 1.0;  // kept (= sum of the 0/1 weights)
             const int32_t id = ids[e];
-            p2plane_add<T, DIM, NV>(acc, px, py, pz, gld(ref, id), gld(nrm, id));
+            p2plane_add<T, DIM, NV>(acc, px, py, pz, gld(ref, (int64_t)id * rs), gld(nrm, (int64_t)id * rs));
         }
         if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
     }
@@ -176,15 +178,15 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
 }
 
 template <typename T>
-void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, const T* d,
-                            const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim, double* partials,
-                            const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
+void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
+                            const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
+                            double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
     if (dim == 3)
-        hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
-                           ids, chain, k, N, partials, ctl, gd);
+        hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
+                           d, ids, chain, k, N, partials, ctl, gd);
     else
-        hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, d,
-                           ids, chain, k, N, partials, ctl, gd);
+        hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
+                           d, ids, chain, k, N, partials, ctl, gd);
 }
 
 // Sum the per-block partials: one block per accumulator, each thread adds a
@@ -359,7 +361,7 @@ void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, h
 }
 
 #define PMX_INST(T)                                                                                                  \
-    template void launch_p2plane_partial<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const P4<T>*, const T*,      \
+    template void launch_p2plane_partial<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const P4<T>*, int, const T*, \
                                             const int32_t*, const WChain<T>&, int, int64_t, int, double*,           \
                                             const LoopCtl*, const GridDesc<T>*, hipStream_t);                        \
     template void launch_p2point_pass1<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \

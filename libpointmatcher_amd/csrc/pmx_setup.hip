@@ -198,16 +198,23 @@ __global__ void cell_keys_kernel(const P4<T>* __restrict__ p, int64_t n, SetupSh
     idx[i] = (int32_t)i;
 }
 
+// gpn: the point-to-plane reduction's gather records, point and normal side
+// by side (one 32 / 64-byte record per position instead of two gathers from
+// two arrays)
 template <typename T>
 __global__ void grid_gather_kernel(const P4<T>* __restrict__ p, const P4<T>* __restrict__ nrm,
                                    const int32_t* __restrict__ sidx, int64_t valid, P4<T>* __restrict__ gp,
-                                   P4<T>* __restrict__ gn, int32_t* __restrict__ gi) {
+                                   P4<T>* __restrict__ gpn, int32_t* __restrict__ gi) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= valid) return;
     const int32_t j = sidx[i];
-    gp[i] = p[j];
+    const P4<T> q = p[j];
+    gp[i] = q;
     gi[i] = j;
-    if (gn) gn[i] = nrm[j];
+    if (gpn) {
+        gpn[2 * i] = q;
+        gpn[2 * i + 1] = nrm[j];
+    }
 }
 
 static int bits_for(uint64_t v) {
@@ -233,7 +240,7 @@ static size_t scan_temp_bytes(int64_t n) {
 // one grid level (sizes from the host): the layout of pmx_grid.hip
 template <typename T>
 int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const SetupShape& s, int64_t valid,
-                       const SetupScratch& sc, P4<T>* gp, P4<T>* gn, int32_t* gi, uint32_t* gstart, hipStream_t st) {
+                       const SetupScratch& sc, P4<T>* gp, P4<T>* gpn, int32_t* gi, uint32_t* gstart, hipStream_t st) {
     const int64_t C = s.cells;
     hipError_t e = hipMemsetAsync(sc.counts, 0, sizeof(uint32_t) * (size_t)(C + 1), st);
     if (e != hipSuccess) return -1;
@@ -250,7 +257,7 @@ int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const Setu
     if (e != hipSuccess) return -3;
     if (valid > 0)
         hipLaunchKernelGGL(grid_gather_kernel<T>, dim3(blocks_for(valid)), dim3(256), 0, st, pts, nrm, sc.idx_out,
-                           valid, gp, gn, gi);
+                           valid, gp, gpn, gi);
     return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 

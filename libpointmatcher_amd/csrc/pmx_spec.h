@@ -51,6 +51,23 @@ struct KeyOf<double> {
 
 constexpr unsigned kSpecCap = 16384;  // appended keys per iteration
 
+// radix-select digit layout (pmx_select.hip): 11-bit digits from the top,
+// the last one(s) 10-bit
+// f32: [31:21] [20:10] [9:0]          f64: [63:53] [52:42] [41:31] [30:20] [19:10] [9:0]
+__host__ __device__ inline void digit_of(int key_bits, int pass, int& shift, int& bits) {
+    if (key_bits == 32) {
+        const int sh[3] = {21, 10, 0};
+        const int bt[3] = {11, 11, 10};
+        shift = sh[pass];
+        bits = bt[pass];
+    } else {
+        const int sh[6] = {53, 42, 31, 20, 10, 0};
+        const int bt[6] = {11, 11, 11, 11, 10, 10};
+        shift = sh[pass];
+        bits = bt[pass];
+    }
+}
+
 struct SpecSel {
     unsigned long long lo, hi;  // key window (inclusive); valid != 0
     unsigned long long prev;    // last resolved limit key
@@ -183,7 +200,7 @@ struct SpecKeys {
 // they are.  Writes st (as the radix select's last pass would) and sp->hit;
 // resets the append counter.  Block of kThreads.
 template <typename T, int kThreads>
-__device__ __forceinline__ void spec_pick(SpecSel* __restrict__ sp, SelectState* __restrict__ st,
+__device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState* __restrict__ st,
                                           unsigned long long fin, unsigned long long below,
                                           unsigned long long nk_raw, bool overflow, const SpecKeys<T>& src,
                                           uint32_t* lh, unsigned long long* part, unsigned long long* bc) {
@@ -214,7 +231,7 @@ __device__ __forceinline__ void spec_pick(SpecSel* __restrict__ sp, SelectState*
             sp->n_miss += 1;
             sp->n_keys = 0;
         }
-        return;
+        return false;
     }
     unsigned long long r = rank - below;
     // radix select over offsets (key - lo) < 2^nb, 11-bit digits from the top
@@ -282,6 +299,7 @@ __device__ __forceinline__ void spec_pick(SpecSel* __restrict__ sp, SelectState*
         const double width = (double)(hi - lo) + 1.0;
         spec_update<T>(sp, kl, (double)nk / width);
     }
+    return true;
 }
 
 }  // namespace pmx

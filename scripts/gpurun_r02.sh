@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 GPU session: the GPU test suite, the driver's bench command, its
 # kernel trace and its HBM traffic (FETCH_SIZE / WRITE_SIZE, separate
-# rocprofv3 --pmc passes).  Usage: scripts/gpurun_r02.sh [tests|bench|prof|all]
+# rocprofv3 --pmc passes).  Usage: scripts/gpurun_r02.sh [tests|bench|trace|prof|all]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
@@ -21,9 +21,11 @@ fi
 if [ "$what" = bench ] || [ "$what" = all ] || [ "$what" = prof ]; then
   step bench && timeout -k 10 600 "${CMD[@]}" > gpurun_out/bench_driver.json 2> gpurun_out/bench_driver.err || exit $?
 fi
-if [ "$what" = prof ] || [ "$what" = all ]; then
+if [ "$what" = prof ] || [ "$what" = all ] || [ "$what" = trace ]; then
   step trace && (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run \
       --output-format csv -- "${CMD[@]}" > "$R/gpurun_out/prof.log" 2>&1) || exit $?
+fi
+if [ "$what" = prof ] || [ "$what" = all ]; then
   step fetch && (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/pmc_fetch" -o run \
       --output-format csv -- "${CMD[@]}" > "$R/gpurun_out/pmc_fetch.log" 2>&1) || exit $?
   step write && (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/pmc_write" -o run \

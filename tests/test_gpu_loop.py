@@ -203,3 +203,42 @@ def test_quantile_window_is_exact(monkeypatch, dtype, filt, knn, max_dist):
     assert hits + misses == 30 and hits >= 15, (hits, misses)
     assert kept1 == kept0
     assert np.array_equal(tr1, tr0)
+
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("filt,knn,max_dist", [
+    (("TrimmedDistOutlierFilter", 0.85), 1, np.inf),
+    (("TrimmedDistOutlierFilter", 0.7), 3, 0.05),
+    (("MedianDistOutlierFilter", 3.0), 1, np.inf),
+    (("TrimmedDistOutlierFilter", 1.0), 2, np.inf),
+    (("VarTrimmedDistOutlierFilter", 0.05, 0.99, 2.35), 1, np.inf),
+])
+@pytest.mark.parametrize("window", ["0", "1"])
+def test_select_all_passes_in_one_launch(monkeypatch, dtype, filt, knn, max_dist, window):
+    """The radix select with every pass in one launch (select_all_kernel:
+    in-kernel arrival counters, the last block of each pass picks the digit
+    and publishes it) gives the per-pass kernels' limits bit for bit: whole
+    loops are identical, with and without the quantile window (a window hit
+    makes the launch a no-op), for f32 (3 digits) and f64 (6 digits)."""
+    monkeypatch.setenv("PMX_SPEC_SELECT", window)
+    ref, nrm = reference_cloud(60000, dtype)
+    rd = reading_cloud(50000, dtype)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PMX_SELECT_ALL", mode)
+        ctx = _capi.Context(0, dtype)
+        ctx.set_reference(ref, nrm)
+        ctx.set_reading(rd)
+        ctx.loop_begin(knn=knn, max_dist=max_dist, filters=[filt], checkers=[("CounterTransformationChecker", 30)],
+                       keep_trace=True)
+        st = ctx.loop_run(30)
+        out[mode] = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept, st.iterations,
+                     st.last.limit)
+        ctx.close()
+    tr1, s1, kept1, it1, lim1 = out["1"]
+    tr0, s0, kept0, it0, lim0 = out["0"]
+    assert it1 == it0 == 30
+    assert s1 == s0
+    assert kept1 == kept0 and lim1 == lim0
+    assert np.array_equal(tr1, tr0)
