@@ -195,7 +195,10 @@ struct pmx_ctx {
     void* d_spec_keys = nullptr;
     bool spec_allowed = true;
     bool spec_on = false;
-    bool fuse_final = true;       // loop: the minimiser's last finalize inside the step kernel (PMX_FUSE_FINAL=0: off)
+    // loop: the minimiser's last finalize inside the step kernel (PMX_FUSE_FINAL=1).  Off: measured on
+    // MI355X (C3 driver command) 0.0821 ms/step unfused vs 0.0910 fused — the 256-thread step launch
+    // costs more than the finalize kernel and its boundary it saves
+    bool fuse_final = false;
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;

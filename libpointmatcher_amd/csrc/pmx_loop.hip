@@ -114,8 +114,8 @@ __device__ void fused_finalize_n(const double* __restrict__ partials, int nblock
         double x0[NVC], x1[NVC];
 #pragma unroll
         for (int v = 0; v < NVC; ++v) {
-            x0[v] = partials[(int64_t)b * NVC + v];
-            x1[v] = partials[(int64_t)(b + 256) * NVC + v];
+            x0[v] = partials[(int64_t)v * nblocks + b];
+            x1[v] = partials[(int64_t)v * nblocks + b + 256];
         }
 #pragma unroll
         for (int v = 0; v < NVC; ++v) {
@@ -125,7 +125,7 @@ __device__ void fused_finalize_n(const double* __restrict__ partials, int nblock
     }
     for (; b < nblocks; b += 256) {
 #pragma unroll
-        for (int v = 0; v < NVC; ++v) s[v] += partials[(int64_t)b * NVC + v];
+        for (int v = 0; v < NVC; ++v) s[v] += partials[(int64_t)v * nblocks + b];
     }
 #pragma unroll
     for (int v = 0; v < NVC; ++v) {

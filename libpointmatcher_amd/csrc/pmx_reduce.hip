@@ -36,7 +36,8 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// block reduction of NV accumulators; writes partials[blockIdx.x * NV + v]
+// block reduction of NV accumulators; writes partials[v * gridDim.x + blockIdx.x]
+// (value-major: the finalize reads each value's block partials contiguously)
 template <int NV>
 __device__ __forceinline__ void block_store(double (&acc)[NV], double* __restrict__ partials) {
     __shared__ double red[4][NV];
@@ -49,7 +50,7 @@ __device__ __forceinline__ void block_store(double (&acc)[NV], double* __restric
     }
     __syncthreads();
     for (int v = threadIdx.x; v < NV; v += blockDim.x)
-        partials[(int64_t)blockIdx.x * NV + v] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+        partials[(int64_t)v * gridDim.x + blockIdx.x] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
 }
 
 // one kept pair: F and dot in T exactly as PointToPlane.cpp:171-243, the
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict_
     if (ctl && ctl->done) return;
     const int v = blockIdx.x;
     double s = 0.0;
-    for (int b = threadIdx.x; b < nblocks; b += 256) s += partials[(int64_t)b * nv + v];
+    for (int b = threadIdx.x; b < nblocks; b += 256) s += partials[(int64_t)v * nblocks + b];
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
