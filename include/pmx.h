@@ -261,6 +261,29 @@ int pmx_surface_normals(int device, int dtype, const void* feat, int rows, int64
                         unsigned flags, void* normals, void* densities, void* eig_values, void* eig_vectors,
                         void* matched_ids, void* mean_dists, int64_t* degenerate);
 
+/* SamplingSurfaceNormalDataPointsFilter::inPlaceFilter
+ * (DataPointsFilters/SamplingSurfaceNormal.cpp:80-342) on the GPU: the
+ * recursive median split (buildNew) level by level over all boxes, the leaf
+ * statistics (fuseRange) one thread per leaf; the sampling (samplingMethod 0:
+ * rand() < ratio per point of every fitted leaf, the process's rand() state;
+ * 1: the leaf's mean) and the output assembly on the host.  Standalone (a
+ * temporary context on `device`); pmx_last_error(NULL) on failure.
+ * Deterministic where the reference is implementation-defined: ties of the
+ * median split broken by point index, a leaf's points in index order.
+ *   feat: rows x n point-major T; desc: desc_dim x n point-major T (may be
+ *   NULL when desc_dim = 0) — averaged per leaf with PMX_SSN_AVERAGE and
+ *   samplingMethod 1, else the kept point's own
+ *   outputs (point-major, sized for n points, each may be NULL): feat_out
+ *   rows x n_out, desc_out desc_dim x n_out, normals D x n_out, densities
+ *   n_out, eig_values D x n_out (ascending), eig_vectors D*D x n_out
+ *   (serializeEigVec, row-major); unfit: points of dropped leaves. */
+enum { PMX_SSN_NORMALS = 1, PMX_SSN_DENSITIES = 2, PMX_SSN_EIGVALUES = 4, PMX_SSN_EIGVECTORS = 8,
+       PMX_SSN_AVERAGE = 16 };
+int pmx_sampling_surface_normals(int device, int dtype, const void* feat, int rows, int64_t n, const void* desc,
+                                 int desc_dim, int knn, int sampling_method, double ratio, double max_box_dim,
+                                 unsigned flags, void* feat_out, void* desc_out, void* normals, void* densities,
+                                 void* eig_values, void* eig_vectors, int64_t* n_out, int64_t* unfit);
+
 #ifdef __cplusplus
 }
 #endif

@@ -148,6 +148,7 @@ EXPORTS = [
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
     "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_surface_normals",
+    "pmx_sampling_surface_normals",
 ]
 
 
@@ -192,6 +193,9 @@ def lib():
         l.pmx_loop_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         l.pmx_surface_normals.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_double,
                                           C.c_uint] + [C.c_void_p] * 6 + [C.POINTER(C.c_int64)]
+        l.pmx_sampling_surface_normals.argtypes = ([C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
+                                                    C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_uint]
+                                                   + [C.c_void_p] * 6 + [C.POINTER(C.c_int64)] * 2)
         _lib = l
     return _lib
 
@@ -228,6 +232,43 @@ def surface_normals(points, knn=5, max_dist=np.inf, smooth=False, device=0):
         raise_for(rc, l.pmx_last_error(None).decode())
     out["degenerate"] = deg.value
     return out
+
+
+SSN_NORMALS, SSN_DENSITIES, SSN_EIGVALUES, SSN_EIGVECTORS, SSN_AVERAGE = 1, 2, 4, 8, 16
+
+
+def sampling_surface_normals(points, descriptors=None, knn=7, sampling_method=0, ratio=0.5, max_box_dim=np.inf,
+                             flags=SSN_NORMALS | SSN_AVERAGE, device=0):
+    """SamplingSurfaceNormalDataPointsFilter (DataPointsFilters/SamplingSurfaceNormal.cpp:80-342)
+    on the GPU (pmx_sampling_surface_normals).  points (n, rows) with the
+    homogeneous row last; descriptors (n, desc_dim) or None.  Returns the kept
+    points' features, descriptors, normals, densities, eig_values,
+    eig_vectors (point-major) and the unfit count."""
+    pts = np.ascontiguousarray(points)
+    if pts.dtype not in (np.float32, np.float64):
+        pts = pts.astype(np.float32)
+    dt = pts.dtype
+    n, rows = pts.shape
+    D = rows - 1
+    dd = 0 if descriptors is None else descriptors.shape[1]
+    desc = None if descriptors is None else np.ascontiguousarray(descriptors, dtype=dt)
+    out = {"features": np.empty((n, rows), dt), "descriptors": np.empty((n, dd), dt),
+           "normals": np.empty((n, D), dt), "densities": np.empty(n, dt), "eig_values": np.empty((n, D), dt),
+           "eig_vectors": np.empty((n, D * D), dt)}
+    no, unfit = C.c_int64(0), C.c_int64(0)
+    l = lib()
+    rc = l.pmx_sampling_surface_normals(int(device), PMX_F64 if dt == np.float64 else PMX_F32, _ptr(pts), rows, n,
+                                        _ptr(desc), dd, int(knn), int(sampling_method), float(ratio),
+                                        float(max_box_dim), int(flags), _ptr(out["features"]),
+                                        _ptr(out["descriptors"]) if dd else None, _ptr(out["normals"]),
+                                        _ptr(out["densities"]), _ptr(out["eig_values"]), _ptr(out["eig_vectors"]),
+                                        C.byref(no), C.byref(unfit))
+    if rc != PMX_OK:
+        raise_for(rc, l.pmx_last_error(None).decode())
+    m = no.value
+    res = {k: v[:m] for k, v in out.items()}
+    res["unfit"] = unfit.value
+    return res
 
 
 def _ptr(a):

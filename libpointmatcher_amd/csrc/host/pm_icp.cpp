@@ -776,39 +776,92 @@ struct FixStepSamplingDPF : PM<T>::DataPointsFilter {
     bool usesRandState() const override { return true; }
 };
 
-// Reference data filters that are outside the hot path:
-// registered with the reference's parameter docs so chain files validate
-// exactly as in the reference (bounds, unused parameters, module types), but
-// applying one throws — they never run silently.
+// SamplingSurfaceNormalDataPointsFilter (DataPointsFilters/SamplingSurfaceNormal.cpp:80-342,
+// parameters SamplingSurfaceNormal.h:64-79): the recursive median split and
+// the leaf statistics on the GPU, the sampling on the process's rand() state
+// (pmx_sampling_surface_normals, pmx_ssn.hip); existing descriptors averaged
+// per leaf (samplingMethod 1) or kept, the new ones in the reference's label
+// order.
 template <typename T>
-struct UnsupportedDPF : PM<T>::DataPointsFilter {
-    UnsupportedDPF(const std::string& name, const Parametrizable::ParametersDoc& d, const Parametrizable::Parameters& p)
-        : PM<T>::DataPointsFilter(name, d, p) {
-        for (auto& pd : d) this->getParamValueString(pd.name);
+struct SamplingSurfaceNormalDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("ratio", "ratio of points to keep with random subsampling. Matrix (normal, density, etc.) will be "
+                              "associated to all points in the same bin.",
+                     "0.5", "0.0000001", "1.0", &P::Comp<T>),
+                PDoc("knn", "determined how many points are used to compute the normals. Direct link with the "
+                            "rapidity of the computation (large = fast). Technically, limit over which a box is "
+                            "splitted in two",
+                     "7", "3", "2147483647", &P::Comp<unsigned>),
+                PDoc("samplingMethod", "if set to 0, random subsampling using the parameter ratio. If set to 1, bin "
+                                       "subsampling with the resulting number of points being 1/knn.",
+                     "0", "0", "1", &P::Comp<unsigned>),
+                PDoc("maxBoxDim", "maximum length of a box above which the box is discarded", "inf"),
+                PDoc("averageExistingDescriptors",
+                     "whether the filter keep the existing point descriptors and average them or should it drop them",
+                     "1"),
+                PDoc("keepNormals", "whether the normals should be added as descriptors to the resulting cloud", "1"),
+                PDoc("keepDensities", "whether the point densities should be added as descriptors to the resulting cloud",
+                     "0"),
+                PDoc("keepEigenValues", "whether the eigen values should be added as descriptors to the resulting cloud",
+                     "0"),
+                PDoc("keepEigenVectors",
+                     "whether the eigen vectors should be added as descriptors to the resulting cloud", "0")};
     }
-    void inPlaceFilter(DataPoints<T>&) override {
-        throw ConfigurationError(this->className +
-                                 " is outside the MI355X ICP path; pre-filter the clouds (and provide reference "
-                                 "normals) before calling ICP");
+    T ratio;
+    unsigned knn, samplingMethod;
+    T maxBoxDim;
+    bool averageExistingDescriptors, keepNormals, keepDensities, keepEigenValues, keepEigenVectors;
+    explicit SamplingSurfaceNormalDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter("SamplingSurfaceNormalDataPointsFilter", doc(), p),
+          ratio(this->template get<T>("ratio")),
+          knn(this->template get<unsigned>("knn")),
+          samplingMethod(this->template get<unsigned>("samplingMethod")),
+          maxBoxDim(this->template get<T>("maxBoxDim")),
+          averageExistingDescriptors(this->template get<bool>("averageExistingDescriptors")),
+          keepNormals(this->template get<bool>("keepNormals")),
+          keepDensities(this->template get<bool>("keepDensities")),
+          keepEigenValues(this->template get<bool>("keepEigenValues")),
+          keepEigenVectors(this->template get<bool>("keepEigenVectors")) {}
+    bool usesRandState() const override { return samplingMethod == 0; }
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        const int D = cloud.rows - 1;
+        const int64_t n = cloud.n;
+        if (averageExistingDescriptors) {  // (:93-101)
+            int sum = 0;
+            for (auto& l : cloud.descriptorLabels) sum += l.span;
+            if (sum != cloud.descDim)
+                throw InvalidParameter("SamplingSurfaceNormalDataPointsFilter: Error, descriptor labels do not match "
+                                       "descriptor data");
+        }
+        std::vector<T> feat((size_t)(n * cloud.rows)), desc((size_t)(n * cloud.descDim)), nrm, dens, eva, eve;
+        if (keepNormals) nrm.resize((size_t)(n * D));
+        if (keepDensities) dens.resize((size_t)n);
+        if (keepEigenValues) eva.resize((size_t)(n * D));
+        if (keepEigenVectors) eve.resize((size_t)(n * D * D));
+        auto ptr = [](std::vector<T>& v) { return v.empty() ? nullptr : (void*)v.data(); };
+        unsigned flags = (keepNormals ? PMX_SSN_NORMALS : 0u) | (keepDensities ? PMX_SSN_DENSITIES : 0u) |
+                         (keepEigenValues ? PMX_SSN_EIGVALUES : 0u) | (keepEigenVectors ? PMX_SSN_EIGVECTORS : 0u) |
+                         (averageExistingDescriptors ? PMX_SSN_AVERAGE : 0u);
+        int64_t nout = 0, unfit = 0;
+        const int rc = pmx_sampling_surface_normals(
+            this->device, dtype_of<T>(), cloud.features.data(), cloud.rows, n,
+            cloud.descDim ? cloud.descriptors.data() : nullptr, cloud.descDim,
+            (int)std::min<unsigned>(knn, 0x7fffffffu), (int)samplingMethod, (double)ratio, (double)maxBoxDim, flags,
+            feat.data(), ptr(desc), ptr(nrm), ptr(dens), ptr(eva), ptr(eve), &nout, &unfit);
+        if (rc == PMX_E_BAD_PARAM) throw InvalidParameter(pmx_last_error(nullptr));
+        if (rc) throw std::runtime_error(std::string("SamplingSurfaceNormalDataPointsFilter: ") + pmx_last_error(nullptr));
+        cloud.n = nout;
+        feat.resize((size_t)(nout * cloud.rows));
+        cloud.features.swap(feat);
+        desc.resize((size_t)(nout * cloud.descDim));
+        cloud.descriptors.swap(desc);
+        if (keepNormals) cloud.setDescriptor("normals", D, nrm.data());
+        if (keepDensities) cloud.setDescriptor("densities", 1, dens.data());
+        if (keepEigenValues) cloud.setDescriptor("eigValues", D, eva.data());
+        if (keepEigenVectors) cloud.setDescriptor("eigVectors", D * D, eve.data());
     }
 };
-
-template <typename T>
-void register_unsupported_filters(Registrar<typename PM<T>::DataPointsFilter>& R) {
-    typedef Parametrizable::Parameters Ps;
-    typedef Parametrizable P;
-    auto add = [&](const std::string& name, Parametrizable::ParametersDoc d) {
-        R.reg(name, [name, d](const Ps& p) { return std::make_shared<UnsupportedDPF<T>>(name, d, p); }, true);
-    };
-    add("SamplingSurfaceNormalDataPointsFilter",
-        {PDoc("ratio", "ratio of points to keep with random subsampling", "0.5", "0.0000001", "1.0", &P::Comp<T>),
-         PDoc("knn", "how many points are used to compute the normals", "7", "3", "2147483647", &P::Comp<unsigned>),
-         PDoc("samplingMethod", "0: random subsampling, 1: bin subsampling", "0", "0", "1", &P::Comp<unsigned>),
-         PDoc("maxBoxDim", "maximum length of a box above which the box is discarded", "inf"),
-         PDoc("averageExistingDescriptors", "keep and average existing descriptors", "1"),
-         PDoc("keepNormals", "add normals as descriptors", "1"), PDoc("keepDensities", "add densities", "0"),
-         PDoc("keepEigenValues", "add eigen values", "0"), PDoc("keepEigenVectors", "add eigen vectors", "0")});
-}
 
 // no-op stand-in accepting a reference module's parameters (reads them all so
 // the "set but not used" check passes)
@@ -884,7 +937,8 @@ PointMatcher<T>::PointMatcher() {
                                   [](const Ps& p) { return std::make_shared<DistDPF<T, true>>(p); }, true);
     DataPointsFilterRegistrar.reg("MinDistDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<DistDPF<T, false>>(p); }, true);
-    register_unsupported_filters<T>(DataPointsFilterRegistrar);
+    DataPointsFilterRegistrar.reg("SamplingSurfaceNormalDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<SamplingSurfaceNormalDPF<T>>(p); }, true);
     InspectorRegistrar.reg("NullInspector", [](const Ps& p) {
         return std::make_shared<NoOp<Inspector>>("NullInspector", Parametrizable::ParametersDoc(), p);
     }, false);

@@ -1681,6 +1681,128 @@ int surface_normals_impl(int device, const T* feat, int rows, int64_t n, int knn
     return PMX_OK;
 }
 
+// SamplingSurfaceNormalDataPointsFilter::inPlaceFilter
+// (DataPointsFilters/SamplingSurfaceNormal.cpp:80-342): the split and the leaf
+// statistics on the device (pmx_ssn.hip), the sampling and the output cloud
+// here — fuseRange's draws in leaf order (:285-309), the output in index
+// order (:145-164).
+template <typename T>
+int ssn_impl(int device, const T* feat, int rows, int64_t n, const T* desc, int desc_dim, int knn, int method,
+             double ratio_d, double max_box_d, unsigned flags, T* feat_out, T* desc_out, T* o_nrm, T* o_dens,
+             T* o_eval, T* o_evec, int64_t* n_out, int64_t* unfit_out) {
+    if (rows != 3 && rows != 4) {
+        g_err = "SamplingSurfaceNormalDataPointsFilter: clouds must be 2-D or 3-D (3 or 4 homogeneous rows)";
+        return PMX_E_BAD_PARAM;
+    }
+    if (knn < 3) {
+        g_err = "SamplingSurfaceNormalDataPointsFilter: knn must be >= 3";
+        return PMX_E_BAD_PARAM;
+    }
+    if (method != 0 && method != 1) {
+        g_err = "SamplingSurfaceNormalDataPointsFilter: samplingMethod must be 0 or 1";
+        return PMX_E_BAD_PARAM;
+    }
+    if (n > (int64_t)0x7fffffff) {
+        g_err = "SamplingSurfaceNormalDataPointsFilter: more than 2^31 points";
+        return PMX_E_BAD_PARAM;
+    }
+    if (n_out) *n_out = 0;
+    if (unfit_out) *unfit_out = 0;
+    if (n <= 0) return PMX_OK;
+    pmx_ctx* c = nullptr;
+    int rc = pmx_ctx_create(device, sizeof(T) == 8 ? PMX_F64 : PMX_F32, &c);
+    if (rc) {
+        g_err = "SamplingSurfaceNormalDataPointsFilter: no HIP device";
+        return rc;
+    }
+    struct Guard {
+        pmx_ctx* c;
+        ~Guard() { pmx_ctx_destroy(c); }
+    } guard{c};
+    const int D = rows - 1;
+    void* d_pts = nullptr;
+    if (hipMalloc(&d_pts, sizeof(P4<T>) * n) != hipSuccess) {
+        g_err = "SamplingSurfaceNormalDataPointsFilter: device allocation failed";
+        return PMX_E_HIP;
+    }
+    std::unique_ptr<void, void (*)(void*)> free_pts(d_pts, [](void* p) { (void)hipFree(p); });
+    if ((rc = upload_raw(c, feat, sizeof(T) * (size_t)rows * n))) {
+        g_err = c->err;
+        return rc;
+    }
+    launch_pack_p4<T>((const T*)c->d_raw, rows, n, n, (P4<T>*)d_pts, c->stream);
+    const T ratio = (T)ratio_d, max_box = (T)max_box_d;
+    const bool want_eig = (flags & (PMX_SSN_NORMALS | PMX_SSN_EIGVALUES | PMX_SSN_EIGVECTORS)) != 0;
+    std::vector<int32_t> perm, lf, lc, fit;
+    std::vector<T> rec;
+    std::string err;
+    if ((rc = ssn_run<T>((const P4<T>*)d_pts, D, n, knn, max_box, want_eig, c->stream, perm, lf, lc, fit, rec, err))) {
+        g_err = err;
+        return rc;
+    }
+    const int RS = D + D + 1 + D + D * D;
+    // fuseRange's sampling, leaf by leaf in the recursion's order
+    std::vector<int32_t> keep_leaf((size_t)n, -1);  // by point index: the leaf whose record it takes
+    int64_t unfit = 0, kept = 0;
+    for (size_t l = 0; l < lf.size(); ++l) {
+        const int32_t f = lf[l], cnt = lc[l];
+        if (!fit[l]) {
+            unfit += cnt;
+            continue;
+        }
+        if (method == 0) {
+            for (int32_t i = 0; i < cnt; ++i) {
+                const float r = (float)std::rand() / (float)RAND_MAX;
+                if (r < ratio) {
+                    keep_leaf[(size_t)perm[(size_t)(f + i)]] = (int32_t)l;
+                    ++kept;
+                }
+            }
+        } else {  // the smallest index of the leaf carries its mean
+            keep_leaf[(size_t)perm[(size_t)f]] = (int32_t)l;
+            ++kept;
+        }
+    }
+    int64_t o = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        const int32_t l = keep_leaf[(size_t)k];
+        if (l < 0) continue;
+        const T* R = rec.data() + (size_t)l * RS;
+        if (feat_out) {
+            if (method == 0) {
+                for (int r = 0; r < rows; ++r) feat_out[o * rows + r] = feat[k * rows + r];
+            } else {
+                for (int r = 0; r < D; ++r) feat_out[o * rows + r] = R[r];
+                feat_out[o * rows + D] = 1;
+            }
+        }
+        if (desc_out && desc && desc_dim > 0) {
+            if (method == 1 && (flags & PMX_SSN_AVERAGE)) {  // mergedDesc (:320-328)
+                const int32_t f = lf[(size_t)l], cnt = lc[(size_t)l];
+                for (int cc = 0; cc < desc_dim; ++cc) {
+                    T s = 0;
+                    for (int32_t i = 0; i < cnt; ++i) s = s + desc[(int64_t)perm[(size_t)(f + i)] * desc_dim + cc];
+                    desc_out[o * desc_dim + cc] = s / (T)cnt;
+                }
+            } else {
+                for (int cc = 0; cc < desc_dim; ++cc) desc_out[o * desc_dim + cc] = desc[k * desc_dim + cc];
+            }
+        }
+        if (o_nrm)
+            for (int r = 0; r < D; ++r) o_nrm[o * D + r] = R[D + r];
+        if (o_dens) o_dens[o] = R[2 * D];
+        if (o_eval)
+            for (int r = 0; r < D; ++r) o_eval[o * D + r] = R[2 * D + 1 + r];
+        if (o_evec)
+            for (int e = 0; e < D * D; ++e) o_evec[o * D * D + e] = R[3 * D + 1 + e];
+        ++o;
+    }
+    (void)kept;
+    if (n_out) *n_out = o;
+    if (unfit_out) *unfit_out = unfit;
+    return PMX_OK;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1755,6 +1877,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
         preload_loop();
         preload_normals();
         preload_setup();
+        preload_ssn();
         preloaded = true;
     }
     // One small "iteration block" holds everything the host reads back per
@@ -1984,6 +2107,27 @@ int pmx_loop_select_stats(pmx_ctx* c, uint64_t* window_hits, uint64_t* window_mi
     *window_hits = h.n_hit;
     *window_misses = h.n_miss;
     return PMX_OK;
+}
+
+int pmx_sampling_surface_normals(int device, int dtype, const void* feat, int rows, int64_t n, const void* desc,
+                                 int desc_dim, int knn, int sampling_method, double ratio, double max_box_dim,
+                                 unsigned flags, void* feat_out, void* desc_out, void* normals, void* densities,
+                                 void* eig_values, void* eig_vectors, int64_t* n_out, int64_t* unfit) {
+    if ((!feat && n > 0) || (desc_dim > 0 && !desc && n > 0)) {
+        g_err = "null cloud";
+        return PMX_E_BAD_PARAM;
+    }
+    if (dtype == PMX_F32)
+        return ssn_impl<float>(device, (const float*)feat, rows, n, (const float*)desc, desc_dim, knn, sampling_method,
+                               ratio, max_box_dim, flags, (float*)feat_out, (float*)desc_out, (float*)normals,
+                               (float*)densities, (float*)eig_values, (float*)eig_vectors, n_out, unfit);
+    if (dtype == PMX_F64)
+        return ssn_impl<double>(device, (const double*)feat, rows, n, (const double*)desc, desc_dim, knn,
+                                sampling_method, ratio, max_box_dim, flags, (double*)feat_out, (double*)desc_out,
+                                (double*)normals, (double*)densities, (double*)eig_values, (double*)eig_vectors,
+                                n_out, unfit);
+    g_err = "dtype must be PMX_F32 or PMX_F64";
+    return PMX_E_BAD_PARAM;
 }
 
 int pmx_surface_normals(int device, int dtype, const void* feat, int rows, int64_t n, int knn, double maxDist,

@@ -20,6 +20,8 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <string>
+#include <vector>
 
 namespace pmx {
 
@@ -203,8 +205,18 @@ int reading_order_device(const P4<T>* raw, int64_t n, const Mat4<T>& M0, const S
 size_t setup_temp_bytes(int64_t n, int64_t max_cells);
 void launch_unpermute(const void* src, const int32_t* order, int64_t n, int span, size_t esz, void* dst,
                       hipStream_t s);
+// SamplingSurfaceNormalDataPointsFilter's recursive median split and
+// per-leaf statistics (pmx_ssn.hip).  Returns the point order (leaves
+// contiguous, index order inside), the leaves (first, count), their fit flag
+// and records (mean D, normal D, density, eigen values D, eigen vectors D*D);
+// 0 or a PMX_E_* code with err set.
+template <typename T>
+int ssn_run(const P4<T>* d_pts, int D, int64_t n, int knn, T max_box, bool want_eig, hipStream_t st,
+            std::vector<int32_t>& perm, std::vector<int32_t>& leaf_first, std::vector<int32_t>& leaf_cnt,
+            std::vector<int32_t>& fit, std::vector<T>& rec, std::string& err);
 // code-object preloads (one per translation unit, called by pmx_ctx_create)
 void preload_setup();
+void preload_ssn();
 void preload_match();
 void preload_grid();
 void preload_select();

@@ -119,6 +119,16 @@ int pmo_icp_f32(const pmo_cfg* cfg, const float* reading, int rows, int64_t N,
 /* SurfaceNormalDataPointsFilter (DataPointsFilters/SurfaceNormal.cpp:80-290):
  * outputs point-major, any may be NULL (see pmo_impl.inc for the eigen
  * convention); smooth = smoothNormals */
+/* SamplingSurfaceNormalDataPointsFilter (pmo_impl.inc): flags */
+enum { PMO_SSN_NORMALS = 1, PMO_SSN_DENSITIES = 2, PMO_SSN_EIGVALUES = 4, PMO_SSN_EIGVECTORS = 8, PMO_SSN_AVERAGE = 16 };
+int pmo_sampling_surface_normals_f32(const float* pts, int rows, int64_t n, const float* desc, int desc_dim, int knn,
+                                     int sampling_method, float ratio, float max_box_dim, unsigned flags,
+                                     float* feat_out, float* desc_out, float* normals, float* dens, float* evals,
+                                     float* evecs, int64_t* n_out, int64_t* unfit);
+int pmo_sampling_surface_normals_f64(const double* pts, int rows, int64_t n, const double* desc, int desc_dim,
+                                     int knn, int sampling_method, double ratio, double max_box_dim, unsigned flags,
+                                     double* feat_out, double* desc_out, double* normals, double* dens,
+                                     double* evals, double* evecs, int64_t* n_out, int64_t* unfit);
 int pmo_surface_normals_f32(const float* pts, int rows, int64_t n, int k, float maxDist, int threads, int smooth,
                             float* normals, float* dens, float* evals, float* evecs, float* ids, float* mdist,
                             int64_t* degenerate);

@@ -9,8 +9,10 @@ Outputs (data only, no reference source) go to tests/golden/:
       stored as float32 (n, D) arrays;
   - kat.json: known answers transcribed from the reference tests
       (utest/utest.cpp:346-356 validT2d/validT3d; utest/utest.h:49-85
-       tolerances; utest/ui/Outliers.cpp:126-152 VarTrimmed KAT) and the
-      examples/data/icp_data/*.ref_trans regression transforms.
+       tolerances; utest/ui/Outliers.cpp:126-152 VarTrimmed KAT), the
+      examples/data/icp_data/*.ref_trans regression transforms and the
+      icp_data/*.yaml chain configurations they are the answers for (test
+      inputs of utest.cpp:81-160, loaded unchanged by the GPU chain).
 """
 import json
 import os
@@ -65,6 +67,11 @@ def main():
             with open(os.path.join(d, fn)) as f:
                 vals = [float(x) for x in f.read().split()]
             ref_trans[fn[:-len(".ref_trans")]] = np.array(vals).reshape(4, 4).tolist()
+    configs = {}
+    for fn in sorted(os.listdir(d)):
+        if fn.endswith(".yaml"):
+            with open(os.path.join(d, fn)) as f:
+                configs[fn[:-len(".yaml")]] = f.read()
 
     kat = {
         # utest/utest.cpp:346-356 (reading = 2D_twoBoxes / car_cloud401,
@@ -85,6 +92,7 @@ def main():
         # utest/utest.cpp:81-160: median relative displacement < 3 %
         "icp_data_rel_tol": 0.03,
         "icp_data_ref_trans": ref_trans,
+        "icp_data_configs": configs,
     }
     with open(os.path.join(OUT, "kat.json"), "w") as f:
         json.dump(kat, f, indent=1)

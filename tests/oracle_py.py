@@ -231,3 +231,34 @@ def surface_normals(pts, k=5, max_dist=np.inf, threads=8, smooth=False):
     assert rc == OK, rc
     out["degenerate"] = deg.value
     return out
+
+
+SSN_NORMALS, SSN_DENSITIES, SSN_EIGVALUES, SSN_EIGVECTORS, SSN_AVERAGE = 1, 2, 4, 8, 16
+
+
+def sampling_surface_normals(pts, desc=None, knn=7, method=0, ratio=0.5, max_box=np.inf,
+                             flags=SSN_NORMALS | SSN_AVERAGE):
+    """SamplingSurfaceNormalDataPointsFilter restated (pmo_impl.inc).  pts (n, rows);
+    desc (n, desc_dim) or None.  Returns a dict of the kept points' arrays."""
+    pts = np.ascontiguousarray(pts)
+    dt = pts.dtype
+    n, rows = pts.shape
+    D = rows - 1
+    dd = 0 if desc is None else desc.shape[1]
+    desc = None if desc is None else np.ascontiguousarray(desc, dtype=dt)
+    out = {"features": np.zeros((n, rows), dt), "descriptors": np.zeros((n, dd), dt),
+           "normals": np.zeros((n, D), dt), "densities": np.zeros(n, dt), "eig_values": np.zeros((n, D), dt),
+           "eig_vectors": np.zeros((n, D * D), dt)}
+    no = C.c_int64(0)
+    unfit = C.c_int64(0)
+    scal = C.c_float if dt == np.float32 else C.c_double
+    f = getattr(lib(), "pmo_sampling_surface_normals_" + _sfx(dt))
+    rc = f(_p(pts), rows, C.c_int64(n), _p(desc), dd, int(knn), int(method), scal(ratio), scal(max_box),
+           C.c_uint(flags), _p(out["features"]), _p(out["descriptors"]), _p(out["normals"]), _p(out["densities"]),
+           _p(out["eig_values"]), _p(out["eig_vectors"]), C.byref(no), C.byref(unfit))
+    if rc != 0:
+        raise RuntimeError(f"pmo_sampling_surface_normals failed ({rc})")
+    m = no.value
+    res = {k: v[:m] for k, v in out.items()}
+    res["unfit"] = unfit.value
+    return res

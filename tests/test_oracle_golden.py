@@ -259,3 +259,22 @@ def test_surface_normals_oracle_degenerate_and_smoothing(oracle):
             acc = acc + nb if d > 0 else acc - nb
         n[i] = acc / np.float32(len(ids[i]))
     np.testing.assert_allclose(sm["normals"], n, rtol=1e-6, atol=1e-7)
+
+
+def test_sampling_surface_normals_oracle_pinned_by_icp_data(oracle, golden):
+    """The SamplingSurfaceNormal restatement, pinned by the reference's own
+    regression answer: defaultIdentityDataPointsFilter.yaml (knn 10,
+    samplingMethod 1) on cloud.00000, then that config's ICP
+    (TrimmedDist 0.75, point-to-plane, Counter 40 + Differential) from
+    cloud.00001: within 3 % of the stored ref_trans (utest.cpp:81-160)."""
+    g, kat = golden
+    ref, rd = hom(g["vtk0"], np.float32), hom(g["vtk1"], np.float32)
+    o = oracle.sampling_surface_normals(ref, None, knn=10, method=1, ratio=0.666666, flags=oracle.SSN_NORMALS)
+    assert 0 < len(o["features"]) <= -(-ref.shape[0] // 5)
+    assert np.allclose(np.linalg.norm(o["normals"], axis=1), 1.0, atol=1e-5)
+    c = oracle.make_cfg(filters=(("TrimmedDistOutlierFilter", {"ratio": 0.75}),), counter_max=40,
+                        differential=dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4), threads=8)
+    rc, T, st, _ = oracle.icp(c, rd, o["features"], normals=o["normals"])
+    assert rc == 0
+    refT = np.array(kat["icp_data_ref_trans"]["defaultIdentityDataPointsFilter"])
+    assert rel_displacement(T, refT, g["vtk1"]) < kat["icp_data_rel_tol"]
