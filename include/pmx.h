@@ -159,6 +159,23 @@ int pmx_outlier_mediandist(pmx_ctx* ctx, int chain_pos, double factor);
 int pmx_outlier_trimmed(pmx_ctx* ctx, int chain_pos, double ratio);
 int pmx_outlier_vartrimmed(pmx_ctx* ctx, int chain_pos, double minRatio, double maxRatio,
                            double lambda);
+/* RobustOutlierFilter::robustFiltering (OutlierFiltersImpl.cpp:494-598):
+ * real-valued weights w = robust(e^2), e^2 = dist / scale^2; at most one per
+ * chain.  robust_fct: PMX_RF_*; tuning: k (after the berg substitution,
+ * :419-433); approximation: the unsquared threshold (+inf = none); the
+ * scale of this call (the filter's iteration state stays with the caller,
+ * :500-531): PMX_RS_NONE (1), _MAD sqrt(median |d - median d|), _STD
+ * sqrt(std), _BERG_FIRST 1.9 sqrt(quantile(0.5)), _BERG_NEXT 0.85 (s -
+ * berg_target) + berg_target, _KEEP the previous call's scale at this chain
+ * position; point2plane: distanceType point2plane (needs reference normals).
+ * The scale stays on the device; pmx_robust_scale reads it back. */
+enum { PMX_RF_CAUCHY = 0, PMX_RF_WELSCH = 1, PMX_RF_SC = 2, PMX_RF_GM = 3, PMX_RF_TUKEY = 4, PMX_RF_HUBER = 5,
+       PMX_RF_L1 = 6, PMX_RF_STUDENT = 7 };
+enum { PMX_RS_NONE = 0, PMX_RS_MAD = 1, PMX_RS_STD = 2, PMX_RS_BERG_FIRST = 3, PMX_RS_BERG_NEXT = 4,
+       PMX_RS_KEEP = 5 };
+int pmx_outlier_robust(pmx_ctx* ctx, int chain_pos, int robust_fct, double tuning, double approximation,
+                       int scale_mode, double berg_target, int point2plane);
+int pmx_robust_scale(pmx_ctx* ctx, int chain_pos, double* scale);
 
 /* ---------------------------------------------------------- minimizers --- */
 /* Point-to-plane normal equations for the step transform of the last

@@ -144,7 +144,8 @@ EXPORTS = [
     "pmx_ctx_create", "pmx_ctx_destroy", "pmx_last_error", "pmx_device_count", "pmx_version",
     "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_set_reference", "pmx_set_reading", "pmx_set_search", "pmx_match",
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
-    "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed",
+    "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed", "pmx_outlier_robust",
+    "pmx_robust_scale",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
     "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_surface_normals",
@@ -177,6 +178,9 @@ def lib():
         for f in ("maxdist", "mindist", "mediandist", "trimmed"):
             getattr(l, "pmx_outlier_" + f).argtypes = [C.c_void_p, C.c_int, C.c_double]
         l.pmx_outlier_vartrimmed.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_double]
+        l.pmx_outlier_robust.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, C.c_double,
+                                         C.c_int]
+        l.pmx_robust_scale.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
         l.pmx_p2plane_system.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(Stats)]
         l.pmx_p2point_system.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.POINTER(Stats)]
@@ -235,6 +239,9 @@ def surface_normals(points, knn=5, max_dist=np.inf, smooth=False, device=0):
 
 
 SSN_NORMALS, SSN_DENSITIES, SSN_EIGVALUES, SSN_EIGVECTORS, SSN_AVERAGE = 1, 2, 4, 8, 16
+# RobustOutlierFilter functions / scale modes of one call (include/pmx.h PMX_RF_*, PMX_RS_*)
+ROBUST_FCT = {"cauchy": 0, "welsch": 1, "sc": 2, "gm": 3, "tukey": 4, "huber": 5, "L1": 6, "student": 7}
+RS_NONE, RS_MAD, RS_STD, RS_BERG_FIRST, RS_BERG_NEXT, RS_KEEP = range(6)
 
 
 def sampling_surface_normals(points, descriptors=None, knn=7, sampling_method=0, ratio=0.5, max_box_dim=np.inf,
@@ -390,6 +397,18 @@ class Context:
         else:
             raise InvalidParameter(f"unknown outlier filter {name}")
         self._chk(rc)
+
+    def outlier_robust(self, pos=0, fct="cauchy", tuning=1.0, approximation=np.inf, scale_mode=RS_MAD,
+                       berg_target=0.0, point2plane=False):
+        """One RobustOutlierFilter call with the scale mode given (the filter's
+        iteration schedule is the caller's, as libpointmatcher_amd.icp does)."""
+        self._chk(self._l.pmx_outlier_robust(self.h, pos, ROBUST_FCT[fct], float(tuning), float(approximation),
+                                             int(scale_mode), float(berg_target), 1 if point2plane else 0))
+
+    def robust_scale(self, pos=0):
+        v = C.c_double()
+        self._chk(self._l.pmx_robust_scale(self.h, pos, C.byref(v)))
+        return v.value
 
     def p2plane_system(self):
         n = 6 if self.rows == 4 else 3

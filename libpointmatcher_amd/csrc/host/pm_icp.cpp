@@ -3,8 +3,8 @@
 // Module names, parameter names, defaults and bounds are those of the
 // reference so that libpointmatcher YAML chain files load unchanged:
 //   KDTreeMatcher                 MatchersImpl.h:74-103
-//   Null/MaxDist/MinDist/MedianDist/TrimmedDist/VarTrimmedDist OutlierFilter
-//                                 OutlierFiltersImpl.h:51-172
+//   Null/MaxDist/MinDist/MedianDist/TrimmedDist/VarTrimmedDist/Robust OutlierFilter
+//                                 OutlierFiltersImpl.h:51-260
 //   PointToPlane / PointToPoint ErrorMinimizer
 //                                 ErrorMinimizers/PointToPlane.h:61-90, PointToPoint.h
 //   Counter / Differential / Bound TransformationChecker
@@ -268,6 +268,70 @@ struct VarTrimmedDistOF : PM<T>::OutlierFilter {
         cfg.filter_p[pos][1] = (double)maxRatio;
         cfg.filter_p[pos][2] = (double)lambda;
         return true;
+    }
+};
+
+// RobustOutlierFilter (OutlierFiltersImpl.h:220-260, OutlierFiltersImpl.cpp:380-598):
+// the parameters and the filter's state (iteration, berg target, tuning
+// substitution) stay here as in the reference object; the scale and the
+// weights are computed on the device (pmx_outlier_robust).  It has no
+// device-loop form: a chain holding it runs the per-module calls.
+template <typename T>
+struct RobustOF : PM<T>::OutlierFilter {
+    std::string robustFctName, scaleEstimator, distanceType;
+    T tuning, squaredApproximation, approximation;
+    int nbIterationForScale;
+    int robustFctId = -1;
+    int iteration = 1;
+    T berg_target_scale = 0;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("robustFct", "Type of robust function used. Available fct: 'cauchy', 'welsch', 'sc', 'gm', "
+                                  "'tukey', 'huber', 'L1' and 'student'.", "cauchy"),
+                PDoc("tuning", "Tuning parameter used to limit the influence of outliers (the target scale with "
+                               "'berg').", "1.0", "0.0000001", "inf", &Parametrizable::Comp<T>),
+                PDoc("scaleEstimator", "'none', 'mad', 'berg' or 'std'", "mad"),
+                PDoc("nbIterationForScale", "iterations the scale is recomputed for (0: every iteration)", "0", "0",
+                     "100", &Parametrizable::Comp<int>),
+                PDoc("distanceType", "'point2point' or 'point2plane'", "point2point"),
+                PDoc("approximation", "weights of errors above this threshold are forced to zero (inf: none)", "inf",
+                     "0.0", "inf", &Parametrizable::Comp<T>)};
+    }
+    explicit RobustOF(const Parametrizable::Parameters& p)
+        : PM<T>::OutlierFilter("RobustOutlierFilter", doc(), p),
+          robustFctName(this->template get<std::string>("robustFct")),
+          scaleEstimator(this->template get<std::string>("scaleEstimator")),
+          distanceType(this->template get<std::string>("distanceType")),
+          tuning(this->template get<T>("tuning")),
+          approximation(this->template get<T>("approximation")),
+          nbIterationForScale(this->template get<int>("nbIterationForScale")) {
+        squaredApproximation = (T)std::pow(approximation, 2);
+        if (scaleEstimator != "none" && scaleEstimator != "mad" && scaleEstimator != "berg" && scaleEstimator != "std")
+            throw InvalidParameter("Invalid scale estimator name.");
+        if (distanceType != "point2point" && distanceType != "point2plane")
+            throw InvalidParameter("Invalid distance type name.");
+        static const char* names[] = {"cauchy", "welsch", "sc", "gm", "tukey", "huber", "L1", "student"};
+        for (int i = 0; i < 8; ++i)
+            if (robustFctName == names[i]) robustFctId = i;  // (PMX_RF_* order)
+        if (robustFctId < 0) throw InvalidParameter("Invalid robust function name.");
+        if (scaleEstimator == "berg") {  // Bergstrom 2014 tunings (:419-433)
+            berg_target_scale = tuning;
+            if (robustFctId == PMX_RF_CAUCHY) tuning = (T)4.3040;
+            else if (robustFctId == PMX_RF_TUKEY) tuning = (T)7.0589;
+            else if (robustFctId == PMX_RF_HUBER) tuning = (T)2.0138;
+        }
+    }
+    void compute(Device& d, const typename PM<T>::Matches&, int pos) override {
+        // robustFiltering's scale schedule (:500-531); iteration counts the
+        // filter's calls over its lifetime, as the reference member does
+        const bool recompute = iteration <= nbIterationForScale || nbIterationForScale == 0;
+        int mode = PMX_RS_NONE;
+        if (scaleEstimator == "mad") mode = recompute ? PMX_RS_MAD : PMX_RS_KEEP;
+        else if (scaleEstimator == "std") mode = recompute ? PMX_RS_STD : PMX_RS_KEEP;
+        else if (scaleEstimator == "berg")
+            mode = !recompute ? PMX_RS_KEEP : (iteration == 1 ? PMX_RS_BERG_FIRST : PMX_RS_BERG_NEXT);
+        ++iteration;
+        d.check(pmx_outlier_robust(d.ctx, pos, robustFctId, (double)tuning, (double)approximation, mode,
+                                   (double)berg_target_scale, distanceType == "point2plane" ? 1 : 0));
     }
 };
 
@@ -913,6 +977,8 @@ PointMatcher<T>::PointMatcher() {
                                true);
     OutlierFilterRegistrar.reg("VarTrimmedDistOutlierFilter",
                                [](const Ps& p) { return std::make_shared<VarTrimmedDistOF<T>>(p); }, true);
+    OutlierFilterRegistrar.reg("RobustOutlierFilter", [](const Ps& p) { return std::make_shared<RobustOF<T>>(p); },
+                               true);
     ErrorMinimizerRegistrar.reg("PointToPlaneErrorMinimizer",
                                 [](const Ps& p) { return std::make_shared<PointToPlaneEM<T>>(p); }, true);
     ErrorMinimizerRegistrar.reg("PointToPointErrorMinimizer",

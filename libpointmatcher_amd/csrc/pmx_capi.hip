@@ -138,6 +138,17 @@ struct pmx_ctx {
     int chain_type[kMaxChain] = {};
     double chain_thr[kMaxChain] = {};
     bool w_valid = false;  // d_w holds the chain's weights (mirror only)
+    // RobustOutlierFilter (at most one per chain): its parameters, and the
+    // device block of its scale state: SelectState (the MAD's second
+    // select), then the scale of each chain position, then the moment sums
+    int rb_pos = -1, rb_fct = 0, rb_p2pl = 0;
+    double rb_k = 1.0, rb_sqa = INFINITY;
+    void* d_rob = nullptr;
+    void* d_rdev = nullptr;  // |d - median| (T[n])
+    size_t rdev_bytes = 0;
+    double* rob_scale(int pos) const { return (double*)((char*)d_rob + 256) + pos; }
+    double* rob_sums() const { return (double*)((char*)d_rob + 256) + kMaxChain; }
+    SelectState* rob_sel() const { return (SelectState*)d_rob; }
 
     // quantile select: SelectState followed by the per-iteration error word;
     // chain positions >= 1 use their own states (d_sel_more)
@@ -969,6 +980,7 @@ int unpermute(pmx_ctx* c, const std::vector<V>& src, V* dst, int k) {
 
 // record predicate `pos` of the weight chain (position 0 starts a new chain)
 void chain_set(pmx_ctx* c, int pos, int type, double thr) {
+    if (pos == 0 || c->rb_pos >= pos) c->rb_pos = -1;  // (a new chain, or the robust filter's position rewritten)
     c->chain_n = pos + 1;
     c->chain_type[pos] = type;
     c->chain_thr[pos] = thr;
@@ -988,6 +1000,14 @@ WChain<T> chain_of(const pmx_ctx* c) {
         w.type[i] = c->chain_type[i];
         w.thr[i] = (T)c->chain_thr[i];
         w.st[i] = c->sel_slot(i);
+    }
+    if (c->rb_pos >= 0 && c->rb_pos < c->chain_n) {
+        w.robust = 1;
+        w.rb_fct = c->rb_fct;
+        w.rb_k = (T)c->rb_k;
+        w.rb_sqa = (T)c->rb_sqa;
+        w.rb_scale = c->rob_scale(c->rb_pos);
+        w.rb_p2pl = c->rb_p2pl;
     }
     return w;
 }
@@ -1098,6 +1118,81 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
     return PMX_OK;
 }
 
+// RobustOutlierFilter::robustFiltering (OutlierFiltersImpl.cpp:494-598): the
+// scale of this call on the device, then the filter joins the chain as its
+// real-valued factor (evaluated inline by the weighted reductions)
+template <typename T>
+int outlier_robust_impl(pmx_ctx* c, int pos, int fct, double tuning, double approx, int mode, double target,
+                        int p2pl) {
+    int rc = check_match(c);
+    if (rc) return rc;
+    if (pos < 0 || pos >= kMaxChain) return fail(c, PMX_E_BAD_PARAM, "outlier chain longer than 8 filters");
+    if (pos > c->chain_n) return fail(c, PMX_E_BAD_PARAM, "outlier chain positions must be consecutive");
+    if (fct < kRFCauchy || fct > kRFStudent) return fail(c, PMX_E_BAD_PARAM, "Invalid robust function name.");
+    if (mode < kRSNone || mode > kRSKeep) return fail(c, PMX_E_BAD_PARAM, "Invalid scale estimator name.");
+    if (c->rb_pos >= 0 && c->rb_pos < pos && pos <= c->chain_n)
+        return fail(c, PMX_E_BAD_PARAM, "one RobustOutlierFilter per outlier chain on this path");
+    if (p2pl && !c->has_normals)
+        return fail(c, PMX_E_BAD_PARAM, "RobustOutlierFilter point2plane requires \"normals\" on the reference");
+    if (p2pl && c->dim != 3)  // (computePointToPlaneDistance reads 3 feature rows, :472-484)
+        return fail(c, PMX_E_BAD_PARAM, "RobustOutlierFilter point2plane: 3-D clouds only");
+    if (!c->d_rob) {
+        HIPCHK(c, hipMalloc(&c->d_rob, 512));
+        HIPCHK(c, hipMemsetAsync(c->d_rob, 0, 512, c->stream));
+    }
+    const int64_t n = c->N * c->knn;
+    const T* d = (const T*)c->d_dists;
+    SelectState* slot = c->sel_slot(pos);
+    double* scale = c->rob_scale(pos);
+    int smode = mode;
+    switch (mode) {
+    case kRSMad:  // Matches::getMedianAbsDeviation (Matches.cpp:88-122)
+        if ((rc = quantile_select<T>(c, d, n, kRatioMedianIndex, nullptr, slot))) return rc;
+        if ((rc = ensure(c, &c->d_rdev, &c->rdev_bytes, sizeof(T) * (size_t)(n > 0 ? n : 1)))) return rc;
+        launch_abs_dev<T>(d, n, slot, (T*)c->d_rdev, c->stream);
+        if ((rc = quantile_select<T>(c, (const T*)c->d_rdev, n, kRatioMedianIndex, nullptr, c->rob_sel()))) return rc;
+        launch_robust_scale<T>(kRSMad, c->rob_sel(), nullptr, 0, 0.0, scale, c->stream);
+        smode = -1;
+        break;
+    case kRSStd: {  // Matches::getStandardDeviation (Matches.cpp:124-129) over all k x N
+        double* sums = c->rob_sums();
+        launch_moment<T>(d, n, 0, sums, c->d_partials, c->stream);
+        launch_finalize(c->d_partials, kRedBlocks, 1, sums, loop_ctl(c), c->stream);
+        if ((rc = allreduce_f64(c, sums, 1))) return rc;
+        launch_moment<T>(d, n, 1, sums, c->d_partials, c->stream);
+        launch_finalize(c->d_partials, kRedBlocks, 1, sums + 1, loop_ctl(c), c->stream);
+        if ((rc = allreduce_f64(c, sums + 1, 1))) return rc;
+        launch_robust_scale<T>(kRSStd, nullptr, sums, c->N_total * c->knn, 0.0, scale, c->stream);
+        smode = -1;
+        break;
+    }
+    case kRSBergFirst:  // 1.9 sqrt(getDistsQuantile(0.5))
+        if ((rc = quantile_select<T>(c, d, n, 0.5, nullptr, slot))) return rc;
+        launch_robust_scale<T>(kRSBergFirst, slot, nullptr, 0, 0.0, scale, c->stream);
+        smode = -1;
+        break;
+    default: break;
+    }
+    if (smode >= 0) launch_robust_scale<T>(smode, nullptr, nullptr, 0, target, scale, c->stream);
+    chain_set(c, pos, kWPRobust, 0.0);
+    c->rb_pos = pos;
+    c->rb_fct = fct;
+    c->rb_k = (double)(T)tuning;
+    // squaredApproximation = pow(approximation, 2) in T (:400)
+    c->rb_sqa = std::isinf(approx) ? INFINITY : (double)(T)std::pow((double)(T)approx, 2.0);
+    c->rb_p2pl = p2pl;
+    HIPCHK(c, hipGetLastError());
+    return PMX_OK;
+}
+
+template <typename T>
+int robust_scale_impl(pmx_ctx* c, int pos, double* scale) {
+    if (pos < 0 || pos >= kMaxChain || !c->d_rob) return fail(c, PMX_E_STATE, "no RobustOutlierFilter scale at this position");
+    HIPCHK(c, hipMemcpyAsync(scale, c->rob_scale(pos), sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
 // -------------------------------------------------------------- minimizers --
 // one D2H copy of the iteration block, then a stream sync
 int readback(pmx_ctx* c) {
@@ -1143,15 +1238,29 @@ void after_readback(pmx_ctx* c) {
     choose_level(c, v, f);
 }
 
+// the chain's weights into d_w (the host mirror; a point-to-plane robust
+// distance under the point-to-point minimiser)
+template <typename T>
+int materialise_weights(pmx_ctx* c) {
+    if (c->w_valid) return PMX_OK;
+    launch_weights_chain<T>((const T*)c->d_dists, (T*)c->d_w, c->N * c->knn, chain_of<T>(c), (const P4<T>*)c->d_rd,
+                            step_mat<T>(c), (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c), match_rs(c),
+                            c->d_ids, c->knn, c->stream);
+    HIPCHK(c, hipGetLastError());
+    c->w_valid = true;
+    return PMX_OK;
+}
+
 // the point-to-plane system into the iteration block (no host sync);
 // *fuse_nv != 0 on entry: leave the finalize to the loop step (single rank),
 // which gets the value count back in *fuse_nv
 template <typename T>
 int p2plane_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
-    const int NV = p2plane_nv(c->dim);
+    const WChain<T> chain = chain_of<T>(c);
+    const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
-                              match_rs(c), (const T*)c->d_dists, c->d_ids, chain_of<T>(c), c->knn, c->N, c->dim, c->d_partials,
+                              match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
                               loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
     if (fuse_nv && *fuse_nv && !sharded(c)) {
         *fuse_nv = NV;
@@ -1169,7 +1278,12 @@ int p2plane_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
 template <typename T>
 int p2point_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
     Mat4<T> Tm = step_mat<T>(c);
-    const WChain<T> chain = chain_of<T>(c);
+    WChain<T> chain = chain_of<T>(c);
+    if (chain.robust && chain.rb_p2pl) {  // (the point-to-point kernels carry no normals)
+        const int rc = materialise_weights<T>(c);
+        if (rc) return rc;
+        chain.w_arr = (const T*)c->d_w;
+    }
     const GridDesc<T>* gd = (const GridDesc<T>*)c->d_gdesc;
     launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
                             chain, c->knn, c->N, c->d_partials, loop_ctl(c), gd, c->stream);
@@ -1197,24 +1311,27 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     if (!c->has_normals)
         return fail(c, PMX_E_BAD_PARAM, "PointToPlaneErrorMinimizer requires \"normals\" on the reference");
     const int NF = c->dim == 3 ? 6 : 3;
-    const int NS = NF * (NF + 1) / 2;
+    const bool full = c->rb_pos >= 0 && c->rb_pos < c->chain_n;  // (the weighted layout, see p2plane_enqueue)
+    const int NS = full ? NF * NF : NF * (NF + 1) / 2;
     if ((rc = p2plane_enqueue<T>(c))) return rc;
     if ((rc = readback(c))) return rc;
     after_readback(c);
     const double* r = c->h_result;
     const int ierr = host_iter_err(c);
     const int o = NS + NF;
-    // 0/1 weights: sum of kept weights == kept count
-    fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 0], host_limit(c));
+    fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 4], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
     if (ierr == kSelTimeout) return fail(c, PMX_E_HIP, "radix select: device wait timed out");
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[o + 1] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
     if (r[o + 0] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
-    // mirror the upper triangle (exactly symmetric, see pmx_reduce.hip)
-    int a = 0;
-    for (int i = 0; i < NF; ++i)
-        for (int j = i; j < NF; ++j, ++a) A[i * NF + j] = A[j * NF + i] = r[a];
+    if (full) {
+        for (int i = 0; i < NF * NF; ++i) A[i] = r[i];
+    } else {  // mirror the upper triangle (exactly symmetric with 0/1 weights, see pmx_reduce.hip)
+        int a = 0;
+        for (int i = 0; i < NF; ++i)
+            for (int j = i; j < NF; ++j, ++a) A[i * NF + j] = A[j * NF + i] = r[a];
+    }
     for (int i = 0; i < NF; ++i) b[i] = -r[NS + i];
     return PMX_OK;
 }
@@ -1283,11 +1400,7 @@ int get_weights_impl(pmx_ctx* c, void* w) {
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
     if (n <= 0) return PMX_OK;
-    if (!c->w_valid) {  // materialise the chain's 0/1 weights
-        launch_weights_chain<T>((const T*)c->d_dists, (T*)c->d_w, n, chain_of<T>(c), c->stream);
-        HIPCHK(c, hipGetLastError());
-        c->w_valid = true;
-    }
+    if ((rc = materialise_weights<T>(c))) return rc;
     std::vector<T> hw((size_t)n);
     HIPCHK(c, hipMemcpyAsync(hw.data(), c->d_w, sizeof(T) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1922,7 +2035,8 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace,
-                    c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx};
+                    c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
+                    c->d_rob, c->d_rdev};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();
@@ -2036,6 +2150,16 @@ int pmx_get_matches(pmx_ctx* c, void* dists, int32_t* ids) {
     return DISPATCH(c, get_matches_impl<float>(c, dists, ids), get_matches_impl<double>(c, dists, ids));
 }
 
+int pmx_outlier_robust(pmx_ctx* c, int pos, int fct, double tuning, double approx, int mode, double target,
+                       int p2pl) {
+    if (!c) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return DISPATCH(c, outlier_robust_impl<float>(c, pos, fct, tuning, approx, mode, target, p2pl),
+                    outlier_robust_impl<double>(c, pos, fct, tuning, approx, mode, target, p2pl));
+}
+int pmx_robust_scale(pmx_ctx* c, int pos, double* scale) {
+    if (!c || !scale) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return DISPATCH(c, robust_scale_impl<float>(c, pos, scale), robust_scale_impl<double>(c, pos, scale));
+}
 int pmx_get_weights(pmx_ctx* c, void* w) {
     if (!c || !w) return fail(c, PMX_E_BAD_PARAM, "null argument");
     return DISPATCH(c, get_weights_impl<float>(c, w), get_weights_impl<double>(c, w));

@@ -238,7 +238,13 @@ void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, 
 // predicates on the distance.  It is evaluated inline by the reductions (no
 // weight array is written or read on the hot path) and materialised only for
 // the host mirror (pmx_get_weights).
-enum WPred { kWPDefault = 0, kWPNull = 1, kWPLe = 2, kWPGe = 3, kWPState = 4 };
+// The RobustOutlierFilter (OutlierFiltersImpl.cpp:394-598) is the one
+// filter with real-valued weights: w = robust(e^2), e^2 = dist / scale^2,
+// multiplied with the predicates' 0/1 (kWPRobust, at most one per chain; the
+// reductions take the weighted path only then).
+enum WPred { kWPDefault = 0, kWPNull = 1, kWPLe = 2, kWPGe = 3, kWPState = 4, kWPRobust = 5 };
+enum RobustFct { kRFCauchy = 0, kRFWelsch = 1, kRFSC = 2, kRFGM = 3, kRFTukey = 4, kRFHuber = 5, kRFL1 = 6,
+                 kRFStudent = 7 };
 constexpr int kMaxChain = 8;
 template <typename T>
 struct WChain {
@@ -246,7 +252,54 @@ struct WChain {
     int type[kMaxChain] = {};
     T thr[kMaxChain] = {};                        // kWPLe / kWPGe: threshold; kWPState: scale
     const SelectState* st[kMaxChain] = {};        // kWPState: resolved quantile (limit)
+    // kWPRobust (robust != 0): function, tuning k, squared approximation,
+    // the scale (device, T value), point-to-plane distance
+    int robust = 0;
+    int rb_fct = 0;
+    T rb_k = 1;
+    T rb_sqa = 0;
+    const double* rb_scale = nullptr;
+    int rb_p2pl = 0;
+    const T* w_arr = nullptr;  // materialised weights (a robust point-to-plane distance, point-to-point minimiser)
 };
+// robustFiltering's weight of one scaled squared error (OutlierFiltersImpl.cpp:541-596)
+template <typename T>
+__device__ __forceinline__ T robust_weight(int fct, T k, T sqa, T e2) {
+    const T k2 = k * k;
+    T w;
+    switch (fct) {
+    case kRFCauchy: w = (T)1 / ((T)1 + e2 / k2); break;
+    case kRFWelsch: w = exp(-e2 / k2); break;
+    case kRFSC: {
+        const T s = k + e2;
+        w = e2 >= k ? (T)(4.0 * (double)k2) * ((T)1 / (s * s)) : (T)1;
+        break;
+    }
+    case kRFGM: {
+        const T s = k + e2;
+        w = k2 * ((T)1 / (s * s));
+        break;
+    }
+    case kRFTukey: {
+        const T a = (T)1 - e2 / k2;
+        w = e2 >= k2 ? (T)0 : a * a;
+        break;
+    }
+    case kRFHuber: w = e2 >= k2 ? k * ((T)1 / sqrt(e2)) : (T)1; break;
+    case kRFL1: w = (T)1 / sqrt(e2); break;
+    default: {  // Student, d = 3
+        const T d = 3;
+        const T p = pow((T)1 + e2 / k, -(k + d) / (T)2);
+        w = p * (k + d) * ((T)1 / (k + e2));
+        break;
+    }
+    }
+    // ARBITRARY_SMALL_VALUE (1e-50 as T: 0 in float), then the approximation
+    const T tiny = (T)1e-50;
+    w = w <= tiny ? tiny : w;
+    if (sqa != (T)__builtin_huge_val() && e2 >= sqa) w = 0;
+    return w;
+}
 // per-thread resolved thresholds (kWPState: scale * limit in T, as the
 // reference's `factor * quantile`, OutlierFiltersImpl.cpp:121-122)
 // A conjunction of `d <= t` / `d >= t` / `d != inf` predicates is one
@@ -280,6 +333,24 @@ template <typename T>
 __device__ __forceinline__ bool chain_keep(const WRange<T>& r, T d) {
     return (!r.finite || d != (T)__builtin_huge_val()) && d >= r.lo && d <= r.hi;
 }
+
+// ---- robust scale estimators (pmx_robust.hip) ----
+// the exact median index count / 2 (Matches::getMedianAbsDeviation's
+// nth_element, Matches.cpp:110-120) instead of the quantile rule
+// (size_t)((T)count * ratio): passed as the select's ratio
+constexpr double kRatioMedianIndex = 2.0;
+enum RobustScaleMode { kRSNone = 0, kRSMad = 1, kRSStd = 2, kRSBergFirst = 3, kRSBergNext = 4, kRSKeep = 5 };
+// dev[i] = |d[i] - median| for finite d (median: st->limit), +inf otherwise
+template <typename T>
+void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, hipStream_t s);
+// sum of d (pass 0) / of (d - mean)^2 with mean = (T)(sum / n) (pass 1) into
+// partials (kRedBlocks x 1), summed by launch_finalize
+template <typename T>
+void launch_moment(const T* d, int64_t n, int pass, const double* sum, double* partials, hipStream_t s);
+// the scale (a T value stored as double) of the iteration, from the mode
+template <typename T>
+void launch_robust_scale(int mode, const SelectState* st, const double* sums, int64_t n, double target,
+                         double* scale, hipStream_t s);
 
 // ---- quantile / weights (pmx_select.hip) ----
 // one radix-select pass: histogram of digit `pass` among keys matching the
@@ -329,8 +400,10 @@ size_t vartrim_scratch_bytes(int64_t n);
 constexpr int kRedBlocks = PMX_RED_BLOCKS;  // fixed reduction grid (deterministic sums)
 constexpr int kNVMax = 48;
 // point-to-plane result layout: upper triangle of A (NS), b (NF), then kept,
-// nonzero weights, rejected matches, rejected points
-constexpr int p2plane_nv(int dim) { return dim == 3 ? 21 + 6 + 4 : 6 + 3 + 4; }
+// nonzero weights, rejected matches, rejected points, sum of the weights
+constexpr int p2plane_nv(int dim) { return dim == 3 ? 21 + 6 + 5 : 6 + 3 + 5; }
+// the weighted (robust) variant: full A (NF x NF) instead of the upper triangle
+constexpr int p2plane_nv_full(int dim) { return dim == 3 ? 36 + 6 + 5 : 9 + 3 + 5; }
 // ctl / gd (device loop, may be null): early exit, step transform and the
 // grid level whose positions the ids are (ref / nrm then come from gd)
 // rs: index stride of ref / nrm (1: separate arrays; 2: a grid level's
@@ -351,6 +424,7 @@ void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, 
                           const int32_t* ids, const WChain<T>& chain, int k, int64_t N, const T* means_dev,
                           double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 template <typename T>
-void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, hipStream_t s);
+void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, const P4<T>* rd, const Mat4<T>& Tm,
+                          const P4<T>* ref, const P4<T>* nrm, int rs, const int32_t* ids, int k, hipStream_t s);
 
 }  // namespace pmx

@@ -143,8 +143,8 @@ __device__ void fused_finalize_n(const double* __restrict__ partials, int nblock
 __device__ void fused_finalize(const double* __restrict__ partials, int nblocks, int nv, double* __restrict__ out,
                                double* fin) {
     switch (nv) {  // (uniform) the value counts of the minimisers' last reductions
-    case 31: fused_finalize_n<31>(partials, nblocks, out, fin); break;  // point-to-plane 3-D
-    case 13: fused_finalize_n<13>(partials, nblocks, out, fin); break;  // point-to-plane 2-D
+    case 32: fused_finalize_n<32>(partials, nblocks, out, fin); break;  // point-to-plane 3-D
+    case 14: fused_finalize_n<14>(partials, nblocks, out, fin); break;  // point-to-plane 2-D
     default: fused_finalize_n<9>(partials, nblocks, out, fin); break;   // point-to-point pass 2
     }
 }
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
         nz = res[o + 1];
         rejM = res[o + 2];
         rejP = res[o + 3];
-        sw = kept;  // 0/1 weights
+        sw = res[o + 4];
     } else {
         kept = res[7];
         nz = res[8];

@@ -53,10 +53,33 @@ __device__ __forceinline__ void block_store(double (&acc)[NV], double* __restric
         partials[(int64_t)v * gridDim.x + blockIdx.x] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
 }
 
+// The chain's weight of one match when it holds a RobustOutlierFilter:
+// (predicates' 0/1) * robust(e^2), e^2 = dist / scale^2 in T
+// (OutlierFiltersImpl.cpp:537-540); dist = the match distance, or for
+// distanceType point2plane (n^ . (p - q))^2 with the normalised reference
+// normal (computePointToPlaneDistance, :460-489: 0 for an invalid match)
+template <typename T>
+__device__ __forceinline__ T robust_chain_weight(const WChain<T>& c, const WRange<T>& wr, T dist, int64_t e) {
+    if (c.w_arr) return c.w_arr[e];
+    const T pred = chain_keep(wr, dist) ? (T)1 : (T)0;
+    const T s = (T)*c.rb_scale;
+    const T e2 = dist / (s * s);
+    return pred * robust_weight<T>(c.rb_fct, c.rb_k, c.rb_sqa, e2);
+}
+template <typename T>
+__device__ __forceinline__ T p2pl_distance(T px, T py, T pz, const P4<T>& q, const P4<T>& n) {
+    // Eigen normalized(): v / sqrt(squaredNorm), v itself when the norm is 0
+    const T sq = (n.x * n.x + n.y * n.y) + n.z * n.z;
+    const T nn = sq > (T)0 ? sqrt(sq) : (T)1;
+    const T dot = ((n.x / nn) * (px - q.x) + (n.y / nn) * (py - q.y)) + (n.z / nn) * (pz - q.z);
+    return dot * dot;  // (pow(dot, 2) rounds to the same T)
+}
+
 // one kept pair: F and dot in T exactly as PointToPlane.cpp:171-243, the
 // upper triangle of F F^T and F dot added in fp64
 template <typename T, int DIM, int NV>
-__device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz, const P4<T>& q, const P4<T>& n) {
+__device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz, const P4<T>& q, const P4<T>& n,
+                                            T w = (T)1) {
     constexpr int NF = DIM == 3 ? 6 : 3;
     constexpr int NS = NF * (NF + 1) / 2;
     T F[NF];
@@ -75,12 +98,15 @@ __device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz,
         F[2] = n.y;
         dot = (px - q.x) * n.x + (py - q.y) * n.y;
     }
+    // wF = w * F (PointToPlane.cpp:218-227); with the 0/1 weights w = 1 and
+    // wF is F exactly
     int a = 0;
 #pragma unroll
     for (int r = 0; r < NF; ++r) {
+        const T wF = w * F[r];
 #pragma unroll
-        for (int c = r; c < NF; ++c) acc[a++] += (double)(F[r] * F[c]);
-        acc[NS + r] += (double)(F[r] * dot);
+        for (int c = r; c < NF; ++c) acc[a++] += (double)(wF * F[c]);
+        acc[NS + r] += (double)(wF * dot);
     }
 }
 
@@ -97,7 +123,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                                                               const GridDesc<T>* __restrict__ gd) {
     constexpr int NF = DIM == 3 ? 6 : 3;
     constexpr int NS = NF * (NF + 1) / 2;
-    constexpr int NV = NS + NF + 4;
+    constexpr int NV = NS + NF + 5;  // (the fifth counter, sum of w, is the kept count with 0/1 weights)
     if (ctl) {  // device loop
         if (ctl->done) return;
         ctl_transform(ctl, Tm);
@@ -148,6 +174,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                     continue;
                 }
                 acc[NS + NF + 0] += 1.0;
+                acc[NS + NF + 4] += 1.0;
                 T px, py, pz;
                 xform3(Tm, r[u], px, py, pz);
                 p2plane_add<T, DIM, NV>(acc, px, py, pz, q[u], n[u]);
@@ -169,7 +196,8 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                 continue;
             }
             exist = true;
-            acc[NS + NF + 0] += 1.0;  // kept (= sum of the 0/1 weights)
+            acc[NS + NF + 0] += 1.0;  // kept
+            acc[NS + NF + 4] += 1.0;  // sum of the 0/1 weights
             const int32_t id = ids[e];
             p2plane_add<T, DIM, NV>(acc, px, py, pz, gld(ref, (int64_t)id * rs), gld(nrm, (int64_t)id * rs));
         }
@@ -178,10 +206,101 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
     block_store<NV>(acc, partials);
 }
 
+// Real-valued weights (a RobustOutlierFilter in the chain; per-module path):
+// the ErrorElements counts on w != 0, sum of w in the fifth counter.  A is
+// accumulated in full: (w F_r) F_c and (w F_c) F_r round differently, and the
+// reference's wF * F^T keeps that asymmetry (PointToPlane.cpp:218-227).
+template <typename T, int DIM, int NV>
+__device__ __forceinline__ void p2plane_add_full(double (&acc)[NV], T px, T py, T pz, const P4<T>& q,
+                                                 const P4<T>& n, T w) {
+    constexpr int NF = DIM == 3 ? 6 : 3;
+    T F[NF];
+    T dot;
+    if (DIM == 3) {
+        F[0] = py * n.z - pz * n.y;
+        F[1] = pz * n.x - px * n.z;
+        F[2] = px * n.y - py * n.x;
+        F[3] = n.x;
+        F[4] = n.y;
+        F[5] = n.z;
+        dot = ((px - q.x) * n.x + (py - q.y) * n.y) + (pz - q.z) * n.z;
+    } else {
+        F[0] = px * n.y - py * n.x;
+        F[1] = n.x;
+        F[2] = n.y;
+        dot = (px - q.x) * n.x + (py - q.y) * n.y;
+    }
+#pragma unroll
+    for (int r = 0; r < NF; ++r) {
+        const T wF = w * F[r];
+#pragma unroll
+        for (int c = 0; c < NF; ++c) acc[r * NF + c] += (double)(wF * F[c]);
+        acc[NF * NF + r] += (double)(wF * dot);
+    }
+}
+template <typename T, int DIM>
+__global__ __launch_bounds__(256) void p2plane_weighted_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
+                                                               const P4<T>* __restrict__ ref,
+                                                               const P4<T>* __restrict__ nrm, int rs,
+                                                               const T* __restrict__ d,
+                                                               const int32_t* __restrict__ ids, WChain<T> chain,
+                                                               int k, int64_t N, double* __restrict__ partials) {
+    constexpr int NF = DIM == 3 ? 6 : 3;
+    constexpr int NS = NF * NF;  // (full A)
+    constexpr int NV = NS + NF + 5;
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const WRange<T> wr = chain_resolve(chain);
+    const T inf = (T)__builtin_huge_val();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += stride) {
+        T px, py, pz;
+        xform3(Tm, rd[i], px, py, pz);
+        bool exist = false;
+        for (int s = 0; s < k; ++s) {
+            const int64_t e = i * k + s;
+            const T dv = d[e];
+            const int32_t id = ids[e];
+            P4<T> q{}, n{};
+            if (id >= 0) {
+                q = gld(ref, (int64_t)id * rs);
+                n = gld(nrm, (int64_t)id * rs);
+            }
+            const T dist = chain.rb_p2pl ? (id >= 0 ? p2pl_distance(px, py, pz, q, n) : (T)0) : dv;
+            // (the predicates judge the match distance; the robust function the chosen one)
+            const T pred = chain_keep(wr, dv) ? (T)1 : (T)0;
+            const T sc = (T)*chain.rb_scale;
+            const T w = pred * robust_weight<T>(chain.rb_fct, chain.rb_k, chain.rb_sqa, dist / (sc * sc));
+            if (w != (T)0) acc[NS + NF + 1] += 1.0;  // (w != 0).count()
+            if (dv == inf) continue;
+            if (w == (T)0) {
+                acc[NS + NF + 2] += 1.0;  // rejected match
+                continue;
+            }
+            exist = true;
+            acc[NS + NF + 0] += 1.0;
+            acc[NS + NF + 4] += (double)w;
+            p2plane_add_full<T, DIM, NV>(acc, px, py, pz, q, n, w);
+        }
+        if (!exist) acc[NS + NF + 3] += 1.0;
+    }
+    block_store<NV>(acc, partials);
+}
+
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
+    if (chain.robust) {  // (never in the device loop: a robust chain runs the module calls)
+        if (dim == 3)
+            hipLaunchKernelGGL((p2plane_weighted_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
+                               rs, d, ids, chain, k, N, partials);
+        else
+            hipLaunchKernelGGL((p2plane_weighted_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
+                               rs, d, ids, chain, k, N, partials);
+        return;
+    }
     if (dim == 3)
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
                            d, ids, chain, k, N, partials, ctl, gd);
@@ -239,24 +358,25 @@ __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restr
         for (int s = 0; s < k; ++s) {
             const int64_t e = i * k + s;
             const T dv = d[e];
-            const bool keep = chain_keep(wr,dv);
-            if (keep) acc[8] += 1.0;
+            // 0/1 weights, or a robust chain's real weight (point2point distance)
+            const T w = chain.robust ? robust_chain_weight(chain, wr, dv, e) : (chain_keep(wr, dv) ? (T)1 : (T)0);
+            if (w != (T)0) acc[8] += 1.0;
             if (dv == inf) continue;
-            if (!keep) {
+            if (w == (T)0) {
                 acc[9] += 1.0;
                 continue;
             }
             exist = true;
             acc[7] += 1.0;
             const P4<T> q = gld(ref, ids[e]);
-            // w = 1: p * w == p exactly
-            acc[0] += 1.0;
-            acc[1] += (double)px;
-            acc[2] += (double)py;
-            acc[3] += (double)pz;
-            acc[4] += (double)q.x;
-            acc[5] += (double)q.y;
-            acc[6] += (double)q.z;
+            // (with w = 1, p * w == p exactly)
+            acc[0] += (double)w;
+            acc[1] += (double)(px * w);
+            acc[2] += (double)(py * w);
+            acc[3] += (double)(pz * w);
+            acc[4] += (double)(q.x * w);
+            acc[5] += (double)(q.y * w);
+            acc[6] += (double)(q.z * w);
         }
         if (!exist) acc[10] += 1.0;
     }
@@ -318,7 +438,8 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
         for (int s = 0; s < k; ++s) {
             const int64_t e = i * k + s;
             const T dv = d[e];
-            if (dv == inf || !chain_keep(wr,dv)) continue;
+            const T w = chain.robust ? robust_chain_weight(chain, wr, dv, e) : (chain_keep(wr, dv) ? (T)1 : (T)0);
+            if (dv == inf || w == (T)0) continue;
             const P4<T> q4 = gld(ref, ids[e]);
             const T q[3] = {q4.x, q4.y, q4.z};
             T pc[3], qc[3];
@@ -330,7 +451,7 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) acc[r * 3 + c] += (double)(qc[r] * pc[c]);  // (qc * 1) pc
+                for (int c = 0; c < 3; ++c) acc[r * 3 + c] += (double)((qc[r] * w) * pc[c]);  // (qc * w) pc
             }
         }
     }
@@ -345,20 +466,42 @@ void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, 
                        means_dev, partials, ctl, gd);
 }
 
-// materialise the chain's 0/1 weights (host mirror only)
+// materialise the chain's weights (host mirror only); point-to-plane robust
+// distances need the step reading, the match ids and the reference records
 template <typename T>
-__global__ void weights_chain_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n, WChain<T> chain) {
+__global__ void weights_chain_kernel(const T* __restrict__ d, T* __restrict__ w, int64_t n, WChain<T> chain,
+                                     const P4<T>* __restrict__ rd, Mat4<T> Tm, const P4<T>* __restrict__ ref,
+                                     const P4<T>* __restrict__ nrm, int rs, const int32_t* __restrict__ ids, int k) {
     const WRange<T> wr = chain_resolve(chain);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        w[i] = chain_keep(wr,d[i]) ? (T)1 : (T)0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (!chain.robust) {
+            w[i] = chain_keep(wr, d[i]) ? (T)1 : (T)0;
+            continue;
+        }
+        T dist = d[i];
+        if (chain.rb_p2pl) {
+            const int32_t id = ids[i];
+            dist = 0;
+            if (id >= 0) {
+                T px, py, pz;
+                xform3(Tm, rd[i / k], px, py, pz);
+                dist = p2pl_distance(px, py, pz, gld(ref, (int64_t)id * rs), gld(nrm, (int64_t)id * rs));
+            }
+        }
+        const T pred = chain_keep(wr, d[i]) ? (T)1 : (T)0;
+        const T sc = (T)*chain.rb_scale;
+        w[i] = pred * robust_weight<T>(chain.rb_fct, chain.rb_k, chain.rb_sqa, dist / (sc * sc));
+    }
 }
 template <typename T>
-void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, hipStream_t s) {
+void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, const P4<T>* rd, const Mat4<T>& Tm,
+                          const P4<T>* ref, const P4<T>* nrm, int rs, const int32_t* ids, int k, hipStream_t s) {
     if (n <= 0) return;
     int64_t g = (n + 1023) / 1024;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(weights_chain_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, w, n, chain);
+    hipLaunchKernelGGL(weights_chain_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, w, n, chain, rd, Tm, ref, nrm,
+                       rs, ids, k);
 }
 
 #define PMX_INST(T)                                                                                                  \
@@ -372,7 +515,8 @@ void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, h
     template void launch_p2point_pass2<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
                                           const WChain<T>&, int, int64_t, const T*, double*, const LoopCtl*,         \
                                           const GridDesc<T>*, hipStream_t);                                          \
-    template void launch_weights_chain<T>(const T*, T*, int64_t, const WChain<T>&, hipStream_t);
+    template void launch_weights_chain<T>(const T*, T*, int64_t, const WChain<T>&, const P4<T>*, const Mat4<T>&,     \
+                                          const P4<T>*, const P4<T>*, int, const int32_t*, int, hipStream_t);
 PMX_INST(float)
 PMX_INST(double)
 #undef PMX_INST

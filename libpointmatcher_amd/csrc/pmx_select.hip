@@ -234,6 +234,8 @@ __device__ __forceinline__ void pick_phase(uint32_t* __restrict__ hist, SelectSt
             st->ratio = (double)q;
             if (count == 0) {
                 s_err = -2;  // PMX_E_EMPTY_QUANTILE: ConvergenceError("no outlier to filter")
+            } else if (!ratio_dev && ratio_host == kRatioMedianIndex) {
+                st->rank = count / 2;  // nth_element at size / 2 (Matches.cpp:110-120)
             } else if (q < (T)0 || q > (T)1) {
                 s_err = -3;  // ConvergenceError("quantile must be between 0 and 1")
             } else if (q == (T)1) {
@@ -471,6 +473,8 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
             if (pass == 0) {
                 if (total == 0) {
                     err = -2;  // PMX_E_EMPTY_QUANTILE: ConvergenceError("no outlier to filter")
+                } else if (!ratio_dev && ratio_host == kRatioMedianIndex) {
+                    rank = total / 2;  // nth_element at size / 2 (Matches.cpp:110-120)
                 } else if (q < (T)0 || q > (T)1) {
                     err = -3;  // ConvergenceError("quantile must be between 0 and 1")
                 } else if (q == (T)1) {

@@ -45,7 +45,26 @@ enum {
     PMO_OF_MEDIANDIST = 3,  /* MedianDistOutlierFilter(factor) :108-128 */
     PMO_OF_TRIMMED = 4,     /* TrimmedDistOutlierFilter(ratio) :132-150 */
     PMO_OF_VARTRIMMED = 5,  /* VarTrimmedDistOutlierFilter(minRatio,maxRatio,lambda) :153-223 */
+    PMO_OF_ROBUST = 6,      /* RobustOutlierFilter (pmo_cfg.robust) :394-598 */
 };
+
+/* RobustOutlierFilter (OutlierFiltersImpl.cpp:394-598).  The parameters as
+ * the YAML gives them; the filter's state (iteration, scale, the berg
+ * substitution of the tuning, :419-433) lives in the struct: zero it before
+ * the first call, as a freshly constructed filter. */
+enum { PMO_RF_CAUCHY = 0, PMO_RF_WELSCH, PMO_RF_SC, PMO_RF_GM, PMO_RF_TUKEY, PMO_RF_HUBER, PMO_RF_L1, PMO_RF_STUDENT };
+enum { PMO_RS_NONE = 0, PMO_RS_MAD = 1, PMO_RS_STD = 2, PMO_RS_BERG = 3 };
+typedef struct pmo_robust {
+    int fct;             /* PMO_RF_* (robustFct) */
+    int scale_est;       /* PMO_RS_* (scaleEstimator) */
+    int nb_iter;         /* nbIterationForScale */
+    int point2plane;     /* distanceType */
+    double tuning;
+    double approximation;  /* +inf = none */
+    /* state */
+    int iteration;       /* 0 = not constructed yet */
+    double k, target, scale;  /* T values */
+} pmo_robust;
 
 enum { PMO_MIN_P2PLANE = 0, PMO_MIN_P2POINT = 1 };
 enum { PMO_KNN_BRUTE = 0, PMO_KNN_KDTREE = 1 };
@@ -75,6 +94,7 @@ typedef struct pmo_cfg {
     int diff_enabled;
     double diff_rot, diff_trans;
     int diff_smooth;
+    pmo_robust robust;       /* the chain's PMO_OF_ROBUST filter (at most one) */
 } pmo_cfg;
 
 typedef struct pmo_stats {
@@ -103,6 +123,11 @@ int pmo_quantile_f32(const float* dists, int64_t n, float q, float* out);
 int pmo_outlier_f32(int type, const double* p, const float* dists, int k, int64_t N, float* w);
 int pmo_outlier_chain_f32(int n, const int* types, const double* params, const float* dists,
                           int k, int64_t N, float* w);
+/* RobustOutlierFilter::compute: w (k x N) of one call, state updated.
+ * step: the transformed reading (point-major, rows); ref / normals (D per
+ * point) only for point2plane */
+int pmo_robust_weights_f32(pmo_robust* r, const float* dists, const int32_t* ids, int k, int64_t N, const float* step,
+                           int rows, const float* ref, const float* normals, float* w);
 int pmo_vartrimmed_ratio_f32(const float* dists, int64_t n, float minRatio, float maxRatio,
                              float lambda, float* ratio_out);
 void pmo_transform_f32(const float* T, int rows, const float* pts, int64_t N, float* out);
@@ -140,6 +165,8 @@ int pmo_quantile_f64(const double* dists, int64_t n, double q, double* out);
 int pmo_outlier_f64(int type, const double* p, const double* dists, int k, int64_t N, double* w);
 int pmo_outlier_chain_f64(int n, const int* types, const double* params, const double* dists,
                           int k, int64_t N, double* w);
+int pmo_robust_weights_f64(pmo_robust* r, const double* dists, const int32_t* ids, int k, int64_t N,
+                           const double* step, int rows, const double* ref, const double* normals, double* w);
 int pmo_vartrimmed_ratio_f64(const double* dists, int64_t n, double minRatio, double maxRatio,
                              double lambda, double* ratio_out);
 void pmo_transform_f64(const double* T, int rows, const double* pts, int64_t N, double* out);

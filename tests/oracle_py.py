@@ -18,9 +18,43 @@ LIB = os.path.join(ROOT, "oracle", "build", "libpmo.so")
 # error codes (oracle/pmo.h)
 OK, E_NO_POINTS, E_EMPTY_QUANTILE, E_BAD_PARAM, E_TRANSFORMATION, E_NAN = 0, -1, -2, -3, -4, -5
 OF = {"NullOutlierFilter": 0, "MaxDistOutlierFilter": 1, "MinDistOutlierFilter": 2,
-      "MedianDistOutlierFilter": 3, "TrimmedDistOutlierFilter": 4, "VarTrimmedDistOutlierFilter": 5}
+      "MedianDistOutlierFilter": 3, "TrimmedDistOutlierFilter": 4, "VarTrimmedDistOutlierFilter": 5,
+      "RobustOutlierFilter": 6}
 OF_PARAMS = {0: [], 1: [("maxDist", 1.0)], 2: [("minDist", 1.0)], 3: [("factor", 3.0)],
-             4: [("ratio", 0.85)], 5: [("minRatio", 0.05), ("maxRatio", 0.99), ("lambda", 2.35)]}
+             4: [("ratio", 0.85)], 5: [("minRatio", 0.05), ("maxRatio", 0.99), ("lambda", 2.35)], 6: []}
+ROBUST_FCT = {"cauchy": 0, "welsch": 1, "sc": 2, "gm": 3, "tukey": 4, "huber": 5, "L1": 6, "student": 7}
+ROBUST_SCALE = {"none": 0, "mad": 1, "std": 2, "berg": 3}
+
+
+class Robust(C.Structure):
+    """pmo_robust: RobustOutlierFilter parameters + state (zero state = a new filter)."""
+    _fields_ = [("fct", C.c_int), ("scale_est", C.c_int), ("nb_iter", C.c_int), ("point2plane", C.c_int),
+                ("tuning", C.c_double), ("approximation", C.c_double), ("iteration", C.c_int),
+                ("k", C.c_double), ("target", C.c_double), ("scale", C.c_double)]
+
+
+def make_robust(p):
+    r = Robust()
+    r.fct = ROBUST_FCT[p.get("robustFct", "cauchy")]
+    r.scale_est = ROBUST_SCALE[p.get("scaleEstimator", "mad")]
+    r.nb_iter = int(p.get("nbIterationForScale", 0))
+    r.point2plane = 1 if p.get("distanceType", "point2point") == "point2plane" else 0
+    r.tuning = float(p.get("tuning", 1.0))
+    r.approximation = float(p.get("approximation", np.inf))
+    return r
+
+
+def robust_weights(r, dists, ids, step=None, ref=None, normals=None):
+    """One RobustOutlierFilter::compute on (N, k) matches; r (Robust) is updated."""
+    d = np.ascontiguousarray(dists)
+    N, k = d.shape
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    w = np.empty_like(d)
+    rows = step.shape[1] if step is not None else 4
+    f = getattr(lib(), "pmo_robust_weights_" + _sfx(d.dtype))
+    rc = f(C.byref(r), _p(d), _p(ids), k, C.c_int64(N), _p(step), rows, _p(ref),
+           _p(np.ascontiguousarray(normals, dtype=d.dtype) if normals is not None else None), _p(w))
+    return rc, w
 MIN = {"PointToPlaneErrorMinimizer": 0, "PointToPointErrorMinimizer": 1}
 
 
@@ -30,7 +64,7 @@ class Cfg(C.Structure):
                 ("filter_type", C.c_int * 8), ("filter_p", (C.c_double * 3) * 8),
                 ("minimizer", C.c_int), ("acc_mode", C.c_int), ("counter_max", C.c_int),
                 ("diff_enabled", C.c_int), ("diff_rot", C.c_double), ("diff_trans", C.c_double),
-                ("diff_smooth", C.c_int)]
+                ("diff_smooth", C.c_int), ("robust", Robust)]
 
 
 class Stats(C.Structure):
@@ -174,6 +208,9 @@ def make_cfg(knn=1, max_dist=np.inf, method="kdtree", threads=1, filters=(("Trim
     cfg.knn_threads = threads
     cfg.n_filters = len(filters)
     types, params = _filters(filters)
+    for name, p in filters:
+        if name == "RobustOutlierFilter":
+            cfg.robust = make_robust(p)
     for i in range(8):
         cfg.filter_type[i] = int(types[i])
         for j in range(3):

@@ -1,0 +1,179 @@
+"""RobustOutlierFilter on the GPU (pmx_robust.hip scale estimators, the
+weighted reductions of pmx_reduce.hip) against the oracle
+(oracle/pmo_impl.inc pmo_robust_weights, pinned by tests/test_robust_oracle.py).
+
+Bar: the scale bit-exact for mad / berg (order statistics) and to 1 ulp for
+std (fp64 sums in another order); weights to rtol 1e-6 (f32) / 1e-12 (f64)
+(device exp / pow / sqrt vs libm); the weighted normal equations to the same
+relative bound; ErrorElements counts exact.  The reference's regression
+configuration defaultRobustOutlierFilter.yaml runs unchanged through the GPU
+chain (utest.cpp:81-160 3 % rule) and follows the oracle ICP iteration for
+iteration.
+Reference: OutlierFiltersImpl.cpp:394-598, Matches.cpp:88-129,
+PointToPoint.cpp:61-101, PointToPlane.cpp:171-243.
+"""
+import numpy as np
+import pytest
+
+from helpers import hom, rel_displacement
+from libpointmatcher_amd import _capi as P
+from libpointmatcher_amd.icp import ICP
+from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+
+pytestmark = pytest.mark.gpu
+
+TOL = {np.float32: 1e-6, np.float64: 1e-12}
+FCTS = ["cauchy", "welsch", "sc", "gm", "tukey", "huber", "L1", "student"]
+SCALES = ["mad", "std", "berg", "none"]
+
+
+def _T(dtype, ang=0.02, tr=0.01):
+    c, s = np.cos(ang), np.sin(ang)
+    T = np.eye(4)
+    T[:2, :2] = [[c, -s], [s, c]]
+    T[:3, 3] = [tr, -tr, tr / 2]
+    return T.astype(dtype)
+
+
+def _gpu_mode(r_it, scale, nb):
+    """the host class's schedule (libpointmatcher_amd RobustOF::compute)"""
+    rec = r_it <= nb or nb == 0
+    if scale == "mad":
+        return P.RS_MAD if rec else P.RS_KEEP
+    if scale == "std":
+        return P.RS_STD if rec else P.RS_KEEP
+    if scale == "berg":
+        return P.RS_KEEP if not rec else (P.RS_BERG_FIRST if r_it == 1 else P.RS_BERG_NEXT)
+    return P.RS_NONE
+
+
+def _setup(dtype, k, max_dist=np.inf, n=12000, m=16000):
+    ref, nrm = reference_cloud(m, dtype)
+    rd = reading_cloud(n, dtype)
+    ctx = P.Context(0, dtype)
+    ctx.set_reference(ref, nrm)
+    ctx.set_reading(rd)
+    return ctx, ref, nrm, rd
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("scale", SCALES)
+@pytest.mark.parametrize("fct", FCTS)
+def test_robust_weights_and_scale(oracle, dtype, scale, fct):
+    k = 3
+    ctx, ref, nrm, rd = _setup(dtype, k)
+    tol = TOL[dtype]
+    nb, approx = (2, 2.5) if fct in ("cauchy", "huber") else (0, np.inf)
+    p = {"robustFct": fct, "scaleEstimator": scale, "tuning": 0.8, "nbIterationForScale": nb,
+         "approximation": approx}
+    r = oracle.make_robust(p)
+    tg = 0.8 if scale == "berg" else 0.0
+    tuning = 0.8
+    if scale == "berg":
+        tuning = {"cauchy": 4.3040, "tukey": 7.0589, "huber": 2.0138}.get(fct, 0.8)
+    for it in range(1, 4):  # three iterations of the schedule at moving poses
+        T = _T(dtype, ang=0.02 / it, tr=0.01 / it)
+        ctx.match(T, knn=k)
+        ctx.outlier_robust(0, fct, tuning, approx, _gpu_mode(it, scale, nb), tg)
+        w = ctx.get_weights()
+        s = ctx.robust_scale(0)
+        d, i = ctx.get_matches()
+        rc, ow = oracle.robust_weights(r, d, i)
+        assert rc == 0
+        if scale == "std":
+            np.testing.assert_allclose(s, r.scale, rtol=4e-7 if dtype == np.float32 else 1e-13)
+        else:
+            assert s == r.scale
+        np.testing.assert_allclose(w, ow, rtol=tol, atol=tol)
+        assert np.array_equal(w == 0, ow == 0) or scale == "std"
+    ctx.close()
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("minimizer", ["p2plane", "p2point"])
+@pytest.mark.parametrize("chain", ["robust", "trimmed+robust", "robust+maxdist", "p2pl_distance"])
+def test_weighted_systems(oracle, dtype, minimizer, chain):
+    k = 4
+    ctx, ref, nrm, rd = _setup(dtype, k, n=15000, m=20000)
+    T = _T(dtype, ang=0.01, tr=0.008)
+    ctx.match(T, knn=k, max_dist=0.12)
+    p = {"robustFct": "cauchy", "scaleEstimator": "mad", "tuning": 1.0}
+    p2pl = chain == "p2pl_distance"
+    if p2pl:
+        p["distanceType"] = "point2plane"
+    r = oracle.make_robust(p)
+    d, i = ctx.get_matches()
+    step = oracle.transform(T, rd)
+    if chain == "trimmed+robust":
+        ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.8)
+        ctx.outlier_robust(1, "cauchy", 1.0, np.inf, P.RS_MAD, 0.0)
+        _, w0 = oracle.outlier_chain([("TrimmedDistOutlierFilter", {"ratio": 0.8})], d)
+        _, w1 = oracle.robust_weights(r, d, i)
+        ow = w0 * w1
+    elif chain == "robust+maxdist":
+        ctx.outlier_robust(0, "cauchy", 1.0, np.inf, P.RS_MAD, 0.0)
+        ctx.outlier("MaxDistOutlierFilter", 1, maxDist=0.06)
+        _, w0 = oracle.robust_weights(r, d, i)
+        _, w1 = oracle.outlier_chain([("MaxDistOutlierFilter", {"maxDist": 0.06})], d)
+        ow = w0 * w1
+    else:
+        ctx.outlier_robust(0, "cauchy", 1.0, np.inf, P.RS_MAD, 0.0, point2plane=p2pl)
+        _, ow = oracle.robust_weights(r, d, i, step=step, ref=ref, normals=nrm[:, :3] if nrm.shape[1] > 3 else nrm)
+    tol = TOL[dtype]
+    w = ctx.get_weights()
+    np.testing.assert_allclose(w, ow, rtol=tol, atol=tol)
+    if minimizer == "p2plane":
+        A, b, st = ctx.p2plane_system()
+        rc, oA, ob, ost = oracle.p2plane_system(step, ref, nrm, d, i, w)
+        assert rc == 0
+        np.testing.assert_allclose(A, oA, rtol=1e-9, atol=1e-9 * np.abs(oA).max())
+        np.testing.assert_allclose(b, ob, rtol=1e-9, atol=1e-9 * np.abs(ob).max())
+    else:
+        mp, mq, m, st = ctx.p2point_system()
+        rc, dT, ost = oracle.p2point(step, ref, d, i, w)
+        assert rc == 0
+        keep = np.isfinite(d) & (w != 0)
+        ww = np.where(keep, w, 0).astype(np.float64)
+        sw = ww.sum()
+        pm = (step[:, None, :3].astype(np.float64) * ww[..., None]).sum((0, 1)) / sw
+        q = ref[np.where(i >= 0, i, 0), :3].astype(np.float64)
+        qm = (q * ww[..., None]).sum((0, 1)) / sw
+        np.testing.assert_allclose(mp, pm, rtol=1e-5 if dtype == np.float32 else 1e-11, atol=1e-6)
+        np.testing.assert_allclose(mq, qm, rtol=1e-5 if dtype == np.float32 else 1e-11, atol=1e-6)
+        np.testing.assert_allclose(st.sum_w, ost.sum_w, rtol=1e-9)
+    assert st.kept == ost.kept and st.nonzero_weights == ost.nonzero_weights
+    assert st.rejected_matches == ost.rejected_matches and st.rejected_points == ost.rejected_points
+    np.testing.assert_allclose(st.sum_w, ost.sum_w, rtol=1e-9)
+    ctx.close()
+
+
+def test_icp_data_robust_config_unchanged(golden):
+    g, kat = golden
+    text = kat["icp_data_configs"]["defaultRobustOutlierFilter"]
+    icp = ICP(np.float32)
+    icp.load_yaml(text)
+    T = icp.compute(hom(g["vtk1"], np.float32), hom(g["vtk0"], np.float32), None)
+    refT = np.array(kat["icp_data_ref_trans"]["defaultRobustOutlierFilter"])
+    err = rel_displacement(T, refT, g["vtk1"])
+    print(f"defaultRobustOutlierFilter: rel err {err:.4f}, iterations {icp.stats().iterations}")
+    assert err < kat["icp_data_rel_tol"]
+
+
+def test_icp_robust_equals_oracle(golden, oracle):
+    """the same chain through the GPU ICP and the oracle ICP: same iteration
+    count, |dT|_F <= 1e-4 (float weights through exp-free cauchy; the sums'
+    order differs)"""
+    g, kat = golden
+    text = kat["icp_data_configs"]["defaultRobustOutlierFilter"]
+    icp = ICP(np.float32)
+    icp.load_yaml(text)
+    rd, ref = hom(g["vtk1"], np.float32), hom(g["vtk0"], np.float32)
+    Tg = icp.compute(rd, ref, None)
+    c = oracle.make_cfg(knn=10, filters=(("RobustOutlierFilter", {"robustFct": "cauchy", "scaleEstimator": "mad",
+                                                                    "tuning": 1}),),
+                        minimizer="PointToPointErrorMinimizer", counter_max=40,
+                        differential=dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4), threads=8)
+    rc, To, so, _ = oracle.icp(c, rd, ref)
+    assert rc == 0
+    assert icp.stats().iterations == so.iterations
+    assert np.linalg.norm(Tg - To) <= 1e-4

@@ -153,6 +153,21 @@ def test_yaml_errors_like_reference():
         icp.compute(pts, pts)
 
 
+def test_robust_outlier_filter_parameter_errors():
+    # RobustOutlierFilter's constructor checks (OutlierFiltersImpl.cpp:409-417, 447-450)
+    from libpointmatcher_amd import icp as I
+    icp = I.ICP(np.float32)
+    for bad, msg in ((dict(robustFct="foo"), "Invalid robust function name."),
+                     (dict(scaleEstimator="foo"), "Invalid scale estimator name."),
+                     (dict(distanceType="foo"), "Invalid distance type name."),
+                     (dict(tuning=0), "smaller than minimum"),
+                     (dict(nbIterationForScale=101), "larger than maximum")):
+        with pytest.raises(I.InvalidParameter, match=msg):
+            icp.load_yaml(chain_yaml(filters=[("RobustOutlierFilter", bad)]))
+    icp.load_yaml(chain_yaml(filters=[("RobustOutlierFilter", dict(robustFct="student", scaleEstimator="berg",
+                                                                   approximation="inf"))]))
+
+
 def test_yaml_inf_and_numbers():
     from libpointmatcher_amd import icp as I
     icp = I.ICP(np.float64)
