@@ -36,6 +36,13 @@ constexpr size_t kBlkMeans = 1280;
 constexpr size_t kBlkCopy = 1344;
 constexpr size_t kBlkBytes = 2048;
 static_assert(kBlkIterErr + sizeof(int) <= kBlkRatio, "iteration block layout");
+// The status block: the iteration block, then the loop's control word and
+// state, in one allocation, so one copy returns everything the host reads
+// after a batch of device-loop iterations.
+constexpr size_t kStatCtl = kBlkBytes;
+constexpr size_t kStatLoop = kStatCtl + 512;
+constexpr size_t kStatBytes = (kStatLoop + sizeof(LoopState<double>) + 255) & ~(size_t)255;
+static_assert(sizeof(LoopCtl) <= 512, "status block layout");
 
 // one resolution of the uniform grid over the reference (pmx_grid.hip)
 struct GridLevel {
@@ -210,12 +217,13 @@ struct pmx_ctx {
     // MI355X (C3 driver command) 0.0821 ms/step unfused vs 0.0910 fused — the 256-thread step launch
     // costs more than the finalize kernel and its boundary it saves
     bool fuse_final = false;
+    bool fold_counter = false;  // the counter phase in the match's last workgroup (PMX_FOLD_COUNTER=1; measured slower)
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;
     pmx_loop_cfg loop_cfg{};
     LoopCfg loop_dev{};
-    void* h_loop = nullptr;       // pinned: LoopState<T> mirror, then the per-batch stop flags
+    void* h_loop = nullptr;       // pinned: two copies of the status block (the batches in flight)
     hipEvent_t loop_ev[2] = {nullptr, nullptr};  // end of the batches in flight
     int64_t loop_issued = 0;      // iterations enqueued since pmx_loop_begin
     int loop_iters = 0;           // iterations completed (last status)
@@ -858,7 +866,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             e1, c->stream);  // (e1 recorded after the match kernel, before the counter sum)
+                             c->fold_counter, e1, c->stream);  // (e1 recorded after the match kernel, before the counter sum)
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
@@ -1414,15 +1422,8 @@ int get_weights_impl(pmx_ctx* c, void* w) {
 // next batch is already queued, so the GPU never waits for the host; after a
 // stop the queued iterations return at once (every kernel reads LoopCtl.done).
 constexpr int kLoopBatch = 4;
-struct LoopFlag {
-    int iter;
-    int done;
-};
-
-template <typename T>
-LoopFlag* loop_flags(const pmx_ctx* c) {
-    return (LoopFlag*)((char*)c->h_loop + ((sizeof(LoopState<T>) + 63) & ~(size_t)63));
-}
+// pinned status slot s (a copy of the device status block)
+const char* stat_slot(const pmx_ctx* c, int s) { return (const char*)c->h_loop + (size_t)s * kStatBytes; }
 
 
 template <typename T>
@@ -1477,10 +1478,11 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     d.n_local = c->N;
     int rc;
     size_t cap = 0;
-    if (!c->d_loop && (rc = ensure(c, &c->d_loop, &cap, sizeof(LoopState<double>)))) return rc;
+    (void)cap;  // (LoopState lives in the status block)
     cap = 0;
     if (!c->d_loop_T0 && (rc = ensure(c, &c->d_loop_T0, &cap, 16 * sizeof(double)))) return rc;
-    if (!c->h_loop) HIPCHK(c, hipHostMalloc(&c->h_loop, sizeof(LoopState<double>) + 128, hipHostMallocDefault));
+    // pinned: two status-block slots (the batches in flight)
+    if (!c->h_loop) HIPCHK(c, hipHostMalloc(&c->h_loop, 2 * kStatBytes, hipHostMallocDefault));
     for (hipEvent_t& e : c->loop_ev)
         if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->loop_cfg = *cfg;
@@ -1567,9 +1569,8 @@ template <typename T>
 int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
     if (!c->loop_begun) return fail(c, PMX_E_STATE, "pmx_loop_begin must be called first");
     if (n < 0) return fail(c, PMX_E_BAD_PARAM, "negative iteration count");
-    LoopFlag* hf = loop_flags<T>(c);
     int rc = PMX_OK;
-    int issued = 0, slot = 0;
+    int issued = 0, slot = 0, last_slot = -1;
     int fly[2], nfly = 0, head = 0;
     bool stop = c->loop_done;
     c->loop_on = true;
@@ -1581,7 +1582,9 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
             if (rc) break;
             c->loop_issued += b;
             issued += b;
-            hipError_t e = hipMemcpyAsync(&hf[slot], (char*)c->d_loop + offsetof(LoopState<T>, iter), sizeof(LoopFlag),
+            // the whole status block (state, control word, iteration block):
+            // the stop flag of this batch, and the final status if it is the last
+            hipError_t e = hipMemcpyAsync((char*)c->h_loop + (size_t)slot * kStatBytes, c->d_result, kStatBytes,
                                           hipMemcpyDeviceToHost, c->stream);
             if (e == hipSuccess) e = hipEventRecord(c->loop_ev[slot], c->stream);
             if (e != hipSuccess) {
@@ -1590,6 +1593,7 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
             }
             fly[(head + nfly) % 2] = slot;
             ++nfly;
+            last_slot = slot;
             slot ^= 1;
         }
         if (rc || nfly == 0) break;
@@ -1598,19 +1602,33 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
         --nfly;
         const hipError_t e = hipEventSynchronize(c->loop_ev[s]);
         if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
-        if (hf[s].done) stop = true;
+        if (((const LoopState<T>*)(stat_slot(c, s) + kStatLoop))->done) stop = true;
+    }
+    // drain: the last issued batch's copy is the final status
+    while (rc == PMX_OK && nfly > 0) {
+        const hipError_t e = hipEventSynchronize(c->loop_ev[fly[head]]);
+        if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
+        head = (head + 1) % 2;
+        --nfly;
     }
     c->loop_on = false;
     if (rc) {
         (void)hipStreamSynchronize(c->stream);
         return rc;
     }
-    // the final state, the iteration block (limit, counters) and the control word
-    HIPCHK(c, hipMemcpyAsync(c->h_loop, c->d_loop, sizeof(LoopState<T>), hipMemcpyDeviceToHost, c->stream));
-    LoopCtl ctl{};
-    HIPCHK(c, hipMemcpyAsync(&ctl, c->d_ctl, sizeof(LoopCtl), hipMemcpyDeviceToHost, c->stream));
-    if ((rc = readback(c))) return rc;
-    const LoopState<T>& S = *(const LoopState<T>*)c->h_loop;
+    // the final state, the iteration block (limit, counters) and the control
+    // word: the last batch's status copy (no batch issued: one copy now)
+    if (last_slot < 0) {
+        last_slot = 0;
+        HIPCHK(c, hipMemcpyAsync(c->h_loop, c->d_result, kStatBytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    const char* fin = stat_slot(c, last_slot);
+    std::memcpy(c->h_result, fin, kBlkCopy);
+    resolve_events(c);
+    LoopCtl ctl;
+    std::memcpy(&ctl, fin + kStatCtl, sizeof(LoopCtl));
+    const LoopState<T>& S = *(const LoopState<T>*)(fin + kStatLoop);
     c->loop_iters = S.iter;
     c->loop_done = S.done != 0;
     c->level = ctl.level;
@@ -1949,6 +1967,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     c->select_split = std::getenv("PMX_SELECT_SPLIT") != nullptr;
     if (const char* e = std::getenv("PMX_SPEC_SELECT")) c->spec_allowed = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_FUSE_FINAL")) c->fuse_final = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_FOLD_COUNTER")) c->fold_counter = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_SELECT_ALL")) c->select_all = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
@@ -2000,9 +2019,11 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     //   [1152]        VarTrimmed ratio, [1216] pair-evaluation counter
     //   [1280, 1344)  point-to-point means (6 T)
     void* p = nullptr;
-    if (hipMalloc(&p, kBlkBytes) != hipSuccess) return bad(PMX_E_HIP);
-    (void)hipMemset(p, 0, kBlkBytes);
+    if (hipMalloc(&p, kStatBytes) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(p, 0, kStatBytes);
     c->d_result = (double*)p;
+    c->d_ctl = (LoopCtl*)((char*)p + kStatCtl);  // (zero: done = 0, kernels given it run normally)
+    c->d_loop = (char*)p + kStatLoop;
     c->d_sel = (SelectState*)((char*)p + kBlkSel);
     c->d_iter_err = (int*)(c->d_sel + 1);
     c->d_ratio = (double*)((char*)p + kBlkRatio);
@@ -2020,9 +2041,6 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     (void)hipMemset(c->d_selx, 0, selx_bytes());
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
     if (hipHostMalloc((void**)&c->h_result, kBlkBytes, hipHostMallocDefault) != hipSuccess) return bad(PMX_E_HIP);
-    // the device loop's control word (done = 0: kernels given it run normally)
-    if (hipMalloc((void**)&c->d_ctl, sizeof(LoopCtl)) != hipSuccess) return bad(PMX_E_HIP);
-    (void)hipMemset(c->d_ctl, 0, sizeof(LoopCtl));
     *out = c;
     return PMX_OK;
 }
@@ -2034,7 +2052,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     void* bufs[] = {c->d_safe, c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
-                    c->d_sel_more, c->d_ctl, c->d_gdesc, c->d_loop, c->d_loop_T0, c->d_trace,
+                    c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
                     c->d_rob, c->d_rdev};
     for (void* b : bufs)

@@ -460,10 +460,13 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
     __shared__ unsigned long long bc[2];
     const int t = threadIdx.x;
     unsigned long long v[4];
+    // (coherent loads / stores: with the fold the counters were added in this
+    // launch by other workgroups, possibly on other XCDs)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        v[c] = vpart[(size_t)(c * kVSlots + t) * kVStride];
-        vpart[(size_t)(c * kVSlots + t) * kVStride] = 0;  // ready for the next match
+        unsigned long long* p = vpart + (size_t)(c * kVSlots + t) * kVStride;
+        v[c] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next match
     }
     for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
@@ -486,7 +489,7 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
     if (!spec) return;
     if (xseg) {  // several ranks: this rank's segment [fin, below, n, keys...]
         using K = typename KeyOf<T>::K;
-        const unsigned nk = spec->n_keys;
+        const unsigned nk = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned nc = nk < kSpecXCap ? nk : kSpecXCap;
         const K* keys = (const K*)spec->keys;
         if (t == 0) {
@@ -494,14 +497,16 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
             xseg[1] = sum[3];
             xseg[2] = spec->valid ? nk : 0ull;
         }
-        for (unsigned i = t; i < nc; i += kVSlots) xseg[kSpecXHdr + i] = (unsigned long long)keys[i];
+        for (unsigned i = t; i < nc; i += kVSlots)
+            xseg[kSpecXHdr + i] = (unsigned long long)__hip_atomic_load(&keys[i], __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();  // (every lane read n_keys before it is reset)
         if (t == 0) spec->n_keys = 0;
         return;
     }
     SpecKeys<T> src;
     src.local = (const typename KeyOf<T>::K*)spec->keys;
-    const unsigned nk_raw = spec->n_keys;
+    const unsigned nk_raw = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     src.n_local = nk_raw < kSpecCap ? nk_raw : kSpecCap;
     (void)spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part, bc);
 }
@@ -516,6 +521,56 @@ __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long
                                                               unsigned long long* __restrict__ xseg) {
     if (ctl && ctl->done) return;
     counter_phase<T>(vpart, out, iter_err, spec, st, xseg);
+}
+
+// The counter phase folded into the match kernel (PMX_FOLD_COUNTER=1): the
+// last workgroup to finish runs it, one launch fewer per iteration.  Off by
+// default: measured at C3 (driver command) the match grew 22.4 -> 31.6 us
+// against 22.4 + 5.9 us for the two launches — every workgroup must drain its
+// stores before it takes its ticket, and that drain costs more than the
+// boundary it saves.  Every
+// value it reads was published by atomics or write-through (sc1) stores and
+// is read with coherent loads, so each workgroup only drains its memory
+// operations before it takes its ticket (cdna_hip_programming.md §6 G16,
+// the sc1 form of the in-launch reduction).
+// Tickets: one counter per group of workgroups (blockIdx % kTicketGroups, each
+// on its own 128-byte line), then one for the groups — a single counter
+// taken by all 4K workgroups serialises (measured: +27 us at C3).
+constexpr size_t kTicketOff = (size_t)4 * kVSlots * kVStride;  // (unsigned long longs into vpart)
+constexpr int kTicketGroups = 64;
+template <typename T>
+__device__ __forceinline__ void counter_fold(unsigned long long* __restrict__ vpart,
+                                             unsigned long long* __restrict__ out, int* __restrict__ iter_err,
+                                             SpecSel* __restrict__ spec, SelectState* __restrict__ st,
+                                             unsigned long long* __restrict__ xseg) {
+    __shared__ unsigned s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* tk = (unsigned*)(vpart + kTicketOff);  // [group g at g * 32] ..., top at kTicketGroups * 32
+    if (threadIdx.x == 0) {
+        const unsigned G = gridDim.x, b = blockIdx.x;
+        const unsigned g = b % kTicketGroups;
+        const unsigned ng = G < (unsigned)kTicketGroups ? G : (unsigned)kTicketGroups;
+        const unsigned gsize = (G - g + kTicketGroups - 1) / kTicketGroups;  // blocks with this residue
+        unsigned last = 0;
+        const unsigned o = __hip_atomic_fetch_add(tk + g * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o == gsize - 1) {
+            const unsigned t = __hip_atomic_fetch_add(tk + kTicketGroups * 32, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            last = t == ng - 1 ? 1u : 0u;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    counter_phase<T>(vpart, out, iter_err, spec, st, xseg);
+    for (int g = threadIdx.x; g <= kTicketGroups; g += blockDim.x)  // (every group's and the top counter)
+        __hip_atomic_store(tk + g * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Several ranks: resolve the quantile from the all-gathered window segments
@@ -557,7 +612,8 @@ template void launch_spec_pick<double>(const unsigned long long*, int, SpecSel*,
                                        hipStream_t);
 
 // counters: 0 pairs, 1 full-search fallbacks, 2 finite distances, 3 below the quantile window
-size_t grid_counter_bytes() { return sizeof(unsigned long long) * 4 * kVSlots * kVStride; }
+// (+ the fold tickets: kTicketGroups + 1 counters, 128 bytes apart)
+size_t grid_counter_bytes() { return sizeof(unsigned long long) * (4 * kVSlots * kVStride + 16 * (kTicketGroups + 1)); }
 
 // ---------------------------------------------------- temporal reuse --
 // ICP matches the same reading every iteration under a slowly changing
@@ -689,7 +745,9 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
                                                         int reuse, T* __restrict__ safe, Mat4<T> Tprev,
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
-                                                        SpecSel* __restrict__ spec) {
+                                                        SpecSel* __restrict__ spec, unsigned long long* __restrict__ vout,
+                                                        int* __restrict__ iter_err, SelectState* __restrict__ spec_st,
+                                                        unsigned long long* __restrict__ xseg) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -719,6 +777,7 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
             if ((threadIdx.x & 63) == 0 && visited && m) atomicAdd(vslot(visited, 1), (unsigned long long)__popcll(m));
         }
         if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
+        if (vout) counter_fold<T>(visited, vout, iter_err, spec, spec_st, xseg);
         return;
     }
     // Phase 1: every lane tries the certificate.  Phase 2: the block's misses,
@@ -755,6 +814,7 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
     // queries that took the full search (the "fallback" counter)
     if (threadIdx.x == 0 && visited && total) atomicAdd(vslot(visited, 1), (unsigned long long)total);
     if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
+    if (vout) counter_fold<T>(visited, vout, iter_err, spec, spec_st, xseg);
 }
 
 // ------------------------------------------------------------ tile kernel --
@@ -765,11 +825,12 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
+                      unsigned long long* vout, int* iter_err, SelectState* spec_st, unsigned long long* xseg,
                       hipStream_t s) {
     if (mode >= 1) {  // 1: shell search, 2: octant block first
         hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
                            start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe,
-                           ru.Tprev, ctl, gd, spec);
+                           ru.Tprev, ctl, gd, spec, vout, iter_err, spec_st, xseg);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -783,8 +844,9 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                       SelectState* spec_st, unsigned long long* xseg, hipEvent_t ev_end, hipStream_t s) {
+                       SelectState* spec_st, unsigned long long* xseg, bool fold, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
+    fold = fold && mode >= 1 && visited && vout;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -795,7 +857,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, s)
+                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, s)
     // with reuse the list keeps room for the (k+1)-th point (the safe radius)
     const int kl = ru.mode && mode >= 1 && knn < 16 ? knn + 1 : knn;
     if (kl == 1)
@@ -809,8 +871,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     else
         PMX_KT(16);
 #undef PMX_KT
-    if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel alone)
-    if (visited && vout)
+    if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel, with the folded counter phase)
+    if (visited && vout && !fold)  // (folded: the per-lane kernel's last workgroup ran it)
         hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
                            spec_st, xseg);
 }
@@ -820,13 +882,13 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, hipEvent_t, hipStream_t);
+                                       unsigned long long*, bool, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, hipEvent_t, hipStream_t);
+                                        unsigned long long*, bool, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

@@ -120,7 +120,8 @@ __device__ __forceinline__ void spec_acc(SpecAcc<T>& a, T d) {
             a.below += 1;
         } else if (k <= a.hi) {  // rare: a few thousand of k*N
             const unsigned pos = atomicAdd(a.n_keys, 1u);
-            if (pos < kSpecCap) a.keys[pos] = k;
+            // (write-through: the match kernel's last block reads the keys in the same launch)
+            if (pos < kSpecCap) __hip_atomic_store(&a.keys[pos], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -190,7 +191,9 @@ struct SpecKeys {
         return c < kSpecXCap ? (unsigned)c : kSpecXCap;
     }
     __device__ __forceinline__ K key(int s, unsigned i) const {
-        return segs ? (K)segs[(size_t)s * kSpecXStride + kSpecXHdr + i] : local[i];
+        // (local keys: appended in the same launch when the match's last block picks: coherent loads)
+        return segs ? (K)segs[(size_t)s * kSpecXStride + kSpecXHdr + i]
+                    : __hip_atomic_load(&local[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 };
 

@@ -242,3 +242,27 @@ def test_select_all_passes_in_one_launch(monkeypatch, dtype, filt, knn, max_dist
     assert s1 == s0
     assert kept1 == kept0 and lim1 == lim0
     assert np.array_equal(tr1, tr0)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_counter_fold_equals_counter_kernel(monkeypatch, dtype):
+    """PMX_FOLD_COUNTER=1 (the counter phase and the quantile-window pick in
+    the match kernel's last workgroup, two-level tickets, coherent loads of
+    the counters and window keys) leaves whole loops bit-identical to the
+    separate counter_sum kernel."""
+    ref, nrm = reference_cloud(60000, dtype)
+    rd = reading_cloud(50000, dtype)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PMX_FOLD_COUNTER", mode)
+        ctx = _capi.Context(0, dtype)
+        ctx.set_reference(ref, nrm)
+        ctx.set_reading(rd)
+        ctx.loop_begin(filters=[("TrimmedDistOutlierFilter", 0.85)],
+                       checkers=[("CounterTransformationChecker", 30)], keep_trace=True)
+        st = ctx.loop_run(30)
+        out[mode] = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept,
+                     st.point_count_touched, st.last.limit)
+        ctx.close()
+    assert out["1"][1] == out["0"][1] and out["1"][2:] == out["0"][2:]
+    assert np.array_equal(out["1"][0], out["0"][0])
