@@ -129,6 +129,12 @@ int pmx_set_reference(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const
 /* reading shard: rows x N.  T0 (rows x rows, row-major T) is applied once on
  * the device (T_refMean_dataIn, ICP.cpp:345-347). */
 int pmx_set_reading(pmx_ctx* ctx, const void* feat, int rows, int64_t N, const void* T0);
+/* KDTreeVarDistMatcher (MatchersImpl.cpp:106-150): a maximum search radius
+ * per reading point (its maxDistField descriptor, N T values in the order of
+ * pmx_set_reading's points; NULL clears).  While set, pmx_match uses these
+ * radii (squared in T, as libnabo does) instead of its maxDist.  Cleared by
+ * the next pmx_set_reading. */
+int pmx_set_reading_radii(pmx_ctx* ctx, const void* radii);
 
 /* ------------------------------------------------------------- match --- */
 /* search structure, mirroring KDTreeMatcher's searchType
@@ -300,6 +306,17 @@ int pmx_sampling_surface_normals(int device, int dtype, const void* feat, int ro
                                  int desc_dim, int knn, int sampling_method, double ratio, double max_box_dim,
                                  unsigned flags, void* feat_out, void* desc_out, void* normals, void* densities,
                                  void* eig_values, void* eig_vectors, int64_t* n_out, int64_t* unfit);
+
+/* VoxelGridDataPointsFilter (DataPointsFilters/VoxelGrid.cpp:60-343): one
+ * point per occupied voxel (vsize: vSizeX, vSizeY, vSizeZ), the voxel's
+ * first point, with useCentroid its features replaced by the voxel mean, else
+ * feature rows 1..3 set to the voxel centre as the reference does; descriptors
+ * (desc_dim x n, may be NULL) averaged when average_desc.  Kept points in
+ * index order; feat_out / desc_out hold n points.  Bit-identical to the
+ * reference (sequential T sums in point order). */
+int pmx_voxel_grid(int device, int dtype, const void* feat, int rows, int64_t n, const void* desc, int desc_dim,
+                   const double* vsize, int use_centroid, int average_desc, void* feat_out, void* desc_out,
+                   int64_t* n_out);
 
 #ifdef __cplusplus
 }

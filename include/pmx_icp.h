@@ -70,6 +70,12 @@ int pmx_icp_keep_trace(pmx_icp* icp, int on);
 int pmx_icp_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
                     const void* ref_normals, const void* T_init, void* T_out);
 
+/* DataPoints descriptors (PointMatcher.h:207-358) for the next compute /
+ * prepare: cloud 0 = reading, 1 = reference; span rows x n points,
+ * point-major, dtype of the ICP (e.g. the reading's "maxSearchDist" for
+ * KDTreeVarDistMatcher).  Consumed by that call. */
+int pmx_icp_add_descriptor(pmx_icp* icp, int cloud, const char* name, int span, const void* values, int64_t n);
+
 /* the same loop in phases (bench: time the iterations alone) */
 int pmx_icp_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
                     const void* ref_normals, const void* T_init);

@@ -145,11 +145,11 @@ EXPORTS = [
     "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_set_reference", "pmx_set_reading", "pmx_set_search", "pmx_match",
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed", "pmx_outlier_robust",
-    "pmx_robust_scale",
+    "pmx_robust_scale", "pmx_set_reading_radii",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
     "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_surface_normals",
-    "pmx_sampling_surface_normals",
+    "pmx_sampling_surface_normals", "pmx_voxel_grid",
 ]
 
 
@@ -181,6 +181,7 @@ def lib():
         l.pmx_outlier_robust.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, C.c_double,
                                          C.c_int]
         l.pmx_robust_scale.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double)]
+        l.pmx_set_reading_radii.argtypes = [C.c_void_p, C.c_void_p]
         l.pmx_p2plane_system.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(Stats)]
         l.pmx_p2point_system.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.POINTER(Stats)]
@@ -197,6 +198,9 @@ def lib():
         l.pmx_loop_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         l.pmx_surface_normals.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_double,
                                           C.c_uint] + [C.c_void_p] * 6 + [C.POINTER(C.c_int64)]
+        l.pmx_voxel_grid.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int,
+                                     C.POINTER(C.c_double), C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                     C.POINTER(C.c_int64)]
         l.pmx_sampling_surface_normals.argtypes = ([C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
                                                     C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_uint]
                                                    + [C.c_void_p] * 6 + [C.POINTER(C.c_int64)] * 2)
@@ -276,6 +280,32 @@ def sampling_surface_normals(points, descriptors=None, knn=7, sampling_method=0,
     res = {k: v[:m] for k, v in out.items()}
     res["unfit"] = unfit.value
     return res
+
+
+def voxel_grid(points, descriptors=None, vsize=(1.0, 1.0, 1.0), use_centroid=True, average_descriptors=True,
+               device=0):
+    """VoxelGridDataPointsFilter (DataPointsFilters/VoxelGrid.cpp:60-343) on the
+    GPU (pmx_voxel_grid).  points (n, rows) with the homogeneous row last;
+    descriptors (n, desc_dim) or None.  Returns (features, descriptors) of
+    the kept points, in index order."""
+    pts = np.ascontiguousarray(points)
+    if pts.dtype not in (np.float32, np.float64):
+        pts = pts.astype(np.float32)
+    dt = pts.dtype
+    n, rows = pts.shape
+    dd = 0 if descriptors is None else descriptors.shape[1]
+    desc = None if descriptors is None else np.ascontiguousarray(descriptors, dtype=dt)
+    of = np.empty((n, rows), dt)
+    od = np.empty((n, dd), dt)
+    vs = (C.c_double * 3)(*[float(v) for v in vsize])
+    no = C.c_int64(0)
+    l = lib()
+    rc = l.pmx_voxel_grid(int(device), PMX_F64 if dt == np.float64 else PMX_F32, _ptr(pts), rows, n, _ptr(desc), dd,
+                          vs, 1 if use_centroid else 0, 1 if average_descriptors else 0, _ptr(of),
+                          _ptr(od) if dd else None, C.byref(no))
+    if rc != PMX_OK:
+        raise_for(rc, l.pmx_last_error(None).decode())
+    return of[:no.value], od[:no.value]
 
 
 def _ptr(a):
@@ -363,6 +393,11 @@ class Context:
         T0 = self._arr(np.eye(rows) if T0 is None else T0)
         self.N = feat.shape[0]
         self._chk(self._l.pmx_set_reading(self.h, _ptr(feat), rows, feat.shape[0], _ptr(T0)))
+
+    def set_reading_radii(self, radii):
+        """KDTreeVarDistMatcher: one search radius per reading point (None clears)."""
+        r = self._arr(radii) if radii is not None else None
+        self._chk(self._l.pmx_set_reading_radii(self.h, _ptr(r) if r is not None else None))
 
     # --- per-iteration
     def set_search(self, search_type: int):

@@ -9,6 +9,15 @@ using namespace pm;
 
 struct pmx_icp {
     int dtype = 0;
+    // descriptors staged for the next compute / prepare: (cloud 0 reading /
+    // 1 reference, name, span, point-major values as doubles)
+    struct Desc {
+        int cloud;
+        std::string name;
+        int span;
+        std::vector<double> v;
+    };
+    std::vector<Desc> staged;
     std::unique_ptr<PointMatcher<float>::ICP> f;
     std::unique_ptr<PointMatcher<double>::ICP> d;
     std::string err;
@@ -75,6 +84,16 @@ void prepare_impl(pmx_icp* icp, const void* reading, int rows, int64_t N, const 
                   const void* nrm, const void* T_init) {
     auto rd = make_cloud<T>(reading, rows, N, nullptr);
     auto ref = make_cloud<T>(reference, rows, M, nrm);
+    for (const auto& d : icp->staged) {
+        auto& cl = d.cloud == 0 ? rd : ref;
+        const int64_t n = d.cloud == 0 ? N : M;
+        if ((int64_t)d.v.size() != n * d.span)
+            throw InvalidParameter("descriptor " + d.name + ": " + std::to_string(d.v.size() / std::max(d.span, 1)) +
+                                   " points staged for a cloud of " + std::to_string(n));
+        std::vector<T> t(d.v.begin(), d.v.end());
+        cl.addDescriptor(d.name, d.span, t.data());
+    }
+    icp->staged.clear();
     std::vector<T> Ti((size_t)rows * rows, (T)0);
     if (T_init) {
         const T* p = static_cast<const T*>(T_init);
@@ -190,6 +209,17 @@ int pmx_icp_iterate(pmx_icp* icp, int n, int* done) {
 
 int pmx_icp_finish(pmx_icp* icp, void* T_out) {
     return guarded(icp, [&] { BOTH(icp, finish_impl<float>(icp, T_out), finish_impl<double>(icp, T_out)); });
+}
+
+int pmx_icp_add_descriptor(pmx_icp* icp, int cloud, const char* name, int span, const void* values, int64_t n) {
+    if (!icp || !name || span < 1 || (!values && n > 0) || (cloud != 0 && cloud != 1))
+        return PMX_ICP_INVALID_PARAMETER;
+    pmx_icp::Desc d{cloud, name, span, {}};
+    d.v.resize((size_t)(n * span));
+    for (int64_t i = 0; i < n * span; ++i)
+        d.v[(size_t)i] = icp->dtype == 1 ? ((const double*)values)[i] : (double)((const float*)values)[i];
+    icp->staged.push_back(std::move(d));
+    return PMX_ICP_OK;
 }
 
 int pmx_icp_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,

@@ -2,7 +2,7 @@
 //
 // Module names, parameter names, defaults and bounds are those of the
 // reference so that libpointmatcher YAML chain files load unchanged:
-//   KDTreeMatcher                 MatchersImpl.h:74-103
+//   KDTreeMatcher, KDTreeVarDistMatcher  MatchersImpl.h:74-134
 //   Null/MaxDist/MinDist/MedianDist/TrimmedDist/VarTrimmedDist/Robust OutlierFilter
 //                                 OutlierFiltersImpl.h:51-260
 //   PointToPlane / PointToPoint ErrorMinimizer
@@ -99,6 +99,39 @@ template <typename T>
 using PM = PointMatcher<T>;
 
 // ---- KDTreeMatcher on the GPU (exact search; see pmx_match.hip) ----------
+// Matcher::init of both kd-tree matchers: the reference (and its normals,
+// for the point-to-plane minimiser) to HBM, the search structure built there
+template <typename T>
+void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType) {
+    dev.ensure();
+    std::vector<T> nrm;
+    const T* np = nullptr;
+    if (ref.descriptorExists("normals")) {
+        int span = 0;
+        nrm = ref.descriptor("normals", &span);
+        if (span < ref.rows - 1) throw InvalidElement("normals descriptor has fewer rows than the dimension");
+        if (span != ref.rows - 1) {
+            std::vector<T> t((size_t)(ref.rows - 1) * ref.n);
+            for (int64_t i = 0; i < ref.n; ++i)
+                for (int r = 0; r < ref.rows - 1; ++r) t[i * (ref.rows - 1) + r] = nrm[i * span + r];
+            nrm.swap(t);
+        }
+        np = nrm.data();
+    }
+    dev.check(pmx_set_search(dev.ctx, searchType));  // 0: brute force, 1/2: exact grid search
+    dev.check(pmx_set_reference(dev.ctx, ref.features.data(), ref.rows, ref.n, np));
+}
+template <typename T>
+typename PM<T>::Matches device_matches(Device& dev, int knn) {
+    typename PM<T>::Matches m;
+    m.dev = &dev;
+    m.knn = knn;
+    int64_t n = 0;
+    pmx_get_shape(dev.ctx, &n, nullptr);
+    m.n = n;
+    return m;
+}
+
 template <typename T>
 struct KDTreeMatcherGPU : PM<T>::Matcher {
     typedef typename PM<T>::Matches Matches;
@@ -123,40 +156,63 @@ struct KDTreeMatcherGPU : PM<T>::Matcher {
           searchType(this->template get<int>("searchType")),
           maxDist(this->template get<T>("maxDist")) {}
 
-    void init(Device& dev, const DataPoints<T>& ref) override {
-        dev.ensure();
-        std::vector<T> nrm;
-        const T* np = nullptr;
-        if (ref.descriptorExists("normals")) {
-            int span = 0;
-            nrm = ref.descriptor("normals", &span);
-            if (span < ref.rows - 1) throw InvalidElement("normals descriptor has fewer rows than the dimension");
-            if (span != ref.rows - 1) {
-                std::vector<T> t((size_t)(ref.rows - 1) * ref.n);
-                for (int64_t i = 0; i < ref.n; ++i)
-                    for (int r = 0; r < ref.rows - 1; ++r) t[i * (ref.rows - 1) + r] = nrm[i * span + r];
-                nrm.swap(t);
-            }
-            np = nrm.data();
-        }
-        dev.check(pmx_set_search(dev.ctx, searchType));  // 0: brute force, 1/2: exact grid search
-        dev.check(pmx_set_reference(dev.ctx, ref.features.data(), ref.rows, ref.n, np));
-    }
+    void init(Device& dev, const DataPoints<T>& ref) override { matcher_init<T>(dev, ref, searchType); }
     Matches findClosests(Device& dev, const std::vector<T>& T_iter) override {
         // PointCountTouched is added from the minimiser's pmx_stats.visited
         // once the (asynchronous) match has completed, see ICP::step
         dev.check(pmx_match(dev.ctx, T_iter.data(), knn, (double)maxDist, (double)epsilon, nullptr));
-        Matches m;
-        m.dev = &dev;
-        m.knn = knn;
-        int64_t n = 0;
-        pmx_get_shape(dev.ctx, &n, nullptr);
-        m.n = n;
-        return m;
+        return device_matches<T>(dev, knn);
     }
     bool loopConfig(pmx_loop_cfg& cfg) const override {
         cfg.knn = knn;
         cfg.max_dist = (double)maxDist;
+        return true;
+    }
+};
+
+// ---- KDTreeVarDistMatcher (MatchersImpl.h:105-134, MatchersImpl.cpp:106-150):
+// the radius of each reading point is its maxDistField descriptor; the GPU
+// search takes the radii per query (pmx_set_reading_radii)
+template <typename T>
+struct KDTreeVarDistMatcherGPU : PM<T>::Matcher {
+    typedef typename PM<T>::Matches Matches;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("knn", "number of nearest neighbors to consider it the reference", "1", "1", "2147483647",
+                     &Parametrizable::Comp<unsigned>),
+                PDoc("epsilon", "approximation to use for the nearest-neighbor search", "0", "0", "inf",
+                     &Parametrizable::Comp<T>),
+                PDoc("searchType", "Nabo search type (the GPU search is exact for every type)", "1", "0", "2",
+                     &Parametrizable::Comp<unsigned>),
+                PDoc("maxDistField", "descriptor field name used to set a maximum distance to consider for neighbors "
+                                     "per point", "maxSearchDist")};
+    }
+    int knn;
+    T epsilon;
+    int searchType;
+    std::string maxDistField;
+    explicit KDTreeVarDistMatcherGPU(const Parametrizable::Parameters& p)
+        : PM<T>::Matcher("KDTreeVarDistMatcher", doc(), p),
+          knn(this->template get<int>("knn")),
+          epsilon(this->template get<T>("epsilon")),
+          searchType(this->template get<int>("searchType")),
+          maxDistField(this->template get<std::string>("maxDistField")) {}
+    void init(Device& dev, const DataPoints<T>& ref) override { matcher_init<T>(dev, ref, searchType); }
+    void initReading(Device& dev, const DataPoints<T>& reading) override {
+        // getDescriptorViewByName(maxDistField).transpose(): one radius per point
+        int span = 0;
+        const std::vector<T> r = reading.descriptor(maxDistField, &span);
+        if (span != 1)
+            throw InvalidElement("KDTreeVarDistMatcher: descriptor " + maxDistField + " must have one row, not " +
+                                 std::to_string(span));
+        dev.check(pmx_set_reading_radii(dev.ctx, r.data()));
+    }
+    Matches findClosests(Device& dev, const std::vector<T>& T_iter) override {
+        dev.check(pmx_match(dev.ctx, T_iter.data(), knn, INFINITY, (double)epsilon, nullptr));
+        return device_matches<T>(dev, knn);
+    }
+    bool loopConfig(pmx_loop_cfg& cfg) const override {
+        cfg.knn = knn;
+        cfg.max_dist = INFINITY;  // (the per-point radii stay set on the context)
         return true;
     }
 };
@@ -846,6 +902,54 @@ struct FixStepSamplingDPF : PM<T>::DataPointsFilter {
 // (pmx_sampling_surface_normals, pmx_ssn.hip); existing descriptors averaged
 // per leaf (samplingMethod 1) or kept, the new ones in the reference's label
 // order.
+// VoxelGridDataPointsFilter (DataPointsFilters/VoxelGrid.h:40-98,
+// VoxelGrid.cpp:60-343) on the device (pmx_voxel_grid)
+template <typename T>
+struct VoxelGridDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("vSizeX", "Dimension of each voxel cell in x direction", "1.0", "0.001", "+inf", &P::Comp<T>),
+                PDoc("vSizeY", "Dimension of each voxel cell in y direction", "1.0", "0.001", "+inf", &P::Comp<T>),
+                PDoc("vSizeZ", "Dimension of each voxel cell in z direction", "1.0", "0.001", "+inf", &P::Comp<T>),
+                PDoc("useCentroid", "If 1 (true), down-sample by using centroid of voxel cell.  If false (0), use "
+                                    "center of voxel cell.", "1", "0", "1", &P::Comp<bool>),
+                PDoc("averageExistingDescriptors", "whether the filter keep the existing point descriptors and average "
+                                                   "them or should it drop them", "1", "0", "1", &P::Comp<bool>)};
+    }
+    T vSizeX, vSizeY, vSizeZ;
+    bool useCentroid, averageExistingDescriptors;
+    explicit VoxelGridDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter("VoxelGridDataPointsFilter", doc(), p),
+          vSizeX(this->template get<T>("vSizeX")),
+          vSizeY(this->template get<T>("vSizeY")),
+          vSizeZ(this->template get<T>("vSizeZ")),
+          useCentroid(this->template get<bool>("useCentroid")),
+          averageExistingDescriptors(this->template get<bool>("averageExistingDescriptors")) {}
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        if (averageExistingDescriptors) {  // (VoxelGrid.cpp:83-90)
+            int sum = 0;
+            for (auto& l : cloud.descriptorLabels) sum += l.span;
+            if (sum != cloud.descDim)
+                throw InvalidElement("VoxelGridDataPointsFilter: Error, descriptor labels do not match descriptor data");
+        }
+        const int64_t n = cloud.n;
+        std::vector<T> feat((size_t)(n * cloud.rows)), desc((size_t)(n * cloud.descDim));
+        const double vs[3] = {(double)vSizeX, (double)vSizeY, (double)vSizeZ};
+        int64_t nout = 0;
+        const int rc = pmx_voxel_grid(this->device, dtype_of<T>(), cloud.features.data(), cloud.rows, n,
+                                      cloud.descDim ? cloud.descriptors.data() : nullptr, cloud.descDim, vs,
+                                      useCentroid ? 1 : 0, averageExistingDescriptors ? 1 : 0, feat.data(),
+                                      cloud.descDim ? desc.data() : nullptr, &nout);
+        if (rc == PMX_E_BAD_PARAM) throw InvalidParameter(pmx_last_error(nullptr));
+        if (rc) throw std::runtime_error(std::string("VoxelGridDataPointsFilter: ") + pmx_last_error(nullptr));
+        cloud.n = nout;
+        feat.resize((size_t)(nout * cloud.rows));
+        cloud.features.swap(feat);
+        desc.resize((size_t)(nout * cloud.descDim));
+        cloud.descriptors.swap(desc);
+    }
+};
+
 template <typename T>
 struct SamplingSurfaceNormalDPF : PM<T>::DataPointsFilter {
     typedef Parametrizable P;
@@ -968,6 +1072,10 @@ PointMatcher<T>::PointMatcher() {
     typedef Parametrizable::Parameters Ps;
     MatcherRegistrar.reg("KDTreeMatcher", [](const Ps& p) { return std::make_shared<KDTreeMatcherGPU<T>>(p); }, true,
                          "This matcher matches a point from the reading to its closest neighbors in the reference.");
+    MatcherRegistrar.reg("KDTreeVarDistMatcher",
+                         [](const Ps& p) { return std::make_shared<KDTreeVarDistMatcherGPU<T>>(p); }, true,
+                         "This matcher matches a point from the reading to its closest neighbors in the reference. A "
+                         "maximum search radius per point can be defined.");
     OutlierFilterRegistrar.reg("NullOutlierFilter", [](const Ps& p) { return std::make_shared<NullOF<T>>(p); }, false);
     OutlierFilterRegistrar.reg("MaxDistOutlierFilter", [](const Ps& p) { return std::make_shared<MaxDistOF<T>>(p); }, true);
     OutlierFilterRegistrar.reg("MinDistOutlierFilter", [](const Ps& p) { return std::make_shared<MinDistOF<T>>(p); }, true);
@@ -1003,6 +1111,8 @@ PointMatcher<T>::PointMatcher() {
                                   [](const Ps& p) { return std::make_shared<DistDPF<T, true>>(p); }, true);
     DataPointsFilterRegistrar.reg("MinDistDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<DistDPF<T, false>>(p); }, true);
+    DataPointsFilterRegistrar.reg("VoxelGridDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<VoxelGridDPF<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("SamplingSurfaceNormalDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<SamplingSurfaceNormalDPF<T>>(p); }, true);
     InspectorRegistrar.reg("NullInspector", [](const Ps& p) {
@@ -1213,6 +1323,7 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
         throw TransformationError("RigidTransformation: Error, rotation matrix is not orthogonal.");
     // transformations.apply(reading, T_refMean_dataIn): done on the device
     dev.check(pmx_set_reading(dev.ctx, reading.features.data(), dim, reading.n, T_refMean_dataIn_.data()));
+    matcher->initReading(dev, reading);  // (per-reading matcher inputs: KDTreeVarDistMatcher's radii)
     rows_ = dim;
     T_iter_.assign((size_t)dim * dim, (T)0);
     for (int i = 0; i < dim; ++i) T_iter_[i * dim + i] = 1;

@@ -71,6 +71,9 @@ struct PointMatcher {
         void resetVisitCount() { visitCounter = 0; }
         uint64_t getVisitCount() const { return visitCounter; }
         virtual void init(Device& dev, const DataPoints& filteredReference) = 0;
+        // the reading's inputs of the match, once per compute after the
+        // reading upload (KDTreeVarDistMatcher: its per-point radii)
+        virtual void initReading(Device&, const DataPoints&) {}
         virtual Matches findClosests(Device& dev, const TransformationParameters& T_iter) = 0;
         // device loop (pmx_loop_*): describe this module in cfg, or return
         // false to keep the per-module calls (the default for any plugin)

@@ -126,6 +126,10 @@ struct pmx_ctx {
     // reading shard
     int64_t N = 0, N_total = 0, N_max = 0;
     void* d_rd = nullptr;
+    // KDTreeVarDistMatcher: per-point search radii in slot order (pmx_set_reading_radii)
+    void* d_radii = nullptr;
+    size_t radii_bytes = 0;
+    bool has_radii = false;
 
     // matches / weights
     int knn = 0;
@@ -684,6 +688,7 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     const Mat4<T> M0 = embed<T>(T0, rows);
     int rc;
     const int64_t n1 = std::max<int64_t>(N, 1);
+    c->has_radii = false;  // (a new reading: its radii, if any, follow)
     // raw P4 reading (pack), then the slot order, then T_refMean_dataIn
     void* d_p4 = nullptr;
     HIPCHK(c, hipMalloc(&d_p4, sizeof(P4<T>) * n1));
@@ -841,6 +846,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         launch_match<T>((const P4<T>*)c->d_ref, c->M_pad, (const P4<T>*)c->d_rd, c->N, Tm, knn, maxR2,
                         (T*)c->d_dists, c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1,
                         c->cu_count);
+        if (c->has_radii)
+            launch_apply_radii<T>((T*)c->d_dists, c->d_ids, (const T*)c->d_radii, c->N, knn, c->stream);
         c->visited_host = (uint64_t)c->N * (uint64_t)c->M;
         c->ids_grid = false;
         c->safe_valid = false;
@@ -866,7 +873,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->fold_counter, e1, c->stream);  // (e1 recorded after the match kernel, before the counter sum)
+                             c->fold_counter, c->has_radii ? (const T*)c->d_radii : nullptr, e1, c->stream);  // (e1 recorded after the match kernel, before the counter sum)
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
@@ -1190,6 +1197,26 @@ int outlier_robust_impl(pmx_ctx* c, int pos, int fct, double tuning, double appr
     c->rb_sqa = std::isinf(approx) ? INFINITY : (double)(T)std::pow((double)(T)approx, 2.0);
     c->rb_p2pl = p2pl;
     HIPCHK(c, hipGetLastError());
+    return PMX_OK;
+}
+
+template <typename T>
+int set_radii_impl(pmx_ctx* c, const T* radii) {
+    if (!radii) {
+        c->has_radii = false;
+        return PMX_OK;
+    }
+    if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "pmx_set_reading must be called first");
+    const int64_t n1 = std::max<int64_t>(c->N, 1);
+    int rc;
+    if ((rc = ensure(c, &c->d_radii, &c->radii_bytes, 2 * sizeof(T) * (size_t)n1))) return rc;
+    T* raw = (T*)c->d_radii + n1;  // (upload half, then the slot-order half)
+    HIPCHK(c, hipMemcpyAsync(raw, radii, sizeof(T) * (size_t)c->N, hipMemcpyHostToDevice, c->stream));
+    launch_gather_scalar<T>(raw, c->has_order ? c->d_order : nullptr, c->N, (T*)c->d_radii, c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (the caller's buffer may go)
+    c->has_radii = true;
+    c->safe_valid = false;  // (the previous match used other radii)
     return PMX_OK;
 }
 
@@ -1818,6 +1845,54 @@ int surface_normals_impl(int device, const T* feat, int rows, int64_t n, int knn
 // here — fuseRange's draws in leaf order (:285-309), the output in index
 // order (:145-164).
 template <typename T>
+int voxel_impl(int device, const T* feat, int rows, int64_t n, const T* desc, int desc_dim, const double* vsize,
+               bool centroid, bool avg, T* feat_out, T* desc_out, int64_t* n_out) {
+    if (rows != 3 && rows != 4) {
+        g_err = "VoxelGridDataPointsFilter: clouds must be 2-D or 3-D (3 or 4 homogeneous rows)";
+        return PMX_E_BAD_PARAM;
+    }
+    *n_out = 0;
+    if (n <= 0) return PMX_OK;
+    if (hipSetDevice(device) != hipSuccess) {
+        g_err = "VoxelGridDataPointsFilter: no HIP device";
+        return PMX_E_HIP;
+    }
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return PMX_E_HIP;
+    std::unique_ptr<std::remove_pointer<hipStream_t>::type, void (*)(hipStream_t)> free_st(
+        st, [](hipStream_t s) { (void)hipStreamDestroy(s); });
+    const size_t fb = sizeof(T) * (size_t)rows * n, db = sizeof(T) * (size_t)desc_dim * n;
+    char* buf = nullptr;
+    if (hipMalloc(&buf, 2 * (fb + db) + 512) != hipSuccess) {
+        g_err = "VoxelGridDataPointsFilter: device allocation failed";
+        return PMX_E_HIP;
+    }
+    std::unique_ptr<void, void (*)(void*)> free_buf(buf, [](void* p) { (void)hipFree(p); });
+    T* d_f = (T*)buf;
+    T* d_d = (T*)(buf + ((fb + 255) & ~(size_t)255));
+    T* d_of = (T*)((char*)d_d + ((db + 255) & ~(size_t)255));
+    T* d_od = d_of + (size_t)rows * n;
+    if (hipMemcpyAsync(d_f, feat, fb, hipMemcpyHostToDevice, st) != hipSuccess) return PMX_E_HIP;
+    if (db && hipMemcpyAsync(d_d, desc, db, hipMemcpyHostToDevice, st) != hipSuccess) return PMX_E_HIP;
+    std::string err;
+    int64_t m = 0;
+    const int rc = voxel_run<T>(d_f, rows, n, db ? d_d : nullptr, desc_dim, vsize, centroid, avg, d_of, d_od, &m, st,
+                                err);
+    if (rc) {
+        g_err = err.empty() ? std::string("VoxelGridDataPointsFilter: HIP failure") : err;
+        return rc;
+    }
+    if (hipMemcpyAsync(feat_out, d_of, sizeof(T) * (size_t)rows * m, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return PMX_E_HIP;
+    if (db && desc_out &&
+        hipMemcpyAsync(desc_out, d_od, sizeof(T) * (size_t)desc_dim * m, hipMemcpyDeviceToHost, st) != hipSuccess)
+        return PMX_E_HIP;
+    if (hipStreamSynchronize(st) != hipSuccess) return PMX_E_HIP;
+    *n_out = m;
+    return PMX_OK;
+}
+
+template <typename T>
 int ssn_impl(int device, const T* feat, int rows, int64_t n, const T* desc, int desc_dim, int knn, int method,
              double ratio_d, double max_box_d, unsigned flags, T* feat_out, T* desc_out, T* o_nrm, T* o_dens,
              T* o_eval, T* o_evec, int64_t* n_out, int64_t* unfit_out) {
@@ -2054,7 +2129,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
-                    c->d_rob, c->d_rdev};
+                    c->d_rob, c->d_rdev, c->d_radii};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();
@@ -2132,6 +2207,12 @@ int pmx_set_reading(pmx_ctx* c, const void* feat, int rows, int64_t N, const voi
     (void)hipSetDevice(c->device);
     return DISPATCH(c, set_reading_impl<float>(c, (const float*)feat, rows, N, (const float*)T0),
                     set_reading_impl<double>(c, (const double*)feat, rows, N, (const double*)T0));
+}
+
+int pmx_set_reading_radii(pmx_ctx* c, const void* radii) {
+    if (!c) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c, set_radii_impl<float>(c, (const float*)radii), set_radii_impl<double>(c, (const double*)radii));
 }
 
 int pmx_match(pmx_ctx* c, const void* T_iter, int knn, double maxDist, double epsilon, uint64_t* visited) {
@@ -2268,6 +2349,24 @@ int pmx_sampling_surface_normals(int device, int dtype, const void* feat, int ro
                                 sampling_method, ratio, max_box_dim, flags, (double*)feat_out, (double*)desc_out,
                                 (double*)normals, (double*)densities, (double*)eig_values, (double*)eig_vectors,
                                 n_out, unfit);
+    g_err = "dtype must be PMX_F32 or PMX_F64";
+    return PMX_E_BAD_PARAM;
+}
+
+int pmx_voxel_grid(int device, int dtype, const void* feat, int rows, int64_t n, const void* desc, int desc_dim,
+                   const double* vsize, int use_centroid, int average_desc, void* feat_out, void* desc_out,
+                   int64_t* n_out) {
+    if ((!feat && n > 0) || (desc_dim > 0 && !desc && n > 0) || !vsize || !n_out || (!feat_out && n > 0) ||
+        desc_dim < 0) {
+        g_err = "null argument";
+        return PMX_E_BAD_PARAM;
+    }
+    if (dtype == PMX_F32)
+        return voxel_impl<float>(device, (const float*)feat, rows, n, (const float*)desc, desc_dim, vsize,
+                                 use_centroid != 0, average_desc != 0, (float*)feat_out, (float*)desc_out, n_out);
+    if (dtype == PMX_F64)
+        return voxel_impl<double>(device, (const double*)feat, rows, n, (const double*)desc, desc_dim, vsize,
+                                  use_centroid != 0, average_desc != 0, (double*)feat_out, (double*)desc_out, n_out);
     g_err = "dtype must be PMX_F32 or PMX_F64";
     return PMX_E_BAD_PARAM;
 }

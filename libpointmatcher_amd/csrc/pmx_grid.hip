@@ -656,6 +656,16 @@ __device__ __forceinline__ T safe_radius(const T (&kd)[KT], const int32_t (&ki)[
     return (T)(r * (1.0 - 1e-6));  // (rounded down into T)
 }
 
+// the squared search radius of query j: the per-point radii of
+// KDTreeVarDistMatcher (MatchersImpl.cpp:131-146; libnabo squares each in T),
+// else the matcher's maxDist^2
+template <typename T>
+__device__ __forceinline__ T qr2(const T* __restrict__ radii, int64_t j, T maxR2) {
+    if (!radii) return maxR2;
+    const T r = radii[j];
+    return r * r;
+}
+
 // one query from scratch: octant block (oct) or the shell search
 template <typename T, int KT>
 __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
@@ -747,7 +757,8 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
                                                         const GridDesc<T>* __restrict__ gd,
                                                         SpecSel* __restrict__ spec, unsigned long long* __restrict__ vout,
                                                         int* __restrict__ iter_err, SelectState* __restrict__ spec_st,
-                                                        unsigned long long* __restrict__ xseg) {
+                                                        unsigned long long* __restrict__ xseg,
+                                                        const T* __restrict__ radii) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -770,7 +781,8 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
     if (reuse < 2) {
         const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
         if (j < N)
-            full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, maxR2, oct, out_d, out_i, safe, visits, sa);
+            full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, qr2(radii, j, maxR2), oct, out_d, out_i, safe,
+                              visits, sa);
         add_visits(visits, visited);
         if (reuse) {  // every query took the full search (the counter the level choice reads)
             const unsigned long long m = __ballot(j < N);
@@ -792,7 +804,8 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
         const P4<T> p = gld(rd, j);
         T qx, qy, qz;
         gxform(Tm, p, qx, qy, qz);
-        missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, maxR2, out_d, out_i, safe, visits, sa);
+        missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, qr2(radii, j, maxR2), out_d, out_i, safe,
+                                     visits, sa);
     }
     const unsigned long long m = __ballot(missed);
     if (lane == 0) wave_cnt[wave] = __popcll(m);
@@ -808,7 +821,8 @@ __global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict_
     __syncthreads();
     if ((int)threadIdx.x < total) {
         const int64_t j2 = (int64_t)blockIdx.x * blockDim.x + miss[threadIdx.x];
-        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, maxR2, oct, out_d, out_i, safe, visits, sa);
+        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
+                          sa);
     }
     add_visits(visits, visited);
     // queries that took the full search (the "fallback" counter)
@@ -826,15 +840,15 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                       unsigned long long* vout, int* iter_err, SelectState* spec_st, unsigned long long* xseg,
-                      hipStream_t s) {
+                      const T* radii, hipStream_t s) {
     if (mode >= 1) {  // 1: shell search, 2: octant block first
         hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
                            start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe,
-                           ru.Tprev, ctl, gd, spec, vout, iter_err, spec_st, xseg);
+                           ru.Tprev, ctl, gd, spec, vout, iter_err, spec_st, xseg, radii);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
-                           waves, Tm, knn, maxR2, max_pts, dists, ids, visited);
+                           waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii);
     }
 }
 
@@ -844,7 +858,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                       SelectState* spec_st, unsigned long long* xseg, bool fold, hipEvent_t ev_end, hipStream_t s) {
+                       SelectState* spec_st, unsigned long long* xseg, bool fold, const T* radii, hipEvent_t ev_end,
+                       hipStream_t s) {
     if (N <= 0) return;
     fold = fold && mode >= 1 && visited && vout;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
@@ -857,7 +872,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, s)
+                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, s)
     // with reuse the list keeps room for the (k+1)-th point (the safe radius)
     const int kl = ru.mode && mode >= 1 && knn < 16 ? knn + 1 : knn;
     if (kl == 1)
@@ -882,13 +897,13 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, bool, hipEvent_t, hipStream_t);
+                                       unsigned long long*, bool, const float*, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, bool, hipEvent_t, hipStream_t);
+                                        unsigned long long*, bool, const double*, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

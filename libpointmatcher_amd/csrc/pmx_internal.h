@@ -100,6 +100,14 @@ void launch_match(const P4<T>* ref, int64_t M_pad, const P4<T>* rd, int64_t N, c
                   int64_t part_cap, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, int cu_count);
 template <typename T>
 int64_t match_part_elems(int64_t N, int64_t M_pad, int knn, int cu_count);
+// KDTreeVarDistMatcher after the brute-force match: entries beyond their
+// query's radius become (inf, -1) (the k nearest within a radius are the
+// prefix of the k nearest)
+template <typename T>
+void launch_apply_radii(T* dists, int32_t* ids, const T* radii, int64_t N, int k, hipStream_t s);
+// dst[s] = src[order[s]] (order == null: a copy)
+template <typename T>
+void launch_gather_scalar(const T* src, const int32_t* order, int64_t n, T* dst, hipStream_t s);
 
 template <typename T>
 void launch_transform(const P4<T>* in, P4<T>* out, int64_t N, const Mat4<T>& Tm, hipStream_t s);
@@ -160,7 +168,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       unsigned long long* xseg, bool fold, hipEvent_t ev_end, hipStream_t s);
+                       unsigned long long* xseg, bool fold, const T* radii, hipEvent_t ev_end, hipStream_t s);
 // several ranks: the quantile window's pick over the all-gathered segments
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum
 template <typename T>
@@ -214,6 +222,10 @@ template <typename T>
 int ssn_run(const P4<T>* d_pts, int D, int64_t n, int knn, T max_box, bool want_eig, hipStream_t st,
             std::vector<int32_t>& perm, std::vector<int32_t>& leaf_first, std::vector<int32_t>& leaf_cnt,
             std::vector<int32_t>& fit, std::vector<T>& rec, std::string& err);
+// VoxelGridDataPointsFilter (pmx_voxel.hip): device in / out, capacity n
+template <typename T>
+int voxel_run(const T* d_f, int rows, int64_t n, const T* d_desc, int desc_dim, const double vsize[3], bool centroid,
+              bool avg, T* d_of, T* d_od, int64_t* n_out, hipStream_t st, std::string& err);
 // code-object preloads (one per translation unit, called by pmx_ctx_create)
 void preload_setup();
 void preload_ssn();

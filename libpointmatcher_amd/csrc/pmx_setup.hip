@@ -345,6 +345,39 @@ void launch_unpermute(const void* src, const int32_t* order, int64_t n, int span
                            order, n, span, (uint32_t*)dst);
 }
 
+// ---- KDTreeVarDistMatcher radii ----
+template <typename T>
+__global__ void gather_scalar_kernel(const T* __restrict__ src, const int32_t* __restrict__ order, int64_t n,
+                                     T* __restrict__ dst) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = src[order ? order[i] : i];
+}
+template <typename T>
+void launch_gather_scalar(const T* src, const int32_t* order, int64_t n, T* dst, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(gather_scalar_kernel<T>, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256),
+                       0, s, src, order, n, dst);
+}
+template <typename T>
+__global__ void apply_radii_kernel(T* __restrict__ d, int32_t* __restrict__ ids, const T* __restrict__ radii,
+                                   int64_t N, int k) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < N * k; e += stride) {
+        const T r = radii[e / k];
+        if (!(d[e] <= r * r)) {
+            d[e] = (T)__builtin_huge_val();
+            ids[e] = -1;
+        }
+    }
+}
+template <typename T>
+void launch_apply_radii(T* dists, int32_t* ids, const T* radii, int64_t N, int k, hipStream_t s) {
+    if (N <= 0) return;
+    hipLaunchKernelGGL(apply_radii_kernel<T>, dim3((unsigned)std::min<int64_t>((N * k + 255) / 256, 4096)), dim3(256),
+                       0, s, dists, ids, radii, N, k);
+}
+
 #define PMX_SETUP_INST(T)                                                                                            \
     template void launch_pack_p4<T>(const T*, int, int64_t, int64_t, P4<T>*, hipStream_t);                          \
     template void launch_pack_nrm<T>(const T*, int, int64_t, P4<T>*, hipStream_t);                                  \
@@ -357,6 +390,10 @@ void launch_unpermute(const void* src, const int32_t* order, int64_t n, int span
                                          const SetupScratch&, P4<T>*, hipStream_t);
 PMX_SETUP_INST(float)
 PMX_SETUP_INST(double)
+template void launch_gather_scalar<float>(const float*, const int32_t*, int64_t, float*, hipStream_t);
+template void launch_gather_scalar<double>(const double*, const int32_t*, int64_t, double*, hipStream_t);
+template void launch_apply_radii<float>(float*, int32_t*, const float*, int64_t, int, hipStream_t);
+template void launch_apply_radii<double>(double*, int32_t*, const double*, int64_t, int, hipStream_t);
 #undef PMX_SETUP_INST
 
 void preload_setup() {

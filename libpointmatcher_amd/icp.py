@@ -69,6 +69,7 @@ def lib():
         l.pmx_icp_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, _capi.ALLREDUCE_FN, _capi.ALLGATHER_FN,
                                              C.c_void_p]
         l.pmx_icp_keep_trace.argtypes = [C.c_void_p, C.c_int]
+        l.pmx_icp_add_descriptor.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.c_void_p, C.c_int64]
         l.pmx_icp_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int64,
                                       C.c_void_p, C.c_void_p, C.c_void_p]
         l.pmx_icp_prepare.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int64,
@@ -134,6 +135,15 @@ class ICP:
 
     def keep_trace(self, on=True):
         self._chk(self._l.pmx_icp_keep_trace(self.h, 1 if on else 0))
+
+    def add_descriptor(self, cloud, name, values):
+        """Stage a descriptor (n,) or (n, span) for the next compute / prepare;
+        cloud: "reading" or "reference" (e.g. the reading's "maxSearchDist"
+        of KDTreeVarDistMatcher)."""
+        v = np.ascontiguousarray(values, dtype=self.dtype)
+        span = 1 if v.ndim == 1 else v.shape[1]
+        self._chk(self._l.pmx_icp_add_descriptor(self.h, 0 if cloud == "reading" else 1, name.encode(), span, _p(v),
+                                                 v.shape[0]))
 
     # --- run
     def _args(self, reading, reference, normals, T_init):

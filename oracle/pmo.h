@@ -154,6 +154,12 @@ int pmo_sampling_surface_normals_f64(const double* pts, int rows, int64_t n, con
                                      int knn, int sampling_method, double ratio, double max_box_dim, unsigned flags,
                                      double* feat_out, double* desc_out, double* normals, double* dens,
                                      double* evals, double* evecs, int64_t* n_out, int64_t* unfit);
+/* VoxelGridDataPointsFilter (DataPointsFilters/VoxelGrid.cpp:60-343), the
+ * reference's walk restated: outputs capacity n, returns 0 or PMO_E_BAD_PARAM */
+int pmo_voxel_grid_f32(const float* pts, int rows, int64_t n, const float* desc, int desc_dim, const double* vsize,
+                       int use_centroid, int average_desc, float* feat_out, float* desc_out, int64_t* n_out);
+int pmo_voxel_grid_f64(const double* pts, int rows, int64_t n, const double* desc, int desc_dim, const double* vsize,
+                       int use_centroid, int average_desc, double* feat_out, double* desc_out, int64_t* n_out);
 int pmo_surface_normals_f32(const float* pts, int rows, int64_t n, int k, float maxDist, int threads, int smooth,
                             float* normals, float* dens, float* evals, float* evecs, float* ids, float* mdist,
                             int64_t* degenerate);

@@ -299,3 +299,22 @@ def sampling_surface_normals(pts, desc=None, knn=7, method=0, ratio=0.5, max_box
     res = {k: v[:m] for k, v in out.items()}
     res["unfit"] = unfit.value
     return res
+
+
+def voxel_grid(pts, desc=None, vsize=(1.0, 1.0, 1.0), use_centroid=True, average_desc=True):
+    """VoxelGridDataPointsFilter restated (oracle/pmo_impl.inc).  Returns (features, descriptors)."""
+    pts = np.ascontiguousarray(pts)
+    dt = pts.dtype
+    n, rows = pts.shape
+    dd = 0 if desc is None else desc.shape[1]
+    d = None if desc is None else np.ascontiguousarray(desc, dtype=dt)
+    of = np.empty((n, rows), dt)
+    od = np.empty((n, max(dd, 1)), dt)
+    no = C.c_int64(0)
+    vs = np.ascontiguousarray(vsize, dtype=np.float64)
+    rc = getattr(lib(), "pmo_voxel_grid_" + _sfx(dt))(_p(pts), rows, C.c_int64(n), _p(d), dd, _p(vs),
+                                                       1 if use_centroid else 0, 1 if average_desc else 0, _p(of),
+                                                       _p(od), C.byref(no))
+    if rc:
+        raise ValueError(f"pmo_voxel_grid failed ({rc})")
+    return of[:no.value], od[:no.value, :dd]
