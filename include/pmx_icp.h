@@ -76,6 +76,21 @@ int pmx_icp_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, cons
  * KDTreeVarDistMatcher).  Consumed by that call. */
 int pmx_icp_add_descriptor(pmx_icp* icp, int cloud, const char* name, int span, const void* values, int64_t n);
 
+/* DataPoints::load (IO.cpp:374-389; loadCSV :535-800, loadVTK :948-1252):
+ * a .csv or .vtk cloud with the reference's label mapping; features
+ * (rows x n, homogeneous row last) and descriptors (desc_dim x n), both
+ * point-major.  Errors: PMX_ICP_RUNTIME_ERROR, message in
+ * pmx_cloud_last_error(). */
+typedef struct pmx_cloud pmx_cloud;
+int pmx_cloud_load(const char* path, int dtype, pmx_cloud** out);
+void pmx_cloud_destroy(pmx_cloud* cloud);
+const char* pmx_cloud_last_error(void);
+int pmx_cloud_info(const pmx_cloud* cloud, int64_t* n, int* rows, int* desc_dim, int* n_feature_labels,
+                   int* n_descriptor_labels);
+/* which: 0 feature labels, 1 descriptor labels */
+int pmx_cloud_label(const pmx_cloud* cloud, int which, int i, char* name, int cap, int* span);
+int pmx_cloud_data(const pmx_cloud* cloud, void* features, void* descriptors);
+
 /* the same loop in phases (bench: time the iterations alone) */
 int pmx_icp_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
                     const void* ref_normals, const void* T_init);

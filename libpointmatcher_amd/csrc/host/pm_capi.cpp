@@ -280,3 +280,93 @@ int pmx_icp_timing_read(pmx_icp* icp, double* ms, int64_t* launches) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- clouds --
+struct pmx_cloud {
+    int dtype = 0;
+    pm::DataPoints<float> f;
+    pm::DataPoints<double> d;
+};
+
+namespace {
+thread_local std::string g_cloud_err;
+template <typename T>
+const pm::DataPoints<T>& cloud_of(const pmx_cloud* c);
+template <>
+const pm::DataPoints<float>& cloud_of<float>(const pmx_cloud* c) { return c->f; }
+template <>
+const pm::DataPoints<double>& cloud_of<double>(const pmx_cloud* c) { return c->d; }
+template <typename T>
+void cloud_copy(const pmx_cloud* c, void* feat, void* desc) {
+    const auto& dp = cloud_of<T>(c);
+    if (feat) std::memcpy(feat, dp.features.data(), sizeof(T) * dp.features.size());
+    if (desc) std::memcpy(desc, dp.descriptors.data(), sizeof(T) * dp.descriptors.size());
+}
+}  // namespace
+
+extern "C" {
+
+int pmx_cloud_load(const char* path, int dtype, pmx_cloud** out) {
+    if (!path || !out || (dtype != 0 && dtype != 1)) {
+        g_cloud_err = "null argument or bad dtype";
+        return PMX_ICP_INVALID_PARAMETER;
+    }
+    *out = nullptr;
+    try {
+        auto* c = new pmx_cloud;
+        c->dtype = dtype;
+        if (dtype == 1)
+            c->d = pm::load_cloud<double>(path);
+        else
+            c->f = pm::load_cloud<float>(path);
+        *out = c;
+        return PMX_ICP_OK;
+    } catch (const std::exception& e) {
+        g_cloud_err = e.what();
+        return PMX_ICP_RUNTIME_ERROR;
+    }
+}
+
+void pmx_cloud_destroy(pmx_cloud* c) { delete c; }
+
+const char* pmx_cloud_last_error(void) { return g_cloud_err.c_str(); }
+
+int pmx_cloud_info(const pmx_cloud* c, int64_t* n, int* rows, int* desc_dim, int* nfl, int* ndl) {
+    if (!c) return PMX_ICP_INVALID_PARAMETER;
+    auto fill = [&](const auto& dp) {
+        if (n) *n = dp.n;
+        if (rows) *rows = dp.rows;
+        if (desc_dim) *desc_dim = dp.descDim;
+        if (nfl) *nfl = (int)dp.featureLabels.size();
+        if (ndl) *ndl = (int)dp.descriptorLabels.size();
+    };
+    if (c->dtype == 1)
+        fill(c->d);
+    else
+        fill(c->f);
+    return PMX_ICP_OK;
+}
+
+int pmx_cloud_label(const pmx_cloud* c, int which, int i, char* name, int cap, int* span) {
+    if (!c || !name || cap < 1) return PMX_ICP_INVALID_PARAMETER;
+    auto get = [&](const auto& dp) -> int {
+        const auto& ls = which == 0 ? dp.featureLabels : dp.descriptorLabels;
+        if (i < 0 || i >= (int)ls.size()) return PMX_ICP_INVALID_PARAMETER;
+        std::snprintf(name, (size_t)cap, "%s", ls[(size_t)i].text.c_str());
+        if (span) *span = ls[(size_t)i].span;
+        return PMX_ICP_OK;
+    };
+    return c->dtype == 1 ? get(c->d) : get(c->f);
+}
+
+int pmx_cloud_data(const pmx_cloud* c, void* feat, void* desc) {
+    if (!c) return PMX_ICP_INVALID_PARAMETER;
+    if (c->dtype == 1)
+        cloud_copy<double>(c, feat, desc);
+    else
+        cloud_copy<float>(c, feat, desc);
+    return PMX_ICP_OK;
+}
+
+}  // extern "C"
+

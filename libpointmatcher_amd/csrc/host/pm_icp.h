@@ -230,4 +230,8 @@ struct PointMatcher {
     };
 };
 
+// DataPoints::load for .csv / .vtk (pm_io.cpp, IO.cpp:374-389)
+template <typename T>
+DataPoints<T> load_cloud(const std::string& path);
+
 }  // namespace pm

@@ -70,6 +70,13 @@ def lib():
                                              C.c_void_p]
         l.pmx_icp_keep_trace.argtypes = [C.c_void_p, C.c_int]
         l.pmx_icp_add_descriptor.argtypes = [C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.c_void_p, C.c_int64]
+        l.pmx_cloud_load.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]
+        l.pmx_cloud_destroy.argtypes = [C.c_void_p]
+        l.pmx_cloud_last_error.restype = C.c_char_p
+        l.pmx_cloud_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                     C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        l.pmx_cloud_label.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int)]
+        l.pmx_cloud_data.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         l.pmx_icp_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int64,
                                       C.c_void_p, C.c_void_p, C.c_void_p]
         l.pmx_icp_prepare.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int64,
@@ -86,6 +93,54 @@ def lib():
 
 def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class Cloud:
+    """DataPoints loaded from a .csv / .vtk file (DataPoints::load, IO.cpp:374-389)."""
+
+    def __init__(self, features, feature_labels, descriptors, descriptor_labels):
+        self.features = features                  # (n, rows), homogeneous row last
+        self.feature_labels = feature_labels      # [(name, span)]
+        self.descriptors = descriptors            # (n, desc_dim)
+        self.descriptor_labels = descriptor_labels
+
+    def descriptor(self, name):
+        off = 0
+        for lab, span in self.descriptor_labels:
+            if lab == name:
+                return self.descriptors[:, off:off + span]
+            off += span
+        raise KeyError(name)
+
+    def descriptor_exists(self, name):
+        return any(lab == name for lab, _ in self.descriptor_labels)
+
+
+def load_cloud(path, dtype=np.float32):
+    l = lib()
+    dt = np.dtype(dtype)
+    h = C.c_void_p()
+    rc = l.pmx_cloud_load(str(path).encode(), 1 if dt == np.float64 else 0, C.byref(h))
+    if rc:
+        raise _ERR.get(rc, RuntimeError)(l.pmx_cloud_last_error().decode())
+    try:
+        n, rows, dd, nfl, ndl = C.c_int64(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        l.pmx_cloud_info(h, C.byref(n), C.byref(rows), C.byref(dd), C.byref(nfl), C.byref(ndl))
+        labels = []
+        for which, cnt in ((0, nfl.value), (1, ndl.value)):
+            ls = []
+            for i in range(cnt):
+                buf = C.create_string_buffer(256)
+                span = C.c_int()
+                l.pmx_cloud_label(h, which, i, buf, 256, C.byref(span))
+                ls.append((buf.value.decode(), span.value))
+            labels.append(ls)
+        f = np.empty((n.value, rows.value), dt)
+        d = np.empty((n.value, dd.value), dt)
+        l.pmx_cloud_data(h, _p(f), _p(d) if dd.value else None)
+        return Cloud(f, labels[0], d, labels[1])
+    finally:
+        l.pmx_cloud_destroy(h)
 
 
 class ICP:
