@@ -154,7 +154,9 @@ __device__ void fused_finalize(const double* __restrict__ partials, int nblocks,
 // (a single lane walking scratch took ~75 us per iteration at C3).
 // partials != null: the fused finalize above (256 threads), the system then
 // read from LDS; otherwise res holds it (64 threads).
-template <typename T, int ROWS>
+// MIN: the minimiser (0 point-to-plane, 1 point-to-point) as a template
+// parameter, so each kernel holds one minimiser's dense code (registers)
+template <typename T, int ROWS, int MIN>
 __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
                                  const double* __restrict__ res_g, const int* __restrict__ iter_err,
                                  const unsigned long long* __restrict__ visited, const T* __restrict__ means,
@@ -176,7 +178,7 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
     constexpr int rows = ROWS, D = ROWS - 1;
     // statistics of the iteration (ErrorElements, ErrorMinimizer.cpp:133-192)
     double kept, nz, rejM, rejP, sw;
-    if (cfg.minimizer == 0) {
+    if (MIN == 0) {
         const int NF = D == 3 ? 6 : 3, o = NF * (NF + 1) / 2 + NF;
         kept = res[o];
         nz = res[o + 1];
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
     S->touched += visited[0];
     // the step transform
     T dT[16];
-    if (cfg.minimizer == 0) {
+    if constexpr (MIN == 0) {
         constexpr int NF = D == 3 ? 6 : 3;
         T A[NF * NF], b[NF], x[NF];
         p2plane_system_of<T, NF>(res, A, b);
@@ -392,12 +394,21 @@ void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const in
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
                       const double* partials, int nblocks, int nv, double* res_out, hipStream_t s) {
     const unsigned th = partials ? 256 : 64;
-    if (cfg.rows == 4)
-        hipLaunchKernelGGL((loop_step_kernel<T, 4>), dim3(1), dim3(th), 0, s, ctl, S, res, iter_err, visited, means,
-                           cfg, trace, partials, nblocks, nv, res_out);
-    else
-        hipLaunchKernelGGL((loop_step_kernel<T, 3>), dim3(1), dim3(th), 0, s, ctl, S, res, iter_err, visited, means,
-                           cfg, trace, partials, nblocks, nv, res_out);
+#define PMX_STEP(R, M)                                                                                            \
+    hipLaunchKernelGGL((loop_step_kernel<T, R, M>), dim3(1), dim3(th), 0, s, ctl, S, res, iter_err, visited, means, \
+                       cfg, trace, partials, nblocks, nv, res_out)
+    if (cfg.rows == 4) {
+        if (cfg.minimizer == 0)
+            PMX_STEP(4, 0);
+        else
+            PMX_STEP(4, 1);
+    } else {
+        if (cfg.minimizer == 0)
+            PMX_STEP(3, 0);
+        else
+            PMX_STEP(3, 1);
+    }
+#undef PMX_STEP
 }
 
 template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg&, const float*, int, int,
@@ -418,7 +429,7 @@ template void launch_loop_step<double>(LoopCtl*, LoopState<double>*, const doubl
 // first ICP iteration.
 void preload_loop() {
     hipFuncAttributes a;
-    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&loop_step_kernel<float, 4>));
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&loop_step_kernel<float, 4, 0>));
 }
 
 }  // namespace pmx
