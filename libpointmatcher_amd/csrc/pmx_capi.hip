@@ -222,6 +222,8 @@ struct pmx_ctx {
     // costs more than the finalize kernel and its boundary it saves
     bool fuse_final = false;
     bool fold_counter = false;  // the counter phase in the match's last workgroup (PMX_FOLD_COUNTER=1; measured slower)
+    bool defer_counter = true;  // ... or at the start of the next select_all launch (PMX_DEFER_COUNTER=0: off)
+    bool counter_deferred = false;  // the last match left its counter phase to the next select_all
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;
@@ -779,8 +781,17 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
 }
 
 // ------------------------------------------------------------------- match --
+// the match's counter phase, when it was deferred to a select_all that did not come
+template <typename T>
+void flush_counter(pmx_ctx* c) {
+    if (!c->counter_deferred) return;
+    c->counter_deferred = false;
+    launch_counter_sum<T>(c->d_vpart, c->d_visited, c->d_iter_err, loop_ctl(c), c->spec_now(), c->d_sel, c->stream);
+}
+
 template <typename T>
 int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
+    flush_counter<T>(c);
     if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
     if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
     if (knn < 1 || knn > 16) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 16] on the GPU path");
@@ -869,11 +880,16 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // the segments are all-gathered and every rank picks from the union
         SpecSel* spec = c->spec_now();
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx : nullptr;
+        // single rank, window on: the counter phase runs at the start of the
+        // select_all launch that the quantile filter issues next
+        const bool defer = spec && !xseg && c->select_all && !c->select_split && !c->fold_counter &&
+                           c->defer_counter && !c->no_visits && c->grid_mode >= 1;
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->fold_counter, c->has_radii ? (const T*)c->d_radii : nullptr, e1, c->stream);  // (e1 recorded after the match kernel, before the counter sum)
+                             c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, e1, c->stream);
+        c->counter_deferred = defer;  // (e1 recorded after the match kernel, before the counter sum)
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
@@ -916,7 +932,10 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
                 HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
                 c->selx_grid = g;
             }
-            launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
+            const bool pre = c->counter_deferred;  // (the match left its counter phase to this launch)
+            c->counter_deferred = false;
+            launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec,
+                                 pre ? c->d_vpart : nullptr, pre ? c->d_visited : nullptr, c->stream);
             break;
         } else {
             launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, loop_ctl(c),
@@ -1032,6 +1051,7 @@ WChain<T> chain_of(const pmx_ctx* c) {
 // the 0/1 weights themselves are evaluated inline by the minimiser.
 template <typename T>
 int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, double p2) {
+    if (!(chain_pos == 0 && (kind == 4 || kind == 5))) flush_counter<T>(c);  // (4 / 5 consume it in their select)
     int rc = check_match(c);
     if (rc) return rc;
     if (chain_pos < 0 || chain_pos >= kMaxChain) return fail(c, PMX_E_BAD_PARAM, "outlier chain longer than 8 filters");
@@ -1139,6 +1159,7 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
 template <typename T>
 int outlier_robust_impl(pmx_ctx* c, int pos, int fct, double tuning, double approx, int mode, double target,
                         int p2pl) {
+    flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     if (pos < 0 || pos >= kMaxChain) return fail(c, PMX_E_BAD_PARAM, "outlier chain longer than 8 filters");
@@ -1291,6 +1312,7 @@ int materialise_weights(pmx_ctx* c) {
 // which gets the value count back in *fuse_nv
 template <typename T>
 int p2plane_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
+    flush_counter<T>(c);
     const WChain<T> chain = chain_of<T>(c);
     const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
@@ -1312,6 +1334,7 @@ int p2plane_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
 // fuse_nv: as p2plane_enqueue (the second pass's finalize)
 template <typename T>
 int p2point_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
+    flush_counter<T>(c);
     Mat4<T> Tm = step_mat<T>(c);
     WChain<T> chain = chain_of<T>(c);
     if (chain.robust && chain.rb_p2pl) {  // (the point-to-point kernels carry no normals)
@@ -1399,6 +1422,7 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
 
 template <typename T>
 int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
+    flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
@@ -1431,6 +1455,7 @@ int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
 
 template <typename T>
 int get_weights_impl(pmx_ctx* c, void* w) {
+    flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
@@ -2043,6 +2068,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_SPEC_SELECT")) c->spec_allowed = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_FUSE_FINAL")) c->fuse_final = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_FOLD_COUNTER")) c->fold_counter = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_DEFER_COUNTER")) c->defer_counter = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_SELECT_ALL")) c->select_all = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0

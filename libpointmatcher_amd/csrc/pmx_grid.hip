@@ -432,8 +432,6 @@ __device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&k
 // address serialises (~110 us for 16K waves at C3), so every wave adds into
 // one of kVSlots counters, each on its own 128-byte line; counter_sum_kernel
 // folds them into the iteration block after the match.
-constexpr int kVSlots = 256;
-constexpr int kVStride = 16;  // unsigned long longs: 128 bytes
 __device__ __forceinline__ unsigned long long* vslot(unsigned long long* vpart, int which) {
     const unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     return vpart + ((size_t)which * kVSlots + (wave & (kVSlots - 1))) * kVStride;
@@ -442,73 +440,6 @@ __device__ __forceinline__ void add_visits(uint32_t visits, unsigned long long* 
     unsigned long long v = visits;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((threadIdx.x & 63) == 0 && vpart && v) atomicAdd(vslot(vpart, 0), v);
-}
-
-// (also clears the iteration's error word: it runs first after the match,
-// before any filter can raise one).  With a quantile window (pmx_spec.h) it
-// also resolves the iteration's quantile from the window when it can — or,
-// with several ranks (xseg != null), packs this rank's window segment for the
-// exchange and leaves the pick to spec_pick_kernel.
-template <typename T>
-__device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ vpart,
-                                              unsigned long long* __restrict__ out, int* __restrict__ iter_err,
-                                              SpecSel* __restrict__ spec, SelectState* __restrict__ st,
-                                              unsigned long long* __restrict__ xseg) {
-    __shared__ unsigned long long red[4][kVSlots / 64];
-    __shared__ uint32_t lh[2048];
-    __shared__ unsigned long long part[kVSlots];
-    __shared__ unsigned long long bc[2];
-    const int t = threadIdx.x;
-    unsigned long long v[4];
-    // (coherent loads / stores: with the fold the counters were added in this
-    // launch by other workgroups, possibly on other XCDs)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        unsigned long long* p = vpart + (size_t)(c * kVSlots + t) * kVStride;
-        v[c] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next match
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] += __shfl_xor(v[c], off);
-    }
-    if ((t & 63) == 0) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) red[c][t >> 6] = v[c];
-    }
-    __syncthreads();
-    unsigned long long sum[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-        for (int w = 0; w < kVSlots / 64; ++w) sum[c] += red[c][w];
-    if (t == 0) {
-        out[0] = sum[0];
-        out[1] = sum[1];
-        if (iter_err) *iter_err = 0;
-    }
-    if (!spec) return;
-    if (xseg) {  // several ranks: this rank's segment [fin, below, n, keys...]
-        using K = typename KeyOf<T>::K;
-        const unsigned nk = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned nc = nk < kSpecXCap ? nk : kSpecXCap;
-        const K* keys = (const K*)spec->keys;
-        if (t == 0) {
-            xseg[0] = sum[2];
-            xseg[1] = sum[3];
-            xseg[2] = spec->valid ? nk : 0ull;
-        }
-        for (unsigned i = t; i < nc; i += kVSlots)
-            xseg[kSpecXHdr + i] = (unsigned long long)__hip_atomic_load(&keys[i], __ATOMIC_RELAXED,
-                                                                        __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();  // (every lane read n_keys before it is reset)
-        if (t == 0) spec->n_keys = 0;
-        return;
-    }
-    SpecKeys<T> src;
-    src.local = (const typename KeyOf<T>::K*)spec->keys;
-    const unsigned nk_raw = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    src.n_local = nk_raw < kSpecCap ? nk_raw : kSpecCap;
-    (void)spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part, bc);
 }
 
 template <typename T>
@@ -572,6 +503,18 @@ __device__ __forceinline__ void counter_fold(unsigned long long* __restrict__ vp
     for (int g = threadIdx.x; g <= kTicketGroups; g += blockDim.x)  // (every group's and the top counter)
         __hip_atomic_store(tk + g * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// a deferred counter phase that no select_all consumed
+template <typename T>
+void launch_counter_sum(unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
+                        SpecSel* spec, SelectState* st, hipStream_t s) {
+    hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, vpart, vout, iter_err, ctl, spec, st,
+                       nullptr);
+}
+template void launch_counter_sum<float>(unsigned long long*, unsigned long long*, int*, const LoopCtl*, SpecSel*,
+                                        SelectState*, hipStream_t);
+template void launch_counter_sum<double>(unsigned long long*, unsigned long long*, int*, const LoopCtl*, SpecSel*,
+                                         SelectState*, hipStream_t);
 
 // Several ranks: resolve the quantile from the all-gathered window segments
 // (pmx_spec.h).  Every rank runs it on the same segments and writes the same
@@ -858,8 +801,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                       SelectState* spec_st, unsigned long long* xseg, bool fold, const T* radii, hipEvent_t ev_end,
-                       hipStream_t s) {
+                       SelectState* spec_st, unsigned long long* xseg, bool fold, bool defer, const T* radii,
+                       hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     fold = fold && mode >= 1 && visited && vout;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
@@ -887,7 +830,9 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
         PMX_KT(16);
 #undef PMX_KT
     if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel, with the folded counter phase)
-    if (visited && vout && !fold)  // (folded: the per-lane kernel's last workgroup ran it)
+    // (folded: the per-lane kernel's last workgroup ran it; deferred: the
+    // select_all launch that follows runs it, pmx_select.hip)
+    if (visited && vout && !fold && !defer)
         hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
                            spec_st, xseg);
 }
@@ -897,13 +842,13 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, bool, const float*, hipEvent_t, hipStream_t);
+                                       unsigned long long*, bool, bool, const float*, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, bool, const double*, hipEvent_t, hipStream_t);
+                                        unsigned long long*, bool, bool, const double*, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

@@ -168,7 +168,10 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       unsigned long long* xseg, bool fold, const T* radii, hipEvent_t ev_end, hipStream_t s);
+                       unsigned long long* xseg, bool fold, bool defer, const T* radii, hipEvent_t ev_end, hipStream_t s);
+template <typename T>
+void launch_counter_sum(unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
+                        SpecSel* spec, SelectState* st, hipStream_t s);
 // several ranks: the quantile window's pick over the all-gathered segments
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum
 template <typename T>
@@ -394,7 +397,8 @@ int64_t select_all_blocks(int64_t n);
 constexpr int kSelTimeout = -30;  // iteration error: a select_all wait timed out
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
-                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s);
+                       int* iter_err, const LoopCtl* ctl, SpecSel* spec,
+                       unsigned long long* vpart, unsigned long long* vout, hipStream_t s);
 int select_bins(int pass, int key_bits);
 
 // VarTrimmed pieces

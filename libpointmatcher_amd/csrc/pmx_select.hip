@@ -365,6 +365,7 @@ struct SelX {
     unsigned long long rank[kSelMaxPasses];  // rank left inside the prefix after pass p
     unsigned long long tot[kSelMaxPasses];   // keys histogrammed in pass p
     unsigned long long count;                // finite keys (pass 0)
+    unsigned long long pre;                  // gen << 56 | window hit: the deferred counter phase's verdict
 };
 size_t selx_bytes() { return sizeof(SelX) + (size_t)kSelMaxPasses * 2048 * sizeof(uint32_t); }
 int64_t select_all_blocks(int64_t n) { return select_blocks(n); }
@@ -383,7 +384,9 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
                                                          const double* __restrict__ ratio_dev,
                                                          int* __restrict__ iter_err, int agg,
                                                          const LoopCtl* __restrict__ ctl,
-                                                         SpecSel* __restrict__ spec) {
+                                                         SpecSel* __restrict__ spec,
+                                                         unsigned long long* __restrict__ vpart,
+                                                         unsigned long long* __restrict__ vout) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     __shared__ uint32_t lh[2048];
@@ -392,7 +395,45 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
     __shared__ int s_last;
     __shared__ unsigned int s_old;
     if (ctl && ctl->done) return;  // (uniform: no block arrives anywhere)
-    if (spec && spec->hit) return;  // the quantile window resolved it (pmx_spec.h)
+    if (vpart) {
+        // The match's counter phase deferred into this launch (one launch
+        // fewer per iteration): block 0 folds the counters and tries the
+        // window pick, then publishes the verdict (generation-stamped, as the
+        // passes below); a hit ends every block, a miss runs the passes.
+        if (threadIdx.x == 0) s_old = atomicAdd(&sx->arrive[7], 1u);
+        __syncthreads();
+        const unsigned long long pgen = ((unsigned long long)(s_old / gridDim.x) + 1ull) & 0xffull;
+        if (blockIdx.x == 0) {
+            counter_phase<T>(vpart, vout, iter_err, spec, st, nullptr);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const unsigned long long hit = spec && spec->hit ? 1ull : 0ull;
+                (void)ast(&sx->pre, pgen << 56 | hit);
+                s_w[0] = hit;
+            }
+            __syncthreads();
+            if (s_w[0]) return;
+        } else {
+            if (threadIdx.x == 0) {
+                unsigned long long w = 0;
+                bool ok = false;
+                for (int it = 0; it < (1 << 22); ++it) {
+                    w = ald(&sx->pre);
+                    if ((w >> 56) == pgen) {
+                        ok = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                s_w[0] = ok ? (w & 1ull) : 1ull;
+                if (!ok) __hip_atomic_store(iter_err, kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            if (s_w[0]) return;  // the window resolved it (or the wait timed out)
+        }
+    } else if (spec && spec->hit) {
+        return;  // the quantile window resolved it (pmx_spec.h)
+    }
     constexpr int passes = KO::bits == 32 ? 3 : 6;
     uint32_t* hist0 = reinterpret_cast<uint32_t*>(sx + 1);
     const int t = threadIdx.x;
@@ -573,9 +614,10 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
 
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
-                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s) {
+                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, unsigned long long* vpart,
+                       unsigned long long* vout, hipStream_t s) {
     hipLaunchKernelGGL(select_all_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, (SelX*)selx,
-                       st, ratio, ratio_dev, iter_err, select_agg(), ctl, spec);
+                       st, ratio, ratio_dev, iter_err, select_agg(), ctl, spec, vpart, vout);
 }
 
 template <typename T>
@@ -863,9 +905,11 @@ template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, co
 template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
                                          SpecSel*, hipStream_t);
 template void launch_select_all<float>(const float*, int64_t, void*, SelectState*, double, const double*, int*,
-                                       const LoopCtl*, SpecSel*, hipStream_t);
+                                       const LoopCtl*, SpecSel*, unsigned long long*, unsigned long long*,
+                                       hipStream_t);
 template void launch_select_all<double>(const double*, int64_t, void*, SelectState*, double, const double*, int*,
-                                        const LoopCtl*, SpecSel*, hipStream_t);
+                                        const LoopCtl*, SpecSel*, unsigned long long*, unsigned long long*,
+                                        hipStream_t);
 template void launch_select_pass<float>(const float*, int64_t, uint32_t*, SelectState*, int, double, const double*,
                                         unsigned int*, int*, const LoopCtl*, SpecSel*, hipStream_t);
 template void launch_select_pass<double>(const double*, int64_t, uint32_t*, SelectState*, int, double, const double*,

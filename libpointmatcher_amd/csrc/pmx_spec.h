@@ -305,4 +305,76 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
     return true;
 }
 
+// ---- the counter phase after a match (one block of kVSlots threads) ----
+// Pair / fallback / window counters: every wave of the match adds into one of
+// kVSlots spread counters (each on its own 128-byte line); this folds them.
+constexpr int kVSlots = 256;
+constexpr int kVStride = 16;  // unsigned long longs: 128 bytes
+// (also clears the iteration's error word: it runs first after the match,
+// before any filter can raise one).  With a quantile window (pmx_spec.h) it
+// also resolves the iteration's quantile from the window when it can — or,
+// with several ranks (xseg != null), packs this rank's window segment for the
+// exchange and leaves the pick to spec_pick_kernel.
+template <typename T>
+__device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ vpart,
+                                              unsigned long long* __restrict__ out, int* __restrict__ iter_err,
+                                              SpecSel* __restrict__ spec, SelectState* __restrict__ st,
+                                              unsigned long long* __restrict__ xseg) {
+    __shared__ unsigned long long red[4][kVSlots / 64];
+    __shared__ uint32_t lh[2048];
+    __shared__ unsigned long long part[kVSlots];
+    __shared__ unsigned long long bc[2];
+    const int t = threadIdx.x;
+    unsigned long long v[4];
+    // (coherent loads / stores: with the fold the counters were added in this
+    // launch by other workgroups, possibly on other XCDs)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        unsigned long long* p = vpart + (size_t)(c * kVSlots + t) * kVStride;
+        v[c] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next match
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] += __shfl_xor(v[c], off);
+    }
+    if ((t & 63) == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[c][t >> 6] = v[c];
+    }
+    __syncthreads();
+    unsigned long long sum[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        for (int w = 0; w < kVSlots / 64; ++w) sum[c] += red[c][w];
+    if (t == 0) {
+        out[0] = sum[0];
+        out[1] = sum[1];
+        if (iter_err) __hip_atomic_store(iter_err, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (coherent: a select may write it in the same launch)
+    }
+    if (!spec) return;
+    if (xseg) {  // several ranks: this rank's segment [fin, below, n, keys...]
+        using K = typename KeyOf<T>::K;
+        const unsigned nk = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned nc = nk < kSpecXCap ? nk : kSpecXCap;
+        const K* keys = (const K*)spec->keys;
+        if (t == 0) {
+            xseg[0] = sum[2];
+            xseg[1] = sum[3];
+            xseg[2] = spec->valid ? nk : 0ull;
+        }
+        for (unsigned i = t; i < nc; i += kVSlots)
+            xseg[kSpecXHdr + i] = (unsigned long long)__hip_atomic_load(&keys[i], __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();  // (every lane read n_keys before it is reset)
+        if (t == 0) spec->n_keys = 0;
+        return;
+    }
+    SpecKeys<T> src;
+    src.local = (const typename KeyOf<T>::K*)spec->keys;
+    const unsigned nk_raw = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    src.n_local = nk_raw < kSpecCap ? nk_raw : kSpecCap;
+    (void)spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part, bc);
+}
+
 }  // namespace pmx

@@ -245,16 +245,20 @@ def test_select_all_passes_in_one_launch(monkeypatch, dtype, filt, knn, max_dist
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_counter_fold_equals_counter_kernel(monkeypatch, dtype):
-    """PMX_FOLD_COUNTER=1 (the counter phase and the quantile-window pick in
-    the match kernel's last workgroup, two-level tickets, coherent loads of
-    the counters and window keys) leaves whole loops bit-identical to the
+@pytest.mark.parametrize("knob,off", [("PMX_FOLD_COUNTER", "0"), ("PMX_DEFER_COUNTER", "0")])
+def test_counter_fold_equals_counter_kernel(monkeypatch, dtype, knob, off):
+    """The counter phase and the quantile-window pick folded into the match
+    kernel's last workgroup (PMX_FOLD_COUNTER=1: two-level tickets, coherent
+    loads of the counters and window keys) or deferred to the start of the
+    select_all launch (PMX_DEFER_COUNTER, default on: block 0 runs it and
+    publishes the window verdict) leave whole loops bit-identical to the
     separate counter_sum kernel."""
+    monkeypatch.setenv("PMX_DEFER_COUNTER", "0")
     ref, nrm = reference_cloud(60000, dtype)
     rd = reading_cloud(50000, dtype)
     out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("PMX_FOLD_COUNTER", mode)
+    for mode in ("1", off):
+        monkeypatch.setenv(knob, mode)
         ctx = _capi.Context(0, dtype)
         ctx.set_reference(ref, nrm)
         ctx.set_reading(rd)
@@ -264,5 +268,5 @@ def test_counter_fold_equals_counter_kernel(monkeypatch, dtype):
         out[mode] = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept,
                      st.point_count_touched, st.last.limit)
         ctx.close()
-    assert out["1"][1] == out["0"][1] and out["1"][2:] == out["0"][2:]
-    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out[off][1] and out["1"][2:] == out[off][2:]
+    assert np.array_equal(out["1"][0], out[off][0])
