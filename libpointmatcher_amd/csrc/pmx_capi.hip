@@ -224,6 +224,21 @@ struct pmx_ctx {
     bool fold_counter = false;  // the counter phase in the match's last workgroup (PMX_FOLD_COUNTER=1; measured slower)
     bool defer_counter = true;  // ... or at the start of the next select_all launch (PMX_DEFER_COUNTER=0: off)
     bool counter_deferred = false;  // the last match left its counter phase to the next select_all
+    // device loop, point-to-plane: the quantile's select_all launch held back
+    // and issued by the minimiser with the reduction after it (one launch
+    // fewer; PMX_SELECT_P2PLANE=1).  Off: measured at C3 (driver command) the
+    // merged launch took 34.2 us against 10.1 + 17.7 us for the two — the
+    // reduction waits for block 0's window pick before any block starts it,
+    // and 511 polling blocks hold the CUs meanwhile (74.7 vs 67.6 us/iteration)
+    bool select_p2 = false;
+    bool sel_pending = false;
+    const void* selp_d = nullptr;
+    int64_t selp_n = 0;
+    double selp_ratio = 0.0;
+    const double* selp_ratio_dev = nullptr;
+    SelectState* selp_st = nullptr;
+    SpecSel* selp_spec = nullptr;
+    bool selp_pre = false;
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;
@@ -781,9 +796,25 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
 }
 
 // ------------------------------------------------------------------- match --
+// a select held back for the point-to-plane minimiser, issued alone
+template <typename T>
+void flush_select(pmx_ctx* c) {
+    if (!c->sel_pending) return;
+    c->sel_pending = false;
+    const int64_t g = select_all_blocks(c->selp_n);
+    if (g != c->selx_grid) {
+        (void)hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream);
+        c->selx_grid = g;
+    }
+    launch_select_all<T>((const T*)c->selp_d, c->selp_n, c->d_selx, c->selp_st, c->selp_ratio, c->selp_ratio_dev,
+                         c->d_iter_err, loop_ctl(c), c->selp_spec, c->selp_pre ? c->d_vpart : nullptr,
+                         c->selp_pre ? c->d_visited : nullptr, P2Fuse<T>{}, 0, c->stream);
+}
+
 // the match's counter phase, when it was deferred to a select_all that did not come
 template <typename T>
 void flush_counter(pmx_ctx* c) {
+    flush_select<T>(c);
     if (!c->counter_deferred) return;
     c->counter_deferred = false;
     launch_counter_sum<T>(c->d_vpart, c->d_visited, c->d_iter_err, loop_ctl(c), c->spec_now(), c->d_sel, c->stream);
@@ -927,15 +958,27 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
             launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
         } else if (c->select_all) {
             // every pass in one launch (a no-op launch when the window resolved it)
+            const bool pre = c->counter_deferred;  // (the match left its counter phase to this launch)
+            c->counter_deferred = false;
+            if (spec && c->loop_on && c->select_p2 && c->loop_cfg.minimizer == 0) {
+                // held back: the point-to-plane minimiser launches it with its reduction (p2plane_enqueue)
+                c->sel_pending = true;
+                c->selp_d = d;
+                c->selp_n = n;
+                c->selp_ratio = ratio;
+                c->selp_ratio_dev = ratio_dev;
+                c->selp_st = st;
+                c->selp_spec = spec;
+                c->selp_pre = pre;
+                break;
+            }
             const int64_t g = select_all_blocks(n);
             if (g != c->selx_grid) {  // (the arrival generations assume a fixed block count)
                 HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
                 c->selx_grid = g;
             }
-            const bool pre = c->counter_deferred;  // (the match left its counter phase to this launch)
-            c->counter_deferred = false;
             launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec,
-                                 pre ? c->d_vpart : nullptr, pre ? c->d_visited : nullptr, c->stream);
+                                 pre ? c->d_vpart : nullptr, pre ? c->d_visited : nullptr, P2Fuse<T>{}, 0, c->stream);
             break;
         } else {
             launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, loop_ctl(c),
@@ -1051,7 +1094,9 @@ WChain<T> chain_of(const pmx_ctx* c) {
 // the 0/1 weights themselves are evaluated inline by the minimiser.
 template <typename T>
 int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, double p2) {
-    if (!(chain_pos == 0 && (kind == 4 || kind == 5))) flush_counter<T>(c);  // (4 / 5 consume it in their select)
+    // (the fixed predicates only record themselves; a quantile filter at
+    // position 0 takes the deferred counter phase into its select)
+    if (kind == 6 || ((kind == 4 || kind == 5) && chain_pos > 0)) flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     if (chain_pos < 0 || chain_pos >= kMaxChain) return fail(c, PMX_E_BAD_PARAM, "outlier chain longer than 8 filters");
@@ -1312,13 +1357,39 @@ int materialise_weights(pmx_ctx* c) {
 // which gets the value count back in *fuse_nv
 template <typename T>
 int p2plane_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
-    flush_counter<T>(c);
     const WChain<T> chain = chain_of<T>(c);
     const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
-    Mat4<T> Tm = step_mat<T>(c);
-    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
-                              match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
-                              loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+    // the held-back quantile select and this reduction in one launch: the
+    // quantile is chain position 0, every later position a fixed predicate
+    bool merge = c->sel_pending && loop_ctl(c) && !chain.robust && c->selp_st == c->sel_slot(0) && c->has_normals;
+    for (int i = 1; merge && i < chain.n; ++i) merge = chain.type[i] != kWPState;
+    if (merge) {
+        c->sel_pending = false;
+        if ((int64_t)kRedBlocks != c->selx_grid) {  // (the arrival generations assume a fixed block count)
+            HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
+            c->selx_grid = kRedBlocks;
+        }
+        P2Fuse<T> p2;
+        p2.on = 1;
+        p2.dim = c->dim;
+        p2.rd = (const P4<T>*)c->d_rd;
+        p2.d = (const T*)c->d_dists;
+        p2.ids = c->d_ids;
+        p2.chain = chain;
+        p2.k = c->knn;
+        p2.N = c->N;
+        p2.partials = c->d_partials;
+        p2.gd = (const GridDesc<T>*)c->d_gdesc;
+        launch_select_all<T>((const T*)c->selp_d, c->selp_n, c->d_selx, c->selp_st, c->selp_ratio, c->selp_ratio_dev,
+                             c->d_iter_err, loop_ctl(c), c->selp_spec, c->selp_pre ? c->d_vpart : nullptr,
+                             c->selp_pre ? c->d_visited : nullptr, p2, kRedBlocks, c->stream);
+    } else {
+        flush_counter<T>(c);
+        Mat4<T> Tm = step_mat<T>(c);
+        launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
+                                  match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim,
+                                  c->d_partials, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+    }
     if (fuse_nv && *fuse_nv && !sharded(c)) {
         *fuse_nv = NV;
         HIPCHK(c, hipGetLastError());
@@ -2069,6 +2140,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_FUSE_FINAL")) c->fuse_final = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_FOLD_COUNTER")) c->fold_counter = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_DEFER_COUNTER")) c->defer_counter = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_SELECT_P2PLANE")) c->select_p2 = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_SELECT_ALL")) c->select_all = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0

@@ -367,6 +367,22 @@ template <typename T>
 void launch_robust_scale(int mode, const SelectState* st, const double* sums, int64_t n, double target,
                          double* scale, hipStream_t s);
 
+// the point-to-plane reduction run by the select launch once the quantile is
+// resolved (device loop, single rank, PMX_SELECT_P2PLANE): on = 0 leaves the
+// launch a plain select
+template <typename T>
+struct P2Fuse {
+    int on = 0;
+    int dim = 3;
+    const P4<T>* rd = nullptr;
+    const T* d = nullptr;
+    const int32_t* ids = nullptr;
+    WChain<T> chain;
+    int k = 1;
+    int64_t N = 0;
+    double* partials = nullptr;
+    const GridDesc<T>* gd = nullptr;
+};
 // ---- quantile / weights (pmx_select.hip) ----
 // one radix-select pass: histogram of digit `pass` among keys matching the
 // resolved prefix.  hist must be zero on entry (select zeroes it on exit).
@@ -398,7 +414,8 @@ constexpr int kSelTimeout = -30;  // iteration error: a select_all wait timed ou
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
                        int* iter_err, const LoopCtl* ctl, SpecSel* spec,
-                       unsigned long long* vpart, unsigned long long* vout, hipStream_t s);
+                       unsigned long long* vpart, unsigned long long* vout, const P2Fuse<T>& p2, int64_t grid,
+                       hipStream_t s);
 int select_bins(int pass, int key_bits);
 
 // VarTrimmed pieces

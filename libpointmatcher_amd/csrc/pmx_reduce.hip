@@ -20,38 +20,9 @@
 // results are deterministic.  ~56 B per pair (reading 16, dist 4, id 4,
 // gathered point 16, gathered normal 16).
 #include "pmx_internal.h"
+#include "pmx_p2plane.h"
 
 namespace pmx {
-
-template <typename T>
-__device__ __forceinline__ void xform3(const Mat4<T>& M, const P4<T>& p, T& x, T& y, T& z) {
-    x = ((M.m[0] * p.x + M.m[1] * p.y) + M.m[2] * p.z) + M.m[3] * p.w;
-    y = ((M.m[4] * p.x + M.m[5] * p.y) + M.m[6] * p.z) + M.m[7] * p.w;
-    z = ((M.m[8] * p.x + M.m[9] * p.y) + M.m[10] * p.z) + M.m[11] * p.w;
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-
-// block reduction of NV accumulators; writes partials[v * gridDim.x + blockIdx.x]
-// (value-major: the finalize reads each value's block partials contiguously)
-template <int NV>
-__device__ __forceinline__ void block_store(double (&acc)[NV], double* __restrict__ partials) {
-    __shared__ double red[4][NV];
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double s = wave_sum(acc[v]);
-        if (lane == 0) red[wave][v] = s;
-    }
-    __syncthreads();
-    for (int v = threadIdx.x; v < NV; v += blockDim.x)
-        partials[(int64_t)v * gridDim.x + blockIdx.x] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
-}
 
 // The chain's weight of one match when it holds a RobustOutlierFilter:
 // (predicates' 0/1) * robust(e^2), e^2 = dist / scale^2 in T
@@ -75,41 +46,6 @@ __device__ __forceinline__ T p2pl_distance(T px, T py, T pz, const P4<T>& q, con
     return dot * dot;  // (pow(dot, 2) rounds to the same T)
 }
 
-// one kept pair: F and dot in T exactly as PointToPlane.cpp:171-243, the
-// upper triangle of F F^T and F dot added in fp64
-template <typename T, int DIM, int NV>
-__device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz, const P4<T>& q, const P4<T>& n,
-                                            T w = (T)1) {
-    constexpr int NF = DIM == 3 ? 6 : 3;
-    constexpr int NS = NF * (NF + 1) / 2;
-    T F[NF];
-    T dot;
-    if (DIM == 3) {
-        F[0] = py * n.z - pz * n.y;
-        F[1] = pz * n.x - px * n.z;
-        F[2] = px * n.y - py * n.x;
-        F[3] = n.x;
-        F[4] = n.y;
-        F[5] = n.z;
-        dot = ((px - q.x) * n.x + (py - q.y) * n.y) + (pz - q.z) * n.z;
-    } else {
-        F[0] = px * n.y - py * n.x;
-        F[1] = n.x;
-        F[2] = n.y;
-        dot = (px - q.x) * n.x + (py - q.y) * n.y;
-    }
-    // wF = w * F (PointToPlane.cpp:218-227); with the 0/1 weights w = 1 and
-    // wF is F exactly
-    int a = 0;
-#pragma unroll
-    for (int r = 0; r < NF; ++r) {
-        const T wF = w * F[r];
-#pragma unroll
-        for (int c = r; c < NF; ++c) acc[a++] += (double)(wF * F[c]);
-        acc[NS + r] += (double)(wF * dot);
-    }
-}
-
 // result layout: [0, NS) upper triangle of A row-major (r <= c), [NS, NS+NF) b,
 // then kept, nonzero weights, rejected matches, rejected points
 template <typename T, int DIM>
@@ -121,9 +57,6 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                                                               int k, int64_t N, double* __restrict__ partials,
                                                               const LoopCtl* __restrict__ ctl,
                                                               const GridDesc<T>* __restrict__ gd) {
-    constexpr int NF = DIM == 3 ? 6 : 3;
-    constexpr int NS = NF * (NF + 1) / 2;
-    constexpr int NV = NS + NF + 5;  // (the fifth counter, sum of w, is the kept count with 0/1 weights)
     if (ctl) {  // device loop
         if (ctl->done) return;
         ctl_transform(ctl, Tm);
@@ -131,79 +64,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
         nrm = ref + 1;
         rs = 2;
     }
-    double acc[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
-    const WRange<T> wr = chain_resolve(chain);
-    const T inf = (T)__builtin_huge_val();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k == 1) {
-        // k = 1: U slots per round with every load issued up front (the
-        // reduction is latency-bound: slot -> id -> gathered point / normal)
-        constexpr int U = 4;
-        for (; i0 < N; i0 += U * stride) {
-            P4<T> r[U];
-            T dv[U];
-            int32_t id[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t ii = i0 + u * stride;
-                const int64_t jj = ii < N ? ii : i0;
-                r[u] = rd[jj];
-                dv[u] = d[jj];
-                id[u] = ids[jj];
-            }
-            bool kp[U];
-            P4<T> q[U], n[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                kp[u] = i0 + u * stride < N && dv[u] != inf && chain_keep(wr, dv[u]);
-                const int64_t g = (int64_t)(kp[u] ? id[u] : 0) * rs;  // (position 0 always exists)
-                q[u] = gld(ref, g);
-                n[u] = gld(nrm, g);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (i0 + u * stride >= N) continue;
-                const bool keep = chain_keep(wr, dv[u]);
-                if (keep) acc[NS + NF + 1] += 1.0;                 // (w != 0).count()
-                if (dv[u] != inf && !keep) acc[NS + NF + 2] += 1.0;  // rejected match
-                if (!kp[u]) {
-                    acc[NS + NF + 3] += 1.0;  // rejected point
-                    continue;
-                }
-                acc[NS + NF + 0] += 1.0;
-                acc[NS + NF + 4] += 1.0;
-                T px, py, pz;
-                xform3(Tm, r[u], px, py, pz);
-                p2plane_add<T, DIM, NV>(acc, px, py, pz, q[u], n[u]);
-            }
-        }
-    }
-    for (int64_t i = i0; k != 1 && i < N; i += stride) {
-        T px, py, pz;
-        xform3(Tm, rd[i], px, py, pz);
-        bool exist = false;
-        for (int s = 0; s < k; ++s) {
-            const int64_t e = i * k + s;
-            const T dv = d[e];
-            const bool keep = chain_keep(wr,dv);
-            if (keep) acc[NS + NF + 1] += 1.0;  // (w != 0).count()
-            if (dv == inf) continue;
-            if (!keep) {
-                acc[NS + NF + 2] += 1.0;  // rejected match
-                continue;
-            }
-            exist = true;
-            acc[NS + NF + 0] += 1.0;  // kept
-            acc[NS + NF + 4] += 1.0;  // sum of the 0/1 weights
-            const int32_t id = ids[e];
-            p2plane_add<T, DIM, NV>(acc, px, py, pz, gld(ref, (int64_t)id * rs), gld(nrm, (int64_t)id * rs));
-        }
-        if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
-    }
-    block_store<NV>(acc, partials);
+    p2plane_body<T, DIM>(rd, Tm, ref, nrm, rs, d, ids, chain, k, N, partials);
 }
 
 // Real-valued weights (a RobustOutlierFilter in the chain; per-module path):

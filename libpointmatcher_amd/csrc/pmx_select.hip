@@ -20,6 +20,7 @@
 // argmin, then the same radix select with the optimised ratio.
 #include "pmx_internal.h"
 #include "pmx_spec.h"
+#include "pmx_p2plane.h"
 
 #include <algorithm>
 #include <cmath>
@@ -366,6 +367,7 @@ struct SelX {
     unsigned long long tot[kSelMaxPasses];   // keys histogrammed in pass p
     unsigned long long count;                // finite keys (pass 0)
     unsigned long long pre;                  // gen << 56 | window hit: the deferred counter phase's verdict
+    unsigned long long lim;                  // the resolved limit (double bits), for a fused point-to-plane
 };
 size_t selx_bytes() { return sizeof(SelX) + (size_t)kSelMaxPasses * 2048 * sizeof(uint32_t); }
 int64_t select_all_blocks(int64_t n) { return select_blocks(n); }
@@ -378,15 +380,17 @@ __device__ __forceinline__ unsigned long long ast(unsigned long long* p, unsigne
     return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The select itself; true when this block ends with the resolved limit in
+// *L (then, with a fused point-to-plane, it goes on to the reduction).
+// `wait_last`: the non-picker blocks wait for the last pass's publication
+// (they need the limit) instead of leaving.
 template <typename T>
-__global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
-                                                         SelectState* __restrict__ st, double ratio_host,
-                                                         const double* __restrict__ ratio_dev,
-                                                         int* __restrict__ iter_err, int agg,
-                                                         const LoopCtl* __restrict__ ctl,
-                                                         SpecSel* __restrict__ spec,
-                                                         unsigned long long* __restrict__ vpart,
-                                                         unsigned long long* __restrict__ vout) {
+__device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
+                                                SelectState* __restrict__ st, double ratio_host,
+                                                const double* __restrict__ ratio_dev, int* __restrict__ iter_err,
+                                                int agg, SpecSel* __restrict__ spec,
+                                                unsigned long long* __restrict__ vpart,
+                                                unsigned long long* __restrict__ vout, bool wait_last, double* L) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     __shared__ uint32_t lh[2048];
@@ -394,7 +398,6 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
     __shared__ unsigned long long s_w[2];  // (published word, its generation)
     __shared__ int s_last;
     __shared__ unsigned int s_old;
-    if (ctl && ctl->done) return;  // (uniform: no block arrives anywhere)
     if (vpart) {
         // The match's counter phase deferred into this launch (one launch
         // fewer per iteration): block 0 folds the counters and tries the
@@ -408,11 +411,18 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
             __syncthreads();
             if (threadIdx.x == 0) {
                 const unsigned long long hit = spec && spec->hit ? 1ull : 0ull;
+                // the limit first (write-through), then the verdict that covers it
+                const unsigned long long r0 = hit ? ast(&sx->lim, (unsigned long long)__double_as_longlong(st->limit)) : 0ull;
+                asm volatile("" ::"v"(r0));
                 (void)ast(&sx->pre, pgen << 56 | hit);
                 s_w[0] = hit;
+                s_w[1] = (unsigned long long)__double_as_longlong(st->limit);
             }
             __syncthreads();
-            if (s_w[0]) return;
+            if (s_w[0]) {
+                *L = __longlong_as_double((long long)s_w[1]);
+                return true;
+            }
         } else {
             if (threadIdx.x == 0) {
                 unsigned long long w = 0;
@@ -425,14 +435,20 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
                     }
                     __builtin_amdgcn_s_sleep(2);
                 }
-                s_w[0] = ok ? (w & 1ull) : 1ull;
+                s_w[0] = ok ? (w & 1ull) : 2ull;
                 if (!ok) __hip_atomic_store(iter_err, kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (ok && (w & 1ull)) s_w[1] = ald(&sx->lim);
             }
             __syncthreads();
-            if (s_w[0]) return;  // the window resolved it (or the wait timed out)
+            if (s_w[0] == 2ull) return false;  // (the wait timed out)
+            if (s_w[0]) {  // the window resolved it
+                *L = __longlong_as_double((long long)s_w[1]);
+                return true;
+            }
         }
     } else if (spec && spec->hit) {
-        return;  // the quantile window resolved it (pmx_spec.h)
+        *L = st->limit;  // (the window resolved it in the counter kernel before this launch)
+        return true;
     }
     constexpr int passes = KO::bits == 32 ? 3 : 6;
     uint32_t* hist0 = reinterpret_cast<uint32_t*>(sx + 1);
@@ -578,16 +594,21 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
                 } else {
                     r0 |= ast(&sx->rank[pass], nrank);
                 }
+                if (pass == passes - 1 && !err) r0 |= ast(&sx->lim, (unsigned long long)__double_as_longlong((double)KO::val(np)));
                 // publish once the data above has returned (performed where every block reads it)
                 asm volatile("" ::"v"(r0));
                 (void)ast(&sx->go[pass],
                           gen << 56 | (err ? 1ull << 55 : 0ull) | ((unsigned long long)np & ((1ull << 55) - 1)));
             }
-            if (err) return;
+            if (err) return false;
             prefix = np;
             __syncthreads();
+            if (pass == passes - 1) {
+                *L = (double)KO::val(np);
+                return true;
+            }
         } else {
-            if (pass == passes - 1) return;  // (the picker finishes alone)
+            if (pass == passes - 1 && !wait_last) return false;  // (the picker finishes alone)
             // ---- wait for this generation's publication (bounded) ----
             if (t == 0) {
                 unsigned long long w = 0;
@@ -606,18 +627,60 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
             }
             __syncthreads();
             const unsigned long long w = s_w[0];
-            if (!s_w[1] || (w >> 55) & 1ull) return;  // timeout, or the quantile failed
+            if (!s_w[1] || (w >> 55) & 1ull) return false;  // timeout, or the quantile failed
             prefix = (K)(w & ((1ull << 55) - 1));
+            if (pass == passes - 1) {  // (wait_last) the published final limit
+                if (threadIdx.x == 0) s_w[0] = ald(&sx->lim);
+                __syncthreads();
+                *L = __longlong_as_double((long long)s_w[0]);
+                return true;
+            }
         }
     }
+    return false;
+}
+
+// the point-to-plane reduction after the select, with the limit resolved in
+// this launch (read from LDS: the SelectState in HBM was written by another
+// workgroup of this launch)
+template <typename T>
+__device__ __forceinline__ void p2_after_select(const P2Fuse<T>& p2, const LoopCtl* __restrict__ ctl, double L) {
+    __shared__ SelectState s_lim;
+    if (threadIdx.x == 0) s_lim.limit = L;
+    __syncthreads();
+    WChain<T> ch = p2.chain;
+    ch.st[0] = &s_lim;
+    Mat4<T> Tm;
+    ctl_transform(ctl, Tm);
+    const P4<T>* ref = p2.gd[ctl->level].gpn;
+    if (p2.dim == 3)
+        p2plane_body<T, 3>(p2.rd, Tm, ref, ref + 1, 2, p2.d, p2.ids, ch, p2.k, p2.N, p2.partials);
+    else
+        p2plane_body<T, 2>(p2.rd, Tm, ref, ref + 1, 2, p2.d, p2.ids, ch, p2.k, p2.N, p2.partials);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
+                                                         SelectState* __restrict__ st, double ratio_host,
+                                                         const double* __restrict__ ratio_dev,
+                                                         int* __restrict__ iter_err, int agg,
+                                                         const LoopCtl* __restrict__ ctl,
+                                                         SpecSel* __restrict__ spec,
+                                                         unsigned long long* __restrict__ vpart,
+                                                         unsigned long long* __restrict__ vout, P2Fuse<T> p2) {
+    if (ctl && ctl->done) return;  // (uniform: no block arrives anywhere)
+    double L = 0.0;
+    const bool ok = select_all_body<T>(d, n, sx, st, ratio_host, ratio_dev, iter_err, agg, spec, vpart, vout,
+                                       p2.on != 0, &L);
+    if (p2.on && ok) p2_after_select<T>(p2, ctl, L);
 }
 
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
                        int* iter_err, const LoopCtl* ctl, SpecSel* spec, unsigned long long* vpart,
-                       unsigned long long* vout, hipStream_t s) {
-    hipLaunchKernelGGL(select_all_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, (SelX*)selx,
-                       st, ratio, ratio_dev, iter_err, select_agg(), ctl, spec, vpart, vout);
+                       unsigned long long* vout, const P2Fuse<T>& p2, int64_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(select_all_kernel<T>, dim3((unsigned)(grid > 0 ? grid : select_blocks(n))), dim3(256), 0, s, d,
+                       n, (SelX*)selx, st, ratio, ratio_dev, iter_err, select_agg(), ctl, spec, vpart, vout, p2);
 }
 
 template <typename T>
@@ -906,10 +969,10 @@ template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, c
                                          SpecSel*, hipStream_t);
 template void launch_select_all<float>(const float*, int64_t, void*, SelectState*, double, const double*, int*,
                                        const LoopCtl*, SpecSel*, unsigned long long*, unsigned long long*,
-                                       hipStream_t);
+                                       const P2Fuse<float>&, int64_t, hipStream_t);
 template void launch_select_all<double>(const double*, int64_t, void*, SelectState*, double, const double*, int*,
                                         const LoopCtl*, SpecSel*, unsigned long long*, unsigned long long*,
-                                        hipStream_t);
+                                        const P2Fuse<double>&, int64_t, hipStream_t);
 template void launch_select_pass<float>(const float*, int64_t, uint32_t*, SelectState*, int, double, const double*,
                                         unsigned int*, int*, const LoopCtl*, SpecSel*, hipStream_t);
 template void launch_select_pass<double>(const double*, int64_t, uint32_t*, SelectState*, int, double, const double*,

@@ -245,15 +245,18 @@ def test_select_all_passes_in_one_launch(monkeypatch, dtype, filt, knn, max_dist
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("knob,off", [("PMX_FOLD_COUNTER", "0"), ("PMX_DEFER_COUNTER", "0")])
+@pytest.mark.parametrize("knob,off", [("PMX_FOLD_COUNTER", "0"), ("PMX_DEFER_COUNTER", "0"),
+                                      ("PMX_SELECT_P2PLANE", "0")])
 def test_counter_fold_equals_counter_kernel(monkeypatch, dtype, knob, off):
     """The counter phase and the quantile-window pick folded into the match
     kernel's last workgroup (PMX_FOLD_COUNTER=1: two-level tickets, coherent
     loads of the counters and window keys) or deferred to the start of the
     select_all launch (PMX_DEFER_COUNTER, default on: block 0 runs it and
     publishes the window verdict) leave whole loops bit-identical to the
-    separate counter_sum kernel."""
-    monkeypatch.setenv("PMX_DEFER_COUNTER", "0")
+    separate counter_sum kernel; the select and the point-to-plane reduction
+    in one launch (PMX_SELECT_P2PLANE=1, off by default: every block reads the
+    limit published in the launch) leave them identical to the two launches."""
+    monkeypatch.setenv("PMX_DEFER_COUNTER", "0" if knob == "PMX_FOLD_COUNTER" else "1")
     ref, nrm = reference_cloud(60000, dtype)
     rd = reading_cloud(50000, dtype)
     out = {}
