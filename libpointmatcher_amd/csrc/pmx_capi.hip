@@ -222,7 +222,10 @@ struct pmx_ctx {
     // costs more than the finalize kernel and its boundary it saves
     bool fuse_final = false;
     bool fold_counter = false;  // the counter phase in the match's last workgroup (PMX_FOLD_COUNTER=1; measured slower)
-    bool defer_counter = true;  // ... or at the start of the next select_all launch (PMX_DEFER_COUNTER=0: off)
+    // ... or at the start of the next select_all launch (PMX_DEFER_COUNTER=1).  Off: on the driver command
+    // (same box, A/B twice) 0.0884 ms/step deferred vs 0.0861 separate — fewer launches in the converged
+    // iterations (kernel trace 74 -> 68 us), but slower in iterations 5-24 of the timed window
+    bool defer_counter = false;
     bool counter_deferred = false;  // the last match left its counter phase to the next select_all
     // device loop, point-to-plane: the quantile's select_all launch held back
     // and issued by the minimiser with the reduction after it (one launch
@@ -1237,10 +1240,11 @@ int outlier_robust_impl(pmx_ctx* c, int pos, int fct, double tuning, double appr
         break;
     case kRSStd: {  // Matches::getStandardDeviation (Matches.cpp:124-129) over all k x N
         double* sums = c->rob_sums();
-        launch_moment<T>(d, n, 0, sums, c->d_partials, c->stream);
+        const int64_t nt = c->N_total * c->knn;  // (the mean over every rank's distances)
+        launch_moment<T>(d, n, 0, sums, c->d_partials, nt, c->stream);
         launch_finalize(c->d_partials, kRedBlocks, 1, sums, loop_ctl(c), c->stream);
         if ((rc = allreduce_f64(c, sums, 1))) return rc;
-        launch_moment<T>(d, n, 1, sums, c->d_partials, c->stream);
+        launch_moment<T>(d, n, 1, sums, c->d_partials, nt, c->stream);
         launch_finalize(c->d_partials, kRedBlocks, 1, sums + 1, loop_ctl(c), c->stream);
         if ((rc = allreduce_f64(c, sums + 1, 1))) return rc;
         launch_robust_scale<T>(kRSStd, nullptr, sums, c->N_total * c->knn, 0.0, scale, c->stream);

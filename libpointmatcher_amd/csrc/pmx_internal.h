@@ -361,7 +361,8 @@ void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, hipStr
 // sum of d (pass 0) / of (d - mean)^2 with mean = (T)(sum / n) (pass 1) into
 // partials (kRedBlocks x 1), summed by launch_finalize
 template <typename T>
-void launch_moment(const T* d, int64_t n, int pass, const double* sum, double* partials, hipStream_t s);
+void launch_moment(const T* d, int64_t n, int pass, const double* sum, double* partials, int64_t n_total,
+                   hipStream_t s);
 // the scale (a T value stored as double) of the iteration, from the mode
 template <typename T>
 void launch_robust_scale(int mode, const SelectState* st, const double* sums, int64_t n, double target,

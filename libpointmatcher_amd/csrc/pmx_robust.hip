@@ -35,12 +35,14 @@ void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, hipStr
     hipLaunchKernelGGL(abs_dev_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, n, st, dev);
 }
 
-// pass 0: sum d; pass 1: sum (d - mean)^2, mean = (T)(sum / n) (T arithmetic per term)
+// pass 0: sum d; pass 1: sum (d - mean)^2, mean = (T)(sum / n_total) (T
+// arithmetic per term; n_total: every rank's count, the sum being all-reduced)
 template <typename T>
 __global__ __launch_bounds__(256) void moment_kernel(const T* __restrict__ d, int64_t n, int pass,
-                                                     const double* __restrict__ sum, double* __restrict__ partials) {
+                                                     const double* __restrict__ sum, double* __restrict__ partials,
+                                                     int64_t n_total) {
     __shared__ double red[4];
-    const T mean = pass ? (T)(*sum / (double)n) : (T)0;
+    const T mean = pass ? (T)(*sum / (double)n_total) : (T)0;
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -59,8 +61,9 @@ __global__ __launch_bounds__(256) void moment_kernel(const T* __restrict__ d, in
 }
 
 template <typename T>
-void launch_moment(const T* d, int64_t n, int pass, const double* sum, double* partials, hipStream_t s) {
-    hipLaunchKernelGGL(moment_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, d, n, pass, sum, partials);
+void launch_moment(const T* d, int64_t n, int pass, const double* sum, double* partials, int64_t n_total,
+                   hipStream_t s) {
+    hipLaunchKernelGGL(moment_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, d, n, pass, sum, partials, n_total);
 }
 
 template <typename T>
@@ -95,7 +98,7 @@ void launch_robust_scale(int mode, const SelectState* st, const double* sums, in
 
 #define PMX_ROBUST_INST(T)                                                                                  \
     template void launch_abs_dev<T>(const T*, int64_t, const SelectState*, T*, hipStream_t);               \
-    template void launch_moment<T>(const T*, int64_t, int, const double*, double*, hipStream_t);           \
+    template void launch_moment<T>(const T*, int64_t, int, const double*, double*, int64_t, hipStream_t);  \
     template void launch_robust_scale<T>(int, const SelectState*, const double*, int64_t, double, double*, \
                                          hipStream_t);
 PMX_ROBUST_INST(float)

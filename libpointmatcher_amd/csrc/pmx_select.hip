@@ -427,13 +427,14 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
             if (threadIdx.x == 0) {
                 unsigned long long w = 0;
                 bool ok = false;
-                for (int it = 0; it < (1 << 22); ++it) {
+                // (a slow poll: block 0's own coherent loads share the path with these)
+                for (int it = 0; it < (1 << 20); ++it) {
                     w = ald(&sx->pre);
                     if ((w >> 56) == pgen) {
                         ok = true;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_s_sleep(16);
                 }
                 s_w[0] = ok ? (w & 1ull) : 2ull;
                 if (!ok) __hip_atomic_store(iter_err, kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

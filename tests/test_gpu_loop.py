@@ -251,8 +251,8 @@ def test_counter_fold_equals_counter_kernel(monkeypatch, dtype, knob, off):
     """The counter phase and the quantile-window pick folded into the match
     kernel's last workgroup (PMX_FOLD_COUNTER=1: two-level tickets, coherent
     loads of the counters and window keys) or deferred to the start of the
-    select_all launch (PMX_DEFER_COUNTER, default on: block 0 runs it and
-    publishes the window verdict) leave whole loops bit-identical to the
+    select_all launch (PMX_DEFER_COUNTER=1: block 0 runs it and publishes
+    the window verdict) leave whole loops bit-identical to the
     separate counter_sum kernel; the select and the point-to-plane reduction
     in one launch (PMX_SELECT_P2PLANE=1, off by default: every block reads the
     limit published in the launch) leave them identical to the two launches."""

@@ -69,6 +69,8 @@ ICP_RUNS = [
     ("med", (("MedianDistOutlierFilter", {"factor": 3.0}), ("MaxDistOutlierFilter", {"maxDist": 0.5})), P2PLANE,
      20, None, True),
     ("p2pt", (), P2POINT, 10, None, False),
+    ("robust", (("RobustOutlierFilter", {"robustFct": "cauchy", "scaleEstimator": "mad", "tuning": 1}),), P2POINT,
+     15, DIFF, False),
 ]
 
 
@@ -107,6 +109,12 @@ def _worker(rank, world, port, outdir, env):
             ctx.outlier("VarTrimmedDistOutlierFilter", 0, **VT)
             A, b, st = ctx.p2plane_system()
             res[f"{dn}_vt"] = np.concatenate([A.ravel(), b, [st.limit, st.kept]])
+            # RobustOutlierFilter: MAD (two sharded selects) and std (all-reduced moments)
+            for tag, fct, mode in (("rmad", "cauchy", _capi.RS_MAD), ("rstd", "welsch", _capi.RS_STD)):
+                ctx.match(I, knn=2)
+                ctx.outlier_robust(0, fct, 0.8, np.inf, mode, 0.0)
+                A, b, st = ctx.p2plane_system()
+                res[f"{dn}_{tag}"] = np.concatenate([A.ravel(), b, [ctx.robust_scale(0), st.kept, st.sum_w]])
             # the device loop on the context: quantile window exchanged as segments
             ctx.set_reading(shard)
             ctx.loop_begin(filters=[("TrimmedDistOutlierFilter", 0.85)], checkers=[("CounterTransformationChecker", 25)])
@@ -181,6 +189,24 @@ def test_sharded_modules_vs_oracle(two_ranks, oracle, dn):
     rc, w = oracle.outlier_chain([("VarTrimmedDistOutlierFilter", VT)], d)
     assert rc == 0
     assert int(r[0][f"{dn}_vt"][-1]) == int((w != 0).sum())
+    # RobustOutlierFilter over the shards: the global scale (MAD bit-equal, std
+    # to fp64 reassociation), the weighted system (full A) to the weights' tolerance
+    d2, ids2, _ = oracle.knn(ref, rd, k=2)
+    for tag, fct, scale in (("rmad", "cauchy", "mad"), ("rstd", "welsch", "std")):
+        np.testing.assert_array_equal(r[0][f"{dn}_{tag}"], r[1][f"{dn}_{tag}"])
+        rb = oracle.make_robust({"robustFct": fct, "scaleEstimator": scale, "tuning": 0.8})
+        rc, w = oracle.robust_weights(rb, d2, ids2)
+        assert rc == 0
+        rc, A, b, st = oracle.p2plane_system(rd, ref, nrm, d2, ids2, w)
+        got = r[0][f"{dn}_{tag}"]
+        if scale == "mad":
+            assert got[-3] == rb.scale
+        else:
+            np.testing.assert_allclose(got[-3], rb.scale, rtol=4e-7 if dn == "float32" else 1e-13)
+        assert int(got[-2]) == st.kept
+        full = np.concatenate([A.ravel(), b])
+        tol = 1e-6 if dn == "float32" else 1e-11  # (device exp vs libm: the weights to ~1 ulp)
+        np.testing.assert_allclose(got[:42], full, rtol=tol, atol=tol * np.abs(full).max())
 
 
 @pytest.mark.timeout(900)
