@@ -38,12 +38,11 @@ __device__ void loop_fail(LoopCtl* ctl, LoopState<T>* S, int code, int reason) {
 }
 
 template <typename T>
-__device__ void loop_publish(LoopCtl* ctl, const LoopState<T>* S, int rows) {
+__device__ void loop_publish(LoopCtl* ctl, const T* m, int rows) {
     // the next step transform, embedded in 4x4 as the kernels expect
     if (rows == 4) {
-        for (int i = 0; i < 16; ++i) ctl->T[i] = (double)S->Titer[i];
+        for (int i = 0; i < 16; ++i) ctl->T[i] = (double)m[i];
     } else {
-        const T* m = S->Titer;
         const double e[16] = {m[0], m[1], 0, m[2], m[3], m[4], 0, m[5], 0, 0, 1, 0, m[6], m[7], 0, m[8]};
         for (int i = 0; i < 16; ++i) ctl->T[i] = e[i];
     }
@@ -84,6 +83,49 @@ __device__ __noinline__ void loop_solve_rank_deficient(const double* __restrict_
     p2plane_system_of<T, NF>(res, A, b);
     solve_rank_deficient(A, b, NF, x);
     for (int i = 0; i < NF; ++i) xout[i] = x[i];
+}
+
+// A sufficient condition for FullPivHouseholderQR(A).isInvertible() of the
+// SPD point-to-plane system, from its LLT factor: lambda_min(A) >=
+// 1 / ||L^-1||_F^2 and sigma_max(A) <= ||A||_F, so the ratio below bounds
+// sigma_min / sigma_max from below.  At QR step k the trailing block B_k of
+// [R11 R12; 0 B_k] has sigma_min(B_k) >= sigma_min(A) (B_k^-1 is a block of
+// R^-1) and ||B_k|| <= ||A||; the pivot is B_k's largest entry, so |R_kk|
+// (its column's norm) >= max|B_k| >= sigma_min(A) / n, and every pivot and
+// |R_kk| <= sigma_max(A).  The rank threshold is max|R_kk| * n * eps (7.2e-7
+// in float, 1.3e-15 in double): a ratio of 1e-3 (float) / 1e-9 (double)
+// clears it by a factor of 230 / 1e5, far beyond the rounding of every
+// quantity involved (backward error ~n^2 eps ||A||).  Below the ratio (or with a failed / non-finite
+// factor) the QR decides, as before.
+template <typename T, int NF>
+__device__ __forceinline__ bool well_conditioned(const T* A, const T* L) {
+    T inv[NF * NF], rd[NF];  // L^-1 (lower), column by column; 1 / diag (a bound: no exact division needed)
+    T s = 0, fa = 0;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < NF; ++k) {
+        ok = ok && L[k * NF + k] > (T)0;
+        rd[k] = (T)1 / L[k * NF + k];
+    }
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            if (i < j) continue;
+            T v = i == j ? (T)1 : (T)0;
+#pragma unroll
+            for (int k = 0; k < NF; ++k)
+                if (k >= j && k < i) v = v - L[i * NF + k] * inv[k * NF + j];
+            v = v * rd[i];
+            inv[i * NF + j] = v;
+            s = s + v * v;
+        }
+#pragma unroll
+    for (int i = 0; i < NF * NF; ++i) fa = fa + A[i] * A[i];
+    const T ratio = sizeof(T) == 4 ? (T)1e-3 : (T)1e-9;
+    // (NaN / inf fail every comparison below)
+    return ok && s > (T)0 && s < (T)__builtin_huge_val() && fa < (T)__builtin_huge_val() &&
+           (T)1 / s >= ratio * sqrt(fa);
 }
 
 // The minimiser's last finalize, fused (single rank: no all-reduce between
@@ -176,6 +218,19 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
     }
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     constexpr int rows = ROWS, D = ROWS - 1;
+    // Every global read of the step first, together: the data was written
+    // by other XCDs' kernels, so each read is a memory round trip, and in
+    // use order they were serialised (~1.5 us of the kernel, clock64
+    // timestamps per phase on MI355X)
+    const int e = *iter_err;
+    const unsigned long long vis0 = visited[0], vis1 = visited[1];
+    const int level_now = ctl->level;
+    T Tit[ROWS * ROWS];
+#pragma unroll
+    for (int i = 0; i < ROWS * ROWS; ++i) Tit[i] = S->Titer[i];
+    T cnt[kMaxCheckers];
+#pragma unroll
+    for (int ci = 0; ci < kMaxCheckers; ++ci) cnt[ci] = S->cond[ci][0];
     // statistics of the iteration (ErrorElements, ErrorMinimizer.cpp:133-192)
     double kept, nz, rejM, rejP, sw;
     if (MIN == 0) {
@@ -192,11 +247,10 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
         rejP = res[10];
         sw = res[0];
     }
-    S->last_level = ctl->level;  // the level whose positions this iteration's ids are
+    S->last_level = level_now;  // the level whose positions this iteration's ids are
     // the next match may reuse this one's output (pmx_grid.hip temporal reuse)
     for (int i = 0; i < 16; ++i) ctl->Tprev[i] = ctl->T[i];
-    ctl->prev_level = ctl->level;
-    const int e = *iter_err;
+    ctl->prev_level = level_now;
     if (e) {
         loop_fail(ctl, S, e, kLoopError);
         return;
@@ -212,15 +266,27 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
     S->rejM = rejM;
     S->rejP = rejP;
     S->sw = sw;
-    S->last_visited = visited[0];
-    S->touched += visited[0];
+    S->last_visited = vis0;
+    S->touched += vis0;
     // the step transform
     T dT[16];
     if constexpr (MIN == 0) {
         constexpr int NF = D == 3 ? 6 : 3;
-        T A[NF * NF], b[NF], x[NF];
+        T A[NF * NF], b[NF], x[NF], L[NF * NF];
         p2plane_system_of<T, NF>(res, A, b);
-        if (!solve_full_rank(A, b, NF, x)) {
+        // solve_full_rank: FullPivQR(A).isInvertible() -> LLT solve.  The
+        // QR's rank test is skipped when the LLT factor proves A far from
+        // rank-deficient (well_conditioned below): its answer is then known.
+        llt(A, NF, L);
+        bool full = well_conditioned<T, NF>(A, L);
+        if (!full) {
+            FullPivQR<T> qr;
+            qr.compute(A, NF);
+            full = qr.rank() == NF;
+        }
+        if (full) {
+            llt_solve(L, NF, b, x);
+        } else {
             loop_solve_rank_deficient<T, NF>(res, S->xsolve);
             for (int i = 0; i < NF; ++i) x[i] = S->xsolve[i];
         }
@@ -234,14 +300,21 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
         }
         p2point_transform(rows, m, mp, mq, dT);
     }
-    matmul(dT, S->Titer, rows, S->Titer);
+    matmul(dT, Tit, rows, Tit);
+#pragma unroll
+    for (int i = 0; i < ROWS * ROWS; ++i) S->Titer[i] = Tit[i];
     // transformation checkers, in chain order (TransformationCheckers::check)
     bool stop = false;
     for (int ci = 0; ci < cfg.n_checkers; ++ci) {
         const int kind = cfg.checker_kind[ci];
         if (kind == kCheckCounter) {
-            S->cond[ci][0] = S->cond[ci][0] + (T)1;
-            if (S->cond[ci][0] >= (T)cfg.checker_p[ci][0]) {  // MaxNumIterationsReached: ends the loop
+            T cv = cnt[0];  // (cnt[ci] by static indices: registers)
+#pragma unroll
+            for (int u = 1; u < kMaxCheckers; ++u)
+                if (u == ci) cv = cnt[u];
+            cv = cv + (T)1;
+            S->cond[ci][0] = cv;
+            if (cv >= (T)cfg.checker_p[ci][0]) {  // MaxNumIterationsReached: ends the loop
                 stop = true;
                 S->reason = kLoopCounter;
                 break;  // (the exception skips the remaining checkers)
@@ -249,10 +322,10 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
         } else if (kind == kCheckDifferential) {
             const int sl = (int)cfg.checker_p[ci][2];
             T q[4];
-            quat_of(S->Titer, rows, false, q);
+            quat_of(Tit, rows, false, q);
             const int slot = S->nhist % kLoopHist;
             for (int i = 0; i < 4; ++i) S->qhist[slot][i] = q[i];
-            for (int r = 0; r < 3; ++r) S->thist[slot][r] = r < D ? S->Titer[r * rows + D] : (T)0;
+            for (int r = 0; r < 3; ++r) S->thist[slot][r] = r < D ? Tit[r * rows + D] : (T)0;
             ++S->nhist;
             T cv0 = 0, cv1 = 0;
             if (S->nhist > sl) {
@@ -283,17 +356,17 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
             T cv0;
             if (rows == 4) {
                 T q[4];
-                quat_of(S->Titer, rows, false, q);
+                quat_of(Tit, rows, false, q);
                 cv0 = angular_distance(q, S->bq0);
             } else {
-                T v = acos(S->Titer[0]) - S->brot2d0;
+                T v = acos(Tit[0]) - S->brot2d0;
                 while (v > (T)3.14159265358979323846) v -= (T)(2 * 3.14159265358979323846);
                 while (v < (T)-3.14159265358979323846) v += (T)(2 * 3.14159265358979323846);
                 cv0 = v;
             }
             T nn = 0;
             for (int r = 0; r < D; ++r) {
-                const T d = S->Titer[r * rows + D] - S->bt0[r];
+                const T d = Tit[r * rows + D] - S->bt0[r];
                 nn = nn + d * d;
             }
             const T cv1 = sqrt(nn);
@@ -307,7 +380,7 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
     }
     if (trace) {
         T* t = trace + (size_t)S->iter * rows * rows;
-        for (int i = 0; i < rows * rows; ++i) t[i] = S->Titer[i];
+        for (int i = 0; i < rows * rows; ++i) t[i] = Tit[i];
     }
     ++S->iter;
     if (stop) {
@@ -317,23 +390,23 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
     }
     // the next step starts with RigidTransformation::compute's check
     // (TransformationsImpl.cpp:62-63)
-    if (fabs((T)1 - det_rot(S->Titer, rows)) > (T)0.001) {
+    if (fabs((T)1 - det_rot(Tit, rows)) > (T)0.001) {
         loop_fail(ctl, S, kLoopNotRigid, kLoopError);
         return;
     }
     // grid level of the next match (pmx_capi.hip choose_level)
     // (with reuse: judged on the full searches only, kept while fewer than
     // 1/16 of the queries needed one — the rule of choose_level)
-    double q = (double)cfg.n_local, v = (double)visited[0];
+    double q = (double)cfg.n_local, v = (double)vis0;
     bool adapt = cfg.adaptive && cfg.n_levels > 1 && cfg.n_local > 0;
     if (adapt && cfg.reuse) {
-        const double full = (double)visited[1];
+        const double full = (double)vis1;
         adapt = full * 16.0 >= q;
         v -= (double)cfg.knn * (q - full);
         q = full;
     }
     if (adapt) {
-        const int l = ctl->level;
+        const int l = level_now;
         const double cells = v / (q * cfg.level_ppc[l]);
         ++S->match_count;
         S->level_cells[l] = cells;
@@ -347,7 +420,7 @@ __global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ct
         }
         ctl->level = next;
     }
-    loop_publish(ctl, S, rows);
+    loop_publish(ctl, Tit, rows);
 }
 
 // reset the loop state for a new ICP (checkers' init, ICP.cpp:368-369)
@@ -379,7 +452,7 @@ __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __rest
     ctl->level = level;
     ctl->prev_level = prev_level;
     for (int i = 0; i < 16; ++i) ctl->Tprev[i] = Tprev.m[i];
-    loop_publish(ctl, S, rows);
+    loop_publish(ctl, S->Titer, rows);
 }
 
 template <typename T>
