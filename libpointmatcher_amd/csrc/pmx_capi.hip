@@ -99,6 +99,7 @@ struct pmx_ctx {
     bool adaptive = true;
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
+    bool cold_tile = false;       // a new reading's first match on the LDS tile kernel (PMX_COLD_TILE=1: on)
     void* d_safe = nullptr;       // T[N]: safe radius per query
     int64_t safe_cap = 0;
     bool grid_ready = false;
@@ -905,6 +906,10 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // temporal reuse: the output buffers hold this reading's previous
         // match (same k, same level) with its safe radii
         GridReuse<T> ru;
+        // no previous match of this reading at all: the first match runs the
+        // tile kernel's cold form (pmx_grid_tile.inc)
+        const bool cold = c->cold_tile && c->reuse_on && c->grid_mode >= 1 &&
+                          !(c->safe_valid && c->have_match && c->ids_grid);
         if (c->reuse_on && c->grid_mode >= 1) {
             ru.mode = c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
@@ -922,7 +927,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, e1, c->stream);
+                             c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, cold, e1,
+                             c->stream);
         c->counter_deferred = defer;  // (e1 recorded after the match kernel, before the counter sum)
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
@@ -2163,6 +2169,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
+    if (const char* e = std::getenv("PMX_COLD_TILE")) c->cold_tile = std::atoi(e) != 0;
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;

@@ -257,6 +257,130 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
     return false;
 }
 
+// Shell walk with batched row scans (R >= 2).  The rows (and single cells)
+// of a shell that pass the gap test are queued kShellB at a time; a full
+// queue loads all its cell bounds together, then the first kShellU points of
+// every queued range together, so a batch costs two dependent round trips
+// instead of two per row.  The gap test reads the list as it stands when the
+// row is queued; the list only shrinks the limit afterwards, so a queued row
+// may be one the row-at-a-time walk would have skipped — never the reverse:
+// the set of points that can enter the list, and the result, are the same.
+// Off by default (kShellB = 0): measured at C3 the cold match went 0.83 ->
+// 1.7 ms (B = 4) and 1.9 ms (B = 6) — lanes fill their queues at different
+// rows, so the wave runs the flush once per lane group, and the stale limit
+// queues rows the row-at-a-time walk skips.
+#ifndef PMX_SHELL_B
+#define PMX_SHELL_B 0
+#endif
+#ifndef PMX_SHELL_U
+#define PMX_SHELL_U 0
+#endif
+constexpr int kShellB = PMX_SHELL_B;
+constexpr int kShellU = PMX_SHELL_U;
+
+template <typename T, int KT>
+__device__ __forceinline__ void shell_flush(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
+                                            const uint32_t* __restrict__ start, const uint32_t (&ia)[kShellB > 0 ? kShellB : 1],
+                                            const uint32_t (&ib)[kShellB > 0 ? kShellB : 1], int np, T qx, T qy, T qz,
+                                            T (&kd)[KT], int32_t (&ki)[KT], uint32_t& visits) {
+    constexpr int B = kShellB > 0 ? kShellB : 1, U = kShellU;
+    uint32_t ra[B], rb[B];
+#pragma unroll
+    for (int s = 0; s < B; ++s) {
+        const bool ok = s < np;
+        const uint32_t va = gld32(start, ok ? ia[s] : 0u);
+        const uint32_t vb = gld32(start, ok ? ib[s] : 0u);
+        ra[s] = ok ? va : 0u;
+        rb[s] = ok ? vb : 0u;
+    }
+    // (U = 0: only the bounds are batched; most shell cells of a surface
+    // cloud are empty, and an empty range costs nothing past its bounds)
+    P4<T> p[B][U > 0 ? U : 1];
+#pragma unroll
+    for (int s = 0; s < B; ++s)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = ra[s] + u;
+            p[s][u] = gld32(gpts, j < rb[s] ? j : 0u);  // masked: any in-range address
+        }
+#pragma unroll
+    for (int s = 0; s < B; ++s) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t j = ra[s] + u;
+            if (j < rb[s]) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, p[s][u]), kd, ki);
+        }
+        visits += rb[s] - ra[s];
+        if (ra[s] + U < rb[s]) {
+            uint32_t v0 = 0;
+            scan_range<T, KT>(gpts, gidx, ra[s] + U, rb[s], qx, qy, qz, kd, ki, v0);
+        }
+    }
+}
+
+template <typename T, int KT>
+__device__ __forceinline__ void shell_walk_batched(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
+                                                   const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy,
+                                                   T qz, const double q[3], const int c[3], int R, int k,
+                                                   T (&kd)[KT], int32_t (&ki)[KT], uint32_t& visits) {
+    constexpr int B = kShellB > 0 ? kShellB : 1;
+    const double margin = 1.0 - 1e-5;
+    const int y0 = max(c[1] - R, 0), y1 = min(c[1] + R, G.g[1] - 1);
+    const int z0 = max(c[2] - R, 0), z1 = min(c[2] + R, G.g[2] - 1);
+    const int x0 = max(c[0] - R, 0), x1 = min(c[0] + R, G.g[0] - 1);
+    uint32_t ia[B], ib[B];
+    int np = 0;
+    auto push = [&](uint32_t a, uint32_t b) {
+#pragma unroll
+        for (int s = 0; s < B; ++s)
+            if (s == np) {  // (static indexing keeps the queue in registers)
+                ia[s] = a;
+                ib[s] = b;
+            }
+        if (++np == B) {
+            shell_flush<T, KT>(gpts, gidx, start, ia, ib, np, qx, qy, qz, kd, ki, visits);
+            np = 0;
+        }
+    };
+    for (int z = z0; z <= z1; ++z) {
+        const double gz = axis_gap(G, 2, z, q[2]), gz2 = gz * gz;
+        const bool zface = (z == c[2] - R) || (z == c[2] + R);
+        for (int y = y0; y <= y1; ++y) {
+            // the limit of the list as it stands (entry k + 1 when the list
+            // has room for it: the safe radius bound, see lane_search)
+            T dkT;
+            int32_t ikT;
+            kth(kd, ki, k < KT ? k + 1 : k, dkT, ikT);
+            const double lim = ikT == kNoPos ? 1e300 : (double)dkT / margin;
+            if (gz2 > lim) break;  // (the whole z slab: gz does not depend on y)
+            const double gy = axis_gap(G, 1, y, q[1]), g2 = gz2 + gy * gy;
+            if (g2 > lim) continue;
+            const bool yface = (y == c[1] - R) || (y == c[1] + R);
+            const uint32_t row = ((uint32_t)z * (uint32_t)G.g[1] + (uint32_t)y) * (uint32_t)G.g[0];
+            if (zface || yface) {
+                int xa = x0, xb = x1;
+                if (lim < 1e300) {
+                    const double rem = sqrt(lim - g2);
+                    xa = max(x0, cell_x(G, q[0] - rem) - 1);
+                    xb = min(x1, cell_x(G, q[0] + rem) + 1);
+                }
+                if (xa <= xb) push(row + (uint32_t)xa, row + (uint32_t)xb + 1u);
+            } else {
+                const int xl = c[0] - R, xr = c[0] + R;
+                if (xl >= 0) {
+                    const double gx = axis_gap(G, 0, xl, q[0]);
+                    if (g2 + gx * gx <= lim) push(row + (uint32_t)xl, row + (uint32_t)xl + 1u);
+                }
+                if (xr <= G.g[0] - 1) {
+                    const double gx = axis_gap(G, 0, xr, q[0]);
+                    if (g2 + gx * gx <= lim) push(row + (uint32_t)xr, row + (uint32_t)xr + 1u);
+                }
+            }
+        }
+    }
+    if (np > 0) shell_flush<T, KT>(gpts, gidx, start, ia, ib, np, qx, qy, qz, kd, ki, visits);
+}
+
 // Exact shell search for one query (from scratch); kd/ki must be
 // initialised.  Certified on the k-th entry of the list (entries past k, when
 // KT > k, are the next-nearest points visited).  lb_exit: the distance from
@@ -316,7 +440,9 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
         }
     }
     for (int R = 1;; ++R) {
-        if (R >= 2) {
+        if (R >= 2 && kShellB > 0) {
+            shell_walk_batched<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, R, k, kd, ki, visits);
+        } else if (R >= 2) {
             // walk the shell at Chebyshev radius R.  Rows (and the x-range of
             // a face row) whose cells are all farther than the current k-th
             // (k+1-th) distance are skipped: every point there has d > d_k, so it can
@@ -688,8 +814,19 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
 }
 
 // ------------------------------------------------------- per-lane kernel --
+// occupancy hint of the per-lane kernel (waves per SIMD; 0 = the compiler's
+// choice).  The search is bound by dependent gather latency, so more resident
+// waves hide more of it, as long as the register cap does not spill.
+#ifndef PMX_LANE_WPE
+#define PMX_LANE_WPE 0
+#endif
+#if PMX_LANE_WPE > 0
+#define PMX_LANE_ATTR __attribute__((amdgpu_waves_per_eu(PMX_LANE_WPE)))
+#else
+#define PMX_LANE_ATTR
+#endif
 template <typename T, int KT>
-__global__ __launch_bounds__(256) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
+__global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
@@ -783,15 +920,20 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                       unsigned long long* vout, int* iter_err, SelectState* spec_st, unsigned long long* xseg,
-                      const T* radii, hipStream_t s) {
-    if (mode >= 1) {  // 1: shell search, 2: octant block first
+                      const T* radii, bool cold, hipStream_t s) {
+    if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
+        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
+                           G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
+                           ctl, gd, spec, ru.safe);
+    } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
                            start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe,
                            ru.Tprev, ctl, gd, spec, vout, iter_err, spec_st, xseg, radii);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
-                           waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii);
+                           waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 0, (const LoopCtl*)nullptr,
+                           (const GridDesc<T>*)nullptr, (SpecSel*)nullptr, (T*)nullptr);
     }
 }
 
@@ -802,9 +944,10 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                        SelectState* spec_st, unsigned long long* xseg, bool fold, bool defer, const T* radii,
-                       hipEvent_t ev_end, hipStream_t s) {
+                       bool cold, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     fold = fold && mode >= 1 && visited && vout;
+    cold = cold && mode >= 1 && !fold;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -815,9 +958,10 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, s)
-    // with reuse the list keeps room for the (k+1)-th point (the safe radius)
-    const int kl = ru.mode && mode >= 1 && knn < 16 ? knn + 1 : knn;
+                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, cold, s)
+    // with reuse the list keeps room for the (k+1)-th point (the safe radius;
+    // the cold tile writes radius 0 and keeps k entries)
+    const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
     if (kl == 1)
         PMX_KT(1);
     else if (kl <= 2)
@@ -842,13 +986,15 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, bool, bool, const float*, hipEvent_t, hipStream_t);
+                                       unsigned long long*, bool, bool, const float*, bool, hipEvent_t,
+                                       hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, bool, bool, const double*, hipEvent_t, hipStream_t);
+                                        unsigned long long*, bool, bool, const double*, bool, hipEvent_t,
+                                        hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,
