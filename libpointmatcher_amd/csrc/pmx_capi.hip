@@ -91,7 +91,7 @@ struct pmx_ctx {
     std::vector<GridLevel> levels;
     std::vector<double> level_ppc{2.0, 4.0, 8.0, 16.0, 32.0, 64.0};
     int level = 0;      // level of the next grid match
-    double first_ppc = 16.0;  // level of a new reading's first (cold) match (PMX_GRID_FIRST_PPC)
+    double first_ppc = 8.0;   // level of a new reading's first (cold) match (PMX_GRID_FIRST_PPC)
     int ids_level = 0;  // level whose positions the current match ids are
     std::vector<double> level_cells;   // last cells-per-query seen at each level
     std::vector<int64_t> level_seen;   // match count when it was seen (0: never)
@@ -99,7 +99,7 @@ struct pmx_ctx {
     bool adaptive = true;
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
-    bool cold_tile = false;       // a new reading's first match on the LDS tile kernel (PMX_COLD_TILE=1: on)
+    bool cold_tile = true;        // a new reading's first match on the LDS tile kernel (PMX_COLD_TILE=0: off)
     void* d_safe = nullptr;       // T[N]: safe radius per query
     int64_t safe_cap = 0;
     bool grid_ready = false;

@@ -946,8 +946,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        SelectState* spec_st, unsigned long long* xseg, bool fold, bool defer, const T* radii,
                        bool cold, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
-    fold = fold && mode >= 1 && visited && vout;
-    cold = cold && mode >= 1 && !fold;
+    cold = cold && mode >= 1;
+    fold = fold && mode >= 1 && visited && vout && !cold;  // (a cold launch runs the counter kernel after it)
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {

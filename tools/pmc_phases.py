@@ -24,7 +24,8 @@ import glob
 import json
 import sys
 
-KERNELS = {"match": "grid_lane_kernel", "p2plane": "p2plane_partial_kernel", "tail": "loop_tail_kernel",
+# (the match of a new reading's first iteration is the tile kernel's cold form)
+KERNELS = {"match": ("grid_lane_kernel", "grid_tile_kernel"), "p2plane": "p2plane_partial_kernel", "tail": "loop_tail_kernel",
            "step": "loop_step_kernel", "counter_sum": "counter_sum_kernel", "select": "select_pass_kernel",
            "finalize": "finalize_kernel"}
 
@@ -37,7 +38,8 @@ def rows(d, pattern):
 
 
 def series(rs, sub, key):
-    v = [(int(x["Dispatch_Id"]), x) for x in rs if sub in x["Kernel_Name"]]
+    subs = sub if isinstance(sub, tuple) else (sub,)
+    v = [(int(x["Dispatch_Id"]), x) for x in rs if any(t in x["Kernel_Name"] for t in subs)]
     v.sort(key=lambda t: t[0])
     return [key(x) for _, x in v]
 
