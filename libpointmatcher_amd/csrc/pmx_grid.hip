@@ -817,6 +817,10 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
 // occupancy hint of the per-lane kernel (waves per SIMD; 0 = the compiler's
 // choice).  The search is bound by dependent gather latency, so more resident
 // waves hide more of it, as long as the register cap does not spill.
+// XCD-aware block order of the per-lane kernel (PMX_LANE_XCD, default on)
+#ifndef PMX_LANE_XCD
+#define PMX_LANE_XCD 1
+#endif
 #ifndef PMX_LANE_WPE
 #define PMX_LANE_WPE 0
 #endif
@@ -855,11 +859,16 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
     }
     if (!reuse) safe = nullptr;
     uint32_t visits = 0;
+#if PMX_LANE_XCD
+    const int64_t blk = xcd_block();  // (pmx_internal.h: adjacent slot ranges gather through one L2)
+#else
+    const int64_t blk = blockIdx.x;
+#endif
     // quantile window (pmx_spec.h): every written distance is classified
     SpecAcc<T> sa;
     spec_acc_init<T>(sa, spec);
     if (reuse < 2) {
-        const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int64_t j = blk * blockDim.x + threadIdx.x;
         if (j < N)
             full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, qr2(radii, j, maxR2), oct, out_d, out_i, safe,
                               visits, sa);
@@ -878,7 +887,7 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
     __shared__ int miss[256];
     __shared__ int wave_cnt[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t j = blk * blockDim.x + threadIdx.x;
     bool missed = false;
     if (j < N) {
         const P4<T> p = gld(rd, j);
@@ -900,7 +909,7 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
     if (missed) miss[off + __popcll(m & ((1ull << lane) - 1))] = threadIdx.x;
     __syncthreads();
     if ((int)threadIdx.x < total) {
-        const int64_t j2 = (int64_t)blockIdx.x * blockDim.x + miss[threadIdx.x];
+        const int64_t j2 = blk * blockDim.x + miss[threadIdx.x];
         full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
                           sa);
     }

@@ -44,6 +44,17 @@ template <>
 struct Vec4Of<double> {
     typedef double V __attribute__((ext_vector_type(4)));
 };
+// Workgroup index remapped so that consecutive indices share an XCD: blocks
+// are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup
+// dispatch, XCD placement"), so without it the neighbouring tiles of the slot
+// order, which gather the same reference lines, sit in eight different L2s.
+// A bijection on [0, gridDim.x) for any grid size; performance only.
+__device__ __forceinline__ uint32_t xcd_block() {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t q = nb >> 3, r = nb & 7u, x = b & 7u, i = b >> 3;
+    return x < r ? x * (q + 1u) + i : r * (q + 1u) + (x - r) * q + i;
+}
+
 template <typename T>
 __device__ __forceinline__ P4<T> gld(const P4<T>* p, int64_t i) {
     typedef typename Vec4Of<T>::V V;
