@@ -11,7 +11,7 @@ step() { echo "== $(date +%T) $*" >> gpurun_out/steps.log; }
 if [ "$1" = tests ]; then
   shift
   step tests && timeout -k 10 600 python -u -m pytest tests/test_gpu_grid.py tests/test_gpu_loop.py tests/test_gpu_icp.py \
-      tests/test_gpu_vardist.py -m gpu -q --maxfail 10 --timeout 180 --timeout-method thread > gpurun_out/tests_ab.log 2>&1 || exit $?
+      tests/test_gpu_vardist.py tests/test_gpu_kernels.py -m gpu -q --maxfail 10 --timeout 180 --timeout-method thread > gpurun_out/tests_ab.log 2>&1 || exit $?
 fi
 [ "$1" = -- ] && shift
 for rep in 1 2; do
