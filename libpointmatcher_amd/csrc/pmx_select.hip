@@ -161,7 +161,11 @@ static int select_agg() {
 static int64_t select_blocks(int64_t n) {
     static const int64_t cap = [] {
         const char* e = std::getenv("PMX_SELECT_BLOCKS");  // tuning knob
-        return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)256;
+        // (64: the select_all launch is a no-op whenever the quantile window
+        // resolved the limit, and its cost is then the dispatch of its blocks;
+        // same-box A/B at C3, driver command: 256 -> 81.6, 128 -> 80.4,
+        // 64 -> 80.2, 32 -> 81.0 us per iteration)
+        return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)64;
     }();
     int64_t g = (n + 256 * kSelPer - 1) / (256 * kSelPer);
     if (g < 1) g = 1;
