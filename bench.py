@@ -1,25 +1,27 @@
 """Benchmark: ICP iterations/s and matched-pairs/s on the BASELINE.json workload.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c3] [--matcher brute]
+    python bench.py [--gpus N --steps K --warmup W] [--config c3] [--matcher brute] [--scaling strong|weak]
 
 A "step" is one ICP iteration of the hot path — fused transform + k-NN
-match, outlier weighting, normal equations, the host 6x6 solve and the
-checker — over the synthetic cloud of the configuration.
-Default workload = BASELINE config 3: 1M -> 1M float, k = 1, TrimmedDist
-ratio 0.85, point-to-plane, one GPU.  With N GPUs (torchrun, one process per
-GPU) every rank holds its own 1M-point reading shard against the replicated
-1M reference (weak scaling) and each iteration all-reduces the quantile
-histograms and the normal equations over RCCL.
+match, outlier weighting, normal equations, the 6x6 solve and the checker —
+over the synthetic cloud of the configuration.  Default
+workload = BASELINE config 3: 1M -> 1M float, k = 1, TrimmedDist ratio 0.85,
+point-to-plane.  With N GPUs (torchrun, one process per GPU) the GLOBAL
+1M-point reading is split into N contiguous shards against the replicated 1M
+reference (strong scaling, the north_star "1M->1M at 1/2/4/8 MI355X"; weak:
+--scaling weak, 1M per rank), and each iteration exchanges the quantile
+window segments (all-gather) and the normal equations (all-reduce) over RCCL.
 
 Timing: W untimed iterations, then exactly K iterations between a barrier +
 device synchronisation on both sides; the max over ranks is reported.  The
-defaults (K = 40, W = 0) time one whole ICP of 40 iterations from the initial
-pose — the same work the CPU baseline times.  The
 clouds are resident in HBM before the timed region.  The match kernel's
 device time is measured with HIP events on the context stream (pmx_timing_*).
-The CPU baseline (rank 0, N = 1 only) is the oracle's libnabo-style kd-tree
-restatement of the reference CPU path on the same inputs (a bounded number of
-iterations), timed on this host.
+Every run also times one whole ICP from the initial pose (`whole_icp`: 40
+iterations of the same chain, the work the CPU baseline times, cold first
+match included).  The CPU baseline (rank 0, N = 1 only) is the oracle's
+libnabo-style kd-tree restatement of the reference CPU path on the same
+inputs, built -march=native on this host, on every core the job may use and
+on one thread.
 """
 from __future__ import annotations
 
@@ -76,14 +78,55 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer, iters, threads, one_thread_iters):
+def usable_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup
+    CPU quota and by OMP_NUM_THREADS when the launcher set one (the GPU box
+    shares its host: os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    info = {"affinity": n, "host_nproc": os.cpu_count()}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            info["cgroup_quota"] = float(q) / float(per)
+            n = min(n, max(1, int(float(q) / float(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        info["omp_num_threads"] = int(omp)
+        n = min(n, int(omp))
+    return n, info
+
+
+def native_oracle():
+    """The oracle built -march=native on this host (the reference's build,
+    CMakeLists.txt:70 -O3; the prebuilt oracle/build is x86-64-v3).  Returns
+    (library path or None, ISA note)."""
+    import subprocess
+    out = os.path.join(ROOT, "oracle", "build_native", "libpmo.so")
+    src = os.path.join(ROOT, "oracle", "pmo.c")
+    try:
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        subprocess.run(["gcc", "-O3", "-march=native", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
+                        "-shared", "-o", out, src, "-lm"], check=True, capture_output=True, timeout=120)
+        return out, "gcc -O3 -march=native"
+    except Exception as e:  # (no compiler on the host: the prebuilt library)
+        return None, f"gcc -O3 -march=x86-64-v3 (prebuilt; native build failed: {type(e).__name__})"
+
+
+def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer, iters, threads, one_thread_cap_s):
     """The oracle (C restatement of the reference CPU path: libnabo-style
-    kd-tree, nth_element quantile, -O3) on the same inputs, timed on this host.
-    Runs (all cores): the timing chain (Counter `iters`, the workload's chain),
-    the parity chain (+ Differential), and the timing chain with T-precision
-    accumulation of the minimiser sums (the reference's Eigen arithmetic);
-    then a bounded 1-thread sample (the reference's default: no OpenMP,
-    CMakeLists.txt:160)."""
+    kd-tree, nth_element quantile, -O3 -march=native) on the same inputs,
+    timed on this host.  Runs (all usable cores): the timing chain (Counter
+    `iters`, the workload's chain), the parity chain (+ Differential), and the
+    timing chain with T-precision accumulation of the minimiser sums (the
+    reference's Eigen arithmetic); then the timing chain on one thread (the
+    reference's default: no OpenMP, CMakeLists.txt:160), over all `iters`
+    iterations unless that would exceed one_thread_cap_s."""
+    lib, isa = native_oracle()
+    if lib:
+        os.environ["PMO_LIB"] = lib
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
 
@@ -97,17 +140,19 @@ def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer,
         rc, T, st, _ = O.icp(cfg, reading, reference, normals=nrm)
         return rc, T, st, time.perf_counter() - t0
 
+    print(f"[bench] cpu baseline: {threads} threads ({isa})", file=sys.stderr, flush=True)
     rc, T, st, wall = run(threads, iters, None, 0)
     if rc != 0:
         return None, None
     loop = st.loop_seconds
+    cores, cinfo = usable_cores()
     out = {"value": n * knn * st.iterations / loop, "unit": "matched-pairs/s", "cores": threads,
-           "kind": "port", "iters_per_s": st.iterations / loop,
-           "host_cpu": cpu_model(), "host_nproc": os.cpu_count(),
+           "kind": "port", "iters_per_s": st.iterations / loop, "ms_per_iteration": 1e3 * loop / st.iterations,
+           "build": isa, "host_cpu": cpu_model(), "host_cores": cinfo,
            "sample": f"{cfg_name} inputs ({n}->{reference.shape[0]}), the whole timing chain ({st.iterations} ICP "
                      f"iterations from the initial pose), oracle restatement of the reference CPU path "
-                     f"(libnabo-style kd-tree with the incremental box bound, nth_element quantile, gcc -O3), "
-                     f"{threads} threads, loop {loop:.2f} s (setup+loop {wall:.2f} s)"}
+                     f"(libnabo-style kd-tree with the incremental box bound, nth_element quantile, {isa}), "
+                     f"{threads} threads (every core this job may use), loop {loop:.2f} s (setup+loop {wall:.2f} s)"}
     runs = {"counter": {"T": T, "iterations": int(st.iterations), "kept": int(st.kept)}}
     rcd, Td, std, _ = run(threads, iters, PARITY_DIFF, 0)
     if rcd == 0:
@@ -115,12 +160,20 @@ def cpu_baseline(cfg_name, reading, reference, normals, knn, filters, minimizer,
     rcT, TT, stT, _ = run(threads, iters, None, 1)
     if rcT == 0:
         runs["counter_Tsums"] = {"T": TT, "iterations": int(stT.iterations), "kept": int(stT.kept)}
-    rc1, T1, st1, _ = run(1, one_thread_iters, None, 0)
+    # one thread: every iteration of the chain when the estimate (the
+    # all-core loop times its thread count) fits the cap, else the first ones
+    est = loop * threads
+    it1 = iters if est <= one_thread_cap_s else max(2, int(iters * one_thread_cap_s / est))
+    print(f"[bench] cpu baseline: 1 thread, {it1} iterations (estimate {est * it1 / iters:.0f} s)", file=sys.stderr,
+          flush=True)
+    rc1, T1, st1, _ = run(1, it1, None, 0)
     if rc1 == 0:
         out["single_thread"] = {"value": n * knn * st1.iterations / st1.loop_seconds, "unit": "matched-pairs/s",
                                 "cores": 1, "iters_per_s": st1.iterations / st1.loop_seconds,
-                                "sample": f"first {st1.iterations} ICP iterations (the cold, most expensive ones), "
-                                          f"1 thread, loop {st1.loop_seconds:.2f} s"}
+                                "ms_per_iteration": 1e3 * st1.loop_seconds / st1.iterations,
+                                "sample": f"{'the whole timing chain' if it1 == iters else 'the first'} "
+                                          f"({st1.iterations} ICP iterations from the initial pose), 1 thread, "
+                                          f"{isa}, loop {st1.loop_seconds:.2f} s"}
     return out, runs
 
 
@@ -132,20 +185,28 @@ def parity_entry(Tg, sg, ref, tol, chain):
             "kept_gpu": int(sg.kept), "kept_cpu": ref["kept"], "chain": chain}
 
 
+def shard_range(n, world, rank):
+    """Contiguous reading shard of a rank (the multi-rank tests' convention)."""
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # default: one whole ICP of 40 iterations from the initial pose, as the
-    # CPU baseline runs it (SURVEY.md §8(d) timing runs)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--matcher", default="grid", choices=["brute", "grid"],
                     help="KDTreeMatcher searchType 0 (brute force) or 1 (spatial grid)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the configuration's global reading split over the ranks (default); "
+                         "weak: the configuration's reading on every rank")
     ap.add_argument("--cpu-iters", type=int, default=40)
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-one-thread-iters", type=int, default=2,
-                    help="ICP iterations of the bounded single-thread CPU sample")
+    ap.add_argument("--cpu-one-thread-cap", type=float, default=100.0,
+                    help="seconds the 1-thread CPU sample may take (fewer iterations beyond)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist", action="store_true",
                     help="use the torchrun/RCCL multi-rank path even at world size 1 (rehearsal on one GPU)")
@@ -178,15 +239,18 @@ def main():
     from libpointmatcher_amd.icp import ICP
     from libpointmatcher_amd.synth import reading_cloud, reference_cloud
 
-    N, M, dtype, knn, filters, minimizer = CONFIGS[args.config]
+    N_cfg, M, dtype, knn, filters, minimizer = CONFIGS[args.config]
     reference, normals = reference_cloud(M, dtype)
-    # each rank's shard of the global reading (weak scaling: N per rank)
+    strong = args.scaling == "strong"
+    N_global = N_cfg if strong else N_cfg * world
     if dist:
-        full = reading_cloud(N * world, dtype)
-        reading = np.ascontiguousarray(full[rank * N:(rank + 1) * N])
+        full = reading_cloud(N_global, dtype)
+        lo, hi = shard_range(N_global, world, rank)
+        reading = np.ascontiguousarray(full[lo:hi])
         del full
     else:
-        reading = reading_cloud(N, dtype)
+        reading = reading_cloud(N_global, dtype)
+    N = reading.shape[0]  # this rank's shard
 
     search_type = 0 if args.matcher == "brute" else 1
     total_it = args.warmup + args.steps + 10
@@ -199,6 +263,19 @@ def main():
         t = torch.tensor(list(uid), dtype=torch.uint8)
         tdist.broadcast(t, src=0)
         icp.comm_init(bytes(t.tolist()), world, rank)
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+
+    def max_over_ranks(v):
+        if not dist:
+            return v
+        import torch
+
+        e = torch.tensor([v], dtype=torch.float64)
+        tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
+        return float(e.item())
 
     nrm_in = normals if minimizer.startswith("PointToPlane") else None
     # setup (reported separately): reference upload + grid
@@ -215,44 +292,59 @@ def main():
     if args.warmup > 0:
         icp.iterate(args.warmup)
 
-    def barrier():
-        if dist:
-            tdist.barrier()
-
     barrier()
     t0 = time.perf_counter()
-    icp.iterate(args.steps)   # each iteration ends with the system copy-back: device is synchronised
+    icp.iterate(args.steps)   # each batch ends with the status copy-back: device is synchronised
     t1 = time.perf_counter()
     barrier()
-    elapsed = t1 - t0
+    elapsed = max_over_ranks(t1 - t0)
     st = icp.stats()
     # Roofline pass: the same ICP again (prepare resets the pose and the
     # match history), now with HIP events around every match launch on the
     # context stream.  The events are kept out of the timed region above: each
-    # record is a marker packet that adds ~6 us of idle GPU time per record
-    # pair to the iteration (measured in the kernel trace).  The first
-    # iteration's match is a cold search at the initial pose (no previous
-    # k-lists to certify): with --warmup > 0 it is timed on its own.
+    # record is a marker packet that adds idle GPU time to the iteration.
     icp.prepare(reading, reference, nrm_in)
-    cold_launch_ms = None
     if args.warmup > 0:
-        icp.timing(True)
-        icp.iterate(1)
-        cold_ms, cold_n = icp.timing_read()
-        cold_launch_ms = cold_ms / max(cold_n, 1)
-        icp.iterate(args.warmup - 1)
+        icp.iterate(args.warmup)
     icp.timing(True)
     icp.iterate(args.steps)
     match_ms, launches = icp.timing_read()
     icp.timing(False)
-    if dist:
-        import torch
 
-        e = torch.tensor([elapsed], dtype=torch.float64)
-        tdist.all_reduce(e, op=tdist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    # ---- one whole ICP from the initial pose (the representative workload:
+    # what every new scan pays, and what the CPU baseline times): the timing
+    # chain of the CPU baseline (Counter cpu_iters), prepare untimed
+    icp.load_yaml(chain_yaml(knn, filters, minimizer, search_type, args.cpu_iters))
+    icp.prepare(reading, reference, nrm_in)
+    barrier()
+    w0 = time.perf_counter()
+    icp.iterate(args.cpu_iters)
+    w1 = time.perf_counter()
+    barrier()
+    whole_s = max_over_ranks(w1 - w0)
+    wst = icp.stats()
+    hits, misses = icp.select_stats()
+    # the same ICP once more, one iteration per call with HIP events around
+    # each match: the cold first match and the matches of the first iterations
+    icp.prepare(reading, reference, nrm_in)
+    first_match_us = []
+    for _ in range(min(8, args.cpu_iters)):
+        icp.timing(True)
+        icp.iterate(1)
+        ms, nl = icp.timing_read()
+        first_match_us.append(round(1e3 * ms / max(nl, 1), 2))
+    icp.timing(False)
+    whole = {"iterations": int(wst.iterations), "ms": 1e3 * whole_s,
+             "ms_per_iteration": 1e3 * whole_s / max(int(wst.iterations), 1),
+             "matched_pairs_per_s": N_global * knn * int(wst.iterations) / whole_s,
+             "cold_match_ms": first_match_us[0] * 1e-3 if first_match_us else None,
+             "first_matches_us": first_match_us,
+             "window_hits": int(hits), "window_misses": int(misses),
+             "chain": f"the workload's chain, CounterTransformationChecker {args.cpu_iters}, from the initial pose "
+                      f"(prepare untimed, then {args.cpu_iters} iterations timed as the CPU baseline's loop); "
+                      f"first_matches_us: device time of each of the first matches (separate run, HIP events)"}
 
-    pairs = N * world * knn * args.steps
+    pairs = N_global * knn * args.steps
     avg_match_s = match_ms * 1e-3 / max(launches, 1)
     esz = np.dtype(dtype).itemsize
     # algorithmic bytes of one match launch: the reading shard (4 T per point),
@@ -265,27 +357,24 @@ def main():
     if args.matcher == "grid":
         # the grid adds the order / id / cell-range traffic: ids (4 B) of every
         # reference point and the visit order (4 B) of every query
-        alg_bytes_extra = N * 4 + M * 4
-    else:
-        alg_bytes_extra = 0
-    alg_bytes += alg_bytes_extra
+        alg_bytes += N * 4 + M * 4
     achieved_gbs = alg_bytes / avg_match_s / 1e9
     # HBM traffic of the match kernel from the committed PMC passes of this
-    # exact command (profiles/r01/pmc_c3_traffic.json: rocprofv3 FETCH_SIZE x2
-    # (gfx950 correction) + WRITE_SIZE, per launch); null for other configs
+    # exact command (tools/pmc_phases.py: FETCH_SIZE x2 (gfx950 correction) +
+    # WRITE_SIZE per launch, averaged over the launches of the timed steps);
+    # null for other configurations
     traffic, traffic_src = None, None
     if args.config == "c3" and args.matcher == "grid" and world == 1:
-        # the PMC passes of this exact driver command (tools/pmc_phases.py:
-        # FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE per launch, averaged
-        # over the launches of the timed steps)
-        src = os.path.join("profiles", "r02", "pmc_c3_driver.json")
-        try:
-            with open(os.path.join(ROOT, src)) as f:
-                pm = json.load(f)
-            traffic = pm["match"]["timed"]["hbm_bytes_per_launch"]
-            traffic_src = src
-        except (OSError, KeyError, TypeError, ValueError):
-            pass
+        for src in (os.path.join("profiles", "r03", "pmc_c3_driver.json"),
+                    os.path.join("profiles", "r02", "pmc_c3_driver.json")):
+            try:
+                with open(os.path.join(ROOT, src)) as f:
+                    pm = json.load(f)
+                traffic = pm["match"]["timed"]["hbm_bytes_per_launch"]
+                traffic_src = src
+                break
+            except (OSError, KeyError, TypeError, ValueError):
+                pass
     peak_tf = FP32_VALU_TFLOPS if esz == 4 else FP64_VALU_TFLOPS
     metric = "ICP iterations/sec + matched-pairs/sec, 1M→1M pts, k=1, point-to-plane"
     try:
@@ -293,6 +382,12 @@ def main():
             metric = json.load(f)["metric"]
     except Exception:
         pass
+    if dist:
+        par = (f"reading sharded x{world} ({'strong: ' + str(N_global) + ' global' if strong else 'weak: ' + str(N_cfg) + ' per rank'}), "
+               f"reference replicated; RCCL per iteration: quantile window all-gather (+ radix histogram all-reduces "
+               f"on a window miss) and the normal-equation all-reduce")
+    else:
+        par = "one GPU, no communicator"
     result = {
         "metric": metric,
         "value": pairs / elapsed,
@@ -302,26 +397,28 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32" if esz == 4 else "f64",
         "data": "synthetic (box+sphere surface, seeds 1/2, sigma 0.01, SURVEY.md §8(d))",
-        "config": {"workload": f"BASELINE {args.config}: {N * world}->{M} {'float' if esz == 4 else 'double'}, "
+        "config": {"workload": f"BASELINE {args.config}: {N_global}->{M} {'float' if esz == 4 else 'double'}, "
                                f"k={knn}, {', '.join(f[0] for f in filters) or 'no outlier filter'}, {minimizer}",
                    "matcher": f"KDTreeMatcher searchType={search_type} ({args.matcher}, exact)",
-                   "reading_per_gpu": N, "reference": M, "parallelism": f"reading sharded x{world}, RCCL all-reduce"},
+                   "reading_global": N_global, "reading_per_gpu": N, "reference": M, "parallelism": par},
         "icp_iterations_per_s": args.steps / elapsed,
         "kept_pairs_last_iter": st.kept,
+        "whole_icp": whole,
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
+                     "traffic_unit": "bytes per launch past L2 (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                     "traffic_source": traffic_src,
                      "kernel": "match (k-NN + fused transform)", "avg_launch_ms": avg_match_s * 1e3,
                      "algorithmic_bytes_per_launch": alg_bytes,
-                     "cold_launch_ms": cold_launch_ms,
-                     "note": "steady-state launches certify most k-lists from the previous iteration "
-                             "(exact temporal reuse, DESIGN.md §5); with --warmup 0 (default) the timed steps are "
-                             "the whole 40-iteration ICP from the initial pose, cold first iterations included; "
-                             "cold_launch_ms (warmup > 0) is the first iteration's full search"},
+                     "note": "steady-state launches certify most k-lists from the previous iteration (exact temporal "
+                             "reuse, DESIGN.md §5); the ~70 MB C3 working set fits the 256 MB Infinity Cache, so "
+                             "PMC FETCH_SIZE counts L2-miss bytes (MALL hits included) and 8 TB/s HBM is not the "
+                             "binding ceiling of this gather-latency-bound kernel; whole_icp.first_matches_us has "
+                             "the cold (initial-pose) matches"},
         "compute_roofline": {"bound": "valu", "achieved": flops / avg_match_s / 1e12, "peak": peak_tf,
                              "unit": "TFLOP/s", "frac": flops / avg_match_s / 1e12 / peak_tf,
                              "pairs_evaluated_per_launch": pairs_eval,
@@ -337,7 +434,7 @@ def main():
                             "levels built on the device), reading upload + Morton slot order (device sort); "
                             "first_prepare_ms adds the context creation (HIP runtime, code objects)")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = args.cpu_threads or usable_cores()[0]
         # GPU side of the parity checks: whole ICPs from the initial pose
         # with the timing chain and with the parity chain (same inputs)
         gpu = {}
@@ -345,7 +442,7 @@ def main():
             icp.load_yaml(chain_yaml(knn, filters, minimizer, search_type, args.cpu_iters, diff))
             gpu[name] = (icp.compute(reading, reference, nrm_in), icp.stats())
         cb, runs = cpu_baseline(args.config, reading, reference, normals, knn, filters, minimizer,
-                                args.cpu_iters, threads, args.cpu_one_thread_iters)
+                                args.cpu_iters, threads, args.cpu_one_thread_cap)
         result["cpu_baseline"] = cb
         if runs is not None:
             tol = 1e-5 if esz == 4 else 1e-12
@@ -364,6 +461,8 @@ def main():
                     "note": "GPU and oracle sum the normal equations in fp64 from T products; the reference sums "
                             "in T (Eigen GEMM): the size of that deliberate difference here (Counter chain)"}
             result["parity"] = par
+            if cb:
+                result["whole_icp"]["vs_cpu_all_cores"] = whole["matched_pairs_per_s"] / cb["value"]
     else:
         result["cpu_baseline"] = None
     if rank == 0:

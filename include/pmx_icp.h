@@ -104,6 +104,11 @@ int pmx_icp_trace_get(const pmx_icp* icp, void* out, int max_iters);
 /* HIP-event device time of the match kernel over the last iterations */
 int pmx_icp_timing(pmx_icp* icp, int on);
 int pmx_icp_timing_read(pmx_icp* icp, double* match_ms, int64_t* match_launches);
+/* quantile window statistics of the device loop (pmx_loop_select_stats):
+ * iterations since the last prepare whose TrimmedDist / MedianDist quantile
+ * was resolved inside the match's key window, and iterations that ran the
+ * radix passes.  Diagnostics only (no reference counterpart). */
+int pmx_icp_select_stats(pmx_icp* icp, uint64_t* window_hits, uint64_t* window_misses);
 
 #ifdef __cplusplus
 }

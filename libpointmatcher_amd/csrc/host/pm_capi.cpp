@@ -212,14 +212,18 @@ int pmx_icp_finish(pmx_icp* icp, void* T_out) {
 }
 
 int pmx_icp_add_descriptor(pmx_icp* icp, int cloud, const char* name, int span, const void* values, int64_t n) {
-    if (!icp || !name || span < 1 || (!values && n > 0) || (cloud != 0 && cloud != 1))
-        return PMX_ICP_INVALID_PARAMETER;
-    pmx_icp::Desc d{cloud, name, span, {}};
-    d.v.resize((size_t)(n * span));
-    for (int64_t i = 0; i < n * span; ++i)
-        d.v[(size_t)i] = icp->dtype == 1 ? ((const double*)values)[i] : (double)((const float*)values)[i];
-    icp->staged.push_back(std::move(d));
-    return PMX_ICP_OK;
+    if (!icp) return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] {
+        if (!name || span < 1 || n < 0 || (!values && n > 0) || (cloud != 0 && cloud != 1))
+            throw InvalidParameter("pmx_icp_add_descriptor: bad arguments");
+        if (n > 0 && (uint64_t)n > ((uint64_t)1 << 40) / (uint64_t)span)
+            throw InvalidParameter("pmx_icp_add_descriptor: descriptor too large");
+        pmx_icp::Desc d{cloud, name, span, {}};
+        d.v.resize((size_t)(n * span));
+        for (int64_t i = 0; i < n * span; ++i)
+            d.v[(size_t)i] = icp->dtype == 1 ? ((const double*)values)[i] : (double)((const float*)values)[i];
+        icp->staged.push_back(std::move(d));
+    });
 }
 
 int pmx_icp_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
@@ -276,6 +280,15 @@ int pmx_icp_timing_read(pmx_icp* icp, double* ms, int64_t* launches) {
         dev.ensure();
         double other = 0;
         dev.check(pmx_timing_read(dev.ctx, ms, launches, &other));
+    });
+}
+
+int pmx_icp_select_stats(pmx_icp* icp, uint64_t* hits, uint64_t* misses) {
+    if (!icp || !hits || !misses) return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] {
+        Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
+        dev.ensure();
+        dev.check(pmx_loop_select_stats(dev.ctx, hits, misses));
     });
 }
 

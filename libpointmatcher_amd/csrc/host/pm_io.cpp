@@ -115,6 +115,12 @@ template <typename T>
 void assemble(DataPoints<T>& dp, int64_t n, const std::vector<std::pair<std::string, int>>& fl,
               const std::vector<std::vector<T>>& frows, const std::vector<std::pair<std::string, int>>& dl,
               const std::vector<std::vector<T>>& drows) {
+    // every row holds exactly n values (a malformed file must not make the
+    // copies below read past a row)
+    for (const auto& r : frows)
+        if ((int64_t)r.size() != n) throw std::runtime_error("cloud parse error: a feature row does not hold every point");
+    for (const auto& r : drows)
+        if ((int64_t)r.size() != n) throw std::runtime_error("cloud parse error: a descriptor row does not hold every point");
     bool has_pad = false;
     for (auto& l : fl) has_pad = has_pad || l.first == "pad";
     const int fdim = (int)frows.size() + (has_pad ? 0 : 1);
@@ -306,10 +312,13 @@ DataPoints<T> load_vtk(std::istream& is) {
     else
         throw std::runtime_error("Wrong data type, expecting DATASET POLYDATA, found " + line);
     int64_t count = 0;
+    bool have_points = false;
     std::vector<T> pts;
     std::vector<std::pair<std::string, int>> dl;
     std::vector<std::vector<T>> drows;
     auto add_desc = [&](const std::string& name, int dim, const std::vector<T>& v) {  // v: count x dim point-major
+        if ((int64_t)v.size() != count * (int64_t)dim)
+            throw std::runtime_error("VTK parse error: descriptor " + name + " does not hold every point");
         dl.push_back({name, dim});
         for (int r = 0; r < dim; ++r) {
             std::vector<T> row((size_t)count);
@@ -321,7 +330,10 @@ DataPoints<T> load_vtk(std::istream& is) {
     while (is >> field) {
         if (field == "POINTS") {
             std::string type;
+            if (have_points) throw std::runtime_error("VTK parse error: a second POINTS block");
             is >> count >> type;
+            if (!is || count < 0) throw std::runtime_error("VTK parse error: bad POINTS count");
+            have_points = true;
             get_line(is, line);
             if (type != "float" && type != "double") throw std::runtime_error("Field POINTS can only be of type double or float");
             read_typed<T>(is, binary, type, count * 3, pts);
@@ -339,11 +351,13 @@ DataPoints<T> load_vtk(std::istream& is) {
             std::string fname;
             int nfield = 0;
             is >> fname >> nfield;
+            if (!is || nfield < 0) throw std::runtime_error("VTK parse error: bad FIELD header");
             for (int f = 0; f < nfield; ++f) {
                 std::string name, type;
                 int dim = 0;
                 int64_t tuples = 0;
                 is >> name >> dim >> tuples >> type;
+                if (!is || dim < 0 || tuples < 0) throw std::runtime_error("VTK parse error: bad FIELD array " + name);
                 if (type == "vtkIdType") {  // skipped
                     if (binary) {
                         is.seekg(dim * tuples * 4, std::ios_base::cur);
@@ -355,6 +369,9 @@ DataPoints<T> load_vtk(std::istream& is) {
                 }
                 if (type != "float" && type != "double")
                     throw std::runtime_error("Field FIELD is " + type + " but can only be of type double or float");
+                // (point data: the reference reads pointCount tuples, IO.cpp:1082-1083;
+                // a dataset-level array before POINTS has no point count to read)
+                if (!have_points) throw std::runtime_error("VTK parse error: FIELD array " + name + " before POINTS");
                 std::vector<T> v;
                 read_typed<T>(is, binary, type, count * dim, v);
                 add_desc(name, dim, v);
@@ -390,6 +407,8 @@ DataPoints<T> load_vtk(std::istream& is) {
                 throw std::runtime_error("Unknown field name " + field +
                                          ", expecting SCALARS, VECTORS, TENSORS, NORMALS or COLOR_SCALARS.");
             }
+            if (!have_points) throw std::runtime_error("VTK parse error: " + field + " " + name + " before POINTS");
+            if (dim < 0 || dim > 4096) throw std::runtime_error("VTK parse error: bad COLOR_SCALARS dimension");
             get_line(is, line);
             std::vector<T> v;
             if (color && binary) {  // unsigned char / 255 (:1195-1204)

@@ -1305,6 +1305,16 @@ int robust_scale_impl(pmx_ctx* c, int pos, double* scale) {
 }
 
 // -------------------------------------------------------------- minimizers --
+// After a select_all wait timed out, some blocks left without arriving at the
+// later passes: the arrival counters are off a multiple of the grid and some
+// bins were never zeroed.  Start the next launch from zeroed state.
+int select_reset(pmx_ctx* c) {
+    HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
+    c->selx_grid = 0;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
 // one D2H copy of the iteration block, then a stream sync
 int readback(pmx_ctx* c) {
     HIPCHK(c, hipMemcpyAsync(c->h_result, c->d_result, kBlkCopy, hipMemcpyDeviceToHost, c->stream));
@@ -1460,7 +1470,10 @@ int p2plane_impl(pmx_ctx* c, double* A, double* b, pmx_stats* st) {
     const int o = NS + NF;
     fill_stats(c, st, r[o + 0], r[o + 1], r[o + 2], r[o + 3], r[o + 4], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
-    if (ierr == kSelTimeout) return fail(c, PMX_E_HIP, "radix select: device wait timed out");
+    if (ierr == kSelTimeout) {
+        (void)select_reset(c);
+        return fail(c, PMX_E_HIP, "radix select: device wait timed out");
+    }
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[o + 1] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
     if (r[o + 0] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
@@ -1486,7 +1499,10 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
     const int ierr = host_iter_err(c);
     fill_stats(c, st, r[7], r[8], r[9], r[10], r[0], host_limit(c));
     if (ierr == PMX_E_EMPTY_QUANTILE) return fail(c, PMX_E_EMPTY_QUANTILE, "no outlier to filter");
-    if (ierr == kSelTimeout) return fail(c, PMX_E_HIP, "radix select: device wait timed out");
+    if (ierr == kSelTimeout) {
+        (void)select_reset(c);
+        return fail(c, PMX_E_HIP, "radix select: device wait timed out");
+    }
     if (ierr) return fail(c, ierr, "quantile must be between 0 and 1");
     if (r[8] == 0.0 || r[7] == 0.0) return fail(c, PMX_E_NO_POINTS, "ErrorMnimizer: no point to minimize");
     T means[6];
@@ -1780,6 +1796,7 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
             err = PMX_E_EMPTY_QUANTILE;
             msg = "no outlier to filter";
         } else if (e == kSelTimeout) {
+            (void)select_reset(c);
             err = PMX_E_HIP;
             msg = "radix select: a block waited too long for the pass before (device timeout)";
         } else if (e == kLoopNotRigid) {

@@ -170,7 +170,11 @@ static int64_t select_blocks(int64_t n) {
     int64_t g = (n + 256 * kSelPer - 1) / (256 * kSelPer);
     if (g < 1) g = 1;
     if (g > cap) g = cap;
-    return g;
+    // a power of two: select_all_kernel's uint32 arrival counters then wrap
+    // at a multiple of the grid, and the generation stamps stay aligned
+    int64_t p2 = 1;
+    while (p2 * 2 <= g) p2 *= 2;
+    return p2;
 }
 
 template <typename T>

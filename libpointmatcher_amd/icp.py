@@ -87,6 +87,7 @@ def lib():
         l.pmx_icp_trace_get.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         l.pmx_icp_timing.argtypes = [C.c_void_p, C.c_int]
         l.pmx_icp_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+        l.pmx_icp_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _lib = l
     return _lib
 
@@ -195,6 +196,8 @@ class ICP:
         """Stage a descriptor (n,) or (n, span) for the next compute / prepare;
         cloud: "reading" or "reference" (e.g. the reading's "maxSearchDist"
         of KDTreeVarDistMatcher)."""
+        if cloud not in ("reading", "reference"):
+            raise ValueError(f'cloud must be "reading" or "reference", not {cloud!r}')
         v = np.ascontiguousarray(values, dtype=self.dtype)
         span = 1 if v.ndim == 1 else v.shape[1]
         self._chk(self._l.pmx_icp_add_descriptor(self.h, 0 if cloud == "reading" else 1, name.encode(), span, _p(v),
@@ -251,6 +254,12 @@ class ICP:
 
     def timing(self, on=True):
         self._chk(self._l.pmx_icp_timing(self.h, 1 if on else 0))
+
+    def select_stats(self):
+        """(window hits, window misses) of the device loop since the last prepare."""
+        h, m = C.c_uint64(), C.c_uint64()
+        self._chk(self._l.pmx_icp_select_stats(self.h, C.byref(h), C.byref(m)))
+        return h.value, m.value
 
     def timing_read(self):
         ms = C.c_double()

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "oracle", "build", "libpmo.so")
+# (PMO_LIB: another build of the same source, e.g. bench.py's -march=native one)
+LIB = os.environ.get("PMO_LIB") or os.path.join(ROOT, "oracle", "build", "libpmo.so")
 
 # error codes (oracle/pmo.h)
 OK, E_NO_POINTS, E_EMPTY_QUANTILE, E_BAD_PARAM, E_TRANSFORMATION, E_NAN = 0, -1, -2, -3, -4, -5

@@ -174,3 +174,21 @@ def test_yaml_inf_and_numbers():
     icp.load_yaml(chain_yaml(maxdist="inf", filters=[("MaxDistOutlierFilter", {"maxDist": "inf"})]))
     with pytest.raises(I.InvalidParameter):
         icp.load_yaml(chain_yaml(maxdist="-1"))
+
+
+def test_add_descriptor_rejects_bad_arguments():
+    """pmx_icp_add_descriptor is guarded (no exception crosses the C ABI) and
+    the Python binding accepts only the two cloud names."""
+    from libpointmatcher_amd.icp import ICP, lib
+    from libpointmatcher_amd._capi import InvalidParameter
+    icp = ICP(np.float32)
+    with pytest.raises(ValueError, match="reading"):
+        icp.add_descriptor("readings", "maxSearchDist", np.ones(4, np.float32))
+    l = lib()
+    v = np.ones(4, np.float32)
+    assert l.pmx_icp_add_descriptor(icp.h, 0, b"d", 1, v.ctypes.data_as(ctypes.c_void_p), -1) == -3
+    assert l.pmx_icp_add_descriptor(icp.h, 0, b"d", 1, v.ctypes.data_as(ctypes.c_void_p), 1 << 62) == -3
+    assert l.pmx_icp_add_descriptor(icp.h, 2, b"d", 1, v.ctypes.data_as(ctypes.c_void_p), 4) == -3
+    assert "bad arguments" in l.pmx_icp_last_error(icp.h).decode()
+    icp.add_descriptor("reading", "maxSearchDist", v)  # a well-formed one is staged
+    _ = InvalidParameter

@@ -146,3 +146,28 @@ def test_vtk_unstructured_field_and_errors(tmp_path):
         load_cloud(mis)
     with pytest.raises(RuntimeError, match="extension"):
         load_cloud(tmp_path / "x.ply")
+
+
+def test_vtk_malformed_blocks_rejected(tmp_path):
+    """Point data before POINTS, a repeated POINTS block or a negative count
+    raise instead of leaving short descriptor rows (over-read)."""
+    head = b"# vtk DataFile Version 3.0\nx\nASCII\nDATASET POLYDATA\n"
+    pts = b"POINTS 2 float\n0 0 0\n1 1 1\n"
+    p = tmp_path / "f.vtk"
+    p.write_bytes(head + b"FIELD FieldData 1\nTIME 1 1 double\n0.5\n" + pts)
+    with pytest.raises(RuntimeError, match="before POINTS"):
+        load_cloud(p)
+    p.write_bytes(head + b"SCALARS d float 1\nLOOKUP_TABLE default\n1\n2\n" + pts)
+    with pytest.raises(RuntimeError, match="before POINTS"):
+        load_cloud(p)
+    p.write_bytes(head + pts + b"POINTS 3 float\n0 0 0\n1 1 1\n2 2 2\n")
+    with pytest.raises(RuntimeError, match="second POINTS"):
+        load_cloud(p)
+    p.write_bytes(head + b"POINTS -4 float\n")
+    with pytest.raises(RuntimeError, match="bad POINTS count"):
+        load_cloud(p)
+    # well-formed point data after POINTS still loads
+    p.write_bytes(head + pts + b"POINT_DATA 2\nSCALARS d float 1\nLOOKUP_TABLE default\n1\n2\n")
+    c = load_cloud(p)
+    assert c.descriptor_labels == [("d", 1)]
+    np.testing.assert_array_equal(c.descriptor("d")[:, 0], [1, 2])

@@ -250,3 +250,21 @@ def test_two_rank_icp_matches_single_process(two_rank_results):
     assert rc == 0
     assert np.linalg.norm(T1.astype(np.float64) - To) <= tol  # the protocol model is the oracle at N=1
     assert np.linalg.norm(r[0]["T"].astype(np.float64) - To) <= tol
+
+
+def test_set_default_sharded_raises():
+    """setDefault() (ICP.cpp:99-113) puts RandomSampling on the reading and
+    SamplingSurfaceNormal (samplingMethod 0) on the reference: both draw from
+    the process's rand() state, so a sharded ICP refuses the chain with
+    ConfigurationError before any device work.
+    Runs without a GPU: the check precedes the device context."""
+    from libpointmatcher_amd import _capi
+    from libpointmatcher_amd.icp import ICP, ConfigurationError
+    comm = _capi.HostComm(2, 0, lambda a, op: None, lambda a: np.concatenate([a, a]))
+    icp = ICP(np.float32)
+    icp.set_default()
+    icp.comm_init_host(comm)
+    pts = hom(np.random.default_rng(0).normal(size=(64, 3)).astype(np.float32))
+    with pytest.raises(ConfigurationError, match="rand"):
+        icp.compute(pts, pts)
+    icp.close()
