@@ -99,7 +99,15 @@ struct pmx_ctx {
     bool adaptive = true;
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
-    bool cold_tile = true;        // a new reading's first match on the LDS tile kernel (PMX_COLD_TILE=0: off)
+    // LDS box of the blocks' full searches (pmx_grid_box.inc): dynamic LDS
+    // bytes per block (PMX_BOX_LDS, 0: off), the cells a match without usable
+    // reuse grows its boxes by (PMX_BOX_GROW), and the device-loop iterations
+    // after a prepare that launch with it before the fallback counts decide
+    uint32_t box_lds = 0;  // (off by default: measured slower than the per-lane walk so far)
+    int box_grow = 3;
+    int box_first_iters = 4;
+    int64_t box_full_last = -1;   // full searches of the last match known to the host (-1: none yet)
+    int64_t loop_since_prepare = 0;  // device-loop iterations enqueued since the reading was set
     void* d_safe = nullptr;       // T[N]: safe radius per query
     int64_t safe_cap = 0;
     bool grid_ready = false;
@@ -771,6 +779,8 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     c->N = N;
     c->N_total = N;
     c->N_max = N;
+    c->box_full_last = -1;
+    c->loop_since_prepare = 0;
     // A new reading's first match has no previous match to adapt the level
     // from, and the initial pose is usually the worst aligned: a coarse level
     // walks few shells where the finest walks dozens (measured on MI355X, C3).
@@ -906,10 +916,16 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // temporal reuse: the output buffers hold this reading's previous
         // match (same k, same level) with its safe radii
         GridReuse<T> ru;
-        // no previous match of this reading at all: the first match runs the
-        // tile kernel's cold form (pmx_grid_tile.inc)
-        const bool cold = c->cold_tile && c->reuse_on && c->grid_mode >= 1 &&
-                          !(c->safe_valid && c->have_match && c->ids_grid);
+        // the blocks' full searches from an LDS box (pmx_grid_box.inc) while
+        // many queries need one: no usable previous match, the first device-
+        // loop iterations after a new reading (moves too large to certify),
+        // or the last known match's full searches over 1/8 of the queries.
+        // The box costs occupancy, so a converged match launches without it.
+        const bool no_prev = !(c->safe_valid && c->have_match && c->ids_grid && c->knn == knn);
+        const bool many = c->box_full_last >= 0 ? c->box_full_last * 8 >= c->N : !c->loop_on;
+        const bool early = c->loop_on && c->loop_since_prepare < c->box_first_iters;
+        const uint32_t box_bytes = c->grid_mode >= 1 && (no_prev || early || many) ? c->box_lds : 0u;
+        if (c->loop_on) ++c->loop_since_prepare;
         if (c->reuse_on && c->grid_mode >= 1) {
             ru.mode = c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
@@ -927,8 +943,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, cold, e1,
-                             c->stream);
+                             c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, box_bytes,
+                             c->box_grow, e1, c->stream);
         c->counter_deferred = defer;  // (e1 recorded after the match kernel, before the counter sum)
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
@@ -1356,6 +1372,7 @@ void after_readback(pmx_ctx* c) {
     unsigned long long v = 0, f = 0;
     std::memcpy(&v, (const char*)c->h_result + kBlkVisited, sizeof(v));
     std::memcpy(&f, (const char*)c->h_result + kBlkVisited + 8, sizeof(f));
+    c->box_full_last = (int64_t)f;
     choose_level(c, v, f);
 }
 
@@ -1752,6 +1769,11 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
         const hipError_t e = hipEventSynchronize(c->loop_ev[s]);
         if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
         if (((const LoopState<T>*)(stat_slot(c, s) + kStatLoop))->done) stop = true;
+        {  // the full searches of the batch's last match (the LDS box policy of match_impl)
+            unsigned long long f = 0;
+            std::memcpy(&f, stat_slot(c, s) + kBlkVisited + 8, sizeof(f));
+            c->box_full_last = (int64_t)f;
+        }
     }
     // drain: the last issued batch's copy is the final status
     while (rc == PMX_OK && nfly > 0) {
@@ -2186,7 +2208,9 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
-    if (const char* e = std::getenv("PMX_COLD_TILE")) c->cold_tile = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_BOX_LDS")) c->box_lds = (uint32_t)std::min(65536, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("PMX_BOX_GROW")) c->box_grow = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("PMX_BOX_FIRST")) c->box_first_iters = std::max(0, std::atoi(e));
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;

@@ -813,6 +813,9 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
     return true;
 }
 
+// ------------------------------------------------- LDS box full searches --
+#include "pmx_grid_box.inc"
+
 // ------------------------------------------------------- per-lane kernel --
 // occupancy hint of the per-lane kernel (waves per SIMD; 0 = the compiler's
 // choice).  The search is bound by dependent gather latency, so more resident
@@ -829,7 +832,10 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
 #else
 #define PMX_LANE_ATTR
 #endif
-template <typename T, int KT>
+// BOX: the instance with the LDS box path (launched with dynamic LDS while
+// many queries need a full search); the plain instance keeps the reuse
+// path's registers and occupancy
+template <typename T, int KT, bool BOX>
 __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
@@ -842,7 +848,9 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
                                                         SpecSel* __restrict__ spec, unsigned long long* __restrict__ vout,
                                                         int* __restrict__ iter_err, SelectState* __restrict__ spec_st,
                                                         unsigned long long* __restrict__ xseg,
-                                                        const T* __restrict__ radii) {
+                                                        const T* __restrict__ radii, uint32_t box_bytes,
+                                                        int box_grow) {
+    extern __shared__ __attribute__((aligned(16))) char box_lds[];  // (box_bytes: the launch's dynamic LDS)
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -867,29 +875,18 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
     // quantile window (pmx_spec.h): every written distance is classified
     SpecAcc<T> sa;
     spec_acc_init<T>(sa, spec);
-    if (reuse < 2) {
-        const int64_t j = blk * blockDim.x + threadIdx.x;
-        if (j < N)
-            full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, qr2(radii, j, maxR2), oct, out_d, out_i, safe,
-                              visits, sa);
-        add_visits(visits, visited);
-        if (reuse) {  // every query took the full search (the counter the level choice reads)
-            const unsigned long long m = __ballot(j < N);
-            if ((threadIdx.x & 63) == 0 && visited && m) atomicAdd(vslot(visited, 1), (unsigned long long)__popcll(m));
-        }
-        if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
-        if (vout) counter_fold<T>(visited, vout, iter_err, spec, spec_st, xseg);
-        return;
-    }
-    // Phase 1: every lane tries the certificate.  Phase 2: the block's misses,
-    // compacted in slot order, run the full search on consecutive lanes (a
-    // miss does not make its whole wave pay for both paths).
+    // Phase 1: every lane tries the certificate (reuse 2; otherwise every
+    // query misses).  Phase 2: the block's misses, compacted in slot order,
+    // run the full search on consecutive lanes — from an LDS box of the grid
+    // when the launch has one and enough lanes missed (pmx_grid_box.inc),
+    // else the per-lane shell walk (a miss does not make its whole wave pay
+    // for both paths).
     __shared__ int miss[256];
     __shared__ int wave_cnt[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t j = blk * blockDim.x + threadIdx.x;
-    bool missed = false;
-    if (j < N) {
+    bool missed = j < N;
+    if (reuse == 2 && j < N) {
         const P4<T> p = gld(rd, j);
         T qx, qy, qz;
         gxform(Tm, p, qx, qy, qz);
@@ -908,14 +905,17 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
     }
     if (missed) miss[off + __popcll(m & ((1ull << lane) - 1))] = threadIdx.x;
     __syncthreads();
-    if ((int)threadIdx.x < total) {
+    if (BOX && total >= kBoxMinMiss && !oct) {
+        box_phase<T, KT>(gpts, gidx, start, G, rd, blk * blockDim.x, miss, total, Tm, k, maxR2, radii, out_d, out_i,
+                         safe, visits, sa, box_lds, box_bytes, reuse == 2 ? -1 : box_grow, reuse, Tprev);
+    } else if ((int)threadIdx.x < total) {
         const int64_t j2 = blk * blockDim.x + miss[threadIdx.x];
         full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
                           sa);
     }
     add_visits(visits, visited);
-    // queries that took the full search (the "fallback" counter)
-    if (threadIdx.x == 0 && visited && total) atomicAdd(vslot(visited, 1), (unsigned long long)total);
+    // queries that took the full search (the "fallback" counter the level choice reads)
+    if (threadIdx.x == 0 && visited && total && reuse) atomicAdd(vslot(visited, 1), (unsigned long long)total);
     if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
     if (vout) counter_fold<T>(visited, vout, iter_err, spec, spec_st, xseg);
 }
@@ -929,15 +929,17 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                       unsigned long long* vout, int* iter_err, SelectState* spec_st, unsigned long long* xseg,
-                      const T* radii, bool cold, hipStream_t s) {
-    if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
-        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
-                           G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
-                           ctl, gd, spec, ru.safe);
-    } else if (mode >= 1) {  // 1: shell search, 2: octant block first
-        hipLaunchKernelGGL((grid_lane_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, gpts, gidx,
-                           start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe,
-                           ru.Tprev, ctl, gd, spec, vout, iter_err, spec_st, xseg, radii);
+                      const T* radii, uint32_t box_bytes, int box_grow, hipStream_t s) {
+    if (mode >= 1) {  // 1: shell search, 2: octant block first
+#define PMX_LANE(B)                                                                                                  \
+    hipLaunchKernelGGL((grid_lane_kernel<T, KT, B>), dim3((unsigned)((N + 255) / 256)), dim3(256), box_bytes, s, gpts, \
+                       gidx, start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, \
+                       ru.Tprev, ctl, gd, spec, vout, iter_err, spec_st, xseg, radii, box_bytes, box_grow)
+        if (box_bytes > 0)
+            PMX_LANE(true);
+        else
+            PMX_LANE(false);
+#undef PMX_LANE
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -953,10 +955,10 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                        SelectState* spec_st, unsigned long long* xseg, bool fold, bool defer, const T* radii,
-                       bool cold, hipEvent_t ev_end, hipStream_t s) {
+                       uint32_t box_bytes, int box_grow, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
-    cold = cold && mode >= 1;
-    fold = fold && mode >= 1 && visited && vout && !cold;  // (a cold launch runs the counter kernel after it)
+    if (mode < 1) box_bytes = 0;
+    fold = fold && mode >= 1 && visited && vout;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -967,10 +969,9 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, cold, s)
-    // with reuse the list keeps room for the (k+1)-th point (the safe radius;
-    // the cold tile writes radius 0 and keeps k entries)
-    const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
+                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, box_bytes, box_grow, s)
+    // with reuse the list keeps room for the (k+1)-th point (the safe radius)
+    const int kl = ru.mode && mode >= 1 && knn < 16 ? knn + 1 : knn;
     if (kl == 1)
         PMX_KT(1);
     else if (kl <= 2)
@@ -995,14 +996,14 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, bool, bool, const float*, bool, hipEvent_t,
+                                       unsigned long long*, bool, bool, const float*, uint32_t, int, hipEvent_t,
                                        hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, bool, bool, const double*, bool, hipEvent_t,
+                                        unsigned long long*, bool, bool, const double*, uint32_t, int, hipEvent_t,
                                         hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
@@ -1028,7 +1029,7 @@ void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, 
 // first ICP iteration.
 void preload_grid() {
     hipFuncAttributes a;
-    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1>));
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1, false>));
 }
 
 }  // namespace pmx

@@ -172,15 +172,17 @@ __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
 // mode 0 = wave-cooperative LDS tiles, 1 = per-lane shell search (default),
 // 2 = octant block first.  ids written are positions in gpts;
 // launch_pos_to_index maps them back.  ctl / gd (device loop, modes 1-2):
-// transform and level are read on the device.
+// transform and level are read on the device.  box_bytes > 0: the launch's
+// dynamic LDS for the blocks' full searches (pmx_grid_box.inc), box_grow the
+// cells a box of a match without usable reuse grows by.
 template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       unsigned long long* xseg, bool fold, bool defer, const T* radii, bool cold, hipEvent_t ev_end,
-                       hipStream_t s);
+                       unsigned long long* xseg, bool fold, bool defer, const T* radii, uint32_t box_bytes,
+                       int box_grow, hipEvent_t ev_end, hipStream_t s);
 template <typename T>
 void launch_counter_sum(unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
                         SpecSel* spec, SelectState* st, hipStream_t s);

@@ -1,0 +1,360 @@
+// pmx_selectall.h — the radix select with every pass in one launch (the
+// select_all_kernel of pmx_select.hip and the fused post-match launch of
+// pmx_post.hip), and the histogram helpers it shares with the per-pass
+// kernels.
+#pragma once
+
+#include "pmx_internal.h"
+#include "pmx_spec.h"
+
+#include <type_traits>
+
+namespace pmx {
+
+// ------------------------------------------------------------- histogram --
+constexpr int kSelPer = 16;  // keys per thread per tile
+
+// kSelPer consecutive values from i0 (16-byte vector loads when the whole run
+// is in range; +inf pads past n and is excluded like any infinite distance)
+template <typename T>
+__device__ __forceinline__ void load_keys(const T* __restrict__ d, int64_t i0, int64_t n, T (&v)[kSelPer]) {
+    if (i0 + kSelPer <= n) {
+        using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+        constexpr int E = 16 / sizeof(T);
+        const V* p = reinterpret_cast<const V*>(d + i0);  // i0 * sizeof(T) is a multiple of 64
+#pragma unroll
+        for (int q = 0; q < kSelPer / E; ++q) {
+            const V x = p[q];
+            const T* xe = reinterpret_cast<const T*>(&x);
+#pragma unroll
+            for (int e = 0; e < E; ++e) v[q * E + e] = xe[e];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kSelPer; ++j) v[j] = i0 + j < n ? d[i0 + j] : (T)__builtin_huge_val();
+    }
+}
+// ------------------------------------------------------------------ pick --
+// histogram bin reads/resets; kCoherent: device-scope atomics (the fused pass
+// kernel reads bins other blocks - on other XCDs - have just added to)
+template <bool kCoherent>
+__device__ __forceinline__ uint32_t hbin(uint32_t* h) {
+    // (a fetch-add of 0 is performed where the other blocks' adds were)
+    if constexpr (kCoherent) return __hip_atomic_fetch_add(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return *h;
+}
+template <bool kCoherent>
+__device__ __forceinline__ void hzero(uint32_t* h) {
+    if constexpr (kCoherent) {
+        __hip_atomic_store(h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        *h = 0;
+    }
+}
+
+// ------------------------------------------------- all passes, one launch --
+// Every kernel boundary costs ~4.5 us on MI355X (measured: an empty select
+// pass takes 4.6 us in the kernel trace — the dispatch's release / acquire
+// over the 8 XCD L2s), and the three (f64: six) passes of the radix select
+// are three boundaries per iteration even when the quantile window already
+// resolved the limit.  select_all_kernel runs every pass in ONE launch: the
+// blocks histogram a digit, the last block to arrive (arrival counter) picks
+// it and publishes it, the others wait for the publication and go on with
+// the next digit.  A window hit makes the whole launch a no-op.
+//
+// Cross-block traffic uses device-scope atomics only (flushes with returning
+// atomics, as the ticket pass does; reads of what another block wrote with
+// fetch-add 0 / atomic loads): no fence, no L2 write-back.  Nothing is reset:
+// the arrival counters only grow (one launch adds exactly `grid` arrivals per
+// pass it reaches), so arrival a belongs to generation a / grid + 1, and the
+// picker of that generation stamps its publication with it.  The waits are
+// bounded (an exit condition every wave reaches): a timeout raises
+// kSelTimeout in the iteration's error word instead of hanging.  All blocks
+// are resident (grid <= 256 blocks of 256 threads, the only kernel running:
+// the stream's previous kernel has completed).
+constexpr int kSelMaxPasses = 6;
+struct SelX {
+    unsigned int arrive[8];                  // per pass (monotonic)
+    unsigned long long go[kSelMaxPasses];    // gen << 56 | err << 55 | resolved prefix (<= 54 bits)
+    unsigned long long rank[kSelMaxPasses];  // rank left inside the prefix after pass p
+    unsigned long long tot[kSelMaxPasses];   // keys histogrammed in pass p
+    unsigned long long count;                // finite keys (pass 0)
+    unsigned long long pre;                  // gen << 56 | window hit: the deferred counter phase's verdict
+    unsigned long long lim;                  // the resolved limit (double bits), for a fused point-to-plane
+};
+
+__device__ __forceinline__ unsigned long long ald(unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// (returning: the caller makes later publications depend on the return)
+__device__ __forceinline__ unsigned long long ast(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The select itself; true when this block ends with the resolved limit in
+// *L (then, with a fused point-to-plane, it goes on to the reduction).
+// `wait_last`: the non-picker blocks wait for the last pass's publication
+// (they need the limit) instead of leaving.
+template <typename T>
+__device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
+                                                SelectState* __restrict__ st, double ratio_host,
+                                                const double* __restrict__ ratio_dev, int* __restrict__ iter_err,
+                                                int agg, SpecSel* __restrict__ spec,
+                                                unsigned long long* __restrict__ vpart,
+                                                unsigned long long* __restrict__ vout, bool wait_last, double* L,
+                                                bool* hit_out = nullptr) {
+    using KO = KeyOf<T>;
+    using K = typename KO::K;
+    __shared__ uint32_t lh[2048];
+    __shared__ unsigned long long part[256];
+    __shared__ unsigned long long s_w[2];  // (published word, its generation)
+    __shared__ int s_last;
+    __shared__ unsigned int s_old;
+    if (vpart) {
+        // The match's counter phase deferred into this launch (one launch
+        // fewer per iteration): block 0 folds the counters and tries the
+        // window pick, then publishes the verdict (generation-stamped, as the
+        // passes below); a hit ends every block, a miss runs the passes.
+        if (threadIdx.x == 0) s_old = atomicAdd(&sx->arrive[7], 1u);
+        __syncthreads();
+        const unsigned long long pgen = ((unsigned long long)(s_old / gridDim.x) + 1ull) & 0xffull;
+        if (blockIdx.x == 0) {
+            counter_phase<T>(vpart, vout, iter_err, spec, st, nullptr);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const unsigned long long hit = spec && spec->hit ? 1ull : 0ull;
+                // the limit first (write-through), then the verdict that covers it
+                const unsigned long long r0 = hit ? ast(&sx->lim, (unsigned long long)__double_as_longlong(st->limit)) : 0ull;
+                asm volatile("" ::"v"(r0));
+                (void)ast(&sx->pre, pgen << 56 | hit);
+                s_w[0] = hit;
+                s_w[1] = (unsigned long long)__double_as_longlong(st->limit);
+            }
+            __syncthreads();
+            if (s_w[0]) {
+                *L = __longlong_as_double((long long)s_w[1]);
+                if (hit_out) *hit_out = true;
+                return true;
+            }
+        } else {
+            if (threadIdx.x == 0) {
+                unsigned long long w = 0;
+                bool ok = false;
+                // (a slow poll: block 0's own coherent loads share the path with these)
+                for (int it = 0; it < (1 << 20); ++it) {
+                    w = ald(&sx->pre);
+                    if ((w >> 56) == pgen) {
+                        ok = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(16);
+                }
+                s_w[0] = ok ? (w & 1ull) : 2ull;
+                if (!ok) __hip_atomic_store(iter_err, kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (ok && (w & 1ull)) s_w[1] = ald(&sx->lim);
+            }
+            __syncthreads();
+            if (s_w[0] == 2ull) return false;  // (the wait timed out)
+            if (s_w[0]) {  // the window resolved it
+                *L = __longlong_as_double((long long)s_w[1]);
+                if (hit_out) *hit_out = true;
+                return true;
+            }
+        }
+    } else if (spec && spec->hit) {
+        *L = st->limit;  // (the window resolved it in the counter kernel before this launch)
+        if (hit_out) *hit_out = true;
+        return true;
+    }
+    if (hit_out) *hit_out = false;
+    constexpr int passes = KO::bits == 32 ? 3 : 6;
+    uint32_t* hist0 = reinterpret_cast<uint32_t*>(sx + 1);
+    const int t = threadIdx.x;
+    const unsigned G = gridDim.x;
+    K prefix = 0;
+    const T q = ratio_dev ? (T)(*ratio_dev) : (T)ratio_host;
+    for (int pass = 0; pass < passes; ++pass) {
+        int shift, bits;
+        digit_of(KO::bits, pass, shift, bits);
+        const int nb = 1 << bits;
+        uint32_t* hist = hist0 + pass * 2048;
+        // ---- histogram of this digit over the keys inside the prefix ----
+        for (int i = t; i < nb; i += 256) lh[i] = 0;
+        __syncthreads();
+        {
+            const int hs = shift + bits;
+            const int lane = t & 63;
+            const int64_t tile = (int64_t)256 * kSelPer;
+            for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)G * tile) {
+                T v[kSelPer];
+                load_keys<T>(d, base + (int64_t)t * kSelPer, n, v);
+#pragma unroll
+                for (int j = 0; j < kSelPer; ++j) {
+                    const K k = KO::key(v[j]);
+                    int bin = -1;
+                    if (k < KO::inf_key && (pass == 0 || (k >> hs) == prefix))
+                        bin = (int)((uint32_t)(k >> shift) & (uint32_t)(nb - 1));
+                    if (!agg) {
+                        if (bin >= 0) atomicAdd(&lh[bin], 1u);
+                        continue;
+                    }
+                    unsigned long long todo = __ballot(bin >= 0);
+                    while (todo) {
+                        const int leader = __builtin_ctzll(todo);
+                        const int lb = __builtin_amdgcn_readlane(bin, leader);
+                        const unsigned long long same = __ballot(bin == lb);
+                        if (lane == leader) atomicAdd(&lh[lb], (uint32_t)__popcll(same));
+                        todo &= ~same;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t ret = 0;  // returning flushes: done at the coherence point once back
+        for (int i = t; i < nb; i += 256) {
+            const uint32_t c = lh[i];
+            if (c) ret |= atomicAdd(&hist[i], c);
+        }
+        asm volatile("" ::"v"(ret));
+        __syncthreads();
+        if (t == 0) {
+            const unsigned old = atomicAdd(&sx->arrive[pass], 1u);
+            s_old = old;
+            s_last = (old + 1) % G == 0;
+        }
+        __syncthreads();
+        const unsigned long long gen = ((unsigned long long)(s_old / G) + 1ull) & 0xffull;
+        if (s_last) {
+            // ---- the picker: pick_phase's rule over the flushed bins ----
+            const int per = nb / 256;
+            uint32_t hv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) hv[j] = j < per ? hbin<true>(&hist[t * per + j]) : 0u;
+            unsigned long long mine = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) mine += hv[j];
+            part[t] = mine;
+            __syncthreads();
+            for (int off = 1; off < 256; off <<= 1) {
+                const unsigned long long v = t >= off ? part[t - off] : 0ull;
+                __syncthreads();
+                part[t] += v;
+                __syncthreads();
+            }
+            const unsigned long long total = part[255];
+            unsigned long long rank = 0;
+            int err = 0;
+            if (pass == 0) {
+                if (total == 0) {
+                    err = -2;  // PMX_E_EMPTY_QUANTILE: ConvergenceError("no outlier to filter")
+                } else if (!ratio_dev && ratio_host == kRatioMedianIndex) {
+                    rank = total / 2;  // nth_element at size / 2 (Matches.cpp:110-120)
+                } else if (q < (T)0 || q > (T)1) {
+                    err = -3;  // ConvergenceError("quantile must be between 0 and 1")
+                } else if (q == (T)1) {
+                    rank = total - 1;  // max_element
+                } else {
+                    rank = (unsigned long long)((T)total * q);
+                    if (rank >= total) rank = total - 1;  // reference reads out of range (UB); clamp
+                }
+            } else {
+                rank = __hip_atomic_fetch_add(&sx->rank[pass - 1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (err == 0) {
+                const unsigned long long excl = t > 0 ? part[t - 1] : 0ull;
+                if (rank >= excl && rank < part[t]) {
+                    unsigned long long cum = excl;
+                    for (int j = 0; j < per; ++j) {
+                        const unsigned long long c = hv[j];
+                        if (rank < cum + c) {
+                            s_w[0] = (unsigned long long)(t * per + j);
+                            s_w[1] = rank - cum;
+                            break;
+                        }
+                        cum += c;
+                    }
+                }
+            }
+            __syncthreads();
+            for (int j = 0; j < per; ++j) hzero<true>(&hist[t * per + j]);  // ready for the next launch
+            const K np = err ? (K)0 : (K)((prefix << bits) | (K)s_w[0]);
+            const unsigned long long nrank = err ? 0ull : s_w[1];
+            if (t == 0) {
+                unsigned long long r0 = 0;
+                if (pass == 0) r0 |= ast(&sx->count, total);
+                r0 |= ast(&sx->tot[pass], total);
+                if (err || pass == passes - 1) {
+                    // the final state, as the pass kernels leave it
+                    const unsigned long long count = pass == 0 ? total : ald(&sx->count);
+                    st->err = err;
+                    st->count = count;
+                    st->prefix = (unsigned long long)np;
+                    st->rank = nrank;
+                    st->ratio = (double)q;
+                    if (err) {
+                        st->limit = __builtin_nan("");
+                        *iter_err = err;
+                    } else {
+                        st->limit = (double)KO::val(np);
+                        if (spec) {
+                            // density for the next window: the finest bucket with >= 64 keys
+                            double dens = -1.0;
+                            for (int p = 0; p < passes; ++p) {
+                                int sh, bt;
+                                digit_of(KO::bits, p, sh, bt);
+                                const unsigned long long c = p == pass ? total : ald(&sx->tot[p]);
+                                if (c >= 64) dens = (double)c / ldexp(1.0, sh + bt);
+                            }
+                            spec_update<T>(spec, np, dens > 0.0 ? dens : (double)(total + 1) / (double)nb);
+                        }
+                    }
+                } else {
+                    r0 |= ast(&sx->rank[pass], nrank);
+                }
+                if (pass == passes - 1 && !err) r0 |= ast(&sx->lim, (unsigned long long)__double_as_longlong((double)KO::val(np)));
+                // publish once the data above has returned (performed where every block reads it)
+                asm volatile("" ::"v"(r0));
+                (void)ast(&sx->go[pass],
+                          gen << 56 | (err ? 1ull << 55 : 0ull) | ((unsigned long long)np & ((1ull << 55) - 1)));
+            }
+            if (err) return false;
+            prefix = np;
+            __syncthreads();
+            if (pass == passes - 1) {
+                *L = (double)KO::val(np);
+                return true;
+            }
+        } else {
+            if (pass == passes - 1 && !wait_last) return false;  // (the picker finishes alone)
+            // ---- wait for this generation's publication (bounded) ----
+            if (t == 0) {
+                unsigned long long w = 0;
+                bool ok = false;
+                for (int it = 0; it < (1 << 22); ++it) {
+                    w = ald(&sx->go[pass]);
+                    if ((w >> 56) == gen) {
+                        ok = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                s_w[0] = w;
+                s_w[1] = ok ? 1ull : 0ull;
+                if (!ok) *iter_err = kSelTimeout;
+            }
+            __syncthreads();
+            const unsigned long long w = s_w[0];
+            if (!s_w[1] || (w >> 55) & 1ull) return false;  // timeout, or the quantile failed
+            prefix = (K)(w & ((1ull << 55) - 1));
+            if (pass == passes - 1) {  // (wait_last) the published final limit
+                if (threadIdx.x == 0) s_w[0] = ald(&sx->lim);
+                __syncthreads();
+                *L = __longlong_as_double((long long)s_w[0]);
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
+}  // namespace pmx

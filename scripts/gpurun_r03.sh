@@ -12,8 +12,12 @@ want() { [[ " $* " == *" all "* ]] || [[ " $ARGS " == *" $1 "* ]]; }
 ARGS=" $* "
 rc=0
 if [[ "$ARGS" == *" tests "* ]]; then
-  step tests && timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests_gpu.log 2>&1 || { tail -30 gpurun_out/tests_gpu.log; exit 1; }
+  step tests && timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/tests_gpu.log 2>&1 || { tail -30 gpurun_out/tests_gpu.log; exit 1; }
   tail -3 gpurun_out/tests_gpu.log
+fi
+if [[ "$ARGS" == *" quick "* ]]; then
+  step bench_quick && timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || { tail -20 gpurun_out/bench_quick.err; exit 1; }
+  step bench_driver && timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_driver.json 2> gpurun_out/bench_driver.err || { tail -20 gpurun_out/bench_driver.err; exit 1; }
 fi
 if [[ "$ARGS" == *" bench "* ]]; then
   step bench && timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
