@@ -944,7 +944,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, box_bytes,
-                             c->box_grow, e1, c->stream);
+                             c->box_grow, no_prev && c->reuse_on, e1, c->stream);
         c->counter_deferred = defer;  // (e1 recorded after the match kernel, before the counter sum)
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)

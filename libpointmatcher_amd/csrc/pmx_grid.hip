@@ -929,8 +929,12 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                       unsigned long long* vout, int* iter_err, SelectState* spec_st, unsigned long long* xseg,
-                      const T* radii, uint32_t box_bytes, int box_grow, hipStream_t s) {
-    if (mode >= 1) {  // 1: shell search, 2: octant block first
+                      const T* radii, uint32_t box_bytes, int box_grow, bool cold, hipStream_t s) {
+    if (cold) {  // a new reading's first match without an LDS box: the tile kernel's cold form (pmx_grid_tile.inc)
+        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
+                           G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
+                           ctl, gd, spec, ru.safe);
+    } else if (mode >= 1) {  // 1: shell search, 2: octant block first
 #define PMX_LANE(B)                                                                                                  \
     hipLaunchKernelGGL((grid_lane_kernel<T, KT, B>), dim3((unsigned)((N + 255) / 256)), dim3(256), box_bytes, s, gpts, \
                        gidx, start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, \
@@ -955,10 +959,11 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                        SelectState* spec_st, unsigned long long* xseg, bool fold, bool defer, const T* radii,
-                       uint32_t box_bytes, int box_grow, hipEvent_t ev_end, hipStream_t s) {
+                       uint32_t box_bytes, int box_grow, bool cold, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     if (mode < 1) box_bytes = 0;
-    fold = fold && mode >= 1 && visited && vout;
+    cold = cold && mode >= 1 && box_bytes == 0;
+    fold = fold && mode >= 1 && visited && vout && !cold;  // (a cold launch runs the counter kernel after it)
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -969,9 +974,11 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.inv_h = 1.0 / h;
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, box_bytes, box_grow, s)
-    // with reuse the list keeps room for the (k+1)-th point (the safe radius)
-    const int kl = ru.mode && mode >= 1 && knn < 16 ? knn + 1 : knn;
+                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, box_bytes, box_grow, cold, \
+                     s)
+    // with reuse the list keeps room for the (k+1)-th point (the safe radius;
+    // the cold tile writes radius 0 and keeps k entries)
+    const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
     if (kl == 1)
         PMX_KT(1);
     else if (kl <= 2)
@@ -996,15 +1003,15 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, bool, bool, const float*, uint32_t, int, hipEvent_t,
-                                       hipStream_t);
+                                       unsigned long long*, bool, bool, const float*, uint32_t, int, bool,
+                                       hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, bool, bool, const double*, uint32_t, int, hipEvent_t,
-                                        hipStream_t);
+                                        unsigned long long*, bool, bool, const double*, uint32_t, int, bool,
+                                        hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

@@ -182,7 +182,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
                        unsigned long long* xseg, bool fold, bool defer, const T* radii, uint32_t box_bytes,
-                       int box_grow, hipEvent_t ev_end, hipStream_t s);
+                       int box_grow, bool cold, hipEvent_t ev_end, hipStream_t s);
 template <typename T>
 void launch_counter_sum(unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
                         SpecSel* spec, SelectState* st, hipStream_t s);

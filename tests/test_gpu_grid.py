@@ -12,14 +12,15 @@ from libpointmatcher_amd.synth import random_cloud, reading_cloud, reference_clo
 
 pytestmark = pytest.mark.gpu
 
-# every test runs against each grid search form: the per-lane kernel with its
-# LDS box for full searches (default, pmx_grid_box.inc), the box off (per-lane
-# shell walk only), a box budget too small for most blocks (whole-block
+# every test runs against each grid search form: the per-lane kernel (default),
+# the same with its LDS box for full searches (pmx_grid_box.inc), a box
+# budget too small for most blocks (whole-block
 # fallback), boxes that never grow (lanes leave the box: per-lane fallback),
 # coarse / fine levels, no temporal reuse, and the wave-cooperative tile kernel
 MODES = {"lane": {}, "lane_coarse": {"PMX_GRID_PPC": "32"}, "octant": {"PMX_GRID_MODE": "octant"},
          "lane_noreuse": {"PMX_GRID_REUSE": "0"}, "lane_fine": {"PMX_GRID_PPC": "1"},
-         "box_off": {"PMX_BOX_LDS": "0"}, "box_tight": {"PMX_BOX_LDS": "3072"}, "box_grow0": {"PMX_BOX_GROW": "0"},
+         "box": {"PMX_BOX_LDS": "49152"}, "box_tight": {"PMX_BOX_LDS": "3072"},
+         "box_grow0": {"PMX_BOX_LDS": "49152", "PMX_BOX_GROW": "0"},
          "tile": {"PMX_GRID_MODE": "tile"}, "tile_fallback": {"PMX_GRID_MODE": "tile", "PMX_GRID_TILE_MAX": "16"}}
 
 
@@ -204,7 +205,7 @@ def test_temporal_reuse_stays_exact(oracle, grid_mode, k):
     od, oi, _ = oracle.knn(ref, oracle.transform(Tg, rd2), k=k, method="kdtree")
     assert np.array_equal(d, od) and np.array_equal(i, oi)
     ctx.close()
-    if grid_mode in ("lane", "lane_coarse", "lane_fine", "box_off", "box_tight", "box_grow0"):
+    if grid_mode in ("lane", "lane_coarse", "lane_fine", "box", "box_tight", "box_grow0"):
         # the repeated pose was certified from the previous match (k pairs per query)
         # (the adaptive level may move during the first repeats: a level change
         # restarts the reuse chain)
