@@ -119,6 +119,11 @@ int pmx_comm_init_host(pmx_ctx* ctx, int nranks, int rank, pmx_allreduce_fn allr
                        void* user);
 /* kind: 0 none, 1 RCCL, 2 host callbacks */
 int pmx_comm_size(const pmx_ctx* ctx, int* nranks, int* rank, int* kind);
+/* Collectives this context has issued since creation (all-reduces,
+ * all-gathers; 0 without a communicator).  A sharded iteration whose
+ * quantile was resolved inside the exchanged key window issues two: the
+ * window segments' all-gather and the normal equations' all-reduce. */
+int pmx_comm_stats(const pmx_ctx* ctx, uint64_t* allreduces, uint64_t* allgathers);
 
 /* ------------------------------------------------------------ clouds --- */
 /* feat: rows x M column-major (point-major) T array, rows = D + 1 with the

@@ -94,8 +94,10 @@ class HostComm:
     def __init__(self, nranks, rank, allreduce, allgather):
         self.nranks, self.rank = nranks, rank
         self.errors = []
+        self.calls = {"allreduce": 0, "allgather": 0}  # (callbacks made, every context on this transport)
 
         def _ar(user, buf, count, typ, op):
+            self.calls["allreduce"] += 1
             try:
                 a = np.ctypeslib.as_array(C.cast(buf, C.POINTER(_COLL_CT[typ])), shape=(count,))
                 allreduce(a, "max" if op == COLL_MAX else "sum")
@@ -105,6 +107,7 @@ class HostComm:
                 return 1
 
         def _ag(user, send, recv, nbytes):
+            self.calls["allgather"] += 1
             try:
                 a = np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(nbytes,))
                 out = np.ctypeslib.as_array(C.cast(recv, C.POINTER(C.c_uint8)), shape=(nbytes * nranks,))
@@ -142,7 +145,7 @@ _lib = None
 
 EXPORTS = [
     "pmx_ctx_create", "pmx_ctx_destroy", "pmx_last_error", "pmx_device_count", "pmx_version",
-    "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_set_reference", "pmx_set_reading", "pmx_set_search", "pmx_match",
+    "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_comm_stats", "pmx_set_reference", "pmx_set_reading", "pmx_set_search", "pmx_match",
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed", "pmx_outlier_robust",
     "pmx_robust_scale", "pmx_set_reading_radii",
@@ -168,6 +171,7 @@ def lib():
         l.pmx_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         l.pmx_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, ALLGATHER_FN, C.c_void_p]
         l.pmx_comm_size.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        l.pmx_comm_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         l.pmx_set_reference.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
         l.pmx_set_reading.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
         l.pmx_set_search.argtypes = [C.c_void_p, C.c_int]
@@ -378,6 +382,12 @@ class Context:
         n, r, k = C.c_int(), C.c_int(), C.c_int()
         self._chk(self._l.pmx_comm_size(self.h, C.byref(n), C.byref(r), C.byref(k)))
         return n.value, r.value, k.value
+
+    def comm_stats(self):
+        """(all-reduces, all-gathers) this context has issued (pmx_comm_stats)."""
+        a, g = C.c_uint64(), C.c_uint64()
+        self._chk(self._l.pmx_comm_stats(self.h, C.byref(a), C.byref(g)))
+        return a.value, g.value
 
     # --- clouds
     def set_reference(self, feat, normals=None):

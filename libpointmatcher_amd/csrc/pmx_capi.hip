@@ -209,6 +209,10 @@ struct pmx_ctx {
     pmx_allgather_fn host_ag = nullptr;
     void* host_user = nullptr;
     void* h_stage = nullptr;      // pinned staging of the host collectives
+    int* h_flags = nullptr;       // pinned: the window verdict a sharded select reads back
+    bool spec_exchanged = false;  // this match all-gathered the window segments and picked
+    bool shard_done_seen = false; // a sharded loop read back its stop flag: no more iterations to enqueue
+    uint64_t n_allreduce = 0, n_allgather = 0;  // collectives issued (pmx_comm_stats)
     size_t h_stage_cap = 0;
     unsigned long long* d_specx = nullptr;  // quantile window exchange: own segment, then nranks gathered
 
@@ -243,6 +247,11 @@ struct pmx_ctx {
     // reduction waits for block 0's window pick before any block starts it,
     // and 511 polling blocks hold the CUs meanwhile (74.7 vs 67.6 us/iteration)
     bool select_p2 = false;
+    // device loop, point-to-plane, single rank: the post-match work in one
+    // launch with the sums fused into the match (pmx_post.hip; PMX_FUSED=0: off)
+    bool fuse_allowed = false;  // (PMX_FUSED=1: measured slower than the module chain so far)
+    double* d_fuse_part = nullptr;  // the match blocks' records [blocks][kFuseNV]
+    int64_t fuse_cap = 0;
     bool sel_pending = false;
     const void* selp_d = nullptr;
     int64_t selp_n = 0;
@@ -353,6 +362,7 @@ int stage_room(pmx_ctx* c, size_t bytes) {
 // in-place all-reduce of `count` elements of device memory
 int coll_allreduce(pmx_ctx* c, void* dbuf, int64_t count, int type, int op) {
     if (!sharded(c) || count <= 0) return PMX_OK;
+    ++c->n_allreduce;
     if (c->comm) {
         const ncclDataType_t dt = type == PMX_COLL_U32 ? ncclUint32 : type == PMX_COLL_U64 ? ncclUint64 : ncclFloat64;
         NCCLCHK(c, ncclAllReduce(dbuf, dbuf, (size_t)count, dt, op == PMX_COLL_MAX ? ncclMax : ncclSum, c->comm,
@@ -376,6 +386,7 @@ int coll_allgather(pmx_ctx* c, const void* dsend, void* drecv, size_t bytes) {
         if (drecv != dsend) HIPCHK(c, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, c->stream));
         return PMX_OK;
     }
+    ++c->n_allgather;
     if (c->comm) {
         NCCLCHK(c, ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, c->stream));
         return PMX_OK;
@@ -835,11 +846,12 @@ void flush_counter(pmx_ctx* c) {
 }
 
 template <typename T>
-int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
+int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited,
+               const FuseAcc<T>* fuse = nullptr) {
     flush_counter<T>(c);
     if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
     if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
-    if (knn < 1 || knn > 16) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 16] on the GPU path");
+    if (knn < 1 || knn > kMaxKnn) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 256] on the GPU path");
     if (!(maxDist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
     const int64_t n = c->N * knn;
     size_t cap = (size_t)c->match_cap * tsize(c);
@@ -899,9 +911,17 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         e1 = get_event(c);
     }
     if (c->search_type == 0 || !c->grid_ready) {
-        launch_match<T>((const P4<T>*)c->d_ref, c->M_pad, (const P4<T>*)c->d_rd, c->N, Tm, knn, maxR2,
-                        (T*)c->d_dists, c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1,
-                        c->cu_count);
+        if (knn > kLaneMaxK) {  // (the wave-per-query search over the whole reference, pmx_knn_wide.hip)
+            if (e0) (void)hipEventRecord(e0, c->stream);
+            launch_knn_wide<T>((const P4<T>*)c->d_ref, nullptr, nullptr, nullptr, c->M, (const P4<T>*)c->d_rd, c->N,
+                               Tm, knn, maxR2, nullptr, (T*)c->d_dists, c->d_ids, nullptr, nullptr, nullptr, nullptr,
+                               c->stream);
+            if (e1) (void)hipEventRecord(e1, c->stream);
+        } else {
+            launch_match<T>((const P4<T>*)c->d_ref, c->M_pad, (const P4<T>*)c->d_rd, c->N, Tm, knn, maxR2,
+                            (T*)c->d_dists, c->d_ids, (T*)c->d_part_d, c->d_part_i, c->part_cap, c->stream, e0, e1,
+                            c->cu_count);
+        }
         if (c->has_radii)
             launch_apply_radii<T>((T*)c->d_dists, c->d_ids, (const T*)c->d_radii, c->N, knn, c->stream);
         c->visited_host = (uint64_t)c->N * (uint64_t)c->M;
@@ -916,6 +936,9 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // temporal reuse: the output buffers hold this reading's previous
         // match (same k, same level) with its safe radii
         GridReuse<T> ru;
+        // (a fused match without a quantile must write its sums: no cold tile
+        // form then; with one, the first match has no window and the post
+        // launch reduces every pair itself)
         // the blocks' full searches from an LDS box (pmx_grid_box.inc) while
         // many queries need one: no usable previous match, the first device-
         // loop iterations after a new reading (moves too large to certify),
@@ -926,7 +949,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         const bool early = c->loop_on && c->loop_since_prepare < c->box_first_iters;
         const uint32_t box_bytes = c->grid_mode >= 1 && (no_prev || early || many) ? c->box_lds : 0u;
         if (c->loop_on) ++c->loop_since_prepare;
-        if (c->reuse_on && c->grid_mode >= 1) {
+        if (c->reuse_on && c->grid_mode >= 1 && knn <= kLaneMaxK) {  // (the wide search keeps no safe radii)
             ru.mode = c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
             for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
@@ -934,6 +957,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // several ranks: the counter sum packs this rank's window segment,
         // the segments are all-gathered and every rank picks from the union
         SpecSel* spec = c->spec_now();
+        c->spec_exchanged = false;
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx : nullptr;
         // single rank, window on: the counter phase runs at the start of the
         // select_all launch that the quantile filter issues next
@@ -944,7 +968,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, box_bytes,
-                             c->box_grow, no_prev && c->reuse_on, e1, c->stream);
+                             c->box_grow, no_prev && c->reuse_on && !(fuse && !fuse->quantile),
+                             fuse ? *fuse : FuseAcc<T>{}, e1, c->stream);
         c->counter_deferred = defer;  // (e1 recorded after the match kernel, before the counter sum)
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
@@ -952,6 +977,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             int rc = coll_allgather(c, xseg, xseg + kSpecXStride, kSpecXStride * sizeof(unsigned long long));
             if (rc) return rc;
             launch_spec_pick<T>(xseg + kSpecXStride, c->nranks, spec, c->d_sel, loop_ctl(c), c->stream);
+            c->spec_exchanged = true;
         }
         c->safe_valid = ru.mode != 0;
         c->visited_host = 0;
@@ -969,11 +995,35 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
 }
 
 // ----------------------------------------------------------------- outliers --
+// Several ranks, after the window segments were exchanged and picked from:
+// 1 when the radix passes (and their histogram all-reduces) can be skipped —
+// the window resolved the limit, or the device loop has converged (the pick
+// then did not run).  Every rank picked from the same union and read the same
+// all-reduced system, so every rank takes the same decision and the
+// collective sequences stay matched.  Costs one stream synchronisation.
+int sharded_window_resolved(pmx_ctx* c, SpecSel* spec) {
+    if (!c->h_flags) HIPCHK(c, hipHostMalloc((void**)&c->h_flags, 64, hipHostMallocDefault));
+    c->h_flags[0] = 0;
+    c->h_flags[1] = 0;
+    HIPCHK(c, hipMemcpyAsync(c->h_flags, &spec->hit, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    const LoopCtl* ctl = loop_ctl(c);
+    if (ctl) HIPCHK(c, hipMemcpyAsync(c->h_flags + 1, &ctl->done, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_flags[1]) c->shard_done_seen = true;  // (the loop's later iterations are not enqueued)
+    return c->h_flags[0] != 0 || c->h_flags[1] != 0 ? 1 : 0;
+}
+
 template <typename T>
 int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const double* ratio_dev, SelectState* st,
                     SpecSel* spec = nullptr) {
     // (no state reset: pass 0 starts a fresh select)
     const int passes = select_passes<T>();
+    if (spec && c->spec_exchanged && sharded(c)) {
+        c->spec_exchanged = false;
+        const int r = sharded_window_resolved(c, spec);
+        if (r < 0) return r;
+        if (r == 1) return PMX_OK;  // (the pass kernels would return at spec->hit; no histogram exchange)
+    }
     for (int p = 0; p < passes; ++p) {
         if (sharded(c) || c->select_split) {
             // the histogram is all-reduced between the two halves of a pass
@@ -1598,7 +1648,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
     if (c->search_type == 0 || !c->grid_ready || c->grid_mode == 0)
         return fail(c, PMX_E_BAD_PARAM, "device loop: needs the per-lane grid matcher (searchType 1 or 2)");
-    if (cfg->knn < 1 || cfg->knn > 16) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 16] on the GPU path");
+    if (cfg->knn < 1 || cfg->knn > kMaxKnn) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 256] on the GPU path");
     if (!(cfg->max_dist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
     if (cfg->n_filters < 0 || cfg->n_filters > kMaxChain)
         return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 outlier filters");
@@ -1668,12 +1718,14 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     if (c->spec_on) {
         if (!c->d_spec) {
             HIPCHK(c, hipMalloc((void**)&c->d_spec, sizeof(SpecSel)));
-            HIPCHK(c, hipMalloc(&c->d_spec_keys, sizeof(unsigned long long) * kSpecCap));
+            // keys, then the fused path's records (pmx_post.hip)
+            HIPCHK(c, hipMalloc(&c->d_spec_keys, 2 * sizeof(unsigned long long) * kSpecCap));
         }
         if (sharded(c) && !c->d_specx)
             HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * (c->nranks + 1)));
         SpecSel init{};
         init.keys = c->d_spec_keys;
+        init.recs = (unsigned long long*)c->d_spec_keys + kSpecCap;
         init.ratio = (double)(T)(k0 == PMX_FILTER_TRIMMED ? cfg->filter_p[0][0] : 0.5);
         c->spec_init = init;
         HIPCHK(c, hipMemcpyAsync(c->d_spec, &c->spec_init, sizeof(SpecSel), hipMemcpyHostToDevice, c->stream));
@@ -1683,6 +1735,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     c->loop_issued = 0;
     c->loop_iters = 0;
     c->loop_done = false;
+    c->shard_done_seen = false;
     c->loop_begun = true;
     return PMX_OK;
 }
@@ -1706,10 +1759,136 @@ int loop_trace_room(pmx_ctx* c, int64_t iters) {
     return PMX_OK;
 }
 
+// The fused iteration (pmx_post.hip): point-to-plane on one rank, an outlier
+// chain of TrimmedDist at position 0 (with the quantile window) and / or the
+// fixed predicates (default / Null / MaxDist / MinDist).  1: fused with the
+// quantile, 2: fused without one, 0: the module sequence.
+constexpr int64_t kSelxPost = -2;  // selx_grid: the state belongs to the post launches
+int fused_kind(const pmx_ctx* c) {
+    const pmx_loop_cfg& cfg = c->loop_cfg;
+    if (!c->fuse_allowed || sharded(c) || cfg.minimizer != 0 || !c->has_normals || c->grid_mode < 1 ||
+        c->search_type == 0 || !c->grid_ready || (c->dim != 3 && c->dim != 2) || cfg.knn > kLaneMaxK)
+        return 0;
+    int q = 0;
+    for (int i = 0; i < cfg.n_filters; ++i) {
+        const int k = cfg.filter_kind[i];
+        if (k == PMX_FILTER_TRIMMED && i == 0 && c->spec_on) {
+            q = 1;
+            continue;
+        }
+        if (k == PMX_FILTER_NULL || k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST ||
+            (k == PMX_FILTER_DEFAULT && i == 0))
+            continue;
+        return 0;
+    }
+    return q ? 1 : 2;
+}
+
+template <typename T>
+int loop_enqueue_fused(pmx_ctx* c, int kind) {
+    const pmx_loop_cfg& cfg = c->loop_cfg;
+    const int64_t fblocks = (c->N + 255) / 256;
+    if (c->fuse_cap < fblocks) {
+        if (c->d_fuse_part) (void)hipFree(c->d_fuse_part);
+        c->d_fuse_part = nullptr;
+        c->fuse_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_fuse_part, sizeof(double) * (size_t)fblocks * kFuseNV));
+        c->fuse_cap = fblocks;
+    }
+    // the chain as the filter calls would record it (no launch: the post
+    // launch resolves the quantile)
+    c->chain_n = 0;
+    c->rb_pos = -1;
+    for (int i = 0; i < cfg.n_filters; ++i) {
+        const int k = cfg.filter_kind[i];
+        const double p0 = cfg.filter_p[i][0];
+        if (k == PMX_FILTER_TRIMMED) {
+            chain_set(c, i, kWPState, 1.0);
+        } else if (k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST) {
+            const T m = (T)p0;
+            chain_set(c, i, k == PMX_FILTER_MAXDIST ? kWPLe : kWPGe, (double)(T)std::pow((double)m, 2.0));
+        } else {
+            chain_set(c, i, k == PMX_FILTER_NULL ? kWPNull : kWPDefault, 0.0);
+        }
+    }
+    // the predicates after the quantile as one interval (chain_resolve's rule)
+    FuseAcc<T> fa;
+    fa.on = 1;
+    fa.quantile = kind == 1;
+    fa.dim = c->dim;
+    fa.partials = c->d_fuse_part;
+    double lo = -INFINITY, hi = INFINITY;
+    int fin = cfg.n_filters == 0 ? 1 : 0;
+    for (int i = fa.quantile ? 1 : 0; i < c->chain_n; ++i) {
+        const int t = c->chain_type[i];
+        const double v = (double)(T)c->chain_thr[i];
+        if (t == kWPDefault) fin = 1;
+        if (t == kWPGe) lo = (std::isnan(v) || std::isnan(lo)) ? v + lo : std::max(v, lo);
+        if (t == kWPLe) hi = (std::isnan(v) || std::isnan(hi)) ? v + hi : std::min(v, hi);
+    }
+    fa.fx_lo = (T)lo;
+    fa.fx_hi = (T)hi;
+    fa.fx_finite = fin;
+    T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
+    for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
+    int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr, &fa);
+    if (rc) return rc;
+    // (match_impl reset the chain: record it again for the mirrors)
+    for (int i = 0; i < cfg.n_filters; ++i) {
+        const int k = cfg.filter_kind[i];
+        if (k == PMX_FILTER_TRIMMED) {
+            chain_set(c, i, kWPState, 1.0);
+        } else if (k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST) {
+            const T m = (T)cfg.filter_p[i][0];
+            chain_set(c, i, k == PMX_FILTER_MAXDIST ? kWPLe : kWPGe, (double)(T)std::pow((double)m, 2.0));
+        } else {
+            chain_set(c, i, k == PMX_FILTER_NULL ? kWPNull : kWPDefault, 0.0);
+        }
+    }
+    if (fa.quantile && c->selx_grid != kSelxPost) {
+        // (the arrival generations assume one grid per launch kind: start the shared state afresh)
+        HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
+        c->selx_grid = kSelxPost;
+    }
+    PostLaunch<T> p;
+    p.d = (const T*)c->d_dists;
+    p.ids = c->d_ids;
+    p.rd = (const P4<T>*)c->d_rd;
+    p.N = c->N;
+    p.k = cfg.knn;
+    p.ctl = c->d_ctl;
+    p.gd = (const GridDesc<T>*)c->d_gdesc;
+    p.quantile = fa.quantile;
+    p.ratio = fa.quantile ? cfg.filter_p[0][0] : 0.0;
+    p.selx = c->d_selx;
+    p.st = c->sel_slot(0);
+    p.spec = c->spec_now();
+    p.iter_err = c->d_iter_err;
+    p.vpart = c->d_vpart;
+    p.vout = c->d_visited;
+    p.fuse_part = c->d_fuse_part;
+    p.fuse_blocks = (int)fblocks;
+    p.part2 = c->d_partials;
+    p.chain = chain_of<T>(c);
+    p.res_out = c->d_result;
+    p.S = (LoopState<T>*)c->d_loop;
+    p.cfg = c->loop_dev;
+    p.trace = cfg.keep_trace ? (T*)c->d_trace : nullptr;
+    p.cu_count = c->cu_count;
+    launch_post<T>(p, c->stream);
+    launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
+                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, nullptr,
+                        kRedBlocks, 0, c->d_result, c->stream);
+    HIPCHK(c, hipGetLastError());
+    return PMX_OK;
+}
+
 // one ICP iteration, device-driven (transform and level from LoopCtl)
 template <typename T>
 int loop_enqueue_iteration(pmx_ctx* c) {
     const pmx_loop_cfg& cfg = c->loop_cfg;
+    if (c->shard_done_seen) return PMX_OK;  // (every rank stops enqueuing at the same iteration)
+    if (const int fk = c->N > 0 ? fused_kind(c) : 0) return loop_enqueue_fused<T>(c, fk);
     T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
     for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
     int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr);
@@ -2191,6 +2370,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_DEFER_COUNTER")) c->defer_counter = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_SELECT_P2PLANE")) c->select_p2 = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_SELECT_ALL")) c->select_all = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_FUSED")) c->fuse_allowed = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
     if (const char* e = std::getenv("PMX_GRID_LEVELS")) {
@@ -2235,6 +2415,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
         preload_normals();
         preload_setup();
         preload_ssn();
+        preload_post();
         preloaded = true;
     }
     // One small "iteration block" holds everything the host reads back per
@@ -2295,7 +2476,9 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->h_flags) (void)hipHostFree(c->h_flags);
     if (c->d_specx) (void)hipFree(c->d_specx);
+    if (c->d_fuse_part) (void)hipFree(c->d_fuse_part);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PMX_OK;
@@ -2332,6 +2515,13 @@ int pmx_comm_init_host(pmx_ctx* c, int nranks, int rank, pmx_allreduce_fn allred
     c->host_user = user;
     c->nranks = nranks;
     c->rank = rank;
+    return PMX_OK;
+}
+
+int pmx_comm_stats(const pmx_ctx* c, uint64_t* allreduces, uint64_t* allgathers) {
+    if (!c || !allreduces || !allgathers) return PMX_E_BAD_PARAM;
+    *allreduces = c->n_allreduce;
+    *allgathers = c->n_allgather;
     return PMX_OK;
 }
 

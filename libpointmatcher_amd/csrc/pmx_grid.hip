@@ -43,6 +43,7 @@
 // per-lane search from LDS (broadcast reads) and measures 0.187 ms at C3: a
 // candidate for QPT > 1 and for very dense references.
 #include "pmx_internal.h"
+#include "pmx_p2plane.h"
 #include "pmx_spec.h"
 
 namespace pmx {
@@ -816,6 +817,75 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
 // ------------------------------------------------- LDS box full searches --
 #include "pmx_grid_box.inc"
 
+// ------------------------------------------------- fused point-to-plane --
+// The point-to-plane sums of one slot's pairs, after the match has written
+// them (pmx_post.hip has the rest of the scheme): the pairs the block can
+// decide are added to the lane's fp64 accumulators (the same T products as
+// p2plane_body, PointToPlane.cpp:194-243), the quantile window's are
+// recorded for the pick.  With TrimmedDist at chain position 0 a pair whose
+// key is below the window is kept once the window resolves the limit (every
+// kept pair: d <= limit with limit inside the window) and a pair above it is
+// not; without a quantile every pair is decided here.  Counters: kept,
+// non-zero weights (no quantile: inf distances may pass the predicates),
+// finite distances, points with a kept pair.
+// (all lanes of the wave call it; act = the lane holds a slot).  The lane's
+// pairs go into its accumulators (this pass only: no array stays live across
+// the searches), then one transposed wave sum adds them to the wave's LDS row.
+template <typename T, int DIM>
+__device__ __forceinline__ void fuse_chunk(const FuseAcc<T>& fa, SpecAcc<T>& sa, unsigned long long* __restrict__ recs,
+                                           const P4<T>* __restrict__ gpn, const P4<T>* __restrict__ rd,
+                                           const Mat4<T>& Tm, const T* __restrict__ out_d,
+                                           const int32_t* __restrict__ out_i, int64_t j, bool act, int k,
+                                           double* __restrict__ wrow) {
+    using KO = KeyOf<T>;
+    constexpr int NSF = DIM == 3 ? 27 : 9;
+    double acc[kFuseNV];
+#pragma unroll
+    for (int v = 0; v < kFuseNV; ++v) acc[v] = 0.0;
+    if (act) {
+        const T inf = (T)__builtin_huge_val();
+        T px, py, pz;
+        gxform(Tm, gld(rd, j), px, py, pz);
+        bool point_kept = false, appended = false;
+        for (int s = 0; s < k; ++s) {
+            const T d = out_d[j * k + s];
+            const int32_t id = out_i[j * k + s];
+            const bool finite = d != inf;
+            const bool fx = (!fa.fx_finite || finite) && d >= fa.fx_lo && d <= fa.fx_hi;
+            if (finite) acc[NSF + 2] += 1.0;
+            bool keep;
+            if (fa.quantile) {
+                keep = false;
+                if (finite) {
+                    const bool below = KO::key(d) < (typename KO::K)sa.lo;
+                    const unsigned pos = spec_acc<T>(sa, d);
+                    if (pos < kSpecCap) {  // inside the window: decided by the pick
+                        const bool head = fx && !point_kept && !appended;
+                        recs[pos] = (unsigned long long)j << 32 | (fx ? kRecFx : 0ull) | (head ? kRecHead : 0ull) |
+                                    ((unsigned long long)id & kRecPos);
+                        appended = appended || fx;
+                    } else {
+                        keep = below && fx;
+                    }
+                }
+            } else {
+                if (fx) acc[NSF + 1] += 1.0;  // (w != 0).count(): may include an infinite distance
+                keep = fx && finite;
+            }
+            if (keep) {
+                acc[NSF] += 1.0;
+                point_kept = true;
+                p2plane_add<T, DIM, kFuseNV>(acc, px, py, pz, gld(gpn, 2 * (int64_t)id),
+                                             gld(gpn, 2 * (int64_t)id + 1));
+            }
+        }
+        if (point_kept) acc[NSF + 3] += 1.0;
+    }
+    int idx;
+    const double w = wave_transpose_sum<kFuseNV>(acc, idx);
+    if (transpose_writer<kFuseNV>()) wrow[idx] += w;
+}
+
 // ------------------------------------------------------- per-lane kernel --
 // occupancy hint of the per-lane kernel (waves per SIMD; 0 = the compiler's
 // choice).  The search is bound by dependent gather latency, so more resident
@@ -835,8 +905,10 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
 // BOX: the instance with the LDS box path (launched with dynamic LDS while
 // many queries need a full search); the plain instance keeps the reuse
 // path's registers and occupancy
-template <typename T, int KT, bool BOX>
-__global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T>* __restrict__ gpts,
+// FUSE: the fused point-to-plane instance (pmx_post.hip): every block
+// writes one record of sums
+template <typename T, int KT, bool BOX, bool FUSE>
+__global__ __launch_bounds__(256, 4) PMX_LANE_ATTR void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
@@ -849,8 +921,9 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
                                                         int* __restrict__ iter_err, SelectState* __restrict__ spec_st,
                                                         unsigned long long* __restrict__ xseg,
                                                         const T* __restrict__ radii, uint32_t box_bytes,
-                                                        int box_grow) {
+                                                        int box_grow, FuseAcc<T> fa) {
     extern __shared__ __attribute__((aligned(16))) char box_lds[];  // (box_bytes: the launch's dynamic LDS)
+    const P4<T>* gpn = nullptr;  // (fused: the level's point / normal records)
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -858,6 +931,7 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
         gidx = D.gidx;
         start = D.start;
         G = D.G;
+        gpn = D.gpn;
         ctl_transform(ctl, Tm);
         if (reuse) {
             reuse = ctl->prev_level == ctl->level ? 2 : 1;
@@ -873,8 +947,17 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
     const int64_t blk = blockIdx.x;
 #endif
     // quantile window (pmx_spec.h): every written distance is classified
+    // (fused: by the fused pass, which also records the window's pairs)
     SpecAcc<T> sa;
     spec_acc_init<T>(sa, spec);
+    SpecAcc<T> sw = sa;  // (the writers' view: off when the fused pass classifies)
+    if (FUSE) sw.on = false;
+    // fused: the window's pairs are recorded only while the window is valid
+    // (no window: the post launch reduces every pair itself)
+    const bool fuse_on = FUSE && (!fa.quantile || sa.on);
+    __shared__ double wacc[4 * kFuseNV];
+    if (FUSE)
+        for (int v = threadIdx.x; v < 4 * kFuseNV; v += blockDim.x) wacc[v] = 0.0;
     // Phase 1: every lane tries the certificate (reuse 2; otherwise every
     // query misses).  Phase 2: the block's misses, compacted in slot order,
     // run the full search on consecutive lanes — from an LDS box of the grid
@@ -884,39 +967,63 @@ __global__ __launch_bounds__(256) PMX_LANE_ATTR void grid_lane_kernel(const P4<T
     __shared__ int miss[256];
     __shared__ int wave_cnt[4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t j = blk * blockDim.x + threadIdx.x;
-    bool missed = j < N;
-    if (reuse == 2 && j < N) {
-        const P4<T> p = gld(rd, j);
-        T qx, qy, qz;
-        gxform(Tm, p, qx, qy, qz);
-        missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, qr2(radii, j, maxR2), out_d, out_i, safe,
-                                     visits, sa);
-    }
-    const unsigned long long m = __ballot(missed);
-    if (lane == 0) wave_cnt[wave] = __popcll(m);
-    __syncthreads();
-    int off = 0, total = 0;
+    unsigned long long full_total = 0;
+    {
+        const int64_t base = blk * 256;
+        const int64_t j = base + threadIdx.x;
+        bool missed = j < N;
+        if (reuse == 2 && j < N) {
+            const P4<T> p = gld(rd, j);
+            T qx, qy, qz;
+            gxform(Tm, p, qx, qy, qz);
+            missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, qr2(radii, j, maxR2), out_d, out_i,
+                                         safe, visits, sw);
+        }
+        const unsigned long long m = __ballot(missed);
+        if (lane == 0) wave_cnt[wave] = __popcll(m);
+        __syncthreads();
+        int off = 0, total = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int cw = wave_cnt[w];
-        off += w < wave ? cw : 0;
-        total += cw;
-    }
-    if (missed) miss[off + __popcll(m & ((1ull << lane) - 1))] = threadIdx.x;
-    __syncthreads();
-    if (BOX && total >= kBoxMinMiss && !oct) {
-        box_phase<T, KT>(gpts, gidx, start, G, rd, blk * blockDim.x, miss, total, Tm, k, maxR2, radii, out_d, out_i,
-                         safe, visits, sa, box_lds, box_bytes, reuse == 2 ? -1 : box_grow, reuse, Tprev);
-    } else if ((int)threadIdx.x < total) {
-        const int64_t j2 = blk * blockDim.x + miss[threadIdx.x];
-        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
-                          sa);
+        for (int w = 0; w < 4; ++w) {
+            const int cw = wave_cnt[w];
+            off += w < wave ? cw : 0;
+            total += cw;
+        }
+        if (missed) miss[off + __popcll(m & ((1ull << lane) - 1))] = threadIdx.x;
+        __syncthreads();
+        if (BOX && total >= kBoxMinMiss && !oct) {
+            box_phase<T, KT>(gpts, gidx, start, G, rd, base, miss, total, Tm, k, maxR2, radii, out_d, out_i, safe,
+                             visits, sw, box_lds, box_bytes, reuse == 2 ? -1 : box_grow, reuse, Tprev);
+        } else if ((int)threadIdx.x < total) {
+            const int64_t j2 = base + miss[threadIdx.x];
+            full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe,
+                              visits, sw);
+        }
+        full_total += (unsigned long long)total;
+        if (FUSE) {
+            __syncthreads();  // (the misses' outputs were written by other lanes of the block)
+            if (fuse_on) {
+                unsigned long long* recs = spec ? spec->recs : nullptr;
+                double* wrow = wacc + wave * kFuseNV;
+                if (fa.dim == 3)
+                    fuse_chunk<T, 3>(fa, sa, recs, gpn, rd, Tm, out_d, out_i, j, j < N, k, wrow);
+                else
+                    fuse_chunk<T, 2>(fa, sa, recs, gpn, rd, Tm, out_d, out_i, j, j < N, k, wrow);
+            }
+        }
     }
     add_visits(visits, visited);
     // queries that took the full search (the "fallback" counter the level choice reads)
-    if (threadIdx.x == 0 && visited && total && reuse) atomicAdd(vslot(visited, 1), (unsigned long long)total);
-    if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
+    if (threadIdx.x == 0 && visited && full_total && reuse) atomicAdd(vslot(visited, 1), full_total);
+    if (sa.on) spec_acc_flush<T>(FUSE ? sa : sw, vslot(visited, 2), vslot(visited, 3));
+    if (FUSE) {
+        __syncthreads();  // (every wave's rows)
+        // the block's record, block-major (the post launch sums the records in block order)
+        if (threadIdx.x < kFuseNV)
+            fa.partials[(int64_t)blockIdx.x * kFuseNV + threadIdx.x] =
+                ((wacc[threadIdx.x] + wacc[kFuseNV + threadIdx.x]) + wacc[2 * kFuseNV + threadIdx.x]) +
+                wacc[3 * kFuseNV + threadIdx.x];
+    }
     if (vout) counter_fold<T>(visited, vout, iter_err, spec, spec_st, xseg);
 }
 
@@ -929,20 +1036,29 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                       unsigned long long* vout, int* iter_err, SelectState* spec_st, unsigned long long* xseg,
-                      const T* radii, uint32_t box_bytes, int box_grow, bool cold, hipStream_t s) {
+                      const T* radii, uint32_t box_bytes, int box_grow, bool cold, const FuseAcc<T>& fa,
+                      hipStream_t s) {
     if (cold) {  // a new reading's first match without an LDS box: the tile kernel's cold form (pmx_grid_tile.inc)
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
                            G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
                            ctl, gd, spec, ru.safe);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
-#define PMX_LANE(B)                                                                                                  \
-    hipLaunchKernelGGL((grid_lane_kernel<T, KT, B>), dim3((unsigned)((N + 255) / 256)), dim3(256), box_bytes, s, gpts, \
-                       gidx, start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, \
-                       ru.Tprev, ctl, gd, spec, vout, iter_err, spec_st, xseg, radii, box_bytes, box_grow)
-        if (box_bytes > 0)
-            PMX_LANE(true);
-        else
-            PMX_LANE(false);
+        const int64_t grid = (N + 255) / 256;
+#define PMX_LANE(B, F)                                                                                                 \
+    hipLaunchKernelGGL((grid_lane_kernel<T, KT, B, F>), dim3((unsigned)grid), dim3(256), box_bytes, s, gpts, gidx, start, \
+                       G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev, ctl, \
+                       gd, spec, vout, iter_err, spec_st, xseg, radii, box_bytes, box_grow, fa)
+        if (box_bytes > 0) {
+            if (fa.on)
+                PMX_LANE(true, true);
+            else
+                PMX_LANE(true, false);
+        } else {
+            if (fa.on)
+                PMX_LANE(false, true);
+            else
+                PMX_LANE(false, false);
+        }
 #undef PMX_LANE
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
@@ -959,7 +1075,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                        SelectState* spec_st, unsigned long long* xseg, bool fold, bool defer, const T* radii,
-                       uint32_t box_bytes, int box_grow, bool cold, hipEvent_t ev_end, hipStream_t s) {
+                       uint32_t box_bytes, int box_grow, bool cold, const FuseAcc<T>& fa, hipEvent_t ev_end,
+                       hipStream_t s) {
     if (N <= 0) return;
     if (mode < 1) box_bytes = 0;
     cold = cold && mode >= 1 && box_bytes == 0;
@@ -972,10 +1089,19 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     }
     G.h = h;
     G.inv_h = 1.0 / h;
+    if (knn > kLaneMaxK) {  // a k-list spread over a wave per query (pmx_knn_wide.hip; no reuse, no fused sums)
+        launch_knn_wide<T>(gpts, gidx, start, &G, 0, rd, N, Tm, knn, maxR2, radii, dists, ids, visited, ctl, gd, spec,
+                           s);
+        if (ev_end) (void)hipEventRecord(ev_end, s);
+        if (visited && vout && !defer)
+            hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
+                               spec_st, xseg);
+        return;
+    }
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
                      ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, box_bytes, box_grow, cold, \
-                     s)
+                     fa, s)
     // with reuse the list keeps room for the (k+1)-th point (the safe radius;
     // the cold tile writes radius 0 and keeps k entries)
     const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
@@ -993,7 +1119,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel, with the folded counter phase)
     // (folded: the per-lane kernel's last workgroup ran it; deferred: the
     // select_all launch that follows runs it, pmx_select.hip)
-    if (visited && vout && !fold && !defer)
+    if (visited && vout && !fold && !defer && !fa.on)
         hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
                            spec_st, xseg);
 }
@@ -1004,14 +1130,14 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
                                        unsigned long long*, bool, bool, const float*, uint32_t, int, bool,
-                                       hipEvent_t, hipStream_t);
+                                       const FuseAcc<float>&, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
                                         unsigned long long*, bool, bool, const double*, uint32_t, int, bool,
-                                        hipEvent_t, hipStream_t);
+                                        const FuseAcc<double>&, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,
@@ -1036,7 +1162,7 @@ void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, 
 // first ICP iteration.
 void preload_grid() {
     hipFuncAttributes a;
-    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1, false>));
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1, false, false>));
 }
 
 }  // namespace pmx

@@ -162,11 +162,44 @@ struct GridReuse {
     T* safe = nullptr;
     Mat4<T> Tprev{};
 };
+// ---- the point-to-plane sums fused into the match (pmx_post.hip) ----
+// Per match block one record of kFuseNV doubles (block-major): the system
+// (NS + NF sums of T products, PointToPlane.cpp:194-243) of the pairs the
+// block could decide, then kept pairs, non-zero weights, finite distances and
+// points with a kept pair.  With TrimmedDist at chain position 0 the pairs
+// whose key lies below the quantile window are the decided ones (kept once
+// the window resolves the limit); the window's own pairs are recorded
+// (SpecSel::recs) and added after the pick.
+constexpr int kFuseNV = 32;
+template <typename T>
+struct FuseAcc {
+    int on = 0;
+    int quantile = 0;           // chain position 0 is TrimmedDist (window decided)
+    int dim = 3;
+    T fx_lo = 0, fx_hi = 0;     // the other predicates as one interval (chain_resolve's form)
+    int fx_finite = 0;
+    double* partials = nullptr; // [match blocks][kFuseNV]
+};
+// result offsets of the fused record (NSF = NS + NF)
+__host__ __device__ constexpr int fuse_nsf(int dim) { return dim == 3 ? 27 : 9; }
+
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) Tm.m[i] = (T)ctl->T[i];
 }
+
+// k-NN for k > kLaneMaxK (pmx_knn_wide.hip): one wave per query, the k-list
+// spread over the wave.  start == null: brute force over pts[0, M) (ids are
+// indices); otherwise a grid level (ids are positions), G its geometry.
+constexpr int kLaneMaxK = 16;   // the per-lane searches' largest k-list
+constexpr int kMaxKnn = 256;    // the wide search's
+template <typename T>
+void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* start, const GridGeom* G, int64_t M,
+                     const P4<T>* rd, int64_t N, const Mat4<T>& Tm, int k, T maxR2, const T* radii, T* out_d,
+                     int32_t* out_i, unsigned long long* visited, const LoopCtl* ctl, const GridDesc<T>* gd,
+                     SpecSel* spec, hipStream_t s);
+
 
 // ---- grid match (pmx_grid.hip) ----
 // mode 0 = wave-cooperative LDS tiles, 1 = per-lane shell search (default),
@@ -182,7 +215,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
                        unsigned long long* xseg, bool fold, bool defer, const T* radii, uint32_t box_bytes,
-                       int box_grow, bool cold, hipEvent_t ev_end, hipStream_t s);
+                       int box_grow, bool cold, const FuseAcc<T>& fa, hipEvent_t ev_end, hipStream_t s);
 template <typename T>
 void launch_counter_sum(unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
                         SpecSel* spec, SelectState* st, hipStream_t s);

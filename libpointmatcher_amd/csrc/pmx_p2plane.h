@@ -20,21 +20,70 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// The wave sums of V per-lane values (V a power of two, <= 64) by a
+// butterfly that halves the values at every step: V - 1 + log2(64 / V)
+// shuffles instead of V * 6 for V separate wave_sums.  On return lane L holds
+// the sum of value idx = (L >> log2(64 / V)) ... in a fixed order (every
+// lane of a group of 64 / V lanes holds the same sum); deterministic.
+template <int V>
+__device__ __forceinline__ double wave_transpose_sum(double (&v)[V], int& idx) {
+    static_assert(V >= 1 && V <= 64 && (V & (V - 1)) == 0, "power of two <= 64");
+    const int lane = threadIdx.x & 63;
+    idx = 0;
+    int d = 32;
+#pragma unroll
+    for (int h = V / 2; h >= 1; h >>= 1, d >>= 1) {
+        const bool up = (lane & d) != 0;
+        // (the halves are exchanged with bit masks: a select between two
+        // elements would become a dynamically indexed load of the array,
+        // which moves the whole array to scratch)
+        const long long m = up ? -1ll : 0ll;
+#pragma unroll
+        for (int i = 0; i < h; ++i) {
+            const long long a = __double_as_longlong(v[i]), b = __double_as_longlong(v[i + h]);
+            const double send = __longlong_as_double((a & m) | (b & ~m));
+            const double keep = __longlong_as_double((b & m) | (a & ~m));
+            v[i] = keep + __shfl_xor(send, d);
+        }
+        idx += up ? h : 0;
+    }
+    double s = v[0];
+#pragma unroll
+    for (; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    return s;
+}
+// the lane that writes value idx of a wave_transpose_sum<V>
+template <int V>
+__device__ __forceinline__ bool transpose_writer() {
+    return ((threadIdx.x & 63) & (64 / V - 1)) == 0;
+}
+
 // block reduction of NV accumulators; writes partials[v * gridDim.x + blockIdx.x]
 // (value-major: the finalize reads each value's block partials contiguously)
-template <int NV>
+// kCoherent: agent-scope atomic stores (another block of the same launch sums
+// the partials: pmx_post.hip's last-block finalize)
+template <int NV, bool kCoherent = false>
 __device__ __forceinline__ void block_store(double (&acc)[NV], double* __restrict__ partials) {
-    __shared__ double red[4][NV];
-    const int lane = threadIdx.x & 63;
+    // (the power of two the transposed wave sum takes)
+    constexpr int V = NV <= 8 ? 8 : NV <= 16 ? 16 : NV <= 32 ? 32 : 64;
+    static_assert(NV <= 64, "block_store: at most 64 values");
+    __shared__ double red[4][V];
     const int wave = threadIdx.x >> 6;
+    double x[V];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double s = wave_sum(acc[v]);
-        if (lane == 0) red[wave][v] = s;
-    }
+    for (int v = 0; v < V; ++v) x[v] = v < NV ? acc[v] : 0.0;
+    int idx;
+    const double s = wave_transpose_sum<V>(x, idx);
+    if (transpose_writer<V>()) red[wave][idx] = s;
     __syncthreads();
-    for (int v = threadIdx.x; v < NV; v += blockDim.x)
-        partials[(int64_t)v * gridDim.x + blockIdx.x] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+    for (int v = threadIdx.x; v < NV; v += blockDim.x) {
+        const double r = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+        double* dst = &partials[(int64_t)v * gridDim.x + blockIdx.x];
+        if (kCoherent)
+            __hip_atomic_store(dst, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            *dst = r;
+    }
 }
 
 // one kept pair: F and dot in T exactly as PointToPlane.cpp:171-243, the
@@ -78,7 +127,7 @@ __device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz,
 #ifndef PMX_P2P_XCD
 #define PMX_P2P_XCD 1
 #endif
-template <typename T, int DIM>
+template <typename T, int DIM, bool kCoherent = false>
 __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const Mat4<T>& Tm,
                                              const P4<T>* __restrict__ ref, const P4<T>* __restrict__ nrm, int rs,
                                              const T* __restrict__ d, const int32_t* __restrict__ ids,
@@ -166,7 +215,7 @@ __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const
         }
         if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
     }
-    block_store<NV>(acc, partials);
+    block_store<NV, kCoherent>(acc, partials);
 }
 
 }  // namespace pmx

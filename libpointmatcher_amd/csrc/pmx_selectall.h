@@ -81,6 +81,9 @@ struct SelX {
     unsigned long long count;                // finite keys (pass 0)
     unsigned long long pre;                  // gen << 56 | window hit: the deferred counter phase's verdict
     unsigned long long lim;                  // the resolved limit (double bits), for a fused point-to-plane
+    unsigned int post_arrive;                // the fused post launch's reduction tickets (pmx_post.hip; monotonic)
+    unsigned int pad_;
+    unsigned long long nused;                // the window pick's key count, published with a hit verdict
 };
 
 __device__ __forceinline__ unsigned long long ald(unsigned long long* p) {
@@ -123,8 +126,10 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
             __syncthreads();
             if (threadIdx.x == 0) {
                 const unsigned long long hit = spec && spec->hit ? 1ull : 0ull;
-                // the limit first (write-through), then the verdict that covers it
-                const unsigned long long r0 = hit ? ast(&sx->lim, (unsigned long long)__double_as_longlong(st->limit)) : 0ull;
+                // the limit and the window's key count first (returning: performed
+                // where every block reads them), then the verdict that covers them
+                unsigned long long r0 = hit ? ast(&sx->lim, (unsigned long long)__double_as_longlong(st->limit)) : 0ull;
+                r0 |= hit ? ast(&sx->nused, (unsigned long long)spec->n_used) : 0ull;
                 asm volatile("" ::"v"(r0));
                 (void)ast(&sx->pre, pgen << 56 | hit);
                 s_w[0] = hit;
@@ -293,7 +298,7 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
                     st->ratio = (double)q;
                     if (err) {
                         st->limit = __builtin_nan("");
-                        *iter_err = err;
+                        __hip_atomic_store(iter_err, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } else {
                         st->limit = (double)KO::val(np);
                         if (spec) {
@@ -340,7 +345,7 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
                 }
                 s_w[0] = w;
                 s_w[1] = ok ? 1ull : 0ull;
-                if (!ok) *iter_err = kSelTimeout;
+                if (!ok) __hip_atomic_store(iter_err, kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __syncthreads();
             const unsigned long long w = s_w[0];

@@ -79,7 +79,15 @@ struct SpecSel {
     int hit;                    // this iteration's limit came from the window
     unsigned long long n_hit, n_miss;  // statistics (host-readable)
     double dens;                // key density estimate of the last radix select (keys per key unit)
+    // the match's point-to-plane sums fused in (pmx_post.hip): one record per
+    // appended key, slot << 32 | passes-the-other-predicates << 31 | first of
+    // its point << 30 | grid position; n_used = the keys the last pick saw
+    unsigned long long* recs;   // [kSpecCap]
+    unsigned int n_used;
+    int pad_;
 };
+// record fields (see SpecSel::recs)
+constexpr unsigned long long kRecFx = 1ull << 31, kRecHead = 1ull << 30, kRecPos = (1ull << 30) - 1;
 
 // ---- match side: classify every distance the match writes ----
 template <typename T>
@@ -109,21 +117,25 @@ __device__ __forceinline__ void spec_acc_init(SpecAcc<T>& a, SpecSel* sp) {
     a.keys = (K*)sp->keys;
     a.n_keys = &sp->n_keys;
 }
+// classify one written distance; returns its append position inside the
+// window's buffers (kSpecCap or more: not appended)
 template <typename T>
-__device__ __forceinline__ void spec_acc(SpecAcc<T>& a, T d) {
+__device__ __forceinline__ unsigned spec_acc(SpecAcc<T>& a, T d) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     const K k = KO::key(d);
+    unsigned pos = kSpecCap;
     if (k < KO::inf_key) {  // (+inf and NaN excluded; distances are >= +0)
         a.fin += 1;
         if (k < a.lo) {
             a.below += 1;
         } else if (k <= a.hi) {  // rare: a few thousand of k*N
-            const unsigned pos = atomicAdd(a.n_keys, 1u);
+            pos = atomicAdd(a.n_keys, 1u);
             // (write-through: the match kernel's last block reads the keys in the same launch)
             if (pos < kSpecCap) __hip_atomic_store(&a.keys[pos], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    return pos;
 }
 // wave sums into the spread counters (all lanes of the wave call it)
 template <typename T>
@@ -232,6 +244,7 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
         if (t == 0) {
             sp->hit = 0;
             sp->n_miss += 1;
+            sp->n_used = 0;
             sp->n_keys = 0;
         }
         return false;
@@ -298,6 +311,7 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
         st->limit = (double)KO::val(kl);
         sp->hit = 1;
         sp->n_hit += 1;
+        sp->n_used = (unsigned)nk;
         sp->n_keys = 0;
         const double width = (double)(hi - lo) + 1.0;
         spec_update<T>(sp, kl, (double)nk / width);
@@ -348,8 +362,9 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
     for (int c = 0; c < 4; ++c)
         for (int w = 0; w < kVSlots / 64; ++w) sum[c] += red[c][w];
     if (t == 0) {
-        out[0] = sum[0];
-        out[1] = sum[1];
+        // (coherent: the fused post launch may read them from another block)
+        __hip_atomic_store(&out[0], sum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&out[1], sum[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (iter_err) __hip_atomic_store(iter_err, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (coherent: a select may write it in the same launch)
     }
     if (!spec) return;

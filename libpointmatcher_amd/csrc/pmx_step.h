@@ -130,7 +130,7 @@ __device__ __forceinline__ bool well_conditioned(const T* A, const T* L) {
 // MIN: the minimiser (0 point-to-plane, 1 point-to-point) as a template
 // parameter, so each kernel holds one minimiser's dense code (registers).
 template <typename T, int ROWS, int MIN>
-__device__ __noinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
+__device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
                                        const double* __restrict__ res, int e, unsigned long long vis0,
                                        unsigned long long vis1, const T* __restrict__ means, const LoopCfg& cfg,
                                        T* __restrict__ trace) {

@@ -19,6 +19,11 @@ if [[ "$ARGS" == *" quick "* ]]; then
   step bench_quick && timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || { tail -20 gpurun_out/bench_quick.err; exit 1; }
   step bench_driver && timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_driver.json 2> gpurun_out/bench_driver.err || { tail -20 gpurun_out/bench_driver.err; exit 1; }
 fi
+if [[ "$ARGS" == *" ab "* ]]; then
+  for v in ${AB:-PMX_FUSED=1}; do
+    step "bench_ab $v" && env $v timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "gpurun_out/bench_ab_$v.json" 2> gpurun_out/bench_ab.err || { tail -20 gpurun_out/bench_ab.err; exit 1; }
+  done
+fi
 if [[ "$ARGS" == *" bench "* ]]; then
   step bench && timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
   step bench_driver && timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_driver.json 2> gpurun_out/bench_driver.err || { tail -20 gpurun_out/bench_driver.err; exit 1; }

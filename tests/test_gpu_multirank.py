@@ -17,7 +17,8 @@ Bars (against the single-process oracle on the WHOLE reading):
     as all-gathered segments): final T within 1e-5 (f32) / 1e-12 (f64) with
     equal iteration counts and kept pairs, every rank the same T;
   * the sharded window resolves quantiles (hits > 0) and equals the radix
-    path (PMX_SPEC_SELECT=0) bit for bit.
+    path (PMX_SPEC_SELECT=0) bit for bit;
+  * a window hit costs an iteration two collectives (pmx_comm_stats).
 Reference semantics: OutlierFilter.cpp:63-103, Matches.cpp:60-87,
 OutlierFiltersImpl.cpp:132-223, PointToPlane.cpp:171-243, ICP.cpp:317-449.
 """
@@ -118,10 +119,16 @@ def _worker(rank, world, port, outdir, env):
             # the device loop on the context: quantile window exchanged as segments
             ctx.set_reading(shard)
             ctx.loop_begin(filters=[("TrimmedDistOutlierFilter", 0.85)], checkers=[("CounterTransformationChecker", 25)])
+            ar0, ag0 = ctx.comm_stats()
+            cb0 = dict(comm.calls)
             ls = ctx.loop_run(25)
             hits, misses = ctx.loop_select_stats()
+            ar1, ag1 = ctx.comm_stats()
             res[f"{dn}_loop"] = np.concatenate([np.asarray(ls.T_iter[:16]), [ls.iterations, ls.last.kept, hits,
                                                                               misses]])
+            # the collectives of the loop: native counter, and the transport's own count
+            res[f"{dn}_coll"] = np.array([ar1 - ar0, ag1 - ag0, comm.calls["allreduce"] - cb0["allreduce"],
+                                          comm.calls["allgather"] - cb0["allgather"], ls.iterations, hits, misses])
             ctx.close()
             # whole ICPs through the host chain (pmx_icp_comm_init_host)
             for tag, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
@@ -244,12 +251,36 @@ def test_sharded_window_equals_radix(two_ranks, two_ranks_radix, dn):
         np.testing.assert_array_equal(two_ranks[0][k], two_ranks_radix[0][k])
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("dn", ["float32", "float64"])
-def test_rccl_one_rank_is_bit_identical(oracle, dn):
+def test_sharded_hit_iterations_two_collectives(two_ranks, two_ranks_radix, dn):
+    """A window hit costs a sharded iteration two collectives (the segments'
+    all-gather, the system's all-reduce); a miss adds the radix passes'
+    histogram all-reduces.  Counted natively (pmx_comm_stats) and by the
+    transport itself."""
+    passes = 3 if dn == "float32" else 6
+    for r in (two_ranks[0], two_ranks[1]):
+        ar, ag, cb_ar, cb_ag, iters, hits, misses = (int(v) for v in r[f"{dn}_coll"])
+        print(f"{dn}: {iters} iterations, {hits} hits / {misses} misses: {ar} all-reduces, {ag} all-gathers")
+        assert (ar, ag) == (cb_ar, cb_ag)  # every collective the library counts reached the transport
+        assert hits > 0 and hits + misses <= ag
+        # per enqueued iteration: one all-gather + the system's all-reduce, and the passes on a miss
+        assert ar == ag + passes * misses
+        assert ag <= iters + 1
+    # the radix path: every iteration runs the passes
+    ar, ag, _, _, iters, hits, _ = (int(v) for v in two_ranks_radix[0][f"{dn}_coll"])
+    assert hits == 0 and ag == 0 and ar % (1 + passes) == 0 and ar // (1 + passes) >= iters
+
+
+@pytest.mark.parametrize("dn", ["float32", "float64"])
+def test_rccl_one_rank_is_bit_identical(oracle, dn, monkeypatch):
     """A communicator issues every collective (RCCL all-reduce / all-gather of
     the histograms, window segments, distances and systems) even at one rank;
-    the result must equal the unsharded run bit for bit."""
+    the result must equal the unsharded run bit for bit.  (The unsharded loop
+    runs the module chain here: its fused iteration sums in another order.)"""
     from libpointmatcher_amd import _capi
+
+    monkeypatch.setenv("PMX_FUSED", "0")
 
     dtype = np.dtype(dn)
     rd, ref, nrm = _clouds(dtype)
