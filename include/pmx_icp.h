@@ -110,6 +110,27 @@ int pmx_icp_timing_read(pmx_icp* icp, double* match_ms, int64_t* match_launches)
  * radix passes.  Diagnostics only (no reference counterpart). */
 int pmx_icp_select_stats(pmx_icp* icp, uint64_t* window_hits, uint64_t* window_misses);
 
+/* ICPSequence (PointMatcher.h:730-764, ICP.cpp:455-609).  set_map replaces
+ * ICPSequence::setMap: the map is centred on its mean, filtered by the
+ * referenceDataPointsFilters and indexed once; it stays resident on the
+ * device.  accepted = 0 for an empty map (ignored, as the reference).
+ * Descriptors staged with pmx_icp_add_descriptor(cloud = 1) go to the map.
+ * sequence_compute replaces ICPSequence::compute(cloudIn, T_refIn_dataIn)
+ * (T_init may be NULL: identity): the reading against the resident map; with
+ * no map T_out is the identity.  sequence_prepare is its first phase
+ * (prepared = 0 without a map), followed by pmx_icp_iterate / pmx_icp_finish.
+ * get_map: the prefiltered map in global coordinates (ICP.cpp:543-554),
+ * rows x n features, point-major; features NULL returns n only.  A
+ * load_yaml / set_default re-indexes a held map (ICP.cpp:520-539). */
+int pmx_icp_set_map(pmx_icp* icp, const void* map, int rows, int64_t M, const void* normals, int* accepted);
+int pmx_icp_clear_map(pmx_icp* icp);
+int pmx_icp_has_map(const pmx_icp* icp, int* has);
+int pmx_icp_get_map(pmx_icp* icp, void* features, int64_t* n);
+int pmx_icp_sequence_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init,
+                             int* prepared);
+int pmx_icp_sequence_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init,
+                             void* T_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,21 +79,26 @@ PointMatcher<double>::ICP& get<double>(pmx_icp* icp) {
     return *icp->d;
 }
 
+// descriptors staged for `cloud` (0 reading, 1 reference) into c
 template <typename T>
-void prepare_impl(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
-                  const void* nrm, const void* T_init) {
-    auto rd = make_cloud<T>(reading, rows, N, nullptr);
-    auto ref = make_cloud<T>(reference, rows, M, nrm);
-    for (const auto& d : icp->staged) {
-        auto& cl = d.cloud == 0 ? rd : ref;
-        const int64_t n = d.cloud == 0 ? N : M;
-        if ((int64_t)d.v.size() != n * d.span)
+void take_staged(pmx_icp* icp, int cloud, DataPoints<T>& c) {
+    std::vector<pmx_icp::Desc> rest;
+    for (auto& d : icp->staged) {
+        if (d.cloud != cloud) {
+            rest.push_back(std::move(d));
+            continue;
+        }
+        if ((int64_t)d.v.size() != c.n * d.span)
             throw InvalidParameter("descriptor " + d.name + ": " + std::to_string(d.v.size() / std::max(d.span, 1)) +
-                                   " points staged for a cloud of " + std::to_string(n));
+                                   " points staged for a cloud of " + std::to_string(c.n));
         std::vector<T> t(d.v.begin(), d.v.end());
-        cl.addDescriptor(d.name, d.span, t.data());
+        c.addDescriptor(d.name, d.span, t.data());
     }
-    icp->staged.clear();
+    icp->staged = std::move(rest);
+}
+
+template <typename T>
+std::vector<T> init_of(const void* T_init, int rows) {
     std::vector<T> Ti((size_t)rows * rows, (T)0);
     if (T_init) {
         const T* p = static_cast<const T*>(T_init);
@@ -101,7 +106,40 @@ void prepare_impl(pmx_icp* icp, const void* reading, int rows, int64_t N, const 
     } else {
         for (int i = 0; i < rows; ++i) Ti[i * rows + i] = 1;
     }
-    get<T>(icp).prepare(rd, ref, Ti);
+    return Ti;
+}
+
+template <typename T>
+void prepare_impl(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* reference, int64_t M,
+                  const void* nrm, const void* T_init) {
+    auto rd = make_cloud<T>(reading, rows, N, nullptr);
+    auto ref = make_cloud<T>(reference, rows, M, nrm);
+    take_staged<T>(icp, 0, rd);
+    take_staged<T>(icp, 1, ref);
+    get<T>(icp).prepare(rd, ref, init_of<T>(T_init, rows));
+}
+
+template <typename T>
+void set_map_impl(pmx_icp* icp, const void* map, int rows, int64_t M, const void* nrm, int* accepted) {
+    auto c = make_cloud<T>(map, rows, M, nrm);
+    take_staged<T>(icp, 1, c);
+    const bool ok = get<T>(icp).setMap(c);
+    if (accepted) *accepted = ok ? 1 : 0;
+}
+
+template <typename T>
+void get_map_impl(pmx_icp* icp, void* feat, int64_t* n) {
+    const auto g = get<T>(icp).getPrefilteredMap();
+    if (n) *n = g.n;
+    if (feat) std::memcpy(feat, g.features.data(), sizeof(T) * g.features.size());
+}
+
+// 1: prepared (iterate / finish follow), 0: no map (T_out = identity)
+template <typename T>
+int seq_prepare_impl(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init) {
+    auto rd = make_cloud<T>(reading, rows, N, nullptr);
+    take_staged<T>(icp, 0, rd);
+    return get<T>(icp).prepareSequence(rd, init_of<T>(T_init, rows)) ? 1 : 0;
 }
 
 template <typename T>
@@ -230,6 +268,65 @@ int pmx_icp_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, cons
                     const void* nrm, const void* T_init, void* T_out) {
     int rc = pmx_icp_prepare(icp, reading, rows, N, reference, M, nrm, T_init);
     if (rc) return rc;
+    int done = 0;
+    while (!done) {
+        rc = pmx_icp_iterate(icp, 1 << 20, &done);
+        if (rc) return rc;
+    }
+    return pmx_icp_finish(icp, T_out);
+}
+
+int pmx_icp_set_map(pmx_icp* icp, const void* map, int rows, int64_t M, const void* nrm, int* accepted) {
+    if (!icp) return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] {
+        if ((!map && M > 0) || M < 0 || (rows != 3 && rows != 4)) throw InvalidParameter("pmx_icp_set_map: bad arguments");
+        BOTH(icp, set_map_impl<float>(icp, map, rows, M, nrm, accepted),
+             set_map_impl<double>(icp, map, rows, M, nrm, accepted));
+    });
+}
+
+int pmx_icp_clear_map(pmx_icp* icp) {
+    if (!icp) return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] { BOTH(icp, icp->f->clearMap(), icp->d->clearMap()); });
+}
+
+int pmx_icp_has_map(const pmx_icp* icp, int* has) {
+    if (!icp || !has) return PMX_ICP_INVALID_PARAMETER;
+    *has = (icp->dtype == 1 ? icp->d->hasMap() : icp->f->hasMap()) ? 1 : 0;
+    return PMX_ICP_OK;
+}
+
+int pmx_icp_get_map(pmx_icp* icp, void* features, int64_t* n) {
+    if (!icp) return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] { BOTH(icp, get_map_impl<float>(icp, features, n), get_map_impl<double>(icp, features, n)); });
+}
+
+int pmx_icp_sequence_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init, int* prepared) {
+    if (!icp) return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] {
+        if (!reading && N > 0) throw InvalidParameter("pmx_icp_sequence_prepare: null reading");
+        const int p = BOTH(icp, seq_prepare_impl<float>(icp, reading, rows, N, T_init),
+                           seq_prepare_impl<double>(icp, reading, rows, N, T_init));
+        if (prepared) *prepared = p;
+    });
+}
+
+int pmx_icp_sequence_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init,
+                             void* T_out) {
+    if (!icp || !T_out) return PMX_ICP_INVALID_PARAMETER;
+    int prepared = 0;
+    int rc = pmx_icp_sequence_prepare(icp, reading, rows, N, T_init, &prepared);
+    if (rc) return rc;
+    if (!prepared) {  // ICP.cpp:599-604: no map, identity
+        for (int i = 0; i < rows * rows; ++i) {
+            const double v = i % (rows + 1) == 0 ? 1.0 : 0.0;
+            if (icp->dtype == 1)
+                ((double*)T_out)[i] = v;
+            else
+                ((float*)T_out)[i] = (float)v;
+        }
+        return PMX_ICP_OK;
+    }
     int done = 0;
     while (!done) {
         rc = pmx_icp_iterate(icp, 1 << 20, &done);

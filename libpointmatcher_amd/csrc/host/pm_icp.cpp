@@ -1203,6 +1203,7 @@ void PointMatcher<T>::ICP::setDefault() {
     transformationCheckers.push_back(pm.TransformationCheckerRegistrar.create("CounterTransformationChecker"));
     transformationCheckers.push_back(pm.TransformationCheckerRegistrar.create("DifferentialTransformationChecker"));
     inspector = pm.InspectorRegistrar.create("NullInspector");
+    reinitMap();  // ICPSequence::setDefault, ICP.cpp:520-528
 }
 
 template <typename T>
@@ -1237,6 +1238,7 @@ void PointMatcher<T>::ICP::loadFromYaml(const std::string& text) {
     one("inspector", pm.InspectorRegistrar, inspector);
     for (const auto& kv : doc.map)  // ICP.cpp:158-166
         if (!used.count(kv.first)) throw InvalidModuleType("Module type " + kv.first + " does not exist");
+    reinitMap();  // ICPSequence::loadFromYaml, ICP.cpp:530-539
 }
 
 template <typename T>
@@ -1297,15 +1299,22 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     }
     dev.ensure();
     matcher->init(dev, reference);  // ICP.cpp:302
+    mapIndexed_ = false;            // (an ICPSequence map is no longer the device's reference)
     referencePreprocessingDuration = since<T>(t);
     prefilteredReferencePtsCount = M;
+    prepareReading(readingIn, T_init);
+}
 
-    // computeWithTransformedReference, ICP.cpp:317-370
+// computeWithTransformedReference up to the loop, ICP.cpp:317-370
+// (T_refIn_refMean_ and the matcher describe the reference)
+template <typename T>
+void PointMatcher<T>::ICP::prepareReading(const DataPoints& readingIn, const TransformationParameters& T_init) {
+    const int dim = (int)std::lround(std::sqrt((double)T_refIn_refMean_.size()));
     if ((int64_t)T_init.size() != (int64_t)dim * dim)
         throw std::runtime_error("The shape of initial transformation matrix must be NxN. Where N is the number of "
                                  "rows in the read/reference scans.");
     if (readingIn.rows != dim) throw std::runtime_error("reading and reference dimensions differ");
-    t = std::chrono::steady_clock::now();
+    const auto t = std::chrono::steady_clock::now();
     DataPoints reading(readingIn);
     readingDataPointsFilters.init();
     readingDataPointsFilters.apply(reading);
@@ -1338,6 +1347,106 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     readingPreprocessingDuration = since<T>(t);
     prefilteredReadingPtsCount = reading.n;
     t0_ = std::chrono::steady_clock::now();
+}
+
+// ------------------------------------------------------------ ICPSequence --
+template <typename T>
+bool PointMatcher<T>::ICP::setMap(const DataPoints& inputCloud) {
+    // ICP.cpp:464-508
+    if (!matcher) throw std::runtime_error("You must setup a matcher before running ICP");
+    if (!inspector) throw std::runtime_error("You must setup an inspector before running ICP");
+    auto t = std::chrono::steady_clock::now();
+    const int dim = inputCloud.rows;
+    const int64_t ptCount = inputCloud.n;
+    if (ptCount == 0) return false;  // "Ignoring attempt to create a map from an empty cloud"
+    if (dim != 3 && dim != 4) throw std::runtime_error("clouds must be 2-D or 3-D (3 or 4 homogeneous rows)");
+    if (dev.sharded())
+        for (const auto& f : referenceDataPointsFilters)
+            if (f->usesRandState())
+                throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
+                                         "the reading shards of a multi-rank ICP");
+    map_ = inputCloud;
+    // the mean of the map BEFORE the reference filters (ICP.cpp:490-497; ICP::compute
+    // filters first), sequential sums in T as prepare
+    T_map_.assign((size_t)dim * dim, (T)0);
+    for (int i = 0; i < dim; ++i) T_map_[i * dim + i] = 1;
+    for (int r = 0; r < dim - 1; ++r) {
+        T s = 0;
+        for (int64_t j = 0; j < ptCount; ++j) s = s + map_.features[j * dim + r];
+        const T mean = s / (T)ptCount;
+        T_map_[r * dim + dim - 1] = mean;
+        for (int64_t j = 0; j < ptCount; ++j) map_.features[j * dim + r] = map_.features[j * dim + r] - mean;
+    }
+    for (auto& f : referenceDataPointsFilters) f->device = dev.device;
+    referenceDataPointsFilters.init();
+    referenceDataPointsFilters.apply(map_);
+    if (map_.n <= 0) throw ConvergenceError("empty reference");
+    dev.ensure();
+    matcher->init(dev, map_);  // ICP.cpp:503 (the grid stays on the device)
+    mapIndexed_ = true;
+    referencePreprocessingDuration = since<T>(t);  // (SetMapDuration)
+    prefilteredReferencePtsCount = map_.n;
+    return true;
+}
+
+template <typename T>
+void PointMatcher<T>::ICP::clearMap() {
+    map_ = DataPoints();
+    T_map_.clear();
+    mapIndexed_ = false;
+}
+
+template <typename T>
+typename PointMatcher<T>::DataPoints PointMatcher<T>::ICP::getPrefilteredMap() const {
+    DataPoints g(map_);
+    if (hasMap()) {
+        const int dim = map_.rows;
+        for (int r = 0; r < dim - 1; ++r) {
+            const T m = T_map_[r * dim + dim - 1];
+            for (int64_t j = 0; j < g.n; ++j) g.features[j * dim + r] = g.features[j * dim + r] + m;
+        }
+    }
+    return g;
+}
+
+template <typename T>
+void PointMatcher<T>::ICP::reinitMap() {
+    if (!hasMap() || !matcher) return;
+    dev.ensure();
+    matcher->init(dev, map_);
+    mapIndexed_ = true;
+}
+
+template <typename T>
+bool PointMatcher<T>::ICP::prepareSequence(const DataPoints& readingIn, const TransformationParameters& T_init) {
+    if (!hasMap()) return false;  // "Ignoring attempt to perform ICP with an empty map"
+    if (!matcher) throw std::runtime_error("You must setup a matcher before running ICP");
+    if (!errorMinimizer) throw std::runtime_error("You must setup an error minimizer before running ICP");
+    if (!inspector) throw std::runtime_error("You must setup an inspector before running ICP");
+    if (dev.sharded())
+        for (const auto& f : readingDataPointsFilters)
+            if (f->usesRandState())
+                throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
+                                         "the reading shards of a multi-rank ICP");
+    for (auto& f : readingDataPointsFilters) f->device = dev.device;
+    if (!mapIndexed_) reinitMap();  // (a plain compute replaced the device's reference)
+    T_refIn_refMean_ = T_map_;
+    prepareReading(readingIn, T_init);
+    return true;
+}
+
+template <typename T>
+typename PointMatcher<T>::TransformationParameters PointMatcher<T>::ICP::computeSequence(
+    const DataPoints& reading, const TransformationParameters& T_init) {
+    if (!prepareSequence(reading, T_init)) {
+        const int dim = reading.rows;
+        TransformationParameters I((size_t)dim * dim, (T)0);
+        for (int i = 0; i < dim; ++i) I[i * dim + i] = 1;
+        return I;
+    }
+    while (iterate(1 << 30)) {
+    }
+    return finish();
 }
 
 template <typename T>

@@ -209,6 +209,22 @@ struct PointMatcher {
         bool deviceLoop = true;
         TransformationParameters finish();    // T_refIn_refMean * T_iter * T_refMean_dataIn
 
+        // ICPSequence (PointMatcher.h:730-764, ICP.cpp:455-609): a map kept
+        // resident on the device (centred, filtered and indexed once by
+        // setMap); every compute matches a new reading against it.
+        bool setMap(const DataPoints& map);   // ICP.cpp:464-508 (false: empty cloud, ignored)
+        void clearMap();                      // ICP.cpp:512-517
+        bool hasMap() const { return map_.n > 0; }   // ICP.cpp:457-460
+        DataPoints getPrefilteredMap() const;        // ICP.cpp:543-554 (global coordinates)
+        const DataPoints& getPrefilteredInternalMap() const { return map_; }  // ICP.cpp:564-567
+        // ICPSequence::compute (ICP.cpp:595-609): identity without a map
+        TransformationParameters computeSequence(const DataPoints& reading, const TransformationParameters& T_init);
+        // its first phase (then iterate / finish as after prepare); false without a map
+        bool prepareSequence(const DataPoints& reading, const TransformationParameters& T_init);
+        // the map's matcher again after a chain reload (ICPSequence::setDefault /
+        // loadFromYaml, ICP.cpp:520-539)
+        void reinitMap();
+
         // statistics (Inspector::addStat names, ICP.cpp:305-307, 363-365, 432-436)
         int64_t iterationCount = 0;
         bool maxNumIterationsReached = false;
@@ -221,6 +237,10 @@ struct PointMatcher {
       private:
         bool stepModules();                   // ICP.cpp:371-430 through the module calls
         bool loopConfig(pmx_loop_cfg& cfg) const;
+        void prepareReading(const DataPoints& readingIn, const TransformationParameters& T_init);
+        DataPoints map_;                      // the map in <refMean>, filtered (mapPointCloud)
+        TransformationParameters T_map_;      // its T_refIn_refMean
+        bool mapIndexed_ = false;             // the device holds the map (no other reference since)
         int loopMode_ = 0;                    // 0 undecided, 1 device loop, -1 module calls
         int64_t loopIters_ = 0, loopTouched_ = 0;
         int rows_ = 0;

@@ -88,6 +88,13 @@ def lib():
         l.pmx_icp_timing.argtypes = [C.c_void_p, C.c_int]
         l.pmx_icp_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         l.pmx_icp_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        l.pmx_icp_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.POINTER(C.c_int)]
+        l.pmx_icp_clear_map.argtypes = [C.c_void_p]
+        l.pmx_icp_has_map.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        l.pmx_icp_get_map.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
+        l.pmx_icp_sequence_prepare.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
+                                               C.POINTER(C.c_int)]
+        l.pmx_icp_sequence_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p]
         _lib = l
     return _lib
 
@@ -266,3 +273,62 @@ class ICP:
         n = C.c_int64()
         self._chk(self._l.pmx_icp_timing_read(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+
+class ICPSequence(ICP):
+    """PointMatcher<T>::ICPSequence (PointMatcher.h:730-764, ICP.cpp:455-609):
+    the map is centred, filtered and indexed once by set_map and stays on the
+    device; compute(reading, T_init) matches each new reading against it."""
+
+    def set_map(self, cloud, normals=None):
+        """ICPSequence::setMap; False for an empty cloud (ignored)."""
+        m = np.ascontiguousarray(cloud, dtype=self.dtype)
+        nrm = np.ascontiguousarray(normals, dtype=self.dtype) if normals is not None else None
+        ok = C.c_int(0)
+        self._chk(self._l.pmx_icp_set_map(self.h, _p(m), m.shape[1], m.shape[0], _p(nrm), C.byref(ok)))
+        self.rows = m.shape[1]
+        return bool(ok.value)
+
+    def clear_map(self):
+        self._chk(self._l.pmx_icp_clear_map(self.h))
+
+    def has_map(self):
+        h = C.c_int(0)
+        self._chk(self._l.pmx_icp_has_map(self.h, C.byref(h)))
+        return bool(h.value)
+
+    def get_map(self):
+        """The prefiltered map in global coordinates (getPrefilteredMap), (n, rows)."""
+        n = C.c_int64(0)
+        self._chk(self._l.pmx_icp_get_map(self.h, None, C.byref(n)))
+        out = np.zeros((n.value, self.rows or 4), self.dtype)
+        self._chk(self._l.pmx_icp_get_map(self.h, _p(out), C.byref(n)))
+        return out
+
+    def _rd(self, reading, T_init):
+        rd = np.ascontiguousarray(reading, dtype=self.dtype)
+        rows = rd.shape[1]
+        Ti = np.ascontiguousarray(np.eye(rows) if T_init is None else T_init, dtype=self.dtype)
+        self.rows = rows
+        self._keep = (rd, Ti)
+        return rd, Ti, rows
+
+    def compute(self, reading, T_init=None):
+        """ICPSequence::compute(cloudIn, T_refIn_dataIn); identity without a map."""
+        rd, Ti, rows = self._rd(reading, T_init)
+        out = np.zeros((rows, rows), self.dtype)
+        self._chk(self._l.pmx_icp_sequence_compute(self.h, _p(rd), rows, rd.shape[0], _p(Ti), _p(out)))
+        return out
+
+    __call__ = compute
+
+    def prepare(self, reading, T_init=None):
+        """The first phase of compute (then iterate / finish); False without a map."""
+        rd, Ti, rows = self._rd(reading, T_init)
+        ok = C.c_int(0)
+        self._chk(self._l.pmx_icp_sequence_prepare(self.h, _p(rd), rows, rd.shape[0], _p(Ti), C.byref(ok)))
+        return bool(ok.value)
+
+    def compute_with_reference(self, reading, reference, normals=None, T_init=None):
+        """ICP::compute on this object (the map is re-indexed by the next sequence compute)."""
+        return ICP.compute(self, reading, reference, normals, T_init)

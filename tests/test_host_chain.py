@@ -192,3 +192,19 @@ def test_add_descriptor_rejects_bad_arguments():
     assert "bad arguments" in l.pmx_icp_last_error(icp.h).decode()
     icp.add_descriptor("reading", "maxSearchDist", v)  # a well-formed one is staged
     _ = InvalidParameter
+
+
+def test_sequence_without_map_is_identity():
+    """ICPSequence::compute with no map returns the identity and an empty
+    setMap is ignored (ICP.cpp:477-481, 599-604); neither touches the GPU."""
+    from libpointmatcher_amd.icp import ICPSequence
+    from libpointmatcher_amd.synth import reading_cloud
+
+    for dt in (np.float32, np.float64):
+        s = ICPSequence(dt)
+        s.set_default()
+        np.testing.assert_array_equal(s.compute(reading_cloud(50, dt)), np.eye(4, dtype=dt))
+        assert not s.set_map(np.zeros((0, 4), dt))
+        assert not s.has_map()
+        assert not s.prepare(reading_cloud(50, dt))
+        s.close()
