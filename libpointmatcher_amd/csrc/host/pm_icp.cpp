@@ -786,6 +786,50 @@ struct DistDPF : PM<T>::DataPointsFilter {
     }
 };
 
+// DistanceLimitDataPointsFilter (DataPointsFilters/DistanceLimit.cpp:57-128,
+// DistanceLimit.h:57-63): MaxDist (removeInside 0: keep < dist) and MinDist
+// (removeInside 1: keep > dist) in one filter, on coordinate dim or the
+// Euclidean norm against |dist| (dim -1); dim >= D throws.
+template <typename T>
+struct DistanceLimitDPF : PM<T>::DataPointsFilter {
+    typedef Parametrizable P;
+    static Parametrizable::ParametersDoc doc() {
+        return {PDoc("dim", "dimension on which the filter will be applied. x=0, y=1, z=2, radius=-1", "-1", "-1", "2",
+                     &P::Comp<int>),
+                PDoc("dist",
+                     "distance limit of the filter. If dim is set to -1 (radius), the absolute value of dist will be used",
+                     "1", "-inf", "inf", &P::Comp<T>),
+                PDoc("removeInside",
+                     "If set to true (1), remove points before the distance limit; else (0), remove points beyond the "
+                     "distance limit",
+                     "1", "0", "1", &P::Comp<bool>)};
+    }
+    const int dim;
+    const T dist;
+    const bool removeInside;
+    explicit DistanceLimitDPF(const Parametrizable::Parameters& p)
+        : PM<T>::DataPointsFilter("DistanceLimitDataPointsFilter", doc(), p),
+          dim(this->template get<int>("dim")),
+          dist(this->template get<T>("dist")),
+          removeInside(this->template get<bool>("removeInside")) {}
+    void inPlaceFilter(DataPoints<T>& cloud) override {
+        const int D = cloud.rows - 1;
+        if (dim >= D)
+            throw InvalidParameter("DistanceLimitDataPointsFilter: Error, filtering on dimension number " +
+                                   std::to_string(dim) + ", larger than authorized axis id " + std::to_string(D - 1));
+        const T absMaxDist = std::abs(dist);
+        compact_points(cloud, [&](const T* f) {
+            if (dim == -1) {
+                T s = 0;
+                for (int r = 0; r < D; ++r) s += f[r] * f[r];
+                const T norm = std::sqrt(s);
+                return removeInside ? (norm > absMaxDist) : (norm < absMaxDist);
+            }
+            return removeInside ? (f[dim] > dist) : (f[dim] < dist);
+        });
+    }
+};
+
 // RandomSamplingDataPointsFilter (DataPointsFilters/RandomSampling.cpp:55-74,
 // RandomSampling.h:59-62): keep point i when (float)std::rand() /
 // (float)RAND_MAX < prob, one draw per point in order — the same C library
@@ -1111,6 +1155,8 @@ PointMatcher<T>::PointMatcher() {
                                   [](const Ps& p) { return std::make_shared<DistDPF<T, true>>(p); }, true);
     DataPointsFilterRegistrar.reg("MinDistDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<DistDPF<T, false>>(p); }, true);
+    DataPointsFilterRegistrar.reg("DistanceLimitDataPointsFilter",
+                                  [](const Ps& p) { return std::make_shared<DistanceLimitDPF<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("VoxelGridDataPointsFilter",
                                   [](const Ps& p) { return std::make_shared<VoxelGridDPF<T>>(p); }, true);
     DataPointsFilterRegistrar.reg("SamplingSurfaceNormalDataPointsFilter",
@@ -1275,7 +1321,8 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     const int dim = referenceIn.rows;
     if (dim != 3 && dim != 4) throw std::runtime_error("clouds must be 2-D or 3-D (3 or 4 homogeneous rows)");
     if (dev.sharded())  // (every rank filters its own reading shard)
-        for (const DataPointsFilters* chain : {&readingDataPointsFilters, &referenceDataPointsFilters})
+        for (const DataPointsFilters* chain :
+             {&readingDataPointsFilters, &readingStepDataPointsFilters, &referenceDataPointsFilters})
             for (const auto& f : *chain)
                 if (f->usesRandState())
                     throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
@@ -1318,9 +1365,6 @@ void PointMatcher<T>::ICP::prepareReading(const DataPoints& readingIn, const Tra
     DataPoints reading(readingIn);
     readingDataPointsFilters.init();
     readingDataPointsFilters.apply(reading);
-    if (!readingStepDataPointsFilters.empty())
-        throw ConfigurationError("readingStepDataPointsFilters are outside the GPU path (the step reading is never "
-                                 "materialised on the host)");
     // T_refMean_dataIn = T_refIn_refMean^-1 * T_init (the inverse of a pure
     // translation is exact), ICP.cpp:345-346
     TransformationParameters inv((size_t)dim * dim, (T)0);
@@ -1333,6 +1377,29 @@ void PointMatcher<T>::ICP::prepareReading(const DataPoints& readingIn, const Tra
     // transformations.apply(reading, T_refMean_dataIn): done on the device
     dev.check(pmx_set_reading(dev.ctx, reading.features.data(), dim, reading.n, T_refMean_dataIn_.data()));
     matcher->initReading(dev, reading);  // (per-reading matcher inputs: KDTreeVarDistMatcher's radii)
+    // readingStepDataPointsFilters (ICP.cpp:349-350, 373-377): the step
+    // filters see the reading in <refMean> every iteration; keep that copy on
+    // the host (the device's transform, restated: the same separately rounded
+    // terms in the same order) — each iteration filters it and uploads the result
+    stepBase_ = DataPoints();
+    if (!readingStepDataPointsFilters.empty()) {
+        stepBase_ = reading;
+        const int D = dim - 1;
+        for (int64_t j = 0; j < reading.n; ++j) {
+            const T* f = &reading.features[(size_t)j * dim];
+            T* o = &stepBase_.features[(size_t)j * dim];
+            for (int r = 0; r < D; ++r) {
+                const T* m = &T_refMean_dataIn_[(size_t)r * dim];
+                T v = m[0] * f[0];
+                v = v + m[1] * f[1];
+                v = v + (D == 3 ? m[2] * f[2] : (T)0 * (T)0);
+                v = v + m[D] * f[D];
+                o[r] = v;
+            }
+        }
+        for (auto& f : readingStepDataPointsFilters) f->device = dev.device;
+        readingStepDataPointsFilters.init();
+    }
     rows_ = dim;
     T_iter_.assign((size_t)dim * dim, (T)0);
     for (int i = 0; i < dim; ++i) T_iter_[i * dim + i] = 1;
@@ -1428,6 +1495,11 @@ bool PointMatcher<T>::ICP::prepareSequence(const DataPoints& readingIn, const Tr
             if (f->usesRandState())
                 throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
                                          "the reading shards of a multi-rank ICP");
+    if (dev.sharded())
+        for (const auto& f : readingStepDataPointsFilters)
+            if (f->usesRandState())
+                throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
+                                         "the reading shards of a multi-rank ICP");
     for (auto& f : readingDataPointsFilters) f->device = dev.device;
     if (!mapIndexed_) reinitMap();  // (a plain compute replaced the device's reference)
     T_refIn_refMean_ = T_map_;
@@ -1477,7 +1549,8 @@ bool PointMatcher<T>::ICP::iterate(int n) {
     if (loopMode_ == 0) {  // first iterations after prepare: pick the mode
         loopMode_ = -1;
         pmx_loop_cfg cfg;
-        if (deviceLoop && loopConfig(cfg)) {
+        // (step filters re-upload the reading every iteration: module calls)
+        if (deviceLoop && readingStepDataPointsFilters.empty() && loopConfig(cfg)) {
             const int rc = pmx_loop_begin(dev.ctx, &cfg, T_iter_.data());
             if (rc == PMX_OK)
                 loopMode_ = 1;
@@ -1526,6 +1599,14 @@ bool PointMatcher<T>::ICP::stepModules() {
     const int dim = rows_;
     if (std::fabs((T)1 - dense::det_rot(T_iter_.data(), dim)) > (T)0.001)  // TransformationsImpl.cpp:62-63
         throw TransformationError("RigidTransformation: Error, rotation matrix is not orthogonal.");
+    if (!readingStepDataPointsFilters.empty()) {  // ICP.cpp:373-377
+        DataPoints stepReading(stepBase_);
+        readingStepDataPointsFilters.apply(stepReading);
+        TransformationParameters I((size_t)dim * dim, (T)0);
+        for (int i = 0; i < dim; ++i) I[(size_t)i * dim + i] = 1;
+        dev.check(pmx_set_reading(dev.ctx, stepReading.features.data(), dim, stepReading.n, I.data()));
+        matcher->initReading(dev, stepReading);
+    }
     const Matches matches = matcher->findClosests(dev, T_iter_);
     outlierFilters.compute(dev, matches);
     const TransformationParameters dT = errorMinimizer->compute(dev, dim);

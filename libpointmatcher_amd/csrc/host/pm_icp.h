@@ -238,6 +238,7 @@ struct PointMatcher {
         bool stepModules();                   // ICP.cpp:371-430 through the module calls
         bool loopConfig(pmx_loop_cfg& cfg) const;
         void prepareReading(const DataPoints& readingIn, const TransformationParameters& T_init);
+        DataPoints stepBase_;                 // the reading in <refMean> (readingStepDataPointsFilters)
         DataPoints map_;                      // the map in <refMean>, filtered (mapPointCloud)
         TransformationParameters T_map_;      // its T_refIn_refMean
         bool mapIndexed_ = false;             // the device holds the map (no other reference since)

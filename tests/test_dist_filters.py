@@ -229,3 +229,68 @@ def test_bounding_box_2d_ignores_z(golden):
     T = icp.compute(hom(g["box2"], np.float32), hom(g["box1"], np.float32), None)
     ok, dt, da = validate2d(T, np.array(kat["validT2d"]), kat["tol2d"])
     assert ok, (dt, da)
+
+
+# ---- DistanceLimit (DistanceLimit.cpp:57-128): MaxDist (removeInside 0) /
+# MinDist (removeInside 1) in one filter
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("remove_inside,dim,dist", [(0, 0, 2.0), (1, 1, -3.0), (0, -1, -20.0), (1, -1, 3.0)])
+def test_distance_limit_equals_prefiltered_reading(golden, dtype, remove_inside, dim, dist):
+    g, _ = golden
+    rd, ref, nrm = g["car401"].astype(dtype), g["car400"].astype(dtype), g["car400_normals"].astype(dtype)
+    keep = keep_rule(rd, "Min" if remove_inside else "Max", dim, dtype(dist))
+    assert 0 < keep.sum() < rd.shape[0]
+    base = chain_yaml(differential=DIFF)
+    a = ICP(dtype)
+    a.load_yaml(with_reading_filter(base, "DistanceLimitDataPointsFilter",
+                                    {"dim": dim, "dist": dist, "removeInside": remove_inside}))
+    Ta = a.compute(hom(rd, dtype), hom(ref, dtype), nrm)
+    b = ICP(dtype)
+    b.load_yaml(base)
+    Tb = b.compute(hom(rd[keep], dtype), hom(ref, dtype), nrm)
+    assert np.array_equal(Ta, Tb)
+
+
+# ---- readingStepDataPointsFilters (ICP.cpp:349-350, 373-377): applied every
+# iteration to the reading in <refMean> (before T_iter).  A deterministic step
+# filter keeps the same points every iteration, so the chain equals the chain
+# without it on the reading pre-filtered in that frame.
+def with_step_filter(yaml, name, params):
+    body = "".join(f"      {k}: {v}\n" for k, v in params.items())
+    return f"readingStepDataPointsFilters:\n  - {name}:\n{body}" + yaml
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("dim,limit", [(0, 1.5), (1, -2.0), (-1, 9.0)])
+def test_step_filter_equals_prefiltered_reading(golden, dtype, dim, limit):
+    g, _ = golden
+    rd, ref, nrm = g["car401"].astype(dtype), g["car400"].astype(dtype), g["car400_normals"].astype(dtype)
+    # <refMean>: the reference mean in T, sequential sums (ICP.cpp:291-297)
+    mean = np.array([np.add.accumulate(ref[:, r].astype(dtype))[-1] / dtype(ref.shape[0]) for r in range(3)],
+                    dtype=dtype)
+    keep = keep_rule((rd[:, :3] + (-mean)).astype(dtype), "Max", dim, dtype(limit))
+    assert 0 < keep.sum() < rd.shape[0]
+    base = chain_yaml(differential=DIFF)
+    a = ICP(dtype)
+    a.load_yaml(with_step_filter(base, "MaxDistDataPointsFilter", {"dim": dim, "maxDist": limit}))
+    Ta = a.compute(hom(rd, dtype), hom(ref, dtype), nrm)
+    b = ICP(dtype)
+    b.load_yaml(base)
+    Tb = b.compute(hom(rd[keep], dtype), hom(ref, dtype), nrm)
+    np.testing.assert_array_equal(Ta, Tb)
+    assert a.stats().iterations == b.stats().iterations
+
+
+@pytest.mark.gpu
+def test_random_step_filter_converges(golden):
+    # a new random subset every iteration (RandomSampling in the step chain):
+    # the reference's validT3d known answer still holds
+    g, kat = golden
+    libc().srand(7)
+    icp = ICP(np.float32)
+    icp.load_yaml(with_step_filter(chain_yaml(differential=DIFF), "RandomSamplingDataPointsFilter", {"prob": 0.7}))
+    T = icp.compute(hom(g["car401"], np.float32), hom(g["car400"], np.float32), g["car400_normals"])
+    ok, dt, da = validate3d(T, np.array(kat["validT3d"]), kat["tol3d"])
+    assert ok, (dt, da)

@@ -114,7 +114,8 @@ def test_ssn_planar_rank_and_small_clouds(oracle):
 # ---------------------------------------------------------------------------
 SUPPORTED = ["SamplingSurfaceNormalDataPointsFilter1", "SamplingSurfaceNormalDataPointsFilter2",
              "SamplingSurfaceNormalDataPointsFilter3", "defaultBoundingBoxDataPointsFilter",
-             "defaultFixStepSamplingDataPointsFilter", "defaultIdentityDataPointsFilter",
+             "defaultDistanceLimitDataPointsFilter", "defaultFixStepSamplingDataPointsFilter",
+             "defaultIdentityDataPointsFilter",
              "defaultMaxDistDataPointsFilter", "defaultPointToPlaneMinDistDataPointsFilter",
              "defaultPointToPointMinDistDataPointsFilter"]
 
