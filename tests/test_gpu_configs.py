@@ -11,7 +11,9 @@ pairs in the last iteration (integer, exact).
   C4  1M -> 1M float, k=4, MaxDist 0.05, PointToPlane (one GPU; the 8-GPU run
       shards the reading, tests/test_gpu_multirank.py covers the sharded path)
   C5  10M -> 1M double, k=1, empty chain, PointToPoint — Counter 5 (the
-      oracle's 10M-query kd-tree search takes seconds per iteration)
+      oracle's 10M-query kd-tree search takes seconds per iteration), and the
+      same chain over 40 iterations on a 2M reading with every iteration's
+      T_iter against the oracle's trace
 """
 import os
 
@@ -75,3 +77,28 @@ def test_c5_full_size_one_gpu(oracle):
     assert sg.iterations == so.iterations == 5
     assert sg.kept == so.kept
     assert frob <= 1e-12
+
+
+def test_c5_chain_40_iterations_traced(oracle):
+    """C5's chain (f64, empty outlier chain, point-to-point) for 40 iterations
+    on a 2M -> 1M pair: every T_iter of the trace within 1e-12 of the
+    oracle's, the same iteration count and kept pairs."""
+    ref, _ = reference_cloud(1_000_000, np.float64)
+    rd = reading_cloud(2_000_000, np.float64)
+    icp = ICP(np.float64)
+    icp.keep_trace(True)
+    icp.load_yaml(chain_yaml(knn=1, filters=[], minimizer="PointToPointErrorMinimizer", maxit=40, differential=None))
+    Tg = icp.compute(rd, ref, None)
+    sg = icp.stats()
+    tg = icp.trace()
+    icp.close()
+    cfg = oracle.make_cfg(knn=1, filters=(), minimizer="PointToPointErrorMinimizer", counter_max=40, threads=THREADS)
+    rc, To, so, to = oracle.icp(cfg, rd, ref, trace=True)
+    assert rc == 0
+    assert sg.iterations == so.iterations == 40
+    assert sg.kept == so.kept
+    worst = max(np.linalg.norm(a - b) for a, b in zip(tg, to[:len(tg)]))
+    print(f"C5x40: |dT|_F = {np.linalg.norm(Tg - To):.3g}, worst iteration {worst:.3g}")
+    assert len(tg) == 40
+    assert worst <= 1e-12
+    assert np.linalg.norm(Tg - To) <= 1e-12

@@ -63,15 +63,19 @@ def _clouds(dtype):
 
 
 P2PLANE, P2POINT = "PointToPlaneErrorMinimizer", "PointToPointErrorMinimizer"
-# whole-ICP cases: (tag, outlier filters, minimizer, Counter max, Differential, reference normals)
+# whole-ICP cases: (tag, knn, outlier filters, minimizer, Counter max, Differential, reference normals)
 ICP_RUNS = [
-    ("trim", (("TrimmedDistOutlierFilter", {"ratio": 0.85}),), P2PLANE, 30, DIFF, True),
-    ("vt", (("VarTrimmedDistOutlierFilter", VT),), P2PLANE, 20, DIFF, True),
-    ("med", (("MedianDistOutlierFilter", {"factor": 3.0}), ("MaxDistOutlierFilter", {"maxDist": 0.5})), P2PLANE,
+    ("trim", 1, (("TrimmedDistOutlierFilter", {"ratio": 0.85}),), P2PLANE, 30, DIFF, True),
+    ("vt", 1, (("VarTrimmedDistOutlierFilter", VT),), P2PLANE, 20, DIFF, True),
+    ("med", 1, (("MedianDistOutlierFilter", {"factor": 3.0}), ("MaxDistOutlierFilter", {"maxDist": 0.5})), P2PLANE,
      20, None, True),
-    ("p2pt", (), P2POINT, 10, None, False),
-    ("robust", (("RobustOutlierFilter", {"robustFct": "cauchy", "scaleEstimator": "mad", "tuning": 1}),), P2POINT,
-     15, DIFF, False),
+    ("p2pt", 1, (), P2POINT, 10, None, False),
+    ("robust", 1, (("RobustOutlierFilter", {"robustFct": "cauchy", "scaleEstimator": "mad", "tuning": 1}),),
+     P2POINT, 15, DIFF, False),
+    # the sharded benchmark chains: C4 (k = 4, MaxDist, point-to-plane) and
+    # C5 (empty chain, point-to-point, 40 iterations)
+    ("c4", 4, (("MaxDistOutlierFilter", {"maxDist": 0.05}),), P2PLANE, 20, DIFF, True),
+    ("c5", 1, (), P2POINT, 40, None, False),
 ]
 
 
@@ -131,10 +135,11 @@ def _worker(rank, world, port, outdir, env):
                                           comm.calls["allgather"] - cb0["allgather"], ls.iterations, hits, misses])
             ctx.close()
             # whole ICPs through the host chain (pmx_icp_comm_init_host)
-            for tag, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
+            for tag, knn, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
                 icp = ICP(dtype)
                 icp.comm_init_host(comm)
-                icp.load_yaml(chain_yaml(filters=filters, minimizer=minimizer, maxit=maxit, differential=diff))
+                icp.load_yaml(chain_yaml(knn=knn, filters=filters, minimizer=minimizer, maxit=maxit,
+                                         differential=diff))
                 T = icp.compute(shard, ref, nrm if with_n else None)
                 s = icp.stats()
                 res[f"{dn}_icp_{tag}"] = np.concatenate([T.astype(np.float64).ravel(), [s.iterations, s.kept]])
@@ -224,10 +229,10 @@ def test_sharded_icp_vs_oracle(two_ranks, oracle, dn):
     rd, ref, nrm = _clouds(dtype)
     from test_gpu_configs import THREADS
 
-    for tag, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
+    for tag, knn, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
         a, b2 = r[0][f"{dn}_icp_{tag}"], r[1][f"{dn}_icp_{tag}"]
         np.testing.assert_array_equal(a, b2)  # every rank ends with the same transform
-        cfg = oracle.make_cfg(filters=filters, minimizer=minimizer, counter_max=maxit, differential=diff,
+        cfg = oracle.make_cfg(knn=knn, filters=filters, minimizer=minimizer, counter_max=maxit, differential=diff,
                               threads=THREADS)
         rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm if with_n else None)
         assert rc == 0
