@@ -81,8 +81,6 @@ struct pmx_ctx {
     int search_type = 1;
     int grid_mode = 1;            // 1 = per-lane shell search (default), 0 = LDS tiles (PMX_GRID_MODE=tile)
     uint32_t tile_max = 4096;     // largest per-wave box scanned from LDS (PMX_GRID_TILE_MAX)
-    bool no_visits = false;       // experiment knob: skip the pair counter (PMX_NO_VISITS)
-    bool select_split = false;    // experiment knob: hist + pick kernels per pass (PMX_SELECT_SPLIT)
     // Grid levels of increasing cell size (points per occupied cell:
     // level_ppc, PMX_GRID_LEVELS).  Every level answers exactly; the level of
     // the next match is chosen from the last match's pair count (adaptive:
@@ -99,15 +97,6 @@ struct pmx_ctx {
     bool adaptive = true;
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
-    // LDS box of the blocks' full searches (pmx_grid_box.inc): dynamic LDS
-    // bytes per block (PMX_BOX_LDS, 0: off), the cells a match without usable
-    // reuse grows its boxes by (PMX_BOX_GROW), and the device-loop iterations
-    // after a prepare that launch with it before the fallback counts decide
-    uint32_t box_lds = 0;  // (off by default: measured slower than the per-lane walk so far)
-    int box_grow = 3;
-    int box_first_iters = 4;
-    int64_t box_full_last = -1;   // full searches of the last match known to the host (-1: none yet)
-    int64_t loop_since_prepare = 0;  // device-loop iterations enqueued since the reading was set
     void* d_safe = nullptr;       // T[N]: safe radius per query
     int64_t safe_cap = 0;
     bool grid_ready = false;
@@ -177,10 +166,8 @@ struct pmx_ctx {
     SelectState* d_sel = nullptr;
     int* d_iter_err = nullptr;
     uint32_t* d_hist = nullptr;
-    unsigned int* d_ticket = nullptr;  // inside the d_hist allocation
     void* d_selx = nullptr;            // select_all_kernel's arrivals / publications / per-pass bins
     int64_t selx_grid = 0;             // its block count of the last launch (0: zeroed)
-    bool select_all = true;            // one launch for all radix passes (PMX_SELECT_ALL=0: one per pass)
     double* d_ratio = nullptr;
 
     // VarTrimmed scratch + cached pow table
@@ -230,36 +217,6 @@ struct pmx_ctx {
     void* d_spec_keys = nullptr;
     bool spec_allowed = true;
     bool spec_on = false;
-    // loop: the minimiser's last finalize inside the step kernel (PMX_FUSE_FINAL=1).  Off: measured on
-    // MI355X (C3 driver command) 0.0821 ms/step unfused vs 0.0910 fused — the 256-thread step launch
-    // costs more than the finalize kernel and its boundary it saves
-    bool fuse_final = false;
-    bool fold_counter = false;  // the counter phase in the match's last workgroup (PMX_FOLD_COUNTER=1; measured slower)
-    // ... or at the start of the next select_all launch (PMX_DEFER_COUNTER=1).  Off: on the driver command
-    // (same box, A/B twice) 0.0884 ms/step deferred vs 0.0861 separate — fewer launches in the converged
-    // iterations (kernel trace 74 -> 68 us), but slower in iterations 5-24 of the timed window
-    bool defer_counter = false;
-    bool counter_deferred = false;  // the last match left its counter phase to the next select_all
-    // device loop, point-to-plane: the quantile's select_all launch held back
-    // and issued by the minimiser with the reduction after it (one launch
-    // fewer; PMX_SELECT_P2PLANE=1).  Off: measured at C3 (driver command) the
-    // merged launch took 34.2 us against 10.1 + 17.7 us for the two — the
-    // reduction waits for block 0's window pick before any block starts it,
-    // and 511 polling blocks hold the CUs meanwhile (74.7 vs 67.6 us/iteration)
-    bool select_p2 = false;
-    // device loop, point-to-plane, single rank: the post-match work in one
-    // launch with the sums fused into the match (pmx_post.hip; PMX_FUSED=0: off)
-    bool fuse_allowed = false;  // (PMX_FUSED=1: measured slower than the module chain so far)
-    double* d_fuse_part = nullptr;  // the match blocks' records [blocks][kFuseNV]
-    int64_t fuse_cap = 0;
-    bool sel_pending = false;
-    const void* selp_d = nullptr;
-    int64_t selp_n = 0;
-    double selp_ratio = 0.0;
-    const double* selp_ratio_dev = nullptr;
-    SelectState* selp_st = nullptr;
-    SpecSel* selp_spec = nullptr;
-    bool selp_pre = false;
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;
@@ -790,8 +747,6 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     c->N = N;
     c->N_total = N;
     c->N_max = N;
-    c->box_full_last = -1;
-    c->loop_since_prepare = 0;
     // A new reading's first match has no previous match to adapt the level
     // from, and the initial pose is usually the worst aligned: a coarse level
     // walks few shells where the finest walks dozens (measured on MI355X, C3).
@@ -821,34 +776,8 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
 }
 
 // ------------------------------------------------------------------- match --
-// a select held back for the point-to-plane minimiser, issued alone
 template <typename T>
-void flush_select(pmx_ctx* c) {
-    if (!c->sel_pending) return;
-    c->sel_pending = false;
-    const int64_t g = select_all_blocks(c->selp_n);
-    if (g != c->selx_grid) {
-        (void)hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream);
-        c->selx_grid = g;
-    }
-    launch_select_all<T>((const T*)c->selp_d, c->selp_n, c->d_selx, c->selp_st, c->selp_ratio, c->selp_ratio_dev,
-                         c->d_iter_err, loop_ctl(c), c->selp_spec, c->selp_pre ? c->d_vpart : nullptr,
-                         c->selp_pre ? c->d_visited : nullptr, P2Fuse<T>{}, 0, c->stream);
-}
-
-// the match's counter phase, when it was deferred to a select_all that did not come
-template <typename T>
-void flush_counter(pmx_ctx* c) {
-    flush_select<T>(c);
-    if (!c->counter_deferred) return;
-    c->counter_deferred = false;
-    launch_counter_sum<T>(c->d_vpart, c->d_visited, c->d_iter_err, loop_ctl(c), c->spec_now(), c->d_sel, c->stream);
-}
-
-template <typename T>
-int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited,
-               const FuseAcc<T>* fuse = nullptr) {
-    flush_counter<T>(c);
+int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
     if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
     if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
     if (knn < 1 || knn > kMaxKnn) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 256] on the GPU path");
@@ -903,7 +832,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
     // ([kBlkVisited, kBlkVisited + 16)); the grid match's counter-sum kernel
     // does both itself, which saves a fill launch per iteration
     const bool grid = !(c->search_type == 0 || !c->grid_ready);
-    if (!grid || c->no_visits)
+    if (!grid)
         HIPCHK(c, hipMemsetAsync((char*)c->d_result + kBlkIterErr, 0, kBlkVisited + 16 - kBlkIterErr, c->stream));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
@@ -936,19 +865,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // temporal reuse: the output buffers hold this reading's previous
         // match (same k, same level) with its safe radii
         GridReuse<T> ru;
-        // (a fused match without a quantile must write its sums: no cold tile
-        // form then; with one, the first match has no window and the post
-        // launch reduces every pair itself)
-        // the blocks' full searches from an LDS box (pmx_grid_box.inc) while
-        // many queries need one: no usable previous match, the first device-
-        // loop iterations after a new reading (moves too large to certify),
-        // or the last known match's full searches over 1/8 of the queries.
-        // The box costs occupancy, so a converged match launches without it.
         const bool no_prev = !(c->safe_valid && c->have_match && c->ids_grid && c->knn == knn);
-        const bool many = c->box_full_last >= 0 ? c->box_full_last * 8 >= c->N : !c->loop_on;
-        const bool early = c->loop_on && c->loop_since_prepare < c->box_first_iters;
-        const uint32_t box_bytes = c->grid_mode >= 1 && (no_prev || early || many) ? c->box_lds : 0u;
-        if (c->loop_on) ++c->loop_since_prepare;
         if (c->reuse_on && c->grid_mode >= 1 && knn <= kLaneMaxK) {  // (the wide search keeps no safe radii)
             ru.mode = c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
@@ -959,18 +876,11 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         SpecSel* spec = c->spec_now();
         c->spec_exchanged = false;
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx : nullptr;
-        // single rank, window on: the counter phase runs at the start of the
-        // select_all launch that the quantile filter issues next
-        const bool defer = spec && !xseg && c->select_all && !c->select_split && !c->fold_counter &&
-                           c->defer_counter && !c->no_visits && c->grid_mode >= 1;
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
-                             (T*)c->d_dists, c->d_ids, c->no_visits ? nullptr : c->d_vpart, c->d_visited,
-                             c->d_iter_err, ru, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->fold_counter, defer, c->has_radii ? (const T*)c->d_radii : nullptr, box_bytes,
-                             c->box_grow, no_prev && c->reuse_on && !(fuse && !fuse->quantile),
-                             fuse ? *fuse : FuseAcc<T>{}, e1, c->stream);
-        c->counter_deferred = defer;  // (e1 recorded after the match kernel, before the counter sum)
+                             (T*)c->d_dists, c->d_ids, c->d_vpart, c->d_visited, c->d_iter_err, ru, loop_ctl(c),
+                             (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
+                             c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on, e1, c->stream);
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
@@ -1024,40 +934,21 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
         if (r < 0) return r;
         if (r == 1) return PMX_OK;  // (the pass kernels would return at spec->hit; no histogram exchange)
     }
-    for (int p = 0; p < passes; ++p) {
-        if (sharded(c) || c->select_split) {
+    if (!sharded(c)) {
+        // every pass in one launch (a no-op launch when the window resolved it)
+        const int64_t g = select_all_blocks(n);
+        if (g != c->selx_grid) {  // (the arrival generations assume a fixed block count)
+            HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
+            c->selx_grid = g;
+        }
+        launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
+    } else {
+        for (int p = 0; p < passes; ++p) {
             // the histogram is all-reduced between the two halves of a pass
             launch_select_hist<T>(d, n, c->d_hist, st, p, loop_ctl(c), spec, c->stream);
             int rc = coll_allreduce(c, c->d_hist, select_bins(p, 8 * (int)sizeof(T)), PMX_COLL_U32, PMX_COLL_SUM);
             if (rc) return rc;
             launch_select_pick<T>(c->d_hist, st, p, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
-        } else if (c->select_all) {
-            // every pass in one launch (a no-op launch when the window resolved it)
-            const bool pre = c->counter_deferred;  // (the match left its counter phase to this launch)
-            c->counter_deferred = false;
-            if (spec && c->loop_on && c->select_p2 && c->loop_cfg.minimizer == 0) {
-                // held back: the point-to-plane minimiser launches it with its reduction (p2plane_enqueue)
-                c->sel_pending = true;
-                c->selp_d = d;
-                c->selp_n = n;
-                c->selp_ratio = ratio;
-                c->selp_ratio_dev = ratio_dev;
-                c->selp_st = st;
-                c->selp_spec = spec;
-                c->selp_pre = pre;
-                break;
-            }
-            const int64_t g = select_all_blocks(n);
-            if (g != c->selx_grid) {  // (the arrival generations assume a fixed block count)
-                HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
-                c->selx_grid = g;
-            }
-            launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec,
-                                 pre ? c->d_vpart : nullptr, pre ? c->d_visited : nullptr, P2Fuse<T>{}, 0, c->stream);
-            break;
-        } else {
-            launch_select_pass<T>(d, n, c->d_hist, st, p, ratio, ratio_dev, c->d_ticket, c->d_iter_err, loop_ctl(c),
-                                  spec, c->stream);
         }
     }
     HIPCHK(c, hipGetLastError());
@@ -1169,9 +1060,6 @@ WChain<T> chain_of(const pmx_ctx* c) {
 // the 0/1 weights themselves are evaluated inline by the minimiser.
 template <typename T>
 int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, double p2) {
-    // (the fixed predicates only record themselves; a quantile filter at
-    // position 0 takes the deferred counter phase into its select)
-    if (kind == 6 || ((kind == 4 || kind == 5) && chain_pos > 0)) flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     if (chain_pos < 0 || chain_pos >= kMaxChain) return fail(c, PMX_E_BAD_PARAM, "outlier chain longer than 8 filters");
@@ -1279,7 +1167,6 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
 template <typename T>
 int outlier_robust_impl(pmx_ctx* c, int pos, int fct, double tuning, double approx, int mode, double target,
                         int p2pl) {
-    flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     if (pos < 0 || pos >= kMaxChain) return fail(c, PMX_E_BAD_PARAM, "outlier chain longer than 8 filters");
@@ -1418,11 +1305,10 @@ void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double 
 
 // after a readback: adapt the grid level of the next match
 void after_readback(pmx_ctx* c) {
-    if (c->visited_host || c->no_visits) return;
+    if (c->visited_host) return;
     unsigned long long v = 0, f = 0;
     std::memcpy(&v, (const char*)c->h_result + kBlkVisited, sizeof(v));
     std::memcpy(&f, (const char*)c->h_result + kBlkVisited + 8, sizeof(f));
-    c->box_full_last = (int64_t)f;
     choose_level(c, v, f);
 }
 
@@ -1439,60 +1325,23 @@ int materialise_weights(pmx_ctx* c) {
     return PMX_OK;
 }
 
-// the point-to-plane system into the iteration block (no host sync);
-// *fuse_nv != 0 on entry: leave the finalize to the loop step (single rank),
-// which gets the value count back in *fuse_nv
+// the point-to-plane system into the iteration block (no host sync)
 template <typename T>
-int p2plane_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
+int p2plane_enqueue(pmx_ctx* c) {
     const WChain<T> chain = chain_of<T>(c);
     const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
-    // the held-back quantile select and this reduction in one launch: the
-    // quantile is chain position 0, every later position a fixed predicate
-    bool merge = c->sel_pending && loop_ctl(c) && !chain.robust && c->selp_st == c->sel_slot(0) && c->has_normals;
-    for (int i = 1; merge && i < chain.n; ++i) merge = chain.type[i] != kWPState;
-    if (merge) {
-        c->sel_pending = false;
-        if ((int64_t)kRedBlocks != c->selx_grid) {  // (the arrival generations assume a fixed block count)
-            HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
-            c->selx_grid = kRedBlocks;
-        }
-        P2Fuse<T> p2;
-        p2.on = 1;
-        p2.dim = c->dim;
-        p2.rd = (const P4<T>*)c->d_rd;
-        p2.d = (const T*)c->d_dists;
-        p2.ids = c->d_ids;
-        p2.chain = chain;
-        p2.k = c->knn;
-        p2.N = c->N;
-        p2.partials = c->d_partials;
-        p2.gd = (const GridDesc<T>*)c->d_gdesc;
-        launch_select_all<T>((const T*)c->selp_d, c->selp_n, c->d_selx, c->selp_st, c->selp_ratio, c->selp_ratio_dev,
-                             c->d_iter_err, loop_ctl(c), c->selp_spec, c->selp_pre ? c->d_vpart : nullptr,
-                             c->selp_pre ? c->d_visited : nullptr, p2, kRedBlocks, c->stream);
-    } else {
-        flush_counter<T>(c);
-        Mat4<T> Tm = step_mat<T>(c);
-        launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
-                                  match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim,
-                                  c->d_partials, loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
-    }
-    if (fuse_nv && *fuse_nv && !sharded(c)) {
-        *fuse_nv = NV;
-        HIPCHK(c, hipGetLastError());
-        return PMX_OK;
-    }
-    if (fuse_nv) *fuse_nv = 0;
+    Mat4<T> Tm = step_mat<T>(c);
+    launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
+                              match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
+                              loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result, NV);
 }
 
 // the point-to-point sums, means and cross-covariance (no host sync);
-// fuse_nv: as p2plane_enqueue (the second pass's finalize)
 template <typename T>
-int p2point_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
-    flush_counter<T>(c);
+int p2point_enqueue(pmx_ctx* c) {
     Mat4<T> Tm = step_mat<T>(c);
     WChain<T> chain = chain_of<T>(c);
     if (chain.robust && chain.rb_p2pl) {  // (the point-to-point kernels carry no normals)
@@ -1509,12 +1358,6 @@ int p2point_enqueue(pmx_ctx* c, int* fuse_nv = nullptr) {
     launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, loop_ctl(c), c->stream);
     launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
                             chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, loop_ctl(c), gd, c->stream);
-    if (fuse_nv && *fuse_nv && !sharded(c)) {
-        *fuse_nv = 9;
-        HIPCHK(c, hipGetLastError());
-        return PMX_OK;
-    }
-    if (fuse_nv) *fuse_nv = 0;
     launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result + 16, 9);
@@ -1586,7 +1429,6 @@ int p2point_impl(pmx_ctx* c, double* mean_p, double* mean_q, double* m, pmx_stat
 
 template <typename T>
 int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
-    flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
@@ -1619,7 +1461,6 @@ int get_matches_impl(pmx_ctx* c, void* dists, int32_t* ids) {
 
 template <typename T>
 int get_weights_impl(pmx_ctx* c, void* w) {
-    flush_counter<T>(c);
     int rc = check_match(c);
     if (rc) return rc;
     const int64_t n = c->N * c->knn;
@@ -1686,7 +1527,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
         d.checker_kind[i] = cfg->checker_kind[i];
         for (int j = 0; j < 3; ++j) d.checker_p[i][j] = cfg->checker_p[i][j];
     }
-    d.adaptive = c->adaptive && !c->no_visits ? 1 : 0;
+    d.adaptive = c->adaptive ? 1 : 0;
     d.reuse = c->reuse_on && c->grid_mode >= 1 ? 1 : 0;
     d.knn = cfg->knn;
     d.n_levels = (int)c->levels.size();
@@ -1713,19 +1554,17 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     // quantile window: a fresh window each loop (the first iteration runs the
     // radix passes, which centre the window for the next)
     const int k0 = cfg->n_filters > 0 ? cfg->filter_kind[0] : -1;
-    c->spec_on = c->spec_allowed && !c->no_visits &&
+    c->spec_on = c->spec_allowed &&
                  (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
     if (c->spec_on) {
         if (!c->d_spec) {
             HIPCHK(c, hipMalloc((void**)&c->d_spec, sizeof(SpecSel)));
-            // keys, then the fused path's records (pmx_post.hip)
-            HIPCHK(c, hipMalloc(&c->d_spec_keys, 2 * sizeof(unsigned long long) * kSpecCap));
+            HIPCHK(c, hipMalloc(&c->d_spec_keys, sizeof(unsigned long long) * kSpecCap));
         }
         if (sharded(c) && !c->d_specx)
             HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * (c->nranks + 1)));
         SpecSel init{};
         init.keys = c->d_spec_keys;
-        init.recs = (unsigned long long*)c->d_spec_keys + kSpecCap;
         init.ratio = (double)(T)(k0 == PMX_FILTER_TRIMMED ? cfg->filter_p[0][0] : 0.5);
         c->spec_init = init;
         HIPCHK(c, hipMemcpyAsync(c->d_spec, &c->spec_init, sizeof(SpecSel), hipMemcpyHostToDevice, c->stream));
@@ -1759,136 +1598,11 @@ int loop_trace_room(pmx_ctx* c, int64_t iters) {
     return PMX_OK;
 }
 
-// The fused iteration (pmx_post.hip): point-to-plane on one rank, an outlier
-// chain of TrimmedDist at position 0 (with the quantile window) and / or the
-// fixed predicates (default / Null / MaxDist / MinDist).  1: fused with the
-// quantile, 2: fused without one, 0: the module sequence.
-constexpr int64_t kSelxPost = -2;  // selx_grid: the state belongs to the post launches
-int fused_kind(const pmx_ctx* c) {
-    const pmx_loop_cfg& cfg = c->loop_cfg;
-    if (!c->fuse_allowed || sharded(c) || cfg.minimizer != 0 || !c->has_normals || c->grid_mode < 1 ||
-        c->search_type == 0 || !c->grid_ready || (c->dim != 3 && c->dim != 2) || cfg.knn > kLaneMaxK)
-        return 0;
-    int q = 0;
-    for (int i = 0; i < cfg.n_filters; ++i) {
-        const int k = cfg.filter_kind[i];
-        if (k == PMX_FILTER_TRIMMED && i == 0 && c->spec_on) {
-            q = 1;
-            continue;
-        }
-        if (k == PMX_FILTER_NULL || k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST ||
-            (k == PMX_FILTER_DEFAULT && i == 0))
-            continue;
-        return 0;
-    }
-    return q ? 1 : 2;
-}
-
-template <typename T>
-int loop_enqueue_fused(pmx_ctx* c, int kind) {
-    const pmx_loop_cfg& cfg = c->loop_cfg;
-    const int64_t fblocks = (c->N + 255) / 256;
-    if (c->fuse_cap < fblocks) {
-        if (c->d_fuse_part) (void)hipFree(c->d_fuse_part);
-        c->d_fuse_part = nullptr;
-        c->fuse_cap = 0;
-        HIPCHK(c, hipMalloc((void**)&c->d_fuse_part, sizeof(double) * (size_t)fblocks * kFuseNV));
-        c->fuse_cap = fblocks;
-    }
-    // the chain as the filter calls would record it (no launch: the post
-    // launch resolves the quantile)
-    c->chain_n = 0;
-    c->rb_pos = -1;
-    for (int i = 0; i < cfg.n_filters; ++i) {
-        const int k = cfg.filter_kind[i];
-        const double p0 = cfg.filter_p[i][0];
-        if (k == PMX_FILTER_TRIMMED) {
-            chain_set(c, i, kWPState, 1.0);
-        } else if (k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST) {
-            const T m = (T)p0;
-            chain_set(c, i, k == PMX_FILTER_MAXDIST ? kWPLe : kWPGe, (double)(T)std::pow((double)m, 2.0));
-        } else {
-            chain_set(c, i, k == PMX_FILTER_NULL ? kWPNull : kWPDefault, 0.0);
-        }
-    }
-    // the predicates after the quantile as one interval (chain_resolve's rule)
-    FuseAcc<T> fa;
-    fa.on = 1;
-    fa.quantile = kind == 1;
-    fa.dim = c->dim;
-    fa.partials = c->d_fuse_part;
-    double lo = -INFINITY, hi = INFINITY;
-    int fin = cfg.n_filters == 0 ? 1 : 0;
-    for (int i = fa.quantile ? 1 : 0; i < c->chain_n; ++i) {
-        const int t = c->chain_type[i];
-        const double v = (double)(T)c->chain_thr[i];
-        if (t == kWPDefault) fin = 1;
-        if (t == kWPGe) lo = (std::isnan(v) || std::isnan(lo)) ? v + lo : std::max(v, lo);
-        if (t == kWPLe) hi = (std::isnan(v) || std::isnan(hi)) ? v + hi : std::min(v, hi);
-    }
-    fa.fx_lo = (T)lo;
-    fa.fx_hi = (T)hi;
-    fa.fx_finite = fin;
-    T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
-    for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
-    int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr, &fa);
-    if (rc) return rc;
-    // (match_impl reset the chain: record it again for the mirrors)
-    for (int i = 0; i < cfg.n_filters; ++i) {
-        const int k = cfg.filter_kind[i];
-        if (k == PMX_FILTER_TRIMMED) {
-            chain_set(c, i, kWPState, 1.0);
-        } else if (k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST) {
-            const T m = (T)cfg.filter_p[i][0];
-            chain_set(c, i, k == PMX_FILTER_MAXDIST ? kWPLe : kWPGe, (double)(T)std::pow((double)m, 2.0));
-        } else {
-            chain_set(c, i, k == PMX_FILTER_NULL ? kWPNull : kWPDefault, 0.0);
-        }
-    }
-    if (fa.quantile && c->selx_grid != kSelxPost) {
-        // (the arrival generations assume one grid per launch kind: start the shared state afresh)
-        HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
-        c->selx_grid = kSelxPost;
-    }
-    PostLaunch<T> p;
-    p.d = (const T*)c->d_dists;
-    p.ids = c->d_ids;
-    p.rd = (const P4<T>*)c->d_rd;
-    p.N = c->N;
-    p.k = cfg.knn;
-    p.ctl = c->d_ctl;
-    p.gd = (const GridDesc<T>*)c->d_gdesc;
-    p.quantile = fa.quantile;
-    p.ratio = fa.quantile ? cfg.filter_p[0][0] : 0.0;
-    p.selx = c->d_selx;
-    p.st = c->sel_slot(0);
-    p.spec = c->spec_now();
-    p.iter_err = c->d_iter_err;
-    p.vpart = c->d_vpart;
-    p.vout = c->d_visited;
-    p.fuse_part = c->d_fuse_part;
-    p.fuse_blocks = (int)fblocks;
-    p.part2 = c->d_partials;
-    p.chain = chain_of<T>(c);
-    p.res_out = c->d_result;
-    p.S = (LoopState<T>*)c->d_loop;
-    p.cfg = c->loop_dev;
-    p.trace = cfg.keep_trace ? (T*)c->d_trace : nullptr;
-    p.cu_count = c->cu_count;
-    launch_post<T>(p, c->stream);
-    launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
-                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, nullptr,
-                        kRedBlocks, 0, c->d_result, c->stream);
-    HIPCHK(c, hipGetLastError());
-    return PMX_OK;
-}
-
 // one ICP iteration, device-driven (transform and level from LoopCtl)
 template <typename T>
 int loop_enqueue_iteration(pmx_ctx* c) {
     const pmx_loop_cfg& cfg = c->loop_cfg;
     if (c->shard_done_seen) return PMX_OK;  // (every rank stops enqueuing at the same iteration)
-    if (const int fk = c->N > 0 ? fused_kind(c) : 0) return loop_enqueue_fused<T>(c, fk);
     T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
     for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
     int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr);
@@ -1900,12 +1614,9 @@ int loop_enqueue_iteration(pmx_ctx* c) {
         const double* p = cfg.filter_p[i];
         if ((rc = outlier_impl<T>(c, cfg.filter_kind[i], i, p[0], p[1], p[2]))) return rc;
     }
-    int fuse = c->fuse_final ? 1 : 0;  // (the last finalize into the step kernel; 0 back when not fused)
-    if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c, &fuse) : p2point_enqueue<T>(c, &fuse))) return rc;
-    double* fused_out = cfg.minimizer == 0 ? c->d_result : c->d_result + 16;
+    if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c))) return rc;
     launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
-                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr,
-                        fuse ? c->d_partials : nullptr, kRedBlocks, fuse, fused_out, c->stream);
+                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, c->stream);
     HIPCHK(c, hipGetLastError());
     return PMX_OK;
 }
@@ -1948,11 +1659,6 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
         const hipError_t e = hipEventSynchronize(c->loop_ev[s]);
         if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
         if (((const LoopState<T>*)(stat_slot(c, s) + kStatLoop))->done) stop = true;
-        {  // the full searches of the batch's last match (the LDS box policy of match_impl)
-            unsigned long long f = 0;
-            std::memcpy(&f, stat_slot(c, s) + kBlkVisited + 8, sizeof(f));
-            c->box_full_last = (int64_t)f;
-        }
     }
     // drain: the last issued batch's copy is the final status
     while (rc == PMX_OK && nfly > 0) {
@@ -2362,15 +2068,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_MODE"))
         c->grid_mode = std::strcmp(e, "tile") == 0 ? 0 : std::strcmp(e, "octant") == 0 ? 2 : 1;
     if (const char* e = std::getenv("PMX_GRID_TILE_MAX")) c->tile_max = (uint32_t)std::max(0, std::atoi(e));
-    c->no_visits = std::getenv("PMX_NO_VISITS") != nullptr;
-    c->select_split = std::getenv("PMX_SELECT_SPLIT") != nullptr;
     if (const char* e = std::getenv("PMX_SPEC_SELECT")) c->spec_allowed = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_FUSE_FINAL")) c->fuse_final = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_FOLD_COUNTER")) c->fold_counter = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_DEFER_COUNTER")) c->defer_counter = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_SELECT_P2PLANE")) c->select_p2 = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_SELECT_ALL")) c->select_all = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_FUSED")) c->fuse_allowed = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
     if (const char* e = std::getenv("PMX_GRID_LEVELS")) {
@@ -2388,9 +2086,6 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
-    if (const char* e = std::getenv("PMX_BOX_LDS")) c->box_lds = (uint32_t)std::min(65536, std::max(0, std::atoi(e)));
-    if (const char* e = std::getenv("PMX_BOX_GROW")) c->box_grow = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("PMX_BOX_FIRST")) c->box_first_iters = std::max(0, std::atoi(e));
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
@@ -2415,7 +2110,6 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
         preload_normals();
         preload_setup();
         preload_ssn();
-        preload_post();
         preloaded = true;
     }
     // One small "iteration block" holds everything the host reads back per
@@ -2439,10 +2133,9 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     (void)hipMemset(c->d_sel_more, 0, sizeof(SelectState) * (kMaxChain - 1));
     if (hipMalloc((void**)&c->d_vpart, grid_counter_bytes()) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_vpart, 0, grid_counter_bytes());
-    // 2048 histogram bins, then the fused select pass's ticket counter
-    if (hipMalloc((void**)&c->d_hist, (2048 + 64) * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
-    (void)hipMemset(c->d_hist, 0, (2048 + 64) * sizeof(uint32_t));
-    c->d_ticket = c->d_hist + 2048;
+    // 2048 histogram bins (the sharded select's per-pass histogram)
+    if (hipMalloc((void**)&c->d_hist, 2048 * sizeof(uint32_t)) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_hist, 0, 2048 * sizeof(uint32_t));
     if (hipMalloc(&c->d_selx, selx_bytes()) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_selx, 0, selx_bytes());
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
@@ -2478,7 +2171,6 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_flags) (void)hipHostFree(c->h_flags);
     if (c->d_specx) (void)hipFree(c->d_specx);
-    if (c->d_fuse_part) (void)hipFree(c->d_fuse_part);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PMX_OK;

@@ -43,7 +43,6 @@
 // per-lane search from LDS (broadcast reads) and measures 0.187 ms at C3: a
 // candidate for QPT > 1 and for very dense references.
 #include "pmx_internal.h"
-#include "pmx_p2plane.h"
 #include "pmx_spec.h"
 
 namespace pmx {
@@ -258,130 +257,6 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
     return false;
 }
 
-// Shell walk with batched row scans (R >= 2).  The rows (and single cells)
-// of a shell that pass the gap test are queued kShellB at a time; a full
-// queue loads all its cell bounds together, then the first kShellU points of
-// every queued range together, so a batch costs two dependent round trips
-// instead of two per row.  The gap test reads the list as it stands when the
-// row is queued; the list only shrinks the limit afterwards, so a queued row
-// may be one the row-at-a-time walk would have skipped — never the reverse:
-// the set of points that can enter the list, and the result, are the same.
-// Off by default (kShellB = 0): measured at C3 the cold match went 0.83 ->
-// 1.7 ms (B = 4) and 1.9 ms (B = 6) — lanes fill their queues at different
-// rows, so the wave runs the flush once per lane group, and the stale limit
-// queues rows the row-at-a-time walk skips.
-#ifndef PMX_SHELL_B
-#define PMX_SHELL_B 0
-#endif
-#ifndef PMX_SHELL_U
-#define PMX_SHELL_U 0
-#endif
-constexpr int kShellB = PMX_SHELL_B;
-constexpr int kShellU = PMX_SHELL_U;
-
-template <typename T, int KT>
-__device__ __forceinline__ void shell_flush(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
-                                            const uint32_t* __restrict__ start, const uint32_t (&ia)[kShellB > 0 ? kShellB : 1],
-                                            const uint32_t (&ib)[kShellB > 0 ? kShellB : 1], int np, T qx, T qy, T qz,
-                                            T (&kd)[KT], int32_t (&ki)[KT], uint32_t& visits) {
-    constexpr int B = kShellB > 0 ? kShellB : 1, U = kShellU;
-    uint32_t ra[B], rb[B];
-#pragma unroll
-    for (int s = 0; s < B; ++s) {
-        const bool ok = s < np;
-        const uint32_t va = gld32(start, ok ? ia[s] : 0u);
-        const uint32_t vb = gld32(start, ok ? ib[s] : 0u);
-        ra[s] = ok ? va : 0u;
-        rb[s] = ok ? vb : 0u;
-    }
-    // (U = 0: only the bounds are batched; most shell cells of a surface
-    // cloud are empty, and an empty range costs nothing past its bounds)
-    P4<T> p[B][U > 0 ? U : 1];
-#pragma unroll
-    for (int s = 0; s < B; ++s)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = ra[s] + u;
-            p[s][u] = gld32(gpts, j < rb[s] ? j : 0u);  // masked: any in-range address
-        }
-#pragma unroll
-    for (int s = 0; s < B; ++s) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = ra[s] + u;
-            if (j < rb[s]) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, p[s][u]), kd, ki);
-        }
-        visits += rb[s] - ra[s];
-        if (ra[s] + U < rb[s]) {
-            uint32_t v0 = 0;
-            scan_range<T, KT>(gpts, gidx, ra[s] + U, rb[s], qx, qy, qz, kd, ki, v0);
-        }
-    }
-}
-
-template <typename T, int KT>
-__device__ __forceinline__ void shell_walk_batched(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
-                                                   const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy,
-                                                   T qz, const double q[3], const int c[3], int R, int k,
-                                                   T (&kd)[KT], int32_t (&ki)[KT], uint32_t& visits) {
-    constexpr int B = kShellB > 0 ? kShellB : 1;
-    const double margin = 1.0 - 1e-5;
-    const int y0 = max(c[1] - R, 0), y1 = min(c[1] + R, G.g[1] - 1);
-    const int z0 = max(c[2] - R, 0), z1 = min(c[2] + R, G.g[2] - 1);
-    const int x0 = max(c[0] - R, 0), x1 = min(c[0] + R, G.g[0] - 1);
-    uint32_t ia[B], ib[B];
-    int np = 0;
-    auto push = [&](uint32_t a, uint32_t b) {
-#pragma unroll
-        for (int s = 0; s < B; ++s)
-            if (s == np) {  // (static indexing keeps the queue in registers)
-                ia[s] = a;
-                ib[s] = b;
-            }
-        if (++np == B) {
-            shell_flush<T, KT>(gpts, gidx, start, ia, ib, np, qx, qy, qz, kd, ki, visits);
-            np = 0;
-        }
-    };
-    for (int z = z0; z <= z1; ++z) {
-        const double gz = axis_gap(G, 2, z, q[2]), gz2 = gz * gz;
-        const bool zface = (z == c[2] - R) || (z == c[2] + R);
-        for (int y = y0; y <= y1; ++y) {
-            // the limit of the list as it stands (entry k + 1 when the list
-            // has room for it: the safe radius bound, see lane_search)
-            T dkT;
-            int32_t ikT;
-            kth(kd, ki, k < KT ? k + 1 : k, dkT, ikT);
-            const double lim = ikT == kNoPos ? 1e300 : (double)dkT / margin;
-            if (gz2 > lim) break;  // (the whole z slab: gz does not depend on y)
-            const double gy = axis_gap(G, 1, y, q[1]), g2 = gz2 + gy * gy;
-            if (g2 > lim) continue;
-            const bool yface = (y == c[1] - R) || (y == c[1] + R);
-            const uint32_t row = ((uint32_t)z * (uint32_t)G.g[1] + (uint32_t)y) * (uint32_t)G.g[0];
-            if (zface || yface) {
-                int xa = x0, xb = x1;
-                if (lim < 1e300) {
-                    const double rem = sqrt(lim - g2);
-                    xa = max(x0, cell_x(G, q[0] - rem) - 1);
-                    xb = min(x1, cell_x(G, q[0] + rem) + 1);
-                }
-                if (xa <= xb) push(row + (uint32_t)xa, row + (uint32_t)xb + 1u);
-            } else {
-                const int xl = c[0] - R, xr = c[0] + R;
-                if (xl >= 0) {
-                    const double gx = axis_gap(G, 0, xl, q[0]);
-                    if (g2 + gx * gx <= lim) push(row + (uint32_t)xl, row + (uint32_t)xl + 1u);
-                }
-                if (xr <= G.g[0] - 1) {
-                    const double gx = axis_gap(G, 0, xr, q[0]);
-                    if (g2 + gx * gx <= lim) push(row + (uint32_t)xr, row + (uint32_t)xr + 1u);
-                }
-            }
-        }
-    }
-    if (np > 0) shell_flush<T, KT>(gpts, gidx, start, ia, ib, np, qx, qy, qz, kd, ki, visits);
-}
-
 // Exact shell search for one query (from scratch); kd/ki must be
 // initialised.  Certified on the k-th entry of the list (entries past k, when
 // KT > k, are the next-nearest points visited).  lb_exit: the distance from
@@ -441,9 +316,7 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
         }
     }
     for (int R = 1;; ++R) {
-        if (R >= 2 && kShellB > 0) {
-            shell_walk_batched<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, R, k, kd, ki, visits);
-        } else if (R >= 2) {
+        if (R >= 2) {
             // walk the shell at Chebyshev radius R.  Rows (and the x-range of
             // a face row) whose cells are all farther than the current k-th
             // (k+1-th) distance are skipped: every point there has d > d_k, so it can
@@ -581,68 +454,6 @@ __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long
     counter_phase<T>(vpart, out, iter_err, spec, st, xseg);
 }
 
-// The counter phase folded into the match kernel (PMX_FOLD_COUNTER=1): the
-// last workgroup to finish runs it, one launch fewer per iteration.  Off by
-// default: measured at C3 (driver command) the match grew 22.4 -> 31.6 us
-// against 22.4 + 5.9 us for the two launches — every workgroup must drain its
-// stores before it takes its ticket, and that drain costs more than the
-// boundary it saves.  Every
-// value it reads was published by atomics or write-through (sc1) stores and
-// is read with coherent loads, so each workgroup only drains its memory
-// operations before it takes its ticket (cdna_hip_programming.md §6 G16,
-// the sc1 form of the in-launch reduction).
-// Tickets: one counter per group of workgroups (blockIdx % kTicketGroups, each
-// on its own 128-byte line), then one for the groups — a single counter
-// taken by all 4K workgroups serialises (measured: +27 us at C3).
-constexpr size_t kTicketOff = (size_t)4 * kVSlots * kVStride;  // (unsigned long longs into vpart)
-constexpr int kTicketGroups = 64;
-template <typename T>
-__device__ __forceinline__ void counter_fold(unsigned long long* __restrict__ vpart,
-                                             unsigned long long* __restrict__ out, int* __restrict__ iter_err,
-                                             SpecSel* __restrict__ spec, SelectState* __restrict__ st,
-                                             unsigned long long* __restrict__ xseg) {
-    __shared__ unsigned s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned* tk = (unsigned*)(vpart + kTicketOff);  // [group g at g * 32] ..., top at kTicketGroups * 32
-    if (threadIdx.x == 0) {
-        const unsigned G = gridDim.x, b = blockIdx.x;
-        const unsigned g = b % kTicketGroups;
-        const unsigned ng = G < (unsigned)kTicketGroups ? G : (unsigned)kTicketGroups;
-        const unsigned gsize = (G - g + kTicketGroups - 1) / kTicketGroups;  // blocks with this residue
-        unsigned last = 0;
-        const unsigned o = __hip_atomic_fetch_add(tk + g * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (o == gsize - 1) {
-            const unsigned t = __hip_atomic_fetch_add(tk + kTicketGroups * 32, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            last = t == ng - 1 ? 1u : 0u;
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    counter_phase<T>(vpart, out, iter_err, spec, st, xseg);
-    for (int g = threadIdx.x; g <= kTicketGroups; g += blockDim.x)  // (every group's and the top counter)
-        __hip_atomic_store(tk + g * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// a deferred counter phase that no select_all consumed
-template <typename T>
-void launch_counter_sum(unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
-                        SpecSel* spec, SelectState* st, hipStream_t s) {
-    hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, vpart, vout, iter_err, ctl, spec, st,
-                       nullptr);
-}
-template void launch_counter_sum<float>(unsigned long long*, unsigned long long*, int*, const LoopCtl*, SpecSel*,
-                                        SelectState*, hipStream_t);
-template void launch_counter_sum<double>(unsigned long long*, unsigned long long*, int*, const LoopCtl*, SpecSel*,
-                                         SelectState*, hipStream_t);
-
 // Several ranks: resolve the quantile from the all-gathered window segments
 // (pmx_spec.h).  Every rank runs it on the same segments and writes the same
 // limit; a miss leaves the radix passes (with their histogram all-reduce) to
@@ -683,7 +494,7 @@ template void launch_spec_pick<double>(const unsigned long long*, int, SpecSel*,
 
 // counters: 0 pairs, 1 full-search fallbacks, 2 finite distances, 3 below the quantile window
 // (+ the fold tickets: kTicketGroups + 1 counters, 128 bytes apart)
-size_t grid_counter_bytes() { return sizeof(unsigned long long) * (4 * kVSlots * kVStride + 16 * (kTicketGroups + 1)); }
+size_t grid_counter_bytes() { return sizeof(unsigned long long) * 4 * kVSlots * kVStride; }
 
 // ---------------------------------------------------- temporal reuse --
 // ICP matches the same reading every iteration under a slowly changing
@@ -814,101 +625,24 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
     return true;
 }
 
-// ------------------------------------------------- LDS box full searches --
-#include "pmx_grid_box.inc"
-
-// ------------------------------------------------- fused point-to-plane --
-// The point-to-plane sums of one slot's pairs, after the match has written
-// them (pmx_post.hip has the rest of the scheme): the pairs the block can
-// decide are added to the lane's fp64 accumulators (the same T products as
-// p2plane_body, PointToPlane.cpp:194-243), the quantile window's are
-// recorded for the pick.  With TrimmedDist at chain position 0 a pair whose
-// key is below the window is kept once the window resolves the limit (every
-// kept pair: d <= limit with limit inside the window) and a pair above it is
-// not; without a quantile every pair is decided here.  Counters: kept,
-// non-zero weights (no quantile: inf distances may pass the predicates),
-// finite distances, points with a kept pair.
-// (all lanes of the wave call it; act = the lane holds a slot).  The lane's
-// pairs go into its accumulators (this pass only: no array stays live across
-// the searches), then one transposed wave sum adds them to the wave's LDS row.
-template <typename T, int DIM>
-__device__ __forceinline__ void fuse_chunk(const FuseAcc<T>& fa, SpecAcc<T>& sa, unsigned long long* __restrict__ recs,
-                                           const P4<T>* __restrict__ gpn, const P4<T>* __restrict__ rd,
-                                           const Mat4<T>& Tm, const T* __restrict__ out_d,
-                                           const int32_t* __restrict__ out_i, int64_t j, bool act, int k,
-                                           double* __restrict__ wrow) {
-    using KO = KeyOf<T>;
-    constexpr int NSF = DIM == 3 ? 27 : 9;
-    double acc[kFuseNV];
-#pragma unroll
-    for (int v = 0; v < kFuseNV; ++v) acc[v] = 0.0;
-    if (act) {
-        const T inf = (T)__builtin_huge_val();
-        T px, py, pz;
-        gxform(Tm, gld(rd, j), px, py, pz);
-        bool point_kept = false, appended = false;
-        for (int s = 0; s < k; ++s) {
-            const T d = out_d[j * k + s];
-            const int32_t id = out_i[j * k + s];
-            const bool finite = d != inf;
-            const bool fx = (!fa.fx_finite || finite) && d >= fa.fx_lo && d <= fa.fx_hi;
-            if (finite) acc[NSF + 2] += 1.0;
-            bool keep;
-            if (fa.quantile) {
-                keep = false;
-                if (finite) {
-                    const bool below = KO::key(d) < (typename KO::K)sa.lo;
-                    const unsigned pos = spec_acc<T>(sa, d);
-                    if (pos < kSpecCap) {  // inside the window: decided by the pick
-                        const bool head = fx && !point_kept && !appended;
-                        recs[pos] = (unsigned long long)j << 32 | (fx ? kRecFx : 0ull) | (head ? kRecHead : 0ull) |
-                                    ((unsigned long long)id & kRecPos);
-                        appended = appended || fx;
-                    } else {
-                        keep = below && fx;
-                    }
-                }
-            } else {
-                if (fx) acc[NSF + 1] += 1.0;  // (w != 0).count(): may include an infinite distance
-                keep = fx && finite;
-            }
-            if (keep) {
-                acc[NSF] += 1.0;
-                point_kept = true;
-                p2plane_add<T, DIM, kFuseNV>(acc, px, py, pz, gld(gpn, 2 * (int64_t)id),
-                                             gld(gpn, 2 * (int64_t)id + 1));
-            }
-        }
-        if (point_kept) acc[NSF + 3] += 1.0;
-    }
-    int idx;
-    const double w = wave_transpose_sum<kFuseNV>(acc, idx);
-    if (transpose_writer<kFuseNV>()) wrow[idx] += w;
-}
-
 // ------------------------------------------------------- per-lane kernel --
-// occupancy hint of the per-lane kernel (waves per SIMD; 0 = the compiler's
-// choice).  The search is bound by dependent gather latency, so more resident
-// waves hide more of it, as long as the register cap does not spill.
-// XCD-aware block order of the per-lane kernel (PMX_LANE_XCD, default on)
-#ifndef PMX_LANE_XCD
-#define PMX_LANE_XCD 1
-#endif
-#ifndef PMX_LANE_WPE
-#define PMX_LANE_WPE 0
-#endif
-#if PMX_LANE_WPE > 0
-#define PMX_LANE_ATTR __attribute__((amdgpu_waves_per_eu(PMX_LANE_WPE)))
-#else
-#define PMX_LANE_ATTR
-#endif
-// BOX: the instance with the LDS box path (launched with dynamic LDS while
-// many queries need a full search); the plain instance keeps the reuse
-// path's registers and occupancy
-// FUSE: the fused point-to-plane instance (pmx_post.hip): every block
-// writes one record of sums
-template <typename T, int KT, bool BOX, bool FUSE>
-__global__ __launch_bounds__(256, 4) PMX_LANE_ATTR void grid_lane_kernel(const P4<T>* __restrict__ gpts,
+// Phase 1 (the reuse certificate) takes LaneQ slots per thread, its loads
+// staged so that a thread keeps every slot's chain in flight; phase 2 (full
+// searches) takes the block's misses 256 at a time.  One slot per thread:
+// measured at C3 with 4 (blocks of 1024 slots) the converged match went
+// 25-27 -> 23-26 us, but the first match after the cold one (every query a
+// full search) 217 -> 349 us — a block's four rounds of full searches run
+// back to back instead of being spread over the CUs as separate blocks.
+template <int KT>
+struct LaneQ {
+    static constexpr int value = 1;
+};
+
+// XCD-aware block order of the per-lane kernel (pmx_internal.h xcd_block:
+// adjacent slot ranges gather through one L2; match HBM traffic 75.3 -> 66.5
+// MB per launch at C3)
+template <typename T, int KT, int Q>
+__global__ __launch_bounds__(256, 4) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
@@ -917,13 +651,7 @@ __global__ __launch_bounds__(256, 4) PMX_LANE_ATTR void grid_lane_kernel(const P
                                                         int reuse, T* __restrict__ safe, Mat4<T> Tprev,
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
-                                                        SpecSel* __restrict__ spec, unsigned long long* __restrict__ vout,
-                                                        int* __restrict__ iter_err, SelectState* __restrict__ spec_st,
-                                                        unsigned long long* __restrict__ xseg,
-                                                        const T* __restrict__ radii, uint32_t box_bytes,
-                                                        int box_grow, FuseAcc<T> fa) {
-    extern __shared__ __attribute__((aligned(16))) char box_lds[];  // (box_bytes: the launch's dynamic LDS)
-    const P4<T>* gpn = nullptr;  // (fused: the level's point / normal records)
+                                                        SpecSel* __restrict__ spec, const T* __restrict__ radii) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -931,7 +659,6 @@ __global__ __launch_bounds__(256, 4) PMX_LANE_ATTR void grid_lane_kernel(const P
         gidx = D.gidx;
         start = D.start;
         G = D.G;
-        gpn = D.gpn;
         ctl_transform(ctl, Tm);
         if (reuse) {
             reuse = ctl->prev_level == ctl->level ? 2 : 1;
@@ -941,90 +668,110 @@ __global__ __launch_bounds__(256, 4) PMX_LANE_ATTR void grid_lane_kernel(const P
     }
     if (!reuse) safe = nullptr;
     uint32_t visits = 0;
-#if PMX_LANE_XCD
-    const int64_t blk = xcd_block();  // (pmx_internal.h: adjacent slot ranges gather through one L2)
-#else
-    const int64_t blk = blockIdx.x;
-#endif
     // quantile window (pmx_spec.h): every written distance is classified
-    // (fused: by the fused pass, which also records the window's pairs)
     SpecAcc<T> sa;
     spec_acc_init<T>(sa, spec);
-    SpecAcc<T> sw = sa;  // (the writers' view: off when the fused pass classifies)
-    if (FUSE) sw.on = false;
-    // fused: the window's pairs are recorded only while the window is valid
-    // (no window: the post launch reduces every pair itself)
-    const bool fuse_on = FUSE && (!fa.quantile || sa.on);
-    __shared__ double wacc[4 * kFuseNV];
-    if (FUSE)
-        for (int v = threadIdx.x; v < 4 * kFuseNV; v += blockDim.x) wacc[v] = 0.0;
-    // Phase 1: every lane tries the certificate (reuse 2; otherwise every
-    // query misses).  Phase 2: the block's misses, compacted in slot order,
-    // run the full search on consecutive lanes — from an LDS box of the grid
-    // when the launch has one and enough lanes missed (pmx_grid_box.inc),
-    // else the per-lane shell walk (a miss does not make its whole wave pay
-    // for both paths).
-    __shared__ int miss[256];
-    __shared__ int wave_cnt[4];
+    constexpr int B = 256 * Q;  // slots of the block
+    __shared__ int miss[B];
+    __shared__ int wave_cnt[Q][4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long full_total = 0;
-    {
-        const int64_t base = blk * 256;
-        const int64_t j = base + threadIdx.x;
-        bool missed = j < N;
-        if (reuse == 2 && j < N) {
-            const P4<T> p = gld(rd, j);
-            T qx, qy, qz;
-            gxform(Tm, p, qx, qy, qz);
-            missed = !reuse_query<T, KT>(gpts, gidx, p, qx, qy, qz, Tprev, j, k, qr2(radii, j, maxR2), out_d, out_i,
-                                         safe, visits, sw);
+    const int64_t base = (int64_t)xcd_block() * B;
+    bool missed[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) missed[q] = base + q * 256 + threadIdx.x < N;
+    if (reuse == 2) {
+        // the certificate (reuse_query's rule) for the thread's Q slots, in
+        // stages so that each stage's loads are in flight together.  A list
+        // kept for reuse holds k <= KT - 1 entries (room for the (k+1)-th:
+        // the safe radius); KT = 16 keeps no room and never certifies.
+        constexpr int KR = KT > 1 ? KT - 1 : 1;
+        P4<T> p[Q];
+        T rs[Q], dkp[Q];
+        int32_t id[Q][KR];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int64_t j = missed[q] ? base + q * 256 + threadIdx.x : base;  // (base < N: an in-range slot)
+            p[q] = gld(rd, j);
+            rs[q] = safe[j];
+            dkp[q] = out_d[j * k + k - 1];
+#pragma unroll
+            for (int s = 0; s < KR; ++s) id[q][s] = s < k ? out_i[j * k + s] : 0;
         }
-        const unsigned long long m = __ballot(missed);
-        if (lane == 0) wave_cnt[wave] = __popcll(m);
-        __syncthreads();
-        int off = 0, total = 0;
+        bool ok[Q];
+        double bq[Q];
+        T qx[Q], qy[Q], qz[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            gxform(Tm, p[q], qx[q], qy[q], qz[q]);
+            bool o = missed[q] && k <= KR && rs[q] > (T)0 && dkp[q] < (T)__builtin_huge_val();
+#pragma unroll
+            for (int s = 0; s < KR; ++s) o = o && id[q][s] >= 0;
+            T ox, oy, oz;
+            gxform(Tprev, p[q], ox, oy, oz);
+            const double ex = (double)qx[q] - (double)ox, ey = (double)qy[q] - (double)oy,
+                         ez = (double)qz[q] - (double)oz;
+            const double delta = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + kReuseMargin);
+            const double av = sqrt((double)dkp[q]) * (1.0 + kReuseMargin) + delta;
+            bq[q] = (double)rs[q] * (1.0 - kReuseMargin) - delta;
+            ok[q] = o && av < bq[q];
+        }
+        P4<T> r[Q][KR];
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+            for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < k ? (uint32_t)id[q][s] : 0u);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (!ok[q]) continue;
+            // the same k points: new distances, sorted as a full search sorts them
+            const int64_t j = base + q * 256 + threadIdx.x;
+            T kd[KT];
+            int32_t ki[KT];
+#pragma unroll
+            for (int s = 0; s < KT; ++s) {
+                kd[s] = (T)__builtin_huge_val();
+                ki[s] = kNoPos;
+            }
+#pragma unroll
+            for (int s = 0; s < KR; ++s)
+                if (s < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx[q], qy[q], qz[q], r[q][s]), id[q][s]);
+            visits += (uint32_t)k;
+            write_out<T, KT>(j, k, qr2(radii, j, maxR2), kd, ki, out_d, out_i, sa);
+            safe[j] = (T)(bq[q] * (1.0 - 1e-6));
+            missed[q] = false;
+        }
+    }
+    // the block's misses, compacted in slot order
+    unsigned long long mq[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        mq[q] = __ballot(missed[q]);
+        if (lane == 0) wave_cnt[q][wave] = __popcll(mq[q]);
+    }
+    __syncthreads();
+    int total = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        int off = total;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-            const int cw = wave_cnt[w];
+            const int cw = wave_cnt[q][w];
             off += w < wave ? cw : 0;
             total += cw;
         }
-        if (missed) miss[off + __popcll(m & ((1ull << lane) - 1))] = threadIdx.x;
-        __syncthreads();
-        if (BOX && total >= kBoxMinMiss && !oct) {
-            box_phase<T, KT>(gpts, gidx, start, G, rd, base, miss, total, Tm, k, maxR2, radii, out_d, out_i, safe,
-                             visits, sw, box_lds, box_bytes, reuse == 2 ? -1 : box_grow, reuse, Tprev);
-        } else if ((int)threadIdx.x < total) {
-            const int64_t j2 = base + miss[threadIdx.x];
-            full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe,
-                              visits, sw);
-        }
-        full_total += (unsigned long long)total;
-        if (FUSE) {
-            __syncthreads();  // (the misses' outputs were written by other lanes of the block)
-            if (fuse_on) {
-                unsigned long long* recs = spec ? spec->recs : nullptr;
-                double* wrow = wacc + wave * kFuseNV;
-                if (fa.dim == 3)
-                    fuse_chunk<T, 3>(fa, sa, recs, gpn, rd, Tm, out_d, out_i, j, j < N, k, wrow);
-                else
-                    fuse_chunk<T, 2>(fa, sa, recs, gpn, rd, Tm, out_d, out_i, j, j < N, k, wrow);
-            }
-        }
+        if (missed[q]) miss[off + __popcll(mq[q] & ((1ull << lane) - 1))] = q * 256 + threadIdx.x;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
+        const int64_t j2 = base + miss[t];
+        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
+                          sa);
+        if (Q == 1) break;
     }
     add_visits(visits, visited);
     // queries that took the full search (the "fallback" counter the level choice reads)
-    if (threadIdx.x == 0 && visited && full_total && reuse) atomicAdd(vslot(visited, 1), full_total);
-    if (sa.on) spec_acc_flush<T>(FUSE ? sa : sw, vslot(visited, 2), vslot(visited, 3));
-    if (FUSE) {
-        __syncthreads();  // (every wave's rows)
-        // the block's record, block-major (the post launch sums the records in block order)
-        if (threadIdx.x < kFuseNV)
-            fa.partials[(int64_t)blockIdx.x * kFuseNV + threadIdx.x] =
-                ((wacc[threadIdx.x] + wacc[kFuseNV + threadIdx.x]) + wacc[2 * kFuseNV + threadIdx.x]) +
-                wacc[3 * kFuseNV + threadIdx.x];
-    }
-    if (vout) counter_fold<T>(visited, vout, iter_err, spec, spec_st, xseg);
+    if (threadIdx.x == 0 && visited && total && reuse) atomicAdd(vslot(visited, 1), (unsigned long long)total);
+    if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
 }
 
 // ------------------------------------------------------------ tile kernel --
@@ -1035,31 +782,17 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                      unsigned long long* vout, int* iter_err, SelectState* spec_st, unsigned long long* xseg,
-                      const T* radii, uint32_t box_bytes, int box_grow, bool cold, const FuseAcc<T>& fa,
-                      hipStream_t s) {
-    if (cold) {  // a new reading's first match without an LDS box: the tile kernel's cold form (pmx_grid_tile.inc)
+                      const T* radii, bool cold, hipStream_t s) {
+    if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
                            G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
                            ctl, gd, spec, ru.safe);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
-        const int64_t grid = (N + 255) / 256;
-#define PMX_LANE(B, F)                                                                                                 \
-    hipLaunchKernelGGL((grid_lane_kernel<T, KT, B, F>), dim3((unsigned)grid), dim3(256), box_bytes, s, gpts, gidx, start, \
-                       G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev, ctl, \
-                       gd, spec, vout, iter_err, spec_st, xseg, radii, box_bytes, box_grow, fa)
-        if (box_bytes > 0) {
-            if (fa.on)
-                PMX_LANE(true, true);
-            else
-                PMX_LANE(true, false);
-        } else {
-            if (fa.on)
-                PMX_LANE(false, true);
-            else
-                PMX_LANE(false, false);
-        }
-#undef PMX_LANE
+        constexpr int Q = LaneQ<KT>::value;
+        const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
+        hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
+                           rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
+                           ctl, gd, spec, radii);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -1074,13 +807,10 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                       SelectState* spec_st, unsigned long long* xseg, bool fold, bool defer, const T* radii,
-                       uint32_t box_bytes, int box_grow, bool cold, const FuseAcc<T>& fa, hipEvent_t ev_end,
+                       SelectState* spec_st, unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end,
                        hipStream_t s) {
     if (N <= 0) return;
-    if (mode < 1) box_bytes = 0;
-    cold = cold && mode >= 1 && box_bytes == 0;
-    fold = fold && mode >= 1 && visited && vout && !cold;  // (a cold launch runs the counter kernel after it)
+    cold = cold && mode >= 1;
     if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
@@ -1089,37 +819,30 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     }
     G.h = h;
     G.inv_h = 1.0 / h;
-    if (knn > kLaneMaxK) {  // a k-list spread over a wave per query (pmx_knn_wide.hip; no reuse, no fused sums)
+    if (knn > kLaneMaxK) {  // a k-list spread over a wave per query (pmx_knn_wide.hip; no reuse)
         launch_knn_wide<T>(gpts, gidx, start, &G, 0, rd, N, Tm, knn, maxR2, radii, dists, ids, visited, ctl, gd, spec,
                            s);
-        if (ev_end) (void)hipEventRecord(ev_end, s);
-        if (visited && vout && !defer)
-            hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
-                               spec_st, xseg);
-        return;
-    }
+    } else {
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, fold ? vout : nullptr, iter_err, spec_st, xseg, radii, box_bytes, box_grow, cold, \
-                     fa, s)
-    // with reuse the list keeps room for the (k+1)-th point (the safe radius;
-    // the cold tile writes radius 0 and keeps k entries)
-    const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
-    if (kl == 1)
-        PMX_KT(1);
-    else if (kl <= 2)
-        PMX_KT(2);
-    else if (kl <= 4)
-        PMX_KT(4);
-    else if (kl <= 8)
-        PMX_KT(8);
-    else
-        PMX_KT(16);
+                     ru, ctl, gd, spec, radii, cold, s)
+        // with reuse the list keeps room for the (k+1)-th point (the safe radius;
+        // the cold tile writes radius 0 and keeps k entries)
+        const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
+        if (kl == 1)
+            PMX_KT(1);
+        else if (kl <= 2)
+            PMX_KT(2);
+        else if (kl <= 4)
+            PMX_KT(4);
+        else if (kl <= 8)
+            PMX_KT(8);
+        else
+            PMX_KT(16);
 #undef PMX_KT
-    if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel, with the folded counter phase)
-    // (folded: the per-lane kernel's last workgroup ran it; deferred: the
-    // select_all launch that follows runs it, pmx_select.hip)
-    if (visited && vout && !fold && !defer && !fa.on)
+    }
+    if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel)
+    if (visited && vout)
         hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
                            spec_st, xseg);
 }
@@ -1129,15 +852,13 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, bool, bool, const float*, uint32_t, int, bool,
-                                       const FuseAcc<float>&, hipEvent_t, hipStream_t);
+                                       unsigned long long*, const float*, bool, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, bool, bool, const double*, uint32_t, int, bool,
-                                        const FuseAcc<double>&, hipEvent_t, hipStream_t);
+                                        unsigned long long*, const double*, bool, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,
@@ -1162,7 +883,7 @@ void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, 
 // first ICP iteration.
 void preload_grid() {
     hipFuncAttributes a;
-    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1, false, false>));
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1, 1>));
 }
 
 }  // namespace pmx

@@ -162,27 +162,6 @@ struct GridReuse {
     T* safe = nullptr;
     Mat4<T> Tprev{};
 };
-// ---- the point-to-plane sums fused into the match (pmx_post.hip) ----
-// Per match block one record of kFuseNV doubles (block-major): the system
-// (NS + NF sums of T products, PointToPlane.cpp:194-243) of the pairs the
-// block could decide, then kept pairs, non-zero weights, finite distances and
-// points with a kept pair.  With TrimmedDist at chain position 0 the pairs
-// whose key lies below the quantile window are the decided ones (kept once
-// the window resolves the limit); the window's own pairs are recorded
-// (SpecSel::recs) and added after the pick.
-constexpr int kFuseNV = 32;
-template <typename T>
-struct FuseAcc {
-    int on = 0;
-    int quantile = 0;           // chain position 0 is TrimmedDist (window decided)
-    int dim = 3;
-    T fx_lo = 0, fx_hi = 0;     // the other predicates as one interval (chain_resolve's form)
-    int fx_finite = 0;
-    double* partials = nullptr; // [match blocks][kFuseNV]
-};
-// result offsets of the fused record (NSF = NS + NF)
-__host__ __device__ constexpr int fuse_nsf(int dim) { return dim == 3 ? 27 : 9; }
-
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
 #pragma unroll
@@ -205,20 +184,15 @@ void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* star
 // mode 0 = wave-cooperative LDS tiles, 1 = per-lane shell search (default),
 // 2 = octant block first.  ids written are positions in gpts;
 // launch_pos_to_index maps them back.  ctl / gd (device loop, modes 1-2):
-// transform and level are read on the device.  box_bytes > 0: the launch's
-// dynamic LDS for the blocks' full searches (pmx_grid_box.inc), box_grow the
-// cells a box of a match without usable reuse grows by.
+// transform and level are read on the device.  cold: a new reading's first
+// match (no previous match to certify from) on the tile kernel's cold form.
 template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       unsigned long long* xseg, bool fold, bool defer, const T* radii, uint32_t box_bytes,
-                       int box_grow, bool cold, const FuseAcc<T>& fa, hipEvent_t ev_end, hipStream_t s);
-template <typename T>
-void launch_counter_sum(unsigned long long* vpart, unsigned long long* vout, int* iter_err, const LoopCtl* ctl,
-                        SpecSel* spec, SelectState* st, hipStream_t s);
+                       unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end, hipStream_t s);
 // several ranks: the quantile window's pick over the all-gathered segments
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum
 template <typename T>
@@ -415,22 +389,6 @@ template <typename T>
 void launch_robust_scale(int mode, const SelectState* st, const double* sums, int64_t n, double target,
                          double* scale, hipStream_t s);
 
-// the point-to-plane reduction run by the select launch once the quantile is
-// resolved (device loop, single rank, PMX_SELECT_P2PLANE): on = 0 leaves the
-// launch a plain select
-template <typename T>
-struct P2Fuse {
-    int on = 0;
-    int dim = 3;
-    const P4<T>* rd = nullptr;
-    const T* d = nullptr;
-    const int32_t* ids = nullptr;
-    WChain<T> chain;
-    int k = 1;
-    int64_t N = 0;
-    double* partials = nullptr;
-    const GridDesc<T>* gd = nullptr;
-};
 // ---- quantile / weights (pmx_select.hip) ----
 // one radix-select pass: histogram of digit `pass` among keys matching the
 // resolved prefix.  hist must be zero on entry (select zeroes it on exit).
@@ -444,13 +402,6 @@ void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState
 template <typename T>
 void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
                         const double* ratio_dev, int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s);
-// hist + pick in one launch (single rank; ticket: zeroed uint32, reset on exit)
-template <typename T>
-// spec (may be null): the pass is skipped when the window resolved the
-// quantile; the last pass re-centres the window on the limit it finds
-void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
-                        const double* ratio_dev, unsigned int* ticket, int* iter_err, const LoopCtl* ctl,
-                        SpecSel* spec, hipStream_t s);
 template <typename T>
 int select_passes();
 // every pass in one launch (single rank; pmx_select.hip select_all_kernel):
@@ -461,9 +412,7 @@ int64_t select_all_blocks(int64_t n);
 constexpr int kSelTimeout = -30;  // iteration error: a select_all wait timed out
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
-                       int* iter_err, const LoopCtl* ctl, SpecSel* spec,
-                       unsigned long long* vpart, unsigned long long* vout, const P2Fuse<T>& p2, int64_t grid,
-                       hipStream_t s);
+                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s);
 int select_bins(int pass, int key_bits);
 
 // VarTrimmed pieces
@@ -475,10 +424,7 @@ template <typename T>
 size_t vartrim_scratch_bytes(int64_t n);
 
 // ---- reductions (pmx_reduce.hip) ----
-#ifndef PMX_RED_BLOCKS
-#define PMX_RED_BLOCKS 512
-#endif
-constexpr int kRedBlocks = PMX_RED_BLOCKS;  // fixed reduction grid (deterministic sums)
+constexpr int kRedBlocks = 512;  // fixed reduction grid (deterministic sums)
 constexpr int kNVMax = 48;
 // point-to-plane result layout: upper triangle of A (NS), b (NF), then kept,
 // nonzero weights, rejected matches, rejected points, sum of the weights

@@ -63,48 +63,12 @@ struct LoopState {
     T xsolve[6];  // the rank-deficient solve's result (loop_solve_rank_deficient)
 };
 
-// the fused post-match launch of a device-loop iteration (pmx_post.hip):
-// window pick / radix select, the point-to-plane sums, the step
-struct SelX;
-template <typename T>
-struct PostLaunch {
-    const T* d;
-    const int32_t* ids;
-    const P4<T>* rd;
-    int64_t N;
-    int k;
-    LoopCtl* ctl;
-    const GridDesc<T>* gd;
-    int quantile;
-    double ratio;
-    void* selx;
-    SelectState* st;
-    SpecSel* spec;
-    int* iter_err;
-    unsigned long long* vpart;
-    unsigned long long* vout;
-    const double* fuse_part;
-    int fuse_blocks;
-    double* part2;
-    WChain<T> chain;
-    double* res_out;
-    LoopState<T>* S;
-    LoopCfg cfg;
-    T* trace;
-    int cu_count;
-};
-template <typename T>
-void launch_post(const PostLaunch<T>& p, hipStream_t s);
-void preload_post();
-
 template <typename T>
 void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int prev_level,
                       const double* Tprev, hipStream_t s);
-// partials (may be null): the minimiser's last finalize fused into the step
-// (nblocks x nv block partials, summed into res_out in finalize's order)
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
-                      const double* partials, int nblocks, int nv, double* res_out, hipStream_t s);
+                      hipStream_t s);
 
 }  // namespace pmx

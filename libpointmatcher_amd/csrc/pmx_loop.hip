@@ -26,90 +26,16 @@
 
 namespace pmx {
 
-// The minimiser's last finalize, fused (single rank: no all-reduce between
-// the reduction and the step).  Every kernel boundary costs ~4.5 us on
-// MI355X (the release / acquire of the dispatch across 8 XCD L2s, measured
-// in the kernel trace), so the block sums of finalize_kernel are done here,
-// by the step kernel's 256 threads, in finalize_kernel's exact order (thread
-// t adds blocks t, t + 256, ...; wave butterflies; (w0 + w1) + (w2 + w3)):
-// the system is bit-identical to the unfused path.  fin: kNVMax doubles of
-// LDS; the sums are also stored to out (the host's iteration block).
-__device__ __forceinline__ double step_wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
-// NVC values per block; every thread's loads issued together (the two
-// blocks it adds at kRedBlocks = 512), then the butterflies
-template <int NVC>
-__device__ void fused_finalize_n(const double* __restrict__ partials, int nblocks, double* __restrict__ out,
-                                 double* fin) {
-    __shared__ double red[4][NVC];
-    const int t = threadIdx.x;
-    double s[NVC];
-#pragma unroll
-    for (int v = 0; v < NVC; ++v) s[v] = 0.0;
-    int b = t;
-    for (; b + 256 < nblocks; b += 512) {
-        double x0[NVC], x1[NVC];
-#pragma unroll
-        for (int v = 0; v < NVC; ++v) {
-            x0[v] = partials[(int64_t)v * nblocks + b];
-            x1[v] = partials[(int64_t)v * nblocks + b + 256];
-        }
-#pragma unroll
-        for (int v = 0; v < NVC; ++v) {
-            s[v] += x0[v];
-            s[v] += x1[v];
-        }
-    }
-    for (; b < nblocks; b += 256) {
-#pragma unroll
-        for (int v = 0; v < NVC; ++v) s[v] += partials[(int64_t)v * nblocks + b];
-    }
-#pragma unroll
-    for (int v = 0; v < NVC; ++v) {
-        const double w = step_wave_sum(s[v]);
-        if ((t & 63) == 0) red[t >> 6][v] = w;
-    }
-    __syncthreads();
-    for (int v = t; v < NVC; v += blockDim.x) {
-        const double r = (red[0][v] + red[1][v]) + (red[2][v] + red[3][v]);
-        fin[v] = r;
-        out[v] = r;
-    }
-    __syncthreads();
-}
-__device__ void fused_finalize(const double* __restrict__ partials, int nblocks, int nv, double* __restrict__ out,
-                               double* fin) {
-    switch (nv) {  // (uniform) the value counts of the minimisers' last reductions
-    case 32: fused_finalize_n<32>(partials, nblocks, out, fin); break;  // point-to-plane 3-D
-    case 14: fused_finalize_n<14>(partials, nblocks, out, fin); break;  // point-to-plane 2-D
-    default: fused_finalize_n<9>(partials, nblocks, out, fin); break;   // point-to-point pass 2
-    }
-}
-
-// The step after the minimiser (pmx_step.h).  partials != null: the fused
-// finalize above (256 threads), the system then read from LDS; otherwise res
-// holds it (64 threads).
+// The step after the minimiser (pmx_step.h); res holds the system (one lane
+// runs it; folding the last finalize into this launch measured slower: the
+// 256-thread step launch costs more than the finalize kernel it saves,
+// 0.0821 vs 0.0910 ms per iteration at C3).
 template <typename T, int ROWS, int MIN>
-__global__ __launch_bounds__(256) void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
-                                 const double* __restrict__ res_g, const int* __restrict__ iter_err,
+__global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
+                                 const double* __restrict__ res, const int* __restrict__ iter_err,
                                  const unsigned long long* __restrict__ visited, const T* __restrict__ means,
-                                 LoopCfg cfg, T* __restrict__ trace, const double* __restrict__ partials,
-                                 int nblocks, int nv, double* __restrict__ res_out) {
-    // LDS view of the iteration block's result area: the fused sums land at
-    // their place (point-to-point: the second pass at +16, after the first
-    // pass's sums, which are copied from res_g)
-    __shared__ double fin[64];
+                                 LoopCfg cfg, T* __restrict__ trace) {
     if (ctl->done) return;  // (uniform)
-    const double* res = res_g;
-    if (partials) {
-        const int off = cfg.minimizer == 0 ? 0 : 16;
-        if ((int)threadIdx.x < off) fin[threadIdx.x] = res_g[threadIdx.x];
-        fused_finalize(partials, nblocks, nv, res_out, fin + off);
-        res = fin;
-    }
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     // (every global read of the step first, together: each is a memory round trip)
     const int e = *iter_err;
@@ -159,11 +85,10 @@ void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
-                      const double* partials, int nblocks, int nv, double* res_out, hipStream_t s) {
-    const unsigned th = partials ? 256 : 64;
+                      hipStream_t s) {
 #define PMX_STEP(R, M)                                                                                            \
-    hipLaunchKernelGGL((loop_step_kernel<T, R, M>), dim3(1), dim3(th), 0, s, ctl, S, res, iter_err, visited, means, \
-                       cfg, trace, partials, nblocks, nv, res_out)
+    hipLaunchKernelGGL((loop_step_kernel<T, R, M>), dim3(1), dim3(64), 0, s, ctl, S, res, iter_err, visited, means, \
+                       cfg, trace)
     if (cfg.rows == 4) {
         if (cfg.minimizer == 0)
             PMX_STEP(4, 0);
@@ -177,17 +102,14 @@ void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const in
     }
 #undef PMX_STEP
 }
-
 template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg&, const float*, int, int,
                                       const double*, hipStream_t);
 template void launch_loop_init<double>(LoopCtl*, LoopState<double>*, const LoopCfg&, const double*, int, int,
                                        const double*, hipStream_t);
 template void launch_loop_step<float>(LoopCtl*, LoopState<float>*, const double*, const int*,
-                                      const unsigned long long*, const float*, const LoopCfg&, float*,
-                                      const double*, int, int, double*, hipStream_t);
+                                      const unsigned long long*, const float*, const LoopCfg&, float*, hipStream_t);
 template void launch_loop_step<double>(LoopCtl*, LoopState<double>*, const double*, const int*,
-                                       const unsigned long long*, const double*, const LoopCfg&, double*,
-                                       const double*, int, int, double*, hipStream_t);
+                                       const unsigned long long*, const double*, const LoopCfg&, double*, hipStream_t);
 
 
 // Load this translation unit's code object now (pmx_ctx_create): HIP loads a

@@ -1,6 +1,5 @@
-// pmx_p2plane.h — the point-to-plane accumulation shared by the reduction
-// kernel (pmx_reduce.hip) and the select launch that runs it after the
-// quantile (pmx_select.hip, PMX_SELECT_P2PLANE).
+// pmx_p2plane.h — the point-to-plane accumulation of the reduction kernel
+// (pmx_reduce.hip).
 #pragma once
 
 #include "pmx_internal.h"

@@ -20,7 +20,6 @@
 // argmin, then the same radix select with the optimised ratio.
 #include "pmx_internal.h"
 #include "pmx_spec.h"
-#include "pmx_p2plane.h"
 #include "pmx_selectall.h"
 
 #include <algorithm>
@@ -49,7 +48,7 @@ int select_passes<double>() {
 // non-empty bin.  Pass 0 starts a fresh select (the state is not read).
 template <typename T>
 __device__ __forceinline__ void hist_phase(const T* __restrict__ d, int64_t n, uint32_t* __restrict__ hist,
-                                           const SelectState* __restrict__ st, int pass, uint32_t* lh, int agg) {
+                                           const SelectState* __restrict__ st, int pass, uint32_t* lh) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     int shift, bits;
@@ -61,12 +60,11 @@ __device__ __forceinline__ void hist_phase(const T* __restrict__ d, int64_t n, u
     const K prefix = pass > 0 ? (K)st->prefix : (K)0;
     const int hs = shift + bits;
     if (!skip) {
-        // Neighbouring slots hold neighbouring queries with similar distances,
-        // so the lanes of a wave mostly hit the same few bins: the wave
-        // aggregates equal bins (ballot) and one lane adds the count.
         // Each thread loads kSelPer consecutive keys at once (vector loads,
-        // all in flight: the pass is latency-bound otherwise).
-        const int lane = threadIdx.x & 63;
+        // all in flight: the pass is latency-bound otherwise).  Plain LDS
+        // atomics: aggregating equal bins per wave first measured slower
+        // (pass 0 at C3: 11.4 us plain vs 39.7 us aggregated — a wave of noisy
+        // neighbouring distances sees ~20-30 distinct bins).
         const int64_t tile = (int64_t)blockDim.x * kSelPer;
         for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)gridDim.x * tile) {  // uniform
             const int64_t i0 = base + (int64_t)threadIdx.x * kSelPer;
@@ -75,31 +73,18 @@ __device__ __forceinline__ void hist_phase(const T* __restrict__ d, int64_t n, u
 #pragma unroll
             for (int j = 0; j < kSelPer; ++j) {
                 const K k = KO::key(v[j]);
-                int bin = -1;
                 // +inf (and NaN, and the padding past n) excluded, Matches.cpp:71;
                 // later passes keep the resolved prefix
                 if (k < KO::inf_key && (pass == 0 || (k >> hs) == prefix))
-                    bin = (int)((uint32_t)(k >> shift) & (uint32_t)(nb - 1));
-                if (!agg) {
-                    if (bin >= 0) atomicAdd(&lh[bin], 1u);
-                    continue;
-                }
-                unsigned long long todo = __ballot(bin >= 0);
-                while (todo) {  // wave-uniform: one round per distinct bin
-                    const int leader = __builtin_ctzll(todo);
-                    const int lb = __builtin_amdgcn_readlane(bin, leader);  // SGPR, no LDS round trip
-                    const unsigned long long same = __ballot(bin == lb);
-                    if (lane == leader) atomicAdd(&lh[lb], (uint32_t)__popcll(same));
-                    todo &= ~same;
-                }
+                    atomicAdd(&lh[(uint32_t)(k >> shift) & (uint32_t)(nb - 1)], 1u);
             }
         }
     }
     __syncthreads();
     // flush with returning atomics and wait for the returns: once they are
     // back the adds are performed at the device coherence point, which is
-    // what the fused pass's ticket relies on (no release fence, which would
-    // write back the whole L2)
+    // what select_all_kernel's arrival counters rely on (no release fence,
+    // which would write back the whole L2)
     uint32_t ret = 0;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) {
         const uint32_t c = lh[i];
@@ -111,40 +96,24 @@ __device__ __forceinline__ void hist_phase(const T* __restrict__ d, int64_t n, u
 template <typename T>
 __global__ __launch_bounds__(256) void select_hist_kernel(const T* __restrict__ d, int64_t n,
                                                           uint32_t* __restrict__ hist,
-                                                          const SelectState* __restrict__ st, int pass, int agg,
+                                                          const SelectState* __restrict__ st, int pass,
                                                           const LoopCtl* __restrict__ ctl,
                                                           const SpecSel* __restrict__ spec) {
     __shared__ uint32_t lh[2048];
     if (ctl && ctl->done) return;
     if (spec && spec->hit) return;  // the quantile window resolved it (pmx_spec.h)
-    hist_phase<T>(d, n, hist, st, pass, lh, agg);
-}
-
-// wave aggregation of equal bins before the LDS atomic (PMX_SELECT_AGG=1: on).
-// Off by default: measured on MI355X (C3, 1M distances) pass 0 takes 11.4 us
-// with plain LDS atomics and 39.7 us aggregated — the distances of
-// neighbouring slots are noisy, so a wave sees ~20-30 distinct bins and the
-// per-bin rounds cost more than the LDS bank conflicts they save.
-static int select_agg() {
-    static const int v = [] {
-        const char* e = std::getenv("PMX_SELECT_AGG");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
+    hist_phase<T>(d, n, hist, st, pass, lh);
 }
 
 // Few blocks: every block flushes its non-empty bins with global atomics, and
 // the first digits of squared distances fall into a handful of bins, so more
 // blocks mostly add same-address atomic traffic.
 static int64_t select_blocks(int64_t n) {
-    static const int64_t cap = [] {
-        const char* e = std::getenv("PMX_SELECT_BLOCKS");  // tuning knob
-        // (64: the select_all launch is a no-op whenever the quantile window
-        // resolved the limit, and its cost is then the dispatch of its blocks;
-        // same-box A/B at C3, driver command: 256 -> 81.6, 128 -> 80.4,
-        // 64 -> 80.2, 32 -> 81.0 us per iteration)
-        return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)64;
-    }();
+    // (64: the select_all launch is a no-op whenever the quantile window
+    // resolved the limit, and its cost is then the dispatch of its blocks;
+    // same-box A/B at C3, driver command: 256 -> 81.6, 128 -> 80.4,
+    // 64 -> 80.2, 32 -> 81.0 us per iteration)
+    constexpr int64_t cap = 64;
     int64_t g = (n + 256 * kSelPer - 1) / (256 * kSelPer);
     if (g < 1) g = 1;
     if (g > cap) g = cap;
@@ -159,7 +128,7 @@ template <typename T>
 void launch_select_hist(const T* d, int64_t n, uint32_t* hist, const SelectState* st, int pass, const LoopCtl* ctl,
                         const SpecSel* spec, hipStream_t s) {
     hipLaunchKernelGGL(select_hist_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
-                       pass, select_agg(), ctl, spec);
+                       pass, ctl, spec);
 }
 
 // one block of 256 threads; each thread owns 8 consecutive bins.  Pass 0
@@ -277,80 +246,24 @@ __global__ __launch_bounds__(256) void select_pick_kernel(uint32_t* __restrict__
     pick_phase<T, false>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err, spec);
 }
 
-// One radix-select pass in one launch (single rank): every block builds and
-// flushes its histogram; the last block to finish (ticket counter) resolves
-// the digit.  Saves a launch per pass and the separate pick kernel.
-template <typename T>
-__global__ __launch_bounds__(256) void select_pass_kernel(const T* __restrict__ d, int64_t n,
-                                                          uint32_t* __restrict__ hist, SelectState* __restrict__ st,
-                                                          int pass, double ratio_host,
-                                                          const double* __restrict__ ratio_dev,
-                                                          int* __restrict__ iter_err, int last,
-                                                          unsigned int* __restrict__ ticket, int agg,
-                                                          const LoopCtl* __restrict__ ctl,
-                                                          SpecSel* __restrict__ spec) {
-    __shared__ uint32_t lh[2048];
-    __shared__ unsigned long long part[256];
-    __shared__ unsigned long long s_rank;
-    __shared__ int s_err;
-    __shared__ bool s_last;
-    if (ctl && ctl->done) return;  // (uniform: no block takes a ticket)
-    if (spec && spec->hit) return;  // the quantile window resolved it (pmx_spec.h)
-    hist_phase<T>(d, n, hist, st, pass, lh, agg);
-    __syncthreads();  // every thread's flush has returned
-    if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
-    // the last block: every other block's flush was performed before its
-    // ticket; the bins are read with device-scope atomics (pick_phase)
-    pick_phase<T, true>(hist, st, pass, ratio_host, ratio_dev, iter_err, last, part, s_rank, s_err, spec);
-    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 size_t selx_bytes() { return sizeof(SelX) + (size_t)kSelMaxPasses * 2048 * sizeof(uint32_t); }
 int64_t select_all_blocks(int64_t n) { return select_blocks(n); }
-
-// the point-to-plane reduction after the select, with the limit resolved in
-// this launch (read from LDS: the SelectState in HBM was written by another
-// workgroup of this launch)
-template <typename T>
-__device__ __forceinline__ void p2_after_select(const P2Fuse<T>& p2, const LoopCtl* __restrict__ ctl, double L) {
-    __shared__ SelectState s_lim;
-    if (threadIdx.x == 0) s_lim.limit = L;
-    __syncthreads();
-    WChain<T> ch = p2.chain;
-    ch.st[0] = &s_lim;
-    Mat4<T> Tm;
-    ctl_transform(ctl, Tm);
-    const P4<T>* ref = p2.gd[ctl->level].gpn;
-    if (p2.dim == 3)
-        p2plane_body<T, 3>(p2.rd, Tm, ref, ref + 1, 2, p2.d, p2.ids, ch, p2.k, p2.N, p2.partials);
-    else
-        p2plane_body<T, 2>(p2.rd, Tm, ref, ref + 1, 2, p2.d, p2.ids, ch, p2.k, p2.N, p2.partials);
-}
 
 template <typename T>
 __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
                                                          SelectState* __restrict__ st, double ratio_host,
                                                          const double* __restrict__ ratio_dev,
-                                                         int* __restrict__ iter_err, int agg,
-                                                         const LoopCtl* __restrict__ ctl,
-                                                         SpecSel* __restrict__ spec,
-                                                         unsigned long long* __restrict__ vpart,
-                                                         unsigned long long* __restrict__ vout, P2Fuse<T> p2) {
+                                                         int* __restrict__ iter_err, const LoopCtl* __restrict__ ctl,
+                                                         SpecSel* __restrict__ spec) {
     if (ctl && ctl->done) return;  // (uniform: no block arrives anywhere)
-    double L = 0.0;
-    const bool ok = select_all_body<T>(d, n, sx, st, ratio_host, ratio_dev, iter_err, agg, spec, vpart, vout,
-                                       p2.on != 0, &L);
-    if (p2.on && ok) p2_after_select<T>(p2, ctl, L);
+    select_all_body<T>(d, n, sx, st, ratio_host, ratio_dev, iter_err, spec);
 }
 
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
-                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, unsigned long long* vpart,
-                       unsigned long long* vout, const P2Fuse<T>& p2, int64_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(select_all_kernel<T>, dim3((unsigned)(grid > 0 ? grid : select_blocks(n))), dim3(256), 0, s, d,
-                       n, (SelX*)selx, st, ratio, ratio_dev, iter_err, select_agg(), ctl, spec, vpart, vout, p2);
+                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s) {
+    hipLaunchKernelGGL(select_all_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, (SelX*)selx, st,
+                       ratio, ratio_dev, iter_err, ctl, spec);
 }
 
 template <typename T>
@@ -359,15 +272,6 @@ void launch_select_pick(uint32_t* hist, SelectState* st, int pass, double ratio,
     const int last = pass == select_passes<T>() - 1;
     hipLaunchKernelGGL(select_pick_kernel<T>, dim3(1), dim3(256), 0, s, hist, st, pass, ratio, ratio_dev,
                        iter_err, last, ctl, spec);
-}
-
-template <typename T>
-void launch_select_pass(const T* d, int64_t n, uint32_t* hist, SelectState* st, int pass, double ratio,
-                        const double* ratio_dev, unsigned int* ticket, int* iter_err, const LoopCtl* ctl,
-                        SpecSel* spec, hipStream_t s) {
-    const int last = pass == select_passes<T>() - 1;
-    hipLaunchKernelGGL(select_pass_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, hist, st,
-                       pass, ratio, ratio_dev, iter_err, last, ticket, select_agg(), ctl, spec);
 }
 
 static unsigned grid_for(int64_t n) {
@@ -638,15 +542,9 @@ template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, co
 template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
                                          SpecSel*, hipStream_t);
 template void launch_select_all<float>(const float*, int64_t, void*, SelectState*, double, const double*, int*,
-                                       const LoopCtl*, SpecSel*, unsigned long long*, unsigned long long*,
-                                       const P2Fuse<float>&, int64_t, hipStream_t);
+                                       const LoopCtl*, SpecSel*, hipStream_t);
 template void launch_select_all<double>(const double*, int64_t, void*, SelectState*, double, const double*, int*,
-                                        const LoopCtl*, SpecSel*, unsigned long long*, unsigned long long*,
-                                        const P2Fuse<double>&, int64_t, hipStream_t);
-template void launch_select_pass<float>(const float*, int64_t, uint32_t*, SelectState*, int, double, const double*,
-                                        unsigned int*, int*, const LoopCtl*, SpecSel*, hipStream_t);
-template void launch_select_pass<double>(const double*, int64_t, uint32_t*, SelectState*, int, double, const double*,
-                                         unsigned int*, int*, const LoopCtl*, SpecSel*, hipStream_t);
+                                        const LoopCtl*, SpecSel*, hipStream_t);
 template void launch_vartrim<float>(const float*, int64_t, int, float, float, const float*, void*, size_t, double*,
                                     int*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,
@@ -661,7 +559,7 @@ template size_t vartrim_scratch_bytes<double>(int64_t);
 // first ICP iteration.
 void preload_select() {
     hipFuncAttributes a;
-    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&select_pass_kernel<float>));
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&select_all_kernel<float>));
 }
 
 }  // namespace pmx

@@ -1,7 +1,6 @@
 // pmx_selectall.h — the radix select with every pass in one launch (the
-// select_all_kernel of pmx_select.hip and the fused post-match launch of
-// pmx_post.hip), and the histogram helpers it shares with the per-pass
-// kernels.
+// select_all_kernel of pmx_select.hip), and the histogram helpers it shares
+// with the per-pass kernels of the sharded select.
 #pragma once
 
 #include "pmx_internal.h"
@@ -69,9 +68,11 @@ __device__ __forceinline__ void hzero(uint32_t* h) {
 // pass it reaches), so arrival a belongs to generation a / grid + 1, and the
 // picker of that generation stamps its publication with it.  The waits are
 // bounded (an exit condition every wave reaches): a timeout raises
-// kSelTimeout in the iteration's error word instead of hanging.  All blocks
-// are resident (grid <= 256 blocks of 256 threads, the only kernel running:
-// the stream's previous kernel has completed).
+// kSelTimeout in the iteration's error word instead of hanging.  The grid
+// is clamped to the blocks the device holds at once (select_all_blocks: at
+// most 64 blocks of 256 threads, far below one block per CU), so every block
+// is resident unless other processes fill the GPU; then the bounded waits
+// turn a starved block into an error, not a hang.
 constexpr int kSelMaxPasses = 6;
 struct SelX {
     unsigned int arrive[8];                  // per pass (monotonic)
@@ -79,11 +80,6 @@ struct SelX {
     unsigned long long rank[kSelMaxPasses];  // rank left inside the prefix after pass p
     unsigned long long tot[kSelMaxPasses];   // keys histogrammed in pass p
     unsigned long long count;                // finite keys (pass 0)
-    unsigned long long pre;                  // gen << 56 | window hit: the deferred counter phase's verdict
-    unsigned long long lim;                  // the resolved limit (double bits), for a fused point-to-plane
-    unsigned int post_arrive;                // the fused post launch's reduction tickets (pmx_post.hip; monotonic)
-    unsigned int pad_;
-    unsigned long long nused;                // the window pick's key count, published with a hit verdict
 };
 
 __device__ __forceinline__ unsigned long long ald(unsigned long long* p) {
@@ -94,18 +90,13 @@ __device__ __forceinline__ unsigned long long ast(unsigned long long* p, unsigne
     return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The select itself; true when this block ends with the resolved limit in
-// *L (then, with a fused point-to-plane, it goes on to the reduction).
-// `wait_last`: the non-picker blocks wait for the last pass's publication
-// (they need the limit) instead of leaving.
+// The select itself (every block of select_all_kernel): the resolved
+// limit and select state in *st, the next window re-centred (spec).
 template <typename T>
-__device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
+__device__ __forceinline__ void select_all_body(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
                                                 SelectState* __restrict__ st, double ratio_host,
                                                 const double* __restrict__ ratio_dev, int* __restrict__ iter_err,
-                                                int agg, SpecSel* __restrict__ spec,
-                                                unsigned long long* __restrict__ vpart,
-                                                unsigned long long* __restrict__ vout, bool wait_last, double* L,
-                                                bool* hit_out = nullptr) {
+                                                SpecSel* __restrict__ spec) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     __shared__ uint32_t lh[2048];
@@ -113,65 +104,7 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
     __shared__ unsigned long long s_w[2];  // (published word, its generation)
     __shared__ int s_last;
     __shared__ unsigned int s_old;
-    if (vpart) {
-        // The match's counter phase deferred into this launch (one launch
-        // fewer per iteration): block 0 folds the counters and tries the
-        // window pick, then publishes the verdict (generation-stamped, as the
-        // passes below); a hit ends every block, a miss runs the passes.
-        if (threadIdx.x == 0) s_old = atomicAdd(&sx->arrive[7], 1u);
-        __syncthreads();
-        const unsigned long long pgen = ((unsigned long long)(s_old / gridDim.x) + 1ull) & 0xffull;
-        if (blockIdx.x == 0) {
-            counter_phase<T>(vpart, vout, iter_err, spec, st, nullptr);
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const unsigned long long hit = spec && spec->hit ? 1ull : 0ull;
-                // the limit and the window's key count first (returning: performed
-                // where every block reads them), then the verdict that covers them
-                unsigned long long r0 = hit ? ast(&sx->lim, (unsigned long long)__double_as_longlong(st->limit)) : 0ull;
-                r0 |= hit ? ast(&sx->nused, (unsigned long long)spec->n_used) : 0ull;
-                asm volatile("" ::"v"(r0));
-                (void)ast(&sx->pre, pgen << 56 | hit);
-                s_w[0] = hit;
-                s_w[1] = (unsigned long long)__double_as_longlong(st->limit);
-            }
-            __syncthreads();
-            if (s_w[0]) {
-                *L = __longlong_as_double((long long)s_w[1]);
-                if (hit_out) *hit_out = true;
-                return true;
-            }
-        } else {
-            if (threadIdx.x == 0) {
-                unsigned long long w = 0;
-                bool ok = false;
-                // (a slow poll: block 0's own coherent loads share the path with these)
-                for (int it = 0; it < (1 << 20); ++it) {
-                    w = ald(&sx->pre);
-                    if ((w >> 56) == pgen) {
-                        ok = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(16);
-                }
-                s_w[0] = ok ? (w & 1ull) : 2ull;
-                if (!ok) __hip_atomic_store(iter_err, kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (ok && (w & 1ull)) s_w[1] = ald(&sx->lim);
-            }
-            __syncthreads();
-            if (s_w[0] == 2ull) return false;  // (the wait timed out)
-            if (s_w[0]) {  // the window resolved it
-                *L = __longlong_as_double((long long)s_w[1]);
-                if (hit_out) *hit_out = true;
-                return true;
-            }
-        }
-    } else if (spec && spec->hit) {
-        *L = st->limit;  // (the window resolved it in the counter kernel before this launch)
-        if (hit_out) *hit_out = true;
-        return true;
-    }
-    if (hit_out) *hit_out = false;
+    if (spec && spec->hit) return;  // (the window resolved it in the counter kernel before this launch)
     constexpr int passes = KO::bits == 32 ? 3 : 6;
     uint32_t* hist0 = reinterpret_cast<uint32_t*>(sx + 1);
     const int t = threadIdx.x;
@@ -188,7 +121,6 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
         __syncthreads();
         {
             const int hs = shift + bits;
-            const int lane = t & 63;
             const int64_t tile = (int64_t)256 * kSelPer;
             for (int64_t base = (int64_t)blockIdx.x * tile; base < n; base += (int64_t)G * tile) {
                 T v[kSelPer];
@@ -196,21 +128,8 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
 #pragma unroll
                 for (int j = 0; j < kSelPer; ++j) {
                     const K k = KO::key(v[j]);
-                    int bin = -1;
                     if (k < KO::inf_key && (pass == 0 || (k >> hs) == prefix))
-                        bin = (int)((uint32_t)(k >> shift) & (uint32_t)(nb - 1));
-                    if (!agg) {
-                        if (bin >= 0) atomicAdd(&lh[bin], 1u);
-                        continue;
-                    }
-                    unsigned long long todo = __ballot(bin >= 0);
-                    while (todo) {
-                        const int leader = __builtin_ctzll(todo);
-                        const int lb = __builtin_amdgcn_readlane(bin, leader);
-                        const unsigned long long same = __ballot(bin == lb);
-                        if (lane == leader) atomicAdd(&lh[lb], (uint32_t)__popcll(same));
-                        todo &= ~same;
-                    }
+                        atomicAdd(&lh[(uint32_t)(k >> shift) & (uint32_t)(nb - 1)], 1u);
                 }
             }
         }
@@ -316,21 +235,17 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
                 } else {
                     r0 |= ast(&sx->rank[pass], nrank);
                 }
-                if (pass == passes - 1 && !err) r0 |= ast(&sx->lim, (unsigned long long)__double_as_longlong((double)KO::val(np)));
                 // publish once the data above has returned (performed where every block reads it)
                 asm volatile("" ::"v"(r0));
                 (void)ast(&sx->go[pass],
                           gen << 56 | (err ? 1ull << 55 : 0ull) | ((unsigned long long)np & ((1ull << 55) - 1)));
             }
-            if (err) return false;
+            if (err) return;
             prefix = np;
             __syncthreads();
-            if (pass == passes - 1) {
-                *L = (double)KO::val(np);
-                return true;
-            }
+            if (pass == passes - 1) return;
         } else {
-            if (pass == passes - 1 && !wait_last) return false;  // (the picker finishes alone)
+            if (pass == passes - 1) return;  // (the picker finishes alone)
             // ---- wait for this generation's publication (bounded) ----
             if (t == 0) {
                 unsigned long long w = 0;
@@ -349,17 +264,10 @@ __device__ __forceinline__ bool select_all_body(const T* __restrict__ d, int64_t
             }
             __syncthreads();
             const unsigned long long w = s_w[0];
-            if (!s_w[1] || (w >> 55) & 1ull) return false;  // timeout, or the quantile failed
+            if (!s_w[1] || (w >> 55) & 1ull) return;  // timeout, or the quantile failed
             prefix = (K)(w & ((1ull << 55) - 1));
-            if (pass == passes - 1) {  // (wait_last) the published final limit
-                if (threadIdx.x == 0) s_w[0] = ald(&sx->lim);
-                __syncthreads();
-                *L = __longlong_as_double((long long)s_w[0]);
-                return true;
-            }
         }
     }
-    return false;
 }
 
 }  // namespace pmx

@@ -79,15 +79,7 @@ struct SpecSel {
     int hit;                    // this iteration's limit came from the window
     unsigned long long n_hit, n_miss;  // statistics (host-readable)
     double dens;                // key density estimate of the last radix select (keys per key unit)
-    // the match's point-to-plane sums fused in (pmx_post.hip): one record per
-    // appended key, slot << 32 | passes-the-other-predicates << 31 | first of
-    // its point << 30 | grid position; n_used = the keys the last pick saw
-    unsigned long long* recs;   // [kSpecCap]
-    unsigned int n_used;
-    int pad_;
 };
-// record fields (see SpecSel::recs)
-constexpr unsigned long long kRecFx = 1ull << 31, kRecHead = 1ull << 30, kRecPos = (1ull << 30) - 1;
 
 // ---- match side: classify every distance the match writes ----
 template <typename T>
@@ -244,7 +236,6 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
         if (t == 0) {
             sp->hit = 0;
             sp->n_miss += 1;
-            sp->n_used = 0;
             sp->n_keys = 0;
         }
         return false;
@@ -311,7 +302,6 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
         st->limit = (double)KO::val(kl);
         sp->hit = 1;
         sp->n_hit += 1;
-        sp->n_used = (unsigned)nk;
         sp->n_keys = 0;
         const double width = (double)(hi - lo) + 1.0;
         spec_update<T>(sp, kl, (double)nk / width);

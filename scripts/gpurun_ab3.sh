@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of env variants on the driver command (interleaved, R rounds),
 # then an optional kernel trace of one variant.
-#   AB="A=1 B=2" R=2 PROF_ENV="PMX_FUSED=1" scripts/gpurun_ab3.sh
+#   AB="A=1 B=2" R=2 PROF_ENV="PMX_GRID_REUSE=0" scripts/gpurun_ab3.sh
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R0="$(pwd)"

@@ -20,7 +20,7 @@ if [[ "$ARGS" == *" quick "* ]]; then
   step bench_driver && timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_driver.json 2> gpurun_out/bench_driver.err || { tail -20 gpurun_out/bench_driver.err; exit 1; }
 fi
 if [[ "$ARGS" == *" ab "* ]]; then
-  for v in ${AB:-PMX_FUSED=1}; do
+  for v in ${AB:-PMX_GRID_REUSE=0}; do
     step "bench_ab $v" && env $v timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "gpurun_out/bench_ab_$v.json" 2> gpurun_out/bench_ab.err || { tail -20 gpurun_out/bench_ab.err; exit 1; }
   done
 fi
@@ -36,5 +36,13 @@ fi
 if [[ "$ARGS" == *" prof "* ]]; then
   step prof && (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1) || { tail -20 gpurun_out/prof.log; exit 1; }
   python tools/kstats_quick.py gpurun_out/prof 24 > gpurun_out/prof_summary.txt 2>&1 || true
+fi
+if [[ "$ARGS" == *" pmc "* ]]; then
+  # the driver command's kernel trace + FETCH_SIZE / WRITE_SIZE in separate passes -> per-phase traffic
+  CMD="$R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --device-warmup 0.05"
+  step pmc_trace && (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/pmc_trace" -o run --output-format csv -- python3 $CMD > "$R/gpurun_out/pmc_trace.log" 2>&1) || exit 1
+  step pmc_fetch && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/pmc_fetch" -o run --output-format csv -- python3 $CMD > "$R/gpurun_out/pmc_fetch.log" 2>&1) || exit 1
+  step pmc_write && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/pmc_write" -o run --output-format csv -- python3 $CMD > "$R/gpurun_out/pmc_write.log" 2>&1) || exit 1
+  python tools/pmc_phases.py gpurun_out/pmc_trace gpurun_out/pmc_fetch gpurun_out/pmc_write 5 20 "python bench.py --steps 20 --warmup 5 --no-cpu-baseline" > gpurun_out/pmc_c3_driver.json 2> gpurun_out/pmc_phases.err || true
 fi
 step "done"

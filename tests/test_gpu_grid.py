@@ -13,21 +13,17 @@ from libpointmatcher_amd.synth import random_cloud, reading_cloud, reference_clo
 pytestmark = pytest.mark.gpu
 
 # every test runs against each grid search form: the per-lane kernel (default),
-# the same with its LDS box for full searches (pmx_grid_box.inc), a box
-# budget too small for most blocks (whole-block
-# fallback), boxes that never grow (lanes leave the box: per-lane fallback),
-# coarse / fine levels, no temporal reuse, and the wave-cooperative tile kernel
+# the octant block first, coarse / fine levels, no temporal reuse, and the
+# wave-cooperative tile kernel (with a box budget that sends most lanes to the
+# per-lane fallback)
 MODES = {"lane": {}, "lane_coarse": {"PMX_GRID_PPC": "32"}, "octant": {"PMX_GRID_MODE": "octant"},
          "lane_noreuse": {"PMX_GRID_REUSE": "0"}, "lane_fine": {"PMX_GRID_PPC": "1"},
-         "box": {"PMX_BOX_LDS": "49152"}, "box_tight": {"PMX_BOX_LDS": "3072"},
-         "box_grow0": {"PMX_BOX_LDS": "49152", "PMX_BOX_GROW": "0"},
          "tile": {"PMX_GRID_MODE": "tile"}, "tile_fallback": {"PMX_GRID_MODE": "tile", "PMX_GRID_TILE_MAX": "16"}}
 
 
 @pytest.fixture(autouse=True, params=sorted(MODES))
 def grid_mode(request, monkeypatch):
-    for k in ("PMX_GRID_MODE", "PMX_GRID_TILE_MAX", "PMX_GRID_PPC", "PMX_GRID_LEVELS", "PMX_GRID_ADAPT", "PMX_GRID_REUSE",
-              "PMX_BOX_LDS", "PMX_BOX_GROW", "PMX_BOX_FIRST"):
+    for k in ("PMX_GRID_MODE", "PMX_GRID_TILE_MAX", "PMX_GRID_PPC", "PMX_GRID_LEVELS", "PMX_GRID_ADAPT", "PMX_GRID_REUSE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in MODES[request.param].items():
         monkeypatch.setenv(k, v)
@@ -205,7 +201,7 @@ def test_temporal_reuse_stays_exact(oracle, grid_mode, k):
     od, oi, _ = oracle.knn(ref, oracle.transform(Tg, rd2), k=k, method="kdtree")
     assert np.array_equal(d, od) and np.array_equal(i, oi)
     ctx.close()
-    if grid_mode in ("lane", "lane_coarse", "lane_fine", "box", "box_tight", "box_grow0"):
+    if grid_mode in ("lane", "lane_coarse", "lane_fine"):
         # the repeated pose was certified from the previous match (k pairs per query)
         # (the adaptive level may move during the first repeats: a level change
         # restarts the reuse chain)

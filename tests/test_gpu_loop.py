@@ -187,7 +187,6 @@ def test_quantile_window_is_exact(monkeypatch, dtype, filt, knn, max_dist):
     radius-limited matches (infinite distances excluded from the count).
     (Oracle parity of the loop with the window on, the default:
     test_loop_equals_modules / _filter_chains.)"""
-    monkeypatch.setenv("PMX_FUSED", "0")  # (the module sequence: bit-exact comparisons)
     ref, nrm = reference_cloud(60000, dtype)
     rd = reading_cloud(50000, dtype)
     out = {}
@@ -208,140 +207,3 @@ def test_quantile_window_is_exact(monkeypatch, dtype, filt, knn, max_dist):
     assert hits + misses == 30 and hits >= 15, (hits, misses)
     assert kept1 == kept0
     assert np.array_equal(tr1, tr0)
-
-
-
-@pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("filt,knn,max_dist", [
-    (("TrimmedDistOutlierFilter", 0.85), 1, np.inf),
-    (("TrimmedDistOutlierFilter", 0.7), 3, 0.05),
-    (("MedianDistOutlierFilter", 3.0), 1, np.inf),
-    (("TrimmedDistOutlierFilter", 1.0), 2, np.inf),
-    (("VarTrimmedDistOutlierFilter", 0.05, 0.99, 2.35), 1, np.inf),
-])
-@pytest.mark.parametrize("window", ["0", "1"])
-def test_select_all_passes_in_one_launch(monkeypatch, dtype, filt, knn, max_dist, window):
-    """The radix select with every pass in one launch (select_all_kernel:
-    in-kernel arrival counters, the last block of each pass picks the digit
-    and publishes it) gives the per-pass kernels' limits bit for bit: whole
-    loops are identical, with and without the quantile window (a window hit
-    makes the launch a no-op), for f32 (3 digits) and f64 (6 digits)."""
-    monkeypatch.setenv("PMX_FUSED", "0")  # (the module sequence: bit-exact comparisons)
-    monkeypatch.setenv("PMX_SPEC_SELECT", window)
-    ref, nrm = reference_cloud(60000, dtype)
-    rd = reading_cloud(50000, dtype)
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("PMX_SELECT_ALL", mode)
-        ctx = _capi.Context(0, dtype)
-        ctx.set_reference(ref, nrm)
-        ctx.set_reading(rd)
-        ctx.loop_begin(knn=knn, max_dist=max_dist, filters=[filt], checkers=[("CounterTransformationChecker", 30)],
-                       keep_trace=True)
-        st = ctx.loop_run(30)
-        out[mode] = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept, st.iterations,
-                     st.last.limit)
-        ctx.close()
-    tr1, s1, kept1, it1, lim1 = out["1"]
-    tr0, s0, kept0, it0, lim0 = out["0"]
-    assert it1 == it0 == 30
-    assert s1 == s0
-    assert kept1 == kept0 and lim1 == lim0
-    assert np.array_equal(tr1, tr0)
-
-
-@pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("knob,off", [("PMX_FOLD_COUNTER", "0"), ("PMX_DEFER_COUNTER", "0"),
-                                      ("PMX_SELECT_P2PLANE", "0")])
-def test_counter_fold_equals_counter_kernel(monkeypatch, dtype, knob, off):
-    """The counter phase and the quantile-window pick folded into the match
-    kernel's last workgroup (PMX_FOLD_COUNTER=1: two-level tickets, coherent
-    loads of the counters and window keys) or deferred to the start of the
-    select_all launch (PMX_DEFER_COUNTER=1: block 0 runs it and publishes
-    the window verdict) leave whole loops bit-identical to the
-    separate counter_sum kernel; the select and the point-to-plane reduction
-    in one launch (PMX_SELECT_P2PLANE=1, off by default: every block reads the
-    limit published in the launch) leave them identical to the two launches."""
-    monkeypatch.setenv("PMX_FUSED", "0")  # (the module sequence: bit-exact comparisons)
-    monkeypatch.setenv("PMX_DEFER_COUNTER", "0" if knob == "PMX_FOLD_COUNTER" else "1")
-    ref, nrm = reference_cloud(60000, dtype)
-    rd = reading_cloud(50000, dtype)
-    out = {}
-    for mode in ("1", off):
-        monkeypatch.setenv(knob, mode)
-        ctx = _capi.Context(0, dtype)
-        ctx.set_reference(ref, nrm)
-        ctx.set_reading(rd)
-        ctx.loop_begin(filters=[("TrimmedDistOutlierFilter", 0.85)],
-                       checkers=[("CounterTransformationChecker", 30)], keep_trace=True)
-        st = ctx.loop_run(30)
-        out[mode] = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept,
-                     st.point_count_touched, st.last.limit)
-        ctx.close()
-    assert out["1"][1] == out[off][1] and out["1"][2:] == out[off][2:]
-    assert np.array_equal(out["1"][0], out[off][0])
-
-
-@pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("filters,knn,max_dist", [
-    ([("TrimmedDistOutlierFilter", {"ratio": 0.85})], 1, np.inf),
-    ([("TrimmedDistOutlierFilter", {"ratio": 0.7}), ("MaxDistOutlierFilter", {"maxDist": 0.05})], 3, np.inf),
-    ([("TrimmedDistOutlierFilter", {"ratio": 0.8}), ("MinDistOutlierFilter", {"minDist": 0.004})], 2, np.inf),
-    ([("TrimmedDistOutlierFilter", {"ratio": 1.0})], 1, 0.05),
-    ([("MaxDistOutlierFilter", {"maxDist": 0.05})], 4, np.inf),
-    ([], 2, 0.08),
-])
-def test_fused_iteration_equals_modules(monkeypatch, oracle, dtype, filters, knn, max_dist):
-    """The fused iteration (pmx_post.hip: the point-to-plane sums in the match,
-    window pick / radix select, the rest of the reduction and the step in one
-    launch) against the module sequence and the oracle: same iteration count,
-    final T within the north-star tolerance, same ErrorElements counts."""
-    ref, nrm = reference_cloud(60000, dtype)
-    rd = reading_cloud(50000, dtype)
-    yaml = chain_yaml(filters=filters, knn=knn, maxdist=max_dist, maxit=20, differential=DIFF)
-    out = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("PMX_FUSED", fused)
-        out[fused] = run_mode(monkeypatch, "loop", yaml, rd, ref, nrm, dtype)
-    (Tf, sf, trf), (Tm, sm, trm) = out["1"], out["0"]
-    assert sf.iterations == sm.iterations
-    assert np.linalg.norm(Tf - Tm) <= TOL[dtype]
-    assert np.abs(trf - trm).max() <= 10 * TOL[dtype]
-    assert abs(sf.kept - sm.kept) <= 1e-4 * sm.kept
-    assert abs(sf.rejected_points - sm.rejected_points) <= 1e-4 * len(rd) + 1
-    assert abs(sf.rejected_matches - sm.rejected_matches) <= 1e-4 * len(rd) * knn + 1
-    cfg = oracle.make_cfg(knn=knn, max_dist=max_dist, filters=tuple((n, p) for n, p in filters), counter_max=20,
-                          differential=DIFF, threads=8)
-    rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm)
-    assert rc == 0 and so.iterations == sf.iterations
-    assert np.linalg.norm(Tf - To) <= TOL[dtype]
-
-
-def test_fused_iteration_2d(monkeypatch, oracle):
-    """2-D point-to-plane (3 x 3 system) through the fused launch."""
-    rng = np.random.default_rng(7)
-    t = rng.uniform(0, 2 * np.pi, 30000)
-    r = 1 + 0.2 * np.sin(5 * t)
-    ref = np.stack([np.cos(t) * r, np.sin(t) * r, np.ones_like(t)], 1).astype(np.float32)
-    tang = np.stack([np.gradient(ref[:, 0]), np.gradient(ref[:, 1])], 1)
-    # normals from the analytic curve: the derivative of (r cos t, r sin t), rotated
-    dr = np.cos(5 * t)
-    dx, dy = dr * np.cos(t) - r * np.sin(t), dr * np.sin(t) + r * np.cos(t)
-    nrm = np.stack([dy, -dx], 1)
-    nrm = (nrm / np.linalg.norm(nrm, axis=1, keepdims=True)).astype(np.float32)
-    del tang
-    c, s = np.cos(0.03), np.sin(0.03)
-    rd = ref.copy()
-    rd[:, :2] = (ref[:, :2].astype(np.float64) @ np.array([[c, -s], [s, c]]).T + [0.01, -0.02]).astype(np.float32)
-    yaml = chain_yaml(filters=[("TrimmedDistOutlierFilter", {"ratio": 0.9})], maxit=25, differential=DIFF)
-    out = {}
-    for fused in ("1", "0"):
-        monkeypatch.setenv("PMX_FUSED", fused)
-        out[fused] = run_mode(monkeypatch, "loop", yaml, rd, ref, nrm, np.float32)
-    (Tf, sf, _), (Tm, sm, _) = out["1"], out["0"]
-    assert sf.iterations == sm.iterations
-    assert np.linalg.norm(Tf - Tm) <= 1e-5
-    cfg = oracle.make_cfg(filters=(("TrimmedDistOutlierFilter", {"ratio": 0.9}),), counter_max=25, differential=DIFF,
-                          threads=8)
-    rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm)
-    assert rc == 0 and so.iterations == sf.iterations and np.linalg.norm(Tf - To) <= 1e-5

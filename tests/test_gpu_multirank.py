@@ -285,7 +285,6 @@ def test_rccl_one_rank_is_bit_identical(oracle, dn, monkeypatch):
     runs the module chain here: its fused iteration sums in another order.)"""
     from libpointmatcher_amd import _capi
 
-    monkeypatch.setenv("PMX_FUSED", "0")
 
     dtype = np.dtype(dn)
     rd, ref, nrm = _clouds(dtype)

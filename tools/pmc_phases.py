@@ -2,14 +2,14 @@
 
 usage: python tools/pmc_phases.py TRACE_DIR FETCH_DIR WRITE_DIR W K "COMMAND" > out.json
 
-bench.py runs, in this order on the context stream (device loop, one ICP
-object): pass A = prepare + W warmup + K timed iterations (the timed region);
-pass B = prepare + 1 cold + W-1 + K iterations with HIP events around every
-match launch (the live roofline measurement); then the parity ICP.  Every
-iteration launches the match kernel once, so the match kernel's n-th dispatch
-belongs to iteration n of that sequence.  This tool averages the kernel trace
-durations and the PMC counters (separate rocprofv3 --pmc runs of the same
-command, dispatches aligned by their order) over:
+bench.py (with --no-cpu-baseline) ends, on the context stream (device loop,
+one ICP object), with pass A = prepare + W warmup + K timed iterations (the
+timed region) and pass B = prepare + W + K iterations with HIP events around
+every match launch (the live roofline measurement); nothing is dispatched
+after pass B.  Every iteration launches the match kernel once, so the last
+2 (W + K) match dispatches are the two passes.  This tool averages the kernel
+trace durations and the PMC counters (separate rocprofv3 --pmc runs of the
+same command, dispatches aligned by their order) over:
   timed      pass A, iterations W .. W+K-1 (what ms_per_step covers)
   roofline   pass B, iterations W .. W+K-1 (what bench.py's live events time)
   cold       pass A, iteration 0 (the first match at the initial pose)
@@ -26,7 +26,7 @@ import sys
 
 # (the match of a new reading's first iteration is the tile kernel's cold form)
 KERNELS = {"match": ("grid_lane_kernel", "grid_tile_kernel"), "p2plane": "p2plane_partial_kernel", "tail": "loop_tail_kernel",
-           "step": "loop_step_kernel", "counter_sum": "counter_sum_kernel", "select": "select_pass_kernel",
+           "step": "loop_step_kernel", "counter_sum": "counter_sum_kernel", "select": "select_all_kernel",
            "finalize": "finalize_kernel"}
 
 
@@ -49,8 +49,9 @@ def main():
     tr = rows(tdir, "*kernel_trace.csv")
     fe = [x for x in rows(fdir, "*counter_collection.csv") if x["Counter_Name"] == "FETCH_SIZE"]
     wr = [x for x in rows(wdir, "*counter_collection.csv") if x["Counter_Name"] == "WRITE_SIZE"]
-    phases = {"timed": (W, W + K), "roofline": (2 * (W + K) + W - (W + K), 2 * (W + K)), "cold": (0, 1)}
-    phases["roofline"] = (W + K + W, W + K + W + K)
+    n = len(series(tr, KERNELS["match"], lambda x: 0))
+    a0 = n - 2 * (W + K)  # (pass A's first match)
+    phases = {"timed": (a0 + W, a0 + W + K), "roofline": (n - K, n), "cold": (a0, a0 + 1)}
     out = {"command": cmd, "warmup": W, "steps": K,
            "unit": "ns per launch; bytes per launch (fetch = 2 x FETCH_SIZE, gfx950 correction; write exact)",
            "phases": {k: f"match dispatches [{a}, {b})" for k, (a, b) in phases.items()}}
@@ -64,18 +65,21 @@ def main():
         res = {"launches": len(dur), "launches_per_match": per_it}
 
         def avg(a, lo, hi):
-            s = a[lo:hi]
+            # (slices counted from the end: the device warm-up before the
+            # passes is time-based, so the runs differ in their first launches)
+            lo_e, hi_e = lo - len(dur), hi - len(dur)
+            s = a[lo_e:hi_e if hi_e < 0 else None] if len(a) >= -lo_e else []
             return sum(s) / len(s) if s else None
 
         def summarize(lo, hi):
             d = avg(dur, lo, hi)
-            ff = avg(f, lo, hi) if len(f) == len(dur) else None
-            ww = avg(w, lo, hi) if len(w) == len(dur) else None
+            ff = avg(f, lo, hi)
+            ww = avg(w, lo, hi)
             return {"avg_ns": d, "fetch_bytes_per_launch": ff, "write_bytes_per_launch": ww,
                     "hbm_bytes_per_launch": (ff + ww) if ff is not None and ww is not None else None,
                     "launches_averaged": len(dur[lo:hi])}
 
-        res["all"] = summarize(0, len(dur))
+        res["all"] = {"avg_ns": sum(dur) / len(dur), "launches_averaged": len(dur)}
         if per_it == 1.0:  # one launch per iteration: phase slices are meaningful
             for ph, (a, b) in phases.items():
                 res[ph] = summarize(a, b)
