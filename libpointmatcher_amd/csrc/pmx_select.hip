@@ -152,13 +152,9 @@ __device__ __forceinline__ void pick_phase(uint32_t* __restrict__ hist, SelectSt
     unsigned long long mine = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) mine += hv[j];
-    part[t] = mine;
-    __syncthreads();
-    // inclusive scan (Hillis-Steele) over 256 partials
-    for (int off = 1; off < 256; off <<= 1) {
-        unsigned long long v = t >= off ? part[t - off] : 0ull;
-        __syncthreads();
-        part[t] += v;
+    {  // inclusive scan over the 256 partials (pmx_spec.h block_incl_scan)
+        __shared__ unsigned long long wsum[4];
+        part[t] = block_incl_scan<256>(mine, wsum);
         __syncthreads();
     }
     if (t == 0) {

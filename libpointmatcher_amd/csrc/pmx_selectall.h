@@ -157,12 +157,9 @@ __device__ __forceinline__ void select_all_body(const T* __restrict__ d, int64_t
             unsigned long long mine = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) mine += hv[j];
-            part[t] = mine;
-            __syncthreads();
-            for (int off = 1; off < 256; off <<= 1) {
-                const unsigned long long v = t >= off ? part[t - off] : 0ull;
-                __syncthreads();
-                part[t] += v;
+            {  // inclusive scan over the 256 partials (pmx_spec.h block_incl_scan)
+                __shared__ unsigned long long wsum[4];
+                part[t] = block_incl_scan<256>(mine, wsum);
                 __syncthreads();
             }
             const unsigned long long total = part[255];

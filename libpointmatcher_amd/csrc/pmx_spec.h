@@ -188,6 +188,7 @@ struct SpecKeys {
     unsigned n_local = 0;
     const unsigned long long* segs = nullptr;    // several ranks: nseg * kSpecXStride
     int nseg = 0;
+    const K* lds = nullptr;                      // single rank: the keys copied to LDS (every pass reads them)
     __device__ __forceinline__ int count() const { return segs ? nseg : 1; }
     __device__ __forceinline__ unsigned n(int s) const {
         if (!segs) return n_local;
@@ -196,10 +197,31 @@ struct SpecKeys {
     }
     __device__ __forceinline__ K key(int s, unsigned i) const {
         // (local keys: appended in the same launch when the match's last block picks: coherent loads)
-        return segs ? (K)segs[(size_t)s * kSpecXStride + kSpecXHdr + i]
-                    : __hip_atomic_load(&local[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lds) return lds[i];
+        return segs ? (K)segs[(size_t)s * kSpecXStride + kSpecXHdr + i] : local[i];
     }
 };
+
+// inclusive scan over a block of kThreads (a multiple of 64, <= 1024):
+// wave scans with shuffles, then the waves' totals (two barriers, against
+// 2 log2(kThreads) for a Hillis-Steele scan through LDS).  wsum: LDS of
+// kThreads / 64 entries.
+template <int kThreads>
+__device__ __forceinline__ unsigned long long block_incl_scan(unsigned long long v, unsigned long long* wsum) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long u = __shfl_up(v, off);
+        if (lane >= off) v += u;
+    }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    unsigned long long before = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) before += w < wave ? wsum[w] : 0ull;
+    __syncthreads();  // (wsum reusable)
+    return before + v;
+}
 
 // ---- counter side: resolve the limit from the window (one block) ----
 // fin / below: the match's counters (global), nk_raw: keys appended inside
@@ -265,16 +287,9 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
         constexpr int per = 2048 / kThreads;
         unsigned long long mine = 0;
         for (int j = 0; j < per; ++j) mine += lh[t * per + j];
-        part[t] = mine;
-        __syncthreads();
-        for (int off = 1; off < kThreads; off <<= 1) {
-            const unsigned long long v = t >= off ? part[t - off] : 0ull;
-            __syncthreads();
-            part[t] += v;
-            __syncthreads();
-        }
-        const unsigned long long excl = t > 0 ? part[t - 1] : 0ull;
-        if (r >= excl && r < part[t]) {
+        const unsigned long long incl = block_incl_scan<kThreads>(mine, part);
+        const unsigned long long excl = incl - mine;
+        if (r >= excl && r < incl) {
             unsigned long long cum = excl;
             for (int j = 0; j < per; ++j) {
                 const unsigned long long c = lh[t * per + j];
@@ -330,8 +345,10 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
     __shared__ unsigned long long bc[2];
     const int t = threadIdx.x;
     unsigned long long v[4];
-    // (coherent loads / stores: with the fold the counters were added in this
-    // launch by other workgroups, possibly on other XCDs)
+    // the window's append count, read with the counters (one round trip)
+    const unsigned nk_raw = spec ? __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    // (coherent loads / stores: the counters of another launch's workgroups,
+    // possibly on other XCDs)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         unsigned long long* p = vpart + (size_t)(c * kVSlots + t) * kVStride;
@@ -360,7 +377,7 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
     if (!spec) return;
     if (xseg) {  // several ranks: this rank's segment [fin, below, n, keys...]
         using K = typename KeyOf<T>::K;
-        const unsigned nk = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned nk = nk_raw;
         const unsigned nc = nk < kSpecXCap ? nk : kSpecXCap;
         const K* keys = (const K*)spec->keys;
         if (t == 0) {
@@ -375,10 +392,18 @@ __device__ __forceinline__ void counter_phase(unsigned long long* __restrict__ v
         if (t == 0) spec->n_keys = 0;
         return;
     }
+    using K = typename KeyOf<T>::K;
     SpecKeys<T> src;
-    src.local = (const typename KeyOf<T>::K*)spec->keys;
-    const unsigned nk_raw = __hip_atomic_load(&spec->n_keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    src.local = (const K*)spec->keys;
     src.n_local = nk_raw < kSpecCap ? nk_raw : kSpecCap;
+    // the keys into LDS once (every radix pass of the pick reads them all)
+    constexpr unsigned kSpecLds = 4096;
+    __shared__ K lkeys[kSpecLds];
+    if (src.n_local <= kSpecLds && spec->valid) {
+        for (unsigned i = t; i < src.n_local; i += kVSlots) lkeys[i] = src.local[i];
+        __syncthreads();
+        src.lds = lkeys;
+    }
     (void)spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part, bc);
 }
 
