@@ -1,0 +1,335 @@
+// pmx_loop_capi.hip — pmx_loop_begin / _run / _trace (include/pmx.h): whole
+// ICP iterations (ICP.cpp:371-430) enqueued back to back on the context
+// stream, transform, level and stop flag kept on the device (pmx_loop.hip).
+#include "pmx_ctx.h"
+
+namespace pmxc {
+
+// ------------------------------------------------------------ device loop --
+// pmx_loop_*: whole ICP iterations enqueued back to back (pmx_loop.hip).  The
+// host checks the stop flag once per batch of kLoopBatch iterations while the
+// next batch is already queued, so the GPU never waits for the host; after a
+// stop the queued iterations return at once (every kernel reads LoopCtl.done).
+constexpr int kLoopBatch = 4;
+// pinned status slot s (a copy of the device status block)
+const char* stat_slot(const pmx_ctx* c, int s) { return (const char*)c->h_loop + (size_t)s * kStatBytes; }
+
+
+template <typename T>
+int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
+    if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
+    if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
+    if (c->search_type == 0 || !c->grid_ready || c->grid_mode == 0)
+        return fail(c, PMX_E_BAD_PARAM, "device loop: needs the per-lane grid matcher (searchType 1 or 2)");
+    if (cfg->knn < 1 || cfg->knn > kMaxKnn) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 256] on the GPU path");
+    if (!(cfg->max_dist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
+    if (cfg->n_filters < 0 || cfg->n_filters > kMaxChain)
+        return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 outlier filters");
+    for (int i = 0; i < cfg->n_filters; ++i) {
+        const int k = cfg->filter_kind[i];
+        const double* p = cfg->filter_p[i];
+        if (k < PMX_FILTER_DEFAULT || k > PMX_FILTER_VARTRIMMED || (k == PMX_FILTER_DEFAULT && i != 0))
+            return fail(c, PMX_E_BAD_PARAM, "device loop: unknown outlier filter");
+        if ((k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST) && !(p[0] >= 1e-7))
+            return fail(c, PMX_E_BAD_PARAM, "device loop: distance threshold < 1e-7");
+        if (k == PMX_FILTER_TRIMMED && !(p[0] >= 1e-7 && p[0] <= 1.0))
+            return fail(c, PMX_E_BAD_PARAM, "TrimmedDistOutlierFilter: ratio out of [1e-7, 1]");
+        if (k == PMX_FILTER_VARTRIMMED && !((T)p[0] < (T)p[1]))
+            return fail(c, PMX_E_BAD_PARAM, "VarTrimmedDistOutlierFilter: minRatio should be smaller than maxRatio");
+    }
+    if (cfg->minimizer != 0 && cfg->minimizer != 1) return fail(c, PMX_E_BAD_PARAM, "device loop: unknown minimizer");
+    if (cfg->minimizer == 0 && !c->has_normals)
+        return fail(c, PMX_E_BAD_PARAM, "PointToPlaneErrorMinimizer requires \"normals\" on the reference");
+    if (cfg->n_checkers < 0 || cfg->n_checkers > kMaxCheckers)
+        return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 transformation checkers");
+    for (int i = 0; i < cfg->n_checkers; ++i) {
+        const int k = cfg->checker_kind[i];
+        if (k < PMX_CHECK_COUNTER || k > PMX_CHECK_BOUND)
+            return fail(c, PMX_E_BAD_PARAM, "device loop: unknown transformation checker");
+        const double sl = cfg->checker_p[i][2];
+        if (k == PMX_CHECK_DIFFERENTIAL && !(sl >= 0 && sl < kLoopHist && sl == std::floor(sl)))
+            return fail(c, PMX_E_BAD_PARAM, "device loop: smoothLength must be an integer in [0, 63]");
+    }
+    if (c->levels.size() > (size_t)kMaxLevels) return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 grid levels");
+    LoopCfg d{};
+    d.rows = c->rows;
+    d.minimizer = cfg->minimizer;
+    d.n_checkers = cfg->n_checkers;
+    for (int i = 0; i < cfg->n_checkers; ++i) {
+        d.checker_kind[i] = cfg->checker_kind[i];
+        for (int j = 0; j < 3; ++j) d.checker_p[i][j] = cfg->checker_p[i][j];
+    }
+    d.adaptive = c->adaptive ? 1 : 0;
+    d.reuse = c->reuse_on && c->grid_mode >= 1 ? 1 : 0;
+    d.knn = cfg->knn;
+    d.n_levels = (int)c->levels.size();
+    for (int l = 0; l < d.n_levels; ++l) d.level_ppc[l] = c->lv(l).ppc;
+    d.n_local = c->N;
+    int rc;
+    size_t cap = 0;
+    (void)cap;  // (LoopState lives in the status block)
+    cap = 0;
+    if (!c->d_loop_T0 && (rc = ensure(c, &c->d_loop_T0, &cap, 16 * sizeof(double)))) return rc;
+    // pinned: two status-block slots (the batches in flight)
+    if (!c->h_loop) HIPCHK(c, hipHostMalloc(&c->h_loop, 2 * kStatBytes, hipHostMallocDefault));
+    for (hipEvent_t& e : c->loop_ev)
+        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->loop_cfg = *cfg;
+    c->loop_dev = d;
+    const int rr = c->rows * c->rows;
+    HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, T0, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
+    // the first loop match may reuse the last classic one
+    const int prev_level =
+        c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn ? c->ids_level : -1;
+    launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, prev_level,
+                        c->Tstep, c->stream);
+    // quantile window: a fresh window each loop (the first iteration runs the
+    // radix passes, which centre the window for the next)
+    const int k0 = cfg->n_filters > 0 ? cfg->filter_kind[0] : -1;
+    c->spec_on = c->spec_allowed &&
+                 (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
+    if (c->spec_on) {
+        if (!c->d_spec) {
+            HIPCHK(c, hipMalloc((void**)&c->d_spec, sizeof(SpecSel)));
+            HIPCHK(c, hipMalloc(&c->d_spec_keys, sizeof(unsigned long long) * kSpecCap));
+        }
+        if (sharded(c) && !c->d_specx)
+            HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * (c->nranks + 1)));
+        SpecSel init{};
+        init.keys = c->d_spec_keys;
+        init.ratio = (double)(T)(k0 == PMX_FILTER_TRIMMED ? cfg->filter_p[0][0] : 0.5);
+        c->spec_init = init;
+        HIPCHK(c, hipMemcpyAsync(c->d_spec, &c->spec_init, sizeof(SpecSel), hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (T0 may be a stack buffer of the caller)
+    c->loop_issued = 0;
+    c->loop_iters = 0;
+    c->loop_done = false;
+    c->shard_done_seen = false;
+    c->loop_begun = true;
+    return PMX_OK;
+}
+
+// trace room for `iters` iterations (the enqueued loop_step kernels hold the
+// old pointer: drain the stream before the old buffer goes)
+template <typename T>
+int loop_trace_room(pmx_ctx* c, int64_t iters) {
+    if (iters <= c->trace_cap && c->d_trace) return PMX_OK;
+    const size_t rb = sizeof(T) * c->rows * c->rows;
+    const int64_t cap = std::max<int64_t>({iters, 2 * c->trace_cap, 64});
+    void* nb = nullptr;
+    HIPCHK(c, hipMalloc(&nb, rb * (size_t)cap));
+    if (c->d_trace) {
+        HIPCHK(c, hipMemcpyAsync(nb, c->d_trace, rb * (size_t)c->trace_cap, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_trace);
+    }
+    c->d_trace = nb;
+    c->trace_cap = cap;
+    return PMX_OK;
+}
+
+// one ICP iteration, device-driven (transform and level from LoopCtl)
+template <typename T>
+int loop_enqueue_iteration(pmx_ctx* c) {
+    const pmx_loop_cfg& cfg = c->loop_cfg;
+    if (c->shard_done_seen) return PMX_OK;  // (every rank stops enqueuing at the same iteration)
+    T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
+    for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
+    int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr);
+    if (rc) return rc;
+    if (cfg.n_filters == 0) {
+        if ((rc = outlier_impl<T>(c, 0, 0, 0, 0, 0))) return rc;
+    }
+    for (int i = 0; i < cfg.n_filters; ++i) {
+        const double* p = cfg.filter_p[i];
+        if ((rc = outlier_impl<T>(c, cfg.filter_kind[i], i, p[0], p[1], p[2]))) return rc;
+    }
+    if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c))) return rc;
+    launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
+                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, c->stream);
+    HIPCHK(c, hipGetLastError());
+    return PMX_OK;
+}
+
+template <typename T>
+int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
+    if (!c->loop_begun) return fail(c, PMX_E_STATE, "pmx_loop_begin must be called first");
+    if (n < 0) return fail(c, PMX_E_BAD_PARAM, "negative iteration count");
+    int rc = PMX_OK;
+    int issued = 0, slot = 0, last_slot = -1;
+    int fly[2], nfly = 0, head = 0;
+    bool stop = c->loop_done;
+    c->loop_on = true;
+    while (!stop && rc == PMX_OK) {
+        while (issued < n && nfly < 2 && rc == PMX_OK) {
+            const int b = std::min(kLoopBatch, n - issued);
+            if (c->loop_cfg.keep_trace && (rc = loop_trace_room<T>(c, c->loop_issued + b))) break;
+            for (int i = 0; i < b && rc == PMX_OK; ++i) rc = loop_enqueue_iteration<T>(c);
+            if (rc) break;
+            c->loop_issued += b;
+            issued += b;
+            // the whole status block (state, control word, iteration block):
+            // the stop flag of this batch, and the final status if it is the last
+            hipError_t e = hipMemcpyAsync((char*)c->h_loop + (size_t)slot * kStatBytes, c->d_result, kStatBytes,
+                                          hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipEventRecord(c->loop_ev[slot], c->stream);
+            if (e != hipSuccess) {
+                rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
+                break;
+            }
+            fly[(head + nfly) % 2] = slot;
+            ++nfly;
+            last_slot = slot;
+            slot ^= 1;
+        }
+        if (rc || nfly == 0) break;
+        const int s = fly[head];
+        head = (head + 1) % 2;
+        --nfly;
+        const hipError_t e = hipEventSynchronize(c->loop_ev[s]);
+        if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
+        if (((const LoopState<T>*)(stat_slot(c, s) + kStatLoop))->done) stop = true;
+    }
+    // drain: the last issued batch's copy is the final status
+    while (rc == PMX_OK && nfly > 0) {
+        const hipError_t e = hipEventSynchronize(c->loop_ev[fly[head]]);
+        if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
+        head = (head + 1) % 2;
+        --nfly;
+    }
+    c->loop_on = false;
+    if (rc) {
+        (void)hipStreamSynchronize(c->stream);
+        return rc;
+    }
+    // the final state, the iteration block (limit, counters) and the control
+    // word: the last batch's status copy (no batch issued: one copy now)
+    if (last_slot < 0) {
+        last_slot = 0;
+        HIPCHK(c, hipMemcpyAsync(c->h_loop, c->d_result, kStatBytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    const char* fin = stat_slot(c, last_slot);
+    std::memcpy(c->h_result, fin, kBlkCopy);
+    resolve_events(c);
+    LoopCtl ctl;
+    std::memcpy(&ctl, fin + kStatCtl, sizeof(LoopCtl));
+    const LoopState<T>& S = *(const LoopState<T>*)(fin + kStatLoop);
+    c->loop_iters = S.iter;
+    c->loop_done = S.done != 0;
+    c->level = ctl.level;
+    c->ids_level = S.last_level;
+    if (S.iter > 0 || S.err)  // the last executed match's step transform (LoopCtl.T moved on)
+        for (int i = 0; i < 16; ++i) c->Tstep[i] = ctl.Tprev[i];
+    // map the device error to the reference's exception and message
+    int err = 0;
+    std::string msg;
+    if (S.err) {
+        const int e = S.err;
+        if (e == kLoopNoPoints) {
+            err = PMX_E_NO_POINTS;
+            msg = "ErrorMnimizer: no point to minimize";
+        } else if (e == PMX_E_EMPTY_QUANTILE) {
+            err = PMX_E_EMPTY_QUANTILE;
+            msg = "no outlier to filter";
+        } else if (e == kSelTimeout) {
+            (void)select_reset(c);
+            err = PMX_E_HIP;
+            msg = "radix select: a block waited too long for the pass before (device timeout)";
+        } else if (e == kLoopNotRigid) {
+            err = PMX_E_TRANSFORMATION;
+            msg = "RigidTransformation: Error, rotation matrix is not orthogonal.";
+        } else if (e == kLoopRotNaN) {
+            err = PMX_E_CONVERGENCE;
+            msg = "abs rotation norm not a number";
+        } else if (e == kLoopTransNaN) {
+            err = PMX_E_CONVERGENCE;
+            msg = "abs translation norm not a number";
+        } else if (e == kLoopBound) {
+            err = PMX_E_CONVERGENCE;
+            // TransformationCheckersImpl.cpp:215-222 (the first bound exceeded)
+            for (int i = 0; i < c->loop_cfg.n_checkers; ++i) {
+                if (c->loop_cfg.checker_kind[i] != PMX_CHECK_BOUND) continue;
+                const T l0 = (T)c->loop_cfg.checker_p[i][0], l1 = (T)c->loop_cfg.checker_p[i][1];
+                if (S.cond[i][0] > l0 || S.cond[i][1] > l1) {
+                    std::ostringstream oss;
+                    oss << "limit out of bounds: rot: " << S.cond[i][0] << "/" << l0 << " tr: " << S.cond[i][1] << "/"
+                        << l1;
+                    msg = oss.str();
+                    break;
+                }
+            }
+        } else {
+            err = e;
+            msg = "quantile must be between 0 and 1";
+        }
+        c->err = msg;
+    }
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->iterations = S.iter;
+        st->done = S.done;
+        st->reason = S.reason;
+        st->error = err;
+        st->point_count_touched = (int64_t)S.touched;
+        fill_stats(c, &st->last, S.kept, S.nz, S.rejM, S.rejP, S.sw, host_limit(c));
+        st->last.visited = (int64_t)S.last_visited;
+        const int rr = c->rows * c->rows;
+        for (int i = 0; i < rr; ++i) st->T_iter[i] = (double)S.Titer[i];
+        for (int i = 0; i < kMaxCheckers; ++i)
+            for (int j = 0; j < 2; ++j) st->cond[i][j] = (double)S.cond[i][j];
+    }
+    return err;
+}
+
+template <typename T>
+int loop_trace_impl(pmx_ctx* c, int first, int count, void* out) {
+    if (!c->loop_begun || !c->loop_cfg.keep_trace) return fail(c, PMX_E_STATE, "no loop trace (keep_trace = 0)");
+    if (first < 0 || count < 0 || first + count > c->loop_iters)
+        return fail(c, PMX_E_BAD_PARAM, "trace range beyond the completed iterations");
+    if (count == 0) return PMX_OK;
+    const size_t rb = sizeof(T) * c->rows * c->rows;
+    HIPCHK(c, hipMemcpyAsync(out, (const char*)c->d_trace + rb * first, rb * count, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
+}  // namespace pmxc
+
+using namespace pmxc;
+
+extern "C" {
+
+int pmx_loop_begin(pmx_ctx* c, const pmx_loop_cfg* cfg, const void* T0) {
+    if (!c || !cfg || !T0) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c, loop_begin_impl<float>(c, cfg, (const float*)T0), loop_begin_impl<double>(c, cfg, (const double*)T0));
+}
+
+int pmx_loop_run(pmx_ctx* c, int n, pmx_loop_status* st) {
+    if (!c) return PMX_E_BAD_PARAM;
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c, loop_run_impl<float>(c, n, st), loop_run_impl<double>(c, n, st));
+}
+
+int pmx_loop_trace(pmx_ctx* c, int first, int count, void* out) {
+    if (!c || (!out && count > 0)) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return DISPATCH(c, loop_trace_impl<float>(c, first, count, out), loop_trace_impl<double>(c, first, count, out));
+}
+
+int pmx_loop_select_stats(pmx_ctx* c, uint64_t* window_hits, uint64_t* window_misses) {
+    if (!c || !window_hits || !window_misses) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    *window_hits = 0;
+    *window_misses = 0;
+    if (!c->d_spec) return PMX_OK;
+    SpecSel h{};
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(&h, c->d_spec, sizeof(SpecSel), hipMemcpyDeviceToHost));
+    *window_hits = h.n_hit;
+    *window_misses = h.n_miss;
+    return PMX_OK;
+}
+
+}  // extern "C"
