@@ -42,6 +42,10 @@ CONFIGS = {
     "c3": (1_000_000, 1_000_000, np.float32, 1, [("TrimmedDistOutlierFilter", {"ratio": 0.85})], "PointToPlaneErrorMinimizer"),
     "c4": (1_000_000, 1_000_000, np.float32, 4, [("MaxDistOutlierFilter", {"maxDist": 0.05})], "PointToPlaneErrorMinimizer"),
     "c5": (10_000_000, 1_000_000, np.float64, 1, [], "PointToPointErrorMinimizer"),
+    # (not a BASELINE config: C3 with the reference's default VarTrimmedDist, to time its device sort + partial_sum)
+    "c3v": (1_000_000, 1_000_000, np.float32, 1,
+            [("VarTrimmedDistOutlierFilter", {"minRatio": 0.05, "maxRatio": 0.99, "lambda": 2.35})],
+            "PointToPlaneErrorMinimizer"),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 FP32_VALU_TFLOPS = 157.3   # MI355X FP32 vector peak (spec)

@@ -502,7 +502,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx : nullptr;
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
-                             (T*)c->d_dists, c->d_ids, c->d_vpart, c->d_visited, c->d_iter_err, ru, loop_ctl(c),
+                             (T*)c->d_dists, c->d_ids, c->d_vpart, c->merge_counter ? nullptr : c->d_visited,
+                             c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on, e1, c->stream);
         if (xseg) {
@@ -565,7 +566,12 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
             HIPCHK(c, hipMemsetAsync(c->d_selx, 0, selx_bytes(), c->stream));
             c->selx_grid = g;
         }
-        launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec, c->stream);
+        // (merged: this launch also runs the match's counter phase)
+        const bool merged = c->merge_counter && spec;
+        launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec,
+                             merged ? c->d_vpart : nullptr, merged ? c->d_visited : nullptr, c->stream);
+        if (merged) c->vpart_dirty = true;
+        c->merge_counter = false;
     } else {
         for (int p = 0; p < passes; ++p) {
             // the histogram is all-reduced between the two halves of a pass
@@ -957,7 +963,9 @@ int p2plane_enqueue(pmx_ctx* c) {
     Mat4<T> Tm = step_mat<T>(c);
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
                               match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
-                              loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->stream);
+                              loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->vpart_dirty ? c->d_vpart : nullptr,
+                              c->stream);
+    c->vpart_dirty = false;
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result, NV);

@@ -221,6 +221,12 @@ struct pmx_ctx {
     void* d_spec_keys = nullptr;
     bool spec_allowed = true;
     bool spec_on = false;
+    // device loop, single rank, window on, quantile at chain position 0: the
+    // match's counter phase runs inside the select launch (every block folds
+    // the counters, pmx_selectall.h counter_merged), one launch fewer per
+    // iteration; the point-to-plane launch then zeroes the spread counters
+    bool merge_counter = false;  // (set for the match being enqueued)
+    bool vpart_dirty = false;    // (the merged counter phase read them: the next reduction zeroes them)
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;

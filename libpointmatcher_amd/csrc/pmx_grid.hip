@@ -811,7 +811,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        hipStream_t s) {
     if (N <= 0) return;
     cold = cold && mode >= 1;
-    if (mode < 1 || !visited || !vout) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
+    if (mode < 1 || !visited) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
     GridGeom G;
     for (int a = 0; a < 3; ++a) {
         G.lo[a] = lo[a];

@@ -186,6 +186,8 @@ void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* star
 // launch_pos_to_index maps them back.  ctl / gd (device loop, modes 1-2):
 // transform and level are read on the device.  cold: a new reading's first
 // match (no previous match to certify from) on the tile kernel's cold form.
+// vout null: no counter-sum launch after the match (its counter phase is
+// merged into the select launch that follows, launch_select_all).
 template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
@@ -410,9 +412,13 @@ int select_passes();
 size_t selx_bytes();
 int64_t select_all_blocks(int64_t n);
 constexpr int kSelTimeout = -30;  // iteration error: a select_all wait timed out
+// vpart / vout (may be null): the match's counter phase merged into this
+// launch (pmx_selectall.h counter_merged); the spread counters are then
+// zeroed by the next point-to-plane launch (launch_p2plane_partial's vzero)
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
-                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s);
+                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, const unsigned long long* vpart,
+                       unsigned long long* vout, hipStream_t s);
 int select_bins(int pass, int key_bits);
 
 // VarTrimmed pieces
@@ -435,10 +441,13 @@ constexpr int p2plane_nv_full(int dim) { return dim == 3 ? 36 + 6 + 5 : 9 + 3 + 
 // grid level whose positions the ids are (ref / nrm then come from gd)
 // rs: index stride of ref / nrm (1: separate arrays; 2: a grid level's
 // interleaved point / normal records, ref = gpn, nrm = gpn + 1)
+// vzero (may be null): the match's spread counters, zeroed by block 0 (a
+// counter phase merged into the select launch read them)
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
-                            double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
+                            double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
+                            hipStream_t s);
 void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,

@@ -137,6 +137,12 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     if (c->shard_done_seen) return PMX_OK;  // (every rank stops enqueuing at the same iteration)
     T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
     for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
+    // the match's counter phase merged into the quantile's select launch
+    // (point-to-plane: its reduction zeroes the spread counters afterwards)
+    const int k0 = cfg.n_filters > 0 ? cfg.filter_kind[0] : -1;
+    c->merge_counter = c->spec_on && !sharded(c) && cfg.minimizer == 0 && c->grid_mode >= 1 && c->N > 0 &&
+                       cfg.knn <= kLaneMaxK && (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
+    c->vpart_dirty = false;
     int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr);
     if (rc) return rc;
     if (cfg.n_filters == 0) {

@@ -250,16 +250,19 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
                                                          SelectState* __restrict__ st, double ratio_host,
                                                          const double* __restrict__ ratio_dev,
                                                          int* __restrict__ iter_err, const LoopCtl* __restrict__ ctl,
-                                                         SpecSel* __restrict__ spec) {
+                                                         SpecSel* __restrict__ spec,
+                                                         const unsigned long long* __restrict__ vpart,
+                                                         unsigned long long* __restrict__ vout) {
     if (ctl && ctl->done) return;  // (uniform: no block arrives anywhere)
-    select_all_body<T>(d, n, sx, st, ratio_host, ratio_dev, iter_err, spec);
+    select_all_body<T>(d, n, sx, st, ratio_host, ratio_dev, iter_err, spec, vpart, vout);
 }
 
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
-                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, hipStream_t s) {
+                       int* iter_err, const LoopCtl* ctl, SpecSel* spec, const unsigned long long* vpart,
+                       unsigned long long* vout, hipStream_t s) {
     hipLaunchKernelGGL(select_all_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, (SelX*)selx, st,
-                       ratio, ratio_dev, iter_err, ctl, spec);
+                       ratio, ratio_dev, iter_err, ctl, spec, vpart, vout);
 }
 
 template <typename T>
@@ -538,9 +541,11 @@ template void launch_select_pick<float>(uint32_t*, SelectState*, int, double, co
 template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, const double*, int*, const LoopCtl*,
                                          SpecSel*, hipStream_t);
 template void launch_select_all<float>(const float*, int64_t, void*, SelectState*, double, const double*, int*,
-                                       const LoopCtl*, SpecSel*, hipStream_t);
+                                       const LoopCtl*, SpecSel*, const unsigned long long*, unsigned long long*,
+                                       hipStream_t);
 template void launch_select_all<double>(const double*, int64_t, void*, SelectState*, double, const double*, int*,
-                                        const LoopCtl*, SpecSel*, hipStream_t);
+                                        const LoopCtl*, SpecSel*, const unsigned long long*, unsigned long long*,
+                                        hipStream_t);
 template void launch_vartrim<float>(const float*, int64_t, int, float, float, const float*, void*, size_t, double*,
                                     int*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,

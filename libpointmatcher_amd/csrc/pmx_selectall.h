@@ -80,6 +80,8 @@ struct SelX {
     unsigned long long rank[kSelMaxPasses];  // rank left inside the prefix after pass p
     unsigned long long tot[kSelMaxPasses];   // keys histogrammed in pass p
     unsigned long long count;                // finite keys (pass 0)
+    unsigned int cread;                      // merged counter phase: blocks done reading (monotonic)
+    unsigned int pad_;
 };
 
 __device__ __forceinline__ unsigned long long ald(unsigned long long* p) {
@@ -90,13 +92,90 @@ __device__ __forceinline__ unsigned long long ast(unsigned long long* p, unsigne
     return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The match's counter phase merged into the select launch (device loop,
+// single rank, window on): EVERY block folds the spread counters and picks
+// from the window keys itself (reads only: the same inputs give every block
+// the same verdict, so no block waits for another's); block 0 then waits
+// until every block has read (an arrival count: the readers never wait, so
+// this needs no co-residency) and writes the results — the iteration
+// block's counters, the error word, the select state and the next window.
+// The spread counters are zeroed by the point-to-plane launch that follows.
+// Returns the verdict (block-uniform).
+template <typename T>
+__device__ __forceinline__ bool counter_merged(const unsigned long long* __restrict__ vpart,
+                                               unsigned long long* __restrict__ out, int* __restrict__ iter_err,
+                                               SpecSel* __restrict__ spec, SelectState* __restrict__ st,
+                                               SelX* __restrict__ sx) {
+    using K = typename KeyOf<T>::K;
+    constexpr unsigned kLds = 4096;
+    __shared__ unsigned long long red[4][kVSlots / 64];
+    __shared__ uint32_t lh[2048];
+    __shared__ unsigned long long part[kVSlots];
+    __shared__ unsigned long long bc[2];
+    __shared__ K lkeys[kLds];
+    const int t = threadIdx.x;
+    const unsigned nk_raw = spec->n_keys;
+    const K lo = (K)spec->lo, hi = (K)spec->hi;
+    const bool valid = spec->valid != 0;
+    unsigned long long v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = vpart[(size_t)(c * kVSlots + t) * kVStride];
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] += __shfl_xor(v[c], off);
+    }
+    if ((t & 63) == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[c][t >> 6] = v[c];
+    }
+    SpecKeys<T> src;
+    src.local = (const K*)spec->keys;
+    src.n_local = nk_raw < kSpecCap ? nk_raw : kSpecCap;
+    if (src.n_local <= kLds && valid) {
+        for (unsigned i = t; i < src.n_local; i += kVSlots) lkeys[i] = src.local[i];
+        src.lds = lkeys;
+    }
+    __syncthreads();
+    unsigned long long sum[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        for (int w = 0; w < kVSlots / 64; ++w) sum[c] += red[c][w];
+    unsigned long long kl = 0;
+    const bool hit = spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part,
+                                           bc, false, &kl);
+    __syncthreads();  // (every thread of the block has read)
+    if (t == 0) {
+        const unsigned old = atomicAdd(&sx->cread, 1u);
+        if (blockIdx.x == 0) {
+            // every block of this launch has read once the count reaches the
+            // generation's end (a power-of-two grid: the count wraps cleanly)
+            const unsigned G = gridDim.x, base = old - old % G;
+            bool all = false;
+            for (int it = 0; it < (1 << 22); ++it) {
+                if (__hip_atomic_load(&sx->cread, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base >= G) {
+                    all = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __hip_atomic_store(&out[0], sum[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&out[1], sum[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(iter_err, all ? 0 : kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            spec_commit<T>(spec, st, hit, lo, hi, (K)kl, sum[2], nk_raw);
+        }
+    }
+    return hit;
+}
+
 // The select itself (every block of select_all_kernel): the resolved
 // limit and select state in *st, the next window re-centred (spec).
 template <typename T>
 __device__ __forceinline__ void select_all_body(const T* __restrict__ d, int64_t n, SelX* __restrict__ sx,
                                                 SelectState* __restrict__ st, double ratio_host,
                                                 const double* __restrict__ ratio_dev, int* __restrict__ iter_err,
-                                                SpecSel* __restrict__ spec) {
+                                                SpecSel* __restrict__ spec,
+                                                const unsigned long long* __restrict__ vpart = nullptr,
+                                                unsigned long long* __restrict__ vout = nullptr) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     __shared__ uint32_t lh[2048];
@@ -104,7 +183,11 @@ __device__ __forceinline__ void select_all_body(const T* __restrict__ d, int64_t
     __shared__ unsigned long long s_w[2];  // (published word, its generation)
     __shared__ int s_last;
     __shared__ unsigned int s_old;
-    if (spec && spec->hit) return;  // (the window resolved it in the counter kernel before this launch)
+    if (vpart) {
+        if (counter_merged<T>(vpart, vout, iter_err, spec, st, sx)) return;  // (the window resolved it)
+    } else if (spec && spec->hit) {
+        return;  // (the window resolved it in the counter kernel before this launch)
+    }
     constexpr int passes = KO::bits == 32 ? 3 : 6;
     uint32_t* hist0 = reinterpret_cast<uint32_t*>(sx + 1);
     const int t = threadIdx.x;

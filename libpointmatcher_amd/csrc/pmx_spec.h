@@ -227,12 +227,38 @@ __device__ __forceinline__ unsigned long long block_incl_scan(unsigned long long
 // fin / below: the match's counters (global), nk_raw: keys appended inside
 // the window (global; more than the buffers hold means a miss), keys: where
 // they are.  Writes st (as the radix select's last pass would) and sp->hit;
-// resets the append counter.  Block of kThreads.
+// resets the append counter (commit = false: reads only, the verdict and the
+// limit key in *kl_out, for spec_commit).  Block of kThreads.
+template <typename T>
+__device__ __forceinline__ void spec_commit(SpecSel* __restrict__ sp, SelectState* __restrict__ st, bool hit,
+                                            typename KeyOf<T>::K lo, typename KeyOf<T>::K hi,
+                                            typename KeyOf<T>::K kl, unsigned long long fin, unsigned long long nk) {
+    using KO = KeyOf<T>;
+    if (!hit) {
+        sp->hit = 0;
+        sp->n_miss += 1;
+        sp->n_keys = 0;
+        return;
+    }
+    st->err = 0;
+    st->count = fin;
+    st->prefix = (unsigned long long)kl;
+    st->rank = 0;
+    st->ratio = (double)(T)sp->ratio;
+    st->limit = (double)KO::val(kl);
+    sp->hit = 1;
+    sp->n_hit += 1;
+    sp->n_keys = 0;
+    const double width = (double)(hi - lo) + 1.0;
+    spec_update<T>(sp, kl, (double)nk / width);
+}
+
 template <typename T, int kThreads>
 __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState* __restrict__ st,
                                           unsigned long long fin, unsigned long long below,
                                           unsigned long long nk_raw, bool overflow, const SpecKeys<T>& src,
-                                          uint32_t* lh, unsigned long long* part, unsigned long long* bc) {
+                                          uint32_t* lh, unsigned long long* part, unsigned long long* bc,
+                                          bool commit = true, unsigned long long* kl_out = nullptr) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     const int t = threadIdx.x;
@@ -255,11 +281,7 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
     ok = ok && rank >= below && rank < below + nk;
     __syncthreads();
     if (!ok) {
-        if (t == 0) {
-            sp->hit = 0;
-            sp->n_miss += 1;
-            sp->n_keys = 0;
-        }
+        if (t == 0 && commit) spec_commit<T>(sp, st, false, lo, hi, (K)0, fin, nk);
         return false;
     }
     unsigned long long r = rank - below;
@@ -307,20 +329,9 @@ __device__ __forceinline__ bool spec_pick(SpecSel* __restrict__ sp, SelectState*
         done_bits += bits;
         __syncthreads();
     }
-    if (t == 0) {
-        const K kl = lo + (K)prefix;
-        st->err = 0;
-        st->count = fin;
-        st->prefix = (unsigned long long)kl;
-        st->rank = 0;
-        st->ratio = (double)q;
-        st->limit = (double)KO::val(kl);
-        sp->hit = 1;
-        sp->n_hit += 1;
-        sp->n_keys = 0;
-        const double width = (double)(hi - lo) + 1.0;
-        spec_update<T>(sp, kl, (double)nk / width);
-    }
+    const K kl = lo + (K)prefix;
+    if (kl_out) *kl_out = (unsigned long long)kl;
+    if (t == 0 && commit) spec_commit<T>(sp, st, true, lo, hi, kl, fin, nk);
     return true;
 }
 
