@@ -245,6 +245,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->h_loop) (void)hipHostFree(c->h_loop);
     for (hipEvent_t e : c->loop_ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->loop_stage_ev) (void)hipEventDestroy(c->loop_stage_ev);
     for (auto& pr : c->ev_pending) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);

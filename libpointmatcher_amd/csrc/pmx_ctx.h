@@ -234,6 +234,7 @@ struct pmx_ctx {
     LoopCfg loop_dev{};
     void* h_loop = nullptr;       // pinned: two copies of the status block (the batches in flight)
     hipEvent_t loop_ev[2] = {nullptr, nullptr};  // end of the batches in flight
+    hipEvent_t loop_stage_ev = nullptr;          // pmx_loop_begin's uploads have left the pinned staging
     int64_t loop_issued = 0;      // iterations enqueued since pmx_loop_begin
     int loop_iters = 0;           // iterations completed (last status)
     bool loop_done = false;       // the loop has stopped (last status)

@@ -13,6 +13,8 @@ namespace pmxc {
 constexpr int kLoopBatch = 4;
 // pinned status slot s (a copy of the device status block)
 const char* stat_slot(const pmx_ctx* c, int s) { return (const char*)c->h_loop + (size_t)s * kStatBytes; }
+// pinned staging of pmx_loop_begin's uploads, after the two status slots
+constexpr size_t kLoopStage = 256 + ((sizeof(SpecSel) + 255) & ~(size_t)255);
 
 
 template <typename T>
@@ -70,14 +72,20 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     (void)cap;  // (LoopState lives in the status block)
     cap = 0;
     if (!c->d_loop_T0 && (rc = ensure(c, &c->d_loop_T0, &cap, 16 * sizeof(double)))) return rc;
-    // pinned: two status-block slots (the batches in flight)
-    if (!c->h_loop) HIPCHK(c, hipHostMalloc(&c->h_loop, 2 * kStatBytes, hipHostMallocDefault));
+    // pinned: two status-block slots (the batches in flight), then the
+    // staging of this call's uploads (T0, the window reset): the uploads are
+    // asynchronous, so the caller's T0 may go away and no host sync is needed
+    if (!c->h_loop) HIPCHK(c, hipHostMalloc(&c->h_loop, 2 * kStatBytes + kLoopStage, hipHostMallocDefault));
     for (hipEvent_t& e : c->loop_ev)
         if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!c->loop_stage_ev) HIPCHK(c, hipEventCreateWithFlags(&c->loop_stage_ev, hipEventDisableTiming));
+    HIPCHK(c, hipEventSynchronize(c->loop_stage_ev));  // (the last call's uploads have left the staging)
+    char* stage = (char*)c->h_loop + 2 * kStatBytes;
     c->loop_cfg = *cfg;
     c->loop_dev = d;
     const int rr = c->rows * c->rows;
-    HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, T0, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
+    std::memcpy(stage, T0, sizeof(T) * rr);
+    HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, stage, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
     // the first loop match may reuse the last classic one
     const int prev_level =
         c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn ? c->ids_level : -1;
@@ -99,10 +107,11 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
         init.keys = c->d_spec_keys;
         init.ratio = (double)(T)(k0 == PMX_FILTER_TRIMMED ? cfg->filter_p[0][0] : 0.5);
         c->spec_init = init;
-        HIPCHK(c, hipMemcpyAsync(c->d_spec, &c->spec_init, sizeof(SpecSel), hipMemcpyHostToDevice, c->stream));
+        std::memcpy(stage + 256, &c->spec_init, sizeof(SpecSel));
+        HIPCHK(c, hipMemcpyAsync(c->d_spec, stage + 256, sizeof(SpecSel), hipMemcpyHostToDevice, c->stream));
     }
+    HIPCHK(c, hipEventRecord(c->loop_stage_ev, c->stream));
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // (T0 may be a stack buffer of the caller)
     c->loop_issued = 0;
     c->loop_iters = 0;
     c->loop_done = false;
