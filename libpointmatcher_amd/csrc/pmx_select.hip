@@ -407,47 +407,335 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ i
     }
 }
 
-// std::partial_sum in T, strictly sequential (one wave; lane l publishes the
-// running sum after adding element l of each 64-chunk)
+// std::partial_sum in T with the sequential rounding, computed in parallel.
+// The running sum s only grows (sorted positive keys), so it stays in one
+// binade [2^e, 2^(e+1)) for long stretches, where every sum is a multiple of
+// u = ulp(2^e) and one IEEE step is exactly
+//     fl(s + x) = s + u * rnd(x / u)      (rnd: nearest; a tie, x / u = m + 1/2,
+//                                          goes to the even result: parity of s/u + m)
+// as long as the result stays below 2^(e+1).  So inside a binade the sums are
+// S_j = S_0 + P_j + C_j in units of u: P_j an integer prefix sum of rnd(x/u)
+// (ties counted as m), C_j the ties that rounded up, resolved in order by one
+// thread from the parity of the sum before each (ties are rare).  The first
+// step whose result reaches 2^(e+1) is done as a plain T addition, and the
+// next stretch starts in the new binade.  Bit-identical to the sequential
+// loop for any input; a chunk with more ties than the LDS list holds is
+// summed sequentially.  One block of kCumThreads, chunks of kCumThreads *
+// kCumPer keys.
+constexpr int kCumThreads = 1024;
+constexpr int kCumPer = 16;
+constexpr int kCumMaxTies = 1024;
 template <typename T>
-__global__ __launch_bounds__(64) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
-                                                       const int* __restrict__ count, T* __restrict__ cum,
-                                                       const LoopCtl* __restrict__ ctl) {
+struct CumBits;
+template <>
+struct CumBits<float> {
+    static constexpr int P = 24;  // significand bits
+    static __device__ __forceinline__ int binade(float s) { return (int)((__float_as_uint(s) >> 23) & 0xffu) - 127; }
+    // s / ulp(2^binade): the significand with its hidden bit (s normal)
+    static __device__ __forceinline__ long long units(float s) {
+        return (long long)((__float_as_uint(s) & 0x7fffffu) | 0x800000u);
+    }
+};
+template <>
+struct CumBits<double> {
+    static constexpr int P = 53;
+    static __device__ __forceinline__ int binade(double s) {
+        return (int)(((unsigned long long)__double_as_longlong(s) >> 52) & 0x7ffull) - 1023;
+    }
+    static __device__ __forceinline__ long long units(double s) {
+        return (long long)(((unsigned long long)__double_as_longlong(s) & 0xfffffffffffffull) | (1ull << 52));
+    }
+};
+__device__ __forceinline__ long long sat_add(long long a, long long b, long long lim) {
+    const long long v = a + b;
+    return v < lim ? v : lim;
+}
+// exclusive saturating scan over the block (values and result <= lim)
+__device__ __forceinline__ long long cum_block_scan(long long v, long long lim, long long* wsum, long long& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    long long incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long u = __shfl_up(incl, off);
+        if (lane >= off) incl = sat_add(incl, u, lim);
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    long long before = 0;
+    total = 0;
+    for (int w = 0; w < kCumThreads / 64; ++w) {
+        before = w < wave ? sat_add(before, wsum[w], lim) : before;
+        total = sat_add(total, wsum[w], lim);
+    }
+    __syncthreads();
+    // exclusive = before + (incl - v), saturated (incl - v is exact: incl < lim, or the chunk has crossed anyway)
+    return sat_add(before, incl - v, lim);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
+                                                                const int* __restrict__ count, T* __restrict__ cum,
+                                                                const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
+    constexpr int P = CumBits<T>::P;
+    constexpr long long LIM = 1ll << P;
+    __shared__ long long wsum[kCumThreads / 64];
+    __shared__ int s_nt;
+    __shared__ int tie_idx[kCumMaxTies];        // chunk-local index, in order
+    __shared__ long long tie_pb[kCumMaxTies];   // P before the tie (ties counted as m)
+    __shared__ long long tie_m[kCumMaxTies];
+    __shared__ int tie_c[kCumMaxTies];          // rounded-up ties up to and including this one
+    __shared__ int s_cross;
+    __shared__ T s_run;                         // the running sum after the chunk
     if (ctl && ctl->done) return;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x;
     const int64_t c = *count;
-    T acc = 0;
-    for (int64_t b = 0; b < c; b += 64) {
-        const int64_t i = b + lane;
-        const T v = i < c ? KO::val(keys[i]) : (T)0;
-        T mine = 0;
-        const int lim = (c - b) < 64 ? (int)(c - b) : 64;
-        for (int l = 0; l < lim; ++l) {
-            const T x = __shfl(v, l);
-            acc = acc + x;  // 0 + x == x exactly, so cum[0] = v[0] as in partial_sum
-            if (lane == l) mine = acc;
+    if (c <= 0) return;
+    // The head sequentially: there the running sum is still of the keys'
+    // size and leaves its binade every few keys (a chunk pass per crossing)
+    constexpr int64_t kHead = 4096;
+    const int64_t ph = c < kHead ? c : kHead;
+    if (t == 0) {
+        T acc = KO::val(keys[0]);  // partial_sum's first output is the first element
+        cum[0] = acc;
+        for (int64_t j = 1; j < ph; ++j) {
+            acc = acc + KO::val(keys[j]);
+            cum[j] = acc;
         }
-        if (i < c) cum[i] = mine;
+        s_run = acc;
+    }
+    __syncthreads();
+    T s = s_run;
+    int64_t p = ph;
+    __syncthreads();
+    while (p < c) {  // (uniform)
+        const int eb = CumBits<T>::binade(s);
+        const double inv_u = ldexp(1.0, P - 1 - eb);  // 1 / ulp(2^eb)
+        const double u = ldexp(1.0, eb - (P - 1));
+        const long long S0 = CumBits<T>::units(s);  // in [2^(P-1), 2^P)
+        // the chunk starts at p rounded down to a multiple of kCumPer (each
+        // thread's keys then come in 16-byte vector loads); keys below p are
+        // inactive (contribute 0, written by an earlier chunk)
+        const int64_t jb = p & ~(int64_t)(kCumPer - 1);
+        const int64_t q1 = jb + (int64_t)kCumThreads * kCumPer < c ? jb + (int64_t)kCumThreads * kCumPer : c;
+        const int64_t j0 = jb + (int64_t)t * kCumPer;
+        using K = typename KO::K;
+        K kv[kCumPer];
+        if (j0 + kCumPer <= c) {
+            using V = typename std::conditional<sizeof(K) == 4, uint4, ulonglong2>::type;
+            constexpr int E = 16 / sizeof(K);
+            const V* vp = reinterpret_cast<const V*>(keys + j0);
+#pragma unroll
+            for (int w = 0; w < kCumPer / E; ++w) {
+                const V x = vp[w];
+                const K* xe = reinterpret_cast<const K*>(&x);
+#pragma unroll
+                for (int e = 0; e < E; ++e) kv[w * E + e] = xe[e];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) kv[i] = j0 + i < c ? keys[j0 + i] : (K)0;
+        }
+        long long r[kCumPer];
+        bool tie[kCumPer];
+        long long loc = 0;
+        int ntie = 0;
+#pragma unroll
+        for (int i = 0; i < kCumPer; ++i) {
+            const int64_t j = j0 + i;
+            r[i] = 0;
+            tie[i] = false;
+            if (j >= p && j < q1) {
+                const double q = (double)KO::val(kv[i]) * inv_u;  // exact (power-of-two scale)
+                if (!(q < (double)LIM)) {
+                    r[i] = LIM;  // (this step alone leaves the binade)
+                } else {
+                    const double m = floor(q), f = q - m;
+                    tie[i] = f == 0.5;
+                    r[i] = (long long)m + (f > 0.5 ? 1 : 0);
+                }
+            }
+            loc = sat_add(loc, r[i], LIM);
+            ntie += tie[i] ? 1 : 0;
+        }
+        long long tot;
+        const long long base = cum_block_scan(loc, LIM, wsum, tot);
+        // the ties, in element order, with the P before each
+        long long tt;
+        const long long tbase = cum_block_scan((long long)ntie, LIM, wsum, tt);
+        if (t == 0) s_nt = (int)tt;
+        if (tt <= kCumMaxTies) {
+            long long run = base;
+            int k = (int)tbase;
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                if (tie[i]) {
+                    tie_idx[k] = t * kCumPer + i;
+                    tie_pb[k] = run;
+                    tie_m[k] = r[i];
+                    ++k;
+                }
+                run = sat_add(run, r[i], LIM);
+            }
+        }
+        __syncthreads();
+        const int nt = s_nt;
+        if (nt > kCumMaxTies) {
+            // (many ties: this chunk sequentially, exactly as partial_sum)
+            if (t == 0) {
+                T acc = s;
+                for (int64_t j = p; j < q1; ++j) {
+                    acc = acc + KO::val(keys[j]);
+                    cum[j] = acc;
+                }
+                s_run = acc;
+            }
+            __syncthreads();
+            s = s_run;
+            p = q1;
+            __syncthreads();
+            continue;
+        }
+        if (t == 0) {
+            int up = 0;
+            for (int k = 0; k < nt; ++k) {
+                const long long before = S0 + tie_pb[k] + up;  // (saturated P: the crossing is before it)
+                up += ((before + tie_m[k]) & 1ll) ? 1 : 0;
+                tie_c[k] = up;
+            }
+            s_cross = 0x7fffffff;
+        }
+        __syncthreads();
+        // every element's sum in units of u; the first that leaves the binade
+        long long run = base;
+        int first = 0x7fffffff;
+        int kt = 0;  // ties at chunk-local index <= the element: binary search over tie_idx
+        {
+            int lo = 0, hi = nt;  // first tie with index >= t * kCumPer
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (tie_idx[mid] < t * kCumPer) lo = mid + 1; else hi = mid;
+            }
+            kt = lo;
+        }
+        long long Sv[kCumPer];
+#pragma unroll
+        for (int i = 0; i < kCumPer; ++i) {
+            run = sat_add(run, r[i], LIM);
+            const int li = t * kCumPer + i;
+            if (kt < nt && tie_idx[kt] == li) ++kt;
+            const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
+            Sv[i] = S0 + run + C;
+            if (j0 + i >= p && j0 + i < q1 && Sv[i] >= LIM && first == 0x7fffffff) first = li;
+        }
+        if (first != 0x7fffffff) atomicMin(&s_cross, first);
+        __syncthreads();
+        const int cross = s_cross;
+#pragma unroll
+        for (int i = 0; i < kCumPer; ++i) {
+            const int li = t * kCumPer + i;
+            const int64_t j = j0 + i;
+            if (j >= p && j < q1 && li < cross) cum[j] = (T)((double)Sv[i] * u);
+            // the running sum: before the crossing, or after the whole chunk
+            if (j >= p && ((cross != 0x7fffffff && li == cross - 1) || (cross == 0x7fffffff && j == q1 - 1)))
+                s_run = (T)((double)Sv[i] * u);
+        }
+        __syncthreads();
+        if (cross == 0x7fffffff) {
+            s = s_run;
+            p = q1;
+        } else {
+            // the crossing step as a plain T addition, then the next binade
+            if (t == 0) {
+                const T prev = jb + cross == p ? s : s_run;  // (the crossing is the chunk's first active key)
+                const T nv = prev + KO::val(keys[jb + cross]);
+                cum[jb + cross] = nv;
+                s_run = nv;
+            }
+            __syncthreads();
+            s = s_run;
+            p = jb + cross + 1;
+        }
+        __syncthreads();
     }
 }
 
 // FRMS_j = (cum[minEl+j] * (1/id)) * ((1/deno)^2), first argmin; writes the
 // optimised ratio (OutlierFiltersImpl.cpp:202-217)
+// (value, index) argmin with the first index on equal values: associative,
+// so block partials combine to the sequential minCoeff's answer (a NaN FRMS
+// value is never taken, as in the sequential scan)
 template <typename T>
-__global__ __launch_bounds__(1024) void vt_frms_kernel(const T* __restrict__ cum, const int* __restrict__ count,
-                                                       const T* __restrict__ deno, int minEl, int maxEl,
-                                                       int points_nbr, double* __restrict__ ratio_dev,
-                                                       int* __restrict__ err, int* __restrict__ iter_err,
-                                                       const LoopCtl* __restrict__ ctl) {
-    __shared__ T sv[1024];
-    __shared__ int si[1024];
+__device__ __forceinline__ void argmin_merge(T& bv, int& bi, T ov, int oi) {
+    if (ov < bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+    }
+}
+template <typename T>
+__device__ __forceinline__ void block_argmin256(T& bv, int& bi, T* sv, int* si) {
+    const int t = threadIdx.x;
+    sv[t] = bv;
+    si[t] = bi;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (t < off) {
+            T v = sv[t];
+            int i = si[t];
+            argmin_merge(v, i, sv[t + off], si[t + off]);
+            sv[t] = v;
+            si[t] = i;
+        }
+        __syncthreads();
+    }
+    bv = sv[0];
+    bi = si[0];
+}
+
+// FRMS_j = (cum[minEl+j] * (1/id)) * ((1/deno)^2) (OutlierFiltersImpl.cpp:202-213),
+// each block's first argmin over a grid-stride slice
+constexpr int kFrmsBlocks = 256;
+template <typename T>
+__global__ __launch_bounds__(256) void vt_frms_part_kernel(const T* __restrict__ cum, const int* __restrict__ count,
+                                                           const T* __restrict__ deno, int minEl, int maxEl,
+                                                           T* __restrict__ part_v, int* __restrict__ part_i,
+                                                           const LoopCtl* __restrict__ ctl) {
+    __shared__ T sv[256];
+    __shared__ int si[256];
+    if (ctl && ctl->done) return;
+    const int c = *count;
+    const int hi = maxEl < c ? maxEl : c;  // reference reads past the filtered count (UB); build clamps
+    const int n = hi - minEl;
+    T bv = (T)__builtin_huge_val();
+    int bi = 0x7fffffff;
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+        const T id = (T)(minEl + 1 + j);
+        const T inv_id = (T)1 / id;
+        const T invd = (T)1 / deno[j];
+        argmin_merge(bv, bi, (cum[minEl + j] * inv_id) * (invd * invd), j);
+    }
+    block_argmin256(bv, bi, sv, si);
+    if (threadIdx.x == 0) {
+        part_v[blockIdx.x] = bv;
+        part_i[blockIdx.x] = bi;
+    }
+}
+
+// the blocks' argmins combined; writes the optimised ratio (:214-217)
+template <typename T>
+__global__ __launch_bounds__(256) void vt_frms_final_kernel(const T* __restrict__ part_v,
+                                                            const int* __restrict__ part_i,
+                                                            const int* __restrict__ count, int minEl, int maxEl,
+                                                            int points_nbr, double* __restrict__ ratio_dev,
+                                                            int* __restrict__ err, int* __restrict__ iter_err,
+                                                            const LoopCtl* __restrict__ ctl) {
+    __shared__ T sv[256];
+    __shared__ int si[256];
     if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     const int c = *count;
-    int hi = maxEl < c ? maxEl : c;  // reference reads past the filtered count (UB); build clamps
-    const int n = hi - minEl;
-    if (c == 0 || n <= 0) {
+    const int hi = maxEl < c ? maxEl : c;
+    if (c == 0 || hi - minEl <= 0) {
         if (t == 0) {
             const int e = c == 0 ? -2 : -3;
             *err = e;
@@ -458,32 +746,10 @@ __global__ __launch_bounds__(1024) void vt_frms_kernel(const T* __restrict__ cum
     }
     T bv = (T)__builtin_huge_val();
     int bi = 0x7fffffff;
-    for (int j = t; j < n; j += 1024) {
-        const T id = (T)(minEl + 1 + j);
-        const T inv_id = (T)1 / id;
-        const T invd = (T)1 / deno[j];
-        const T f = (cum[minEl + j] * inv_id) * (invd * invd);
-        if (f < bv || (f == bv && j < bi)) {
-            bv = f;
-            bi = j;
-        }
-    }
-    sv[t] = bv;
-    si[t] = bi;
-    __syncthreads();
-    for (int off = 512; off > 0; off >>= 1) {
-        if (t < off) {
-            const T ov = sv[t + off];
-            const int oi = si[t + off];
-            if (ov < sv[t] || (ov == sv[t] && oi < si[t])) {
-                sv[t] = ov;
-                si[t] = oi;
-            }
-        }
-        __syncthreads();
-    }
+    for (int b = t; b < kFrmsBlocks; b += 256) argmin_merge(bv, bi, part_v[b], part_i[b]);
+    block_argmin256(bv, bi, sv, si);
     if (t == 0) {
-        const int minIndex = si[0] == 0x7fffffff ? 0 : si[0];
+        const int minIndex = bi == 0x7fffffff ? 0 : bi;
         *ratio_dev = (double)(T)((float)(minIndex + minEl) / (float)points_nbr);
     }
 }
@@ -524,11 +790,16 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
         src = dst;
         dst = tmp;
     }
-    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(64), 0, s, src, hdr, cum, ctl);
+    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ctl);
     const int minEl = (int)std::floor(minRatio * (T)points_nbr);
     const int maxEl = (int)std::floor(maxRatio * (T)points_nbr);
-    hipLaunchKernelGGL(vt_frms_kernel<T>, dim3(1), dim3(1024), 0, s, cum, hdr, deno, minEl, maxEl, points_nbr,
-                       ratio_dev, hdr + 1, err_dev, ctl);
+    // (the radix sort's count / offset scratch, >= 2 KB each, holds the argmin partials)
+    T* part_v = reinterpret_cast<T*>(counts);
+    int* part_i = reinterpret_cast<int*>(offsets);
+    hipLaunchKernelGGL(vt_frms_part_kernel<T>, dim3(kFrmsBlocks), dim3(256), 0, s, cum, hdr, deno, minEl, maxEl, part_v,
+                       part_i, ctl);
+    hipLaunchKernelGGL(vt_frms_final_kernel<T>, dim3(1), dim3(256), 0, s, part_v, part_i, hdr, minEl, maxEl,
+                       points_nbr, ratio_dev, hdr + 1, err_dev, ctl);
 }
 
 // explicit instantiations

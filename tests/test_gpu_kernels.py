@@ -225,3 +225,41 @@ def test_errors_surface_as_reference_exceptions():
     with pytest.raises(P.InvalidParameter):
         ctx.match(np.eye(4, dtype=np.float32), knn=0)
     ctx.close()
+
+
+def _grid_clouds(n_side, dtype, rng):
+    """Reference on a dyadic grid, reading shifted by dyadic offsets: many
+    exactly equal squared distances (ties in VarTrimmed's partial sum)."""
+    g = np.stack(np.meshgrid(*[np.arange(n_side)] * 3, indexing="ij"), -1).reshape(-1, 3).astype(np.float64) * 2.0 ** -6
+    off = rng.integers(0, 4, size=g.shape) * 2.0 ** -9
+    ref = np.hstack([g, np.ones((len(g), 1))]).astype(dtype)
+    rd = np.hstack([g + off, np.ones((len(g), 1))]).astype(dtype)
+    return ref, rd
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("data", ["surface", "dyadic"])
+def test_vartrimmed_parallel_partial_sum(oracle, dtype, data):
+    """VarTrimmed's std::partial_sum in T runs as a binade-segmented integer
+    scan (pmx_select.hip vt_cumsum_kernel): bit-identical to the sequential
+    sum, so the optimised ratio and the weights equal the oracle's — at
+    300k matches, and on dyadic data whose equal distances make the rounding
+    of every step a tie."""
+    rng = np.random.default_rng(11)
+    if data == "surface":
+        ref, nrm = reference_cloud(300000, dtype)
+        rd = reading_cloud(300000, dtype)
+    else:
+        ref, rd = _grid_clouds(48, dtype, rng)
+    filters = [("VarTrimmedDistOutlierFilter", {"minRatio": 0.05, "maxRatio": 0.99, "lambda": 2.35})]
+    ctx = P.Context(0, dtype)
+    ctx.set_reference(ref)
+    ctx.set_reading(rd)
+    ctx.match(np.eye(4, dtype=dtype), knn=1)
+    ctx.outlier(filters[0][0], 0, **filters[0][1])
+    w = ctx.get_weights()
+    d, _ = ctx.get_matches()
+    ctx.close()
+    rc, ow = oracle.outlier_chain(filters, d)
+    assert rc == 0
+    assert np.array_equal(w, ow)
