@@ -22,6 +22,8 @@
 #include "pmx_spec.h"
 #include "pmx_selectall.h"
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -293,26 +295,60 @@ constexpr int kRsTile = 256 * kRsItems;
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+static size_t rs_scan_temp_bytes(int64_t items) {
+    size_t tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)items);
+    return tb;
+}
+
 template <typename T>
 size_t vartrim_scratch_bytes(int64_t n) {
     using K = typename KeyOf<T>::K;
     const int64_t tiles = (n + kRsTile - 1) / kRsTile + 1;
-    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(4 * 256 * tiles);
+    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(4 * 256 * tiles) +
+           al256(rs_scan_temp_bytes(256 * tiles));
 }
 
+// the finite positive distances as keys (OutlierFiltersImpl.cpp:186-188), in
+// any order (sorted next).  One append atomic per block of kCmpPer * 256
+// distances: the compiler already merges a wave's same-address atomics, and
+// the wave-level appends (16 K at C3) serialised at one L2 address for 180 us.
+constexpr int kCmpPer = 16;
 template <typename T>
-__global__ void vt_compact_kernel(const T* __restrict__ d, int64_t n, typename KeyOf<T>::K* __restrict__ keys,
-                                  int* __restrict__ count, const LoopCtl* __restrict__ ctl) {
+__global__ __launch_bounds__(256) void vt_compact_kernel(const T* __restrict__ d, int64_t n,
+                                                         typename KeyOf<T>::K* __restrict__ keys,
+                                                         int* __restrict__ count, const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
+    __shared__ int wtot[4];
+    __shared__ int s_base;
     if (ctl && ctl->done) return;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const T v = d[i];
-        if (v != (T)__builtin_huge_val() && v > (T)0) {  // OutlierFiltersImpl.cpp:186-188
-            const int p = atomicAdd(count, 1);
-            keys[p] = KO::key(v);
-        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kCmpPer;
+    T v[kCmpPer];
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < kCmpPer; ++u) {
+        v[u] = i0 + u < n ? d[i0 + u] : (T)0;
+        c += (v[u] != (T)__builtin_huge_val() && v[u] > (T)0) ? 1 : 0;
     }
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        s_base = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    int pos = s_base + incl - c;
+    for (int w = 0; w < wave; ++w) pos += wtot[w];
+#pragma unroll
+    for (int u = 0; u < kCmpPer; ++u)
+        if (v[u] != (T)__builtin_huge_val() && v[u] > (T)0) keys[pos++] = KO::key(v[u]);
 }
 
 template <typename K>
@@ -331,32 +367,6 @@ __global__ __launch_bounds__(256) void rs_count_kernel(const K* __restrict__ key
     }
     __syncthreads();
     counts[(int64_t)threadIdx.x * tiles + blockIdx.x] = lc[threadIdx.x];
-}
-
-// exclusive scan over 256*tiles counts (digit-major), one block of 1024
-__global__ __launch_bounds__(1024) void rs_scan_kernel(const uint32_t* __restrict__ counts, int64_t total,
-                                                       uint32_t* __restrict__ offsets, const LoopCtl* __restrict__ ctl) {
-    __shared__ uint32_t part[1024];
-    if (ctl && ctl->done) return;
-    const int t = threadIdx.x;
-    const int64_t per = (total + 1023) / 1024;
-    const int64_t lo = t * per;
-    const int64_t hi = lo + per < total ? lo + per : total;
-    uint32_t s = 0;
-    for (int64_t i = lo; i < hi; ++i) s += counts[i];
-    part[t] = s;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = t > 0 ? part[t - 1] : 0u;
-    for (int64_t i = lo; i < hi; ++i) {
-        offsets[i] = run;
-        run += counts[i];
-    }
 }
 
 // stable scatter: keys of a tile are ranked in index order (round-major,
@@ -493,13 +503,19 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     if (c <= 0) return;
     // The head sequentially: there the running sum is still of the keys'
     // size and leaves its binade every few keys (a chunk pass per crossing)
-    constexpr int64_t kHead = 4096;
-    const int64_t ph = c < kHead ? c : kHead;
+    // (keys staged in LDS by the whole block: the one summing thread then
+    // waits on no global load)
+    constexpr int kHead = 4096;
+    __shared__ typename KO::K s_head[kHead];
+    const int ph = c < kHead ? (int)c : kHead;
+    for (int j = t; j < ph; j += kCumThreads) s_head[j] = keys[j];
+    __syncthreads();
     if (t == 0) {
-        T acc = KO::val(keys[0]);  // partial_sum's first output is the first element
+        T acc = KO::val(s_head[0]);  // partial_sum's first output is the first element
         cum[0] = acc;
-        for (int64_t j = 1; j < ph; ++j) {
-            acc = acc + KO::val(keys[j]);
+#pragma unroll 8
+        for (int j = 1; j < ph; ++j) {
+            acc = acc + KO::val(s_head[j]);
             cum[j] = acc;
         }
         s_run = acc;
@@ -773,17 +789,20 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     p += al256(4 * 256 * tiles);
     uint32_t* offsets = reinterpret_cast<uint32_t*>(p);
     p += al256(4 * 256 * tiles);
+    void* scan_temp = p;  // hipcub's scan scratch (the digit counts' exclusive scan)
 
     (void)hipMemsetAsync(hdr, 0, 256, s);
     if (n > 0)
-        hipLaunchKernelGGL(vt_compact_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl);
+        hipLaunchKernelGGL(vt_compact_kernel<T>, dim3((unsigned)((n + 256 * kCmpPer - 1) / (256 * kCmpPer))), dim3(256), 0,
+                           s, d, n, keysA, hdr, ctl);
     const int key_bits = KeyOf<T>::bits;
     K* src = keysA;
     K* dst = keysB;
     for (int shift = 0; shift < key_bits; shift += 8) {
         hipLaunchKernelGGL(rs_count_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, hdr, shift, (int)tiles,
                            counts, ctl);
-        hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(1024), 0, s, counts, (int64_t)256 * tiles, offsets, ctl);
+        size_t tb = rs_scan_temp_bytes(256 * tiles);
+        (void)hipcub::DeviceScan::ExclusiveSum(scan_temp, tb, counts, offsets, (int)(256 * tiles), s);
         hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, dst, hdr, shift,
                            (int)tiles, offsets, ctl);
         K* tmp = src;

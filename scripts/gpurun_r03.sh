@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 measurement session: GPU tests (optional), the default bench line
 # (C3 + CPU baseline + whole ICP), and the kernel-trace summary of the same
-# command without the CPU baseline.  Usage: scripts/gpurun_r03.sh [tests] [bench] [prof] [configs]
+# command without the CPU baseline.  Usage: scripts/gpurun_r03.sh [tests] [quick] [bench] [configs] [vartrim] [prof] [pmc]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R="$(pwd)"
@@ -32,6 +32,10 @@ if [[ "$ARGS" == *" configs "* ]]; then
   for c in c2 c4 c5; do
     step bench_$c && timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || { tail -20 gpurun_out/bench_$c.err; exit 1; }
   done
+fi
+if [[ "$ARGS" == *" vartrim "* ]]; then
+  step bench_c3v && timeout -k 10 300 python bench.py --config c3v --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench_c3v.json 2> gpurun_out/bench_c3v.err || { tail -20 gpurun_out/bench_c3v.err; exit 1; }
+  step prof_c3v && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_c3v" -o run --output-format csv -- python3 "$R/bench.py" --config c3v --steps 10 --warmup 3 --no-cpu-baseline > "$R/gpurun_out/prof_c3v.log" 2>&1) || { tail -20 gpurun_out/prof_c3v.log; exit 1; }
 fi
 if [[ "$ARGS" == *" prof "* ]]; then
   step prof && (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1) || { tail -20 gpurun_out/prof.log; exit 1; }
