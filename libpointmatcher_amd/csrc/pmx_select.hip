@@ -301,13 +301,6 @@ static size_t rs_scan_temp_bytes(int64_t items) {
     return tb;
 }
 
-template <typename T>
-size_t vartrim_scratch_bytes(int64_t n) {
-    using K = typename KeyOf<T>::K;
-    const int64_t tiles = (n + kRsTile - 1) / kRsTile + 1;
-    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(4 * 256 * tiles) +
-           al256(rs_scan_temp_bytes(256 * tiles));
-}
 
 // the finite positive distances as keys (OutlierFiltersImpl.cpp:186-188), in
 // any order (sorted next).  One append atomic per block of kCmpPer * 256
@@ -482,9 +475,246 @@ __device__ __forceinline__ long long cum_block_scan(long long v, long long lim, 
     return sat_add(before, incl - v, lim);
 }
 
+// The head (the first kCumHead keys, where the running sum leaves its binade
+// every few keys) is summed sequentially; the rest is cut into chunks of
+// kCumChunk keys.  A chunk that starts and ends in one binade with few ties
+// is the fast case: given its start sum S0 (exact), its sums are S0 + P_j +
+// C_j with P_j independent of S0, so vt_chunk_prep_kernel computes P for
+// every chunk in parallel under the binade GUESSED from a double prefix of
+// the chunk sums, vt_cumsum_kernel walks the chunks in order with the exact
+// running sum (a fast chunk: the guess checked, its ties resolved by one
+// thread, its end sum in O(ties); any other chunk: the passes below, which
+// write its sums), and vt_chunk_write_kernel writes the fast chunks' sums in
+// parallel.  A wrong guess only sends a chunk to the passes.
+constexpr int kCumChunk = kCumThreads * kCumPer;
+constexpr int kCumHead = 4096;
+constexpr int kFastTies = 256;
+
+struct VtChunk {
+    double sum;   // double sum of the chunk's keys (the guess)
+    long long P;  // integer prefix total under the guessed binade (saturated)
+    double S0;    // exact start sum (T value), fast chunks
+    int e;        // guessed binade
+    int nt;       // ties (kFastTies + 1: too many)
+    int ok;       // 1: a fast chunk (vt_chunk_write_kernel writes it)
+    int pad;
+};
+
+static int64_t vt_chunks(int64_t n) { return n > kCumHead ? (n - kCumHead + kCumChunk - 1) / kCumChunk : 0; }
+
+template <typename T>
+size_t vartrim_scratch_bytes(int64_t n) {
+    using K = typename KeyOf<T>::K;
+    const int64_t tiles = (n + kRsTile - 1) / kRsTile + 1;
+    const int64_t nch = vt_chunks(n);
+    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(4 * 256 * tiles) +
+           al256(rs_scan_temp_bytes(256 * tiles)) + al256(sizeof(VtChunk) * (nch + 1)) +
+           al256((size_t)kFastTies * nch * (2 * sizeof(int) + 2 * sizeof(long long)));
+}
+
+// this thread's kCumPer keys from j0 (16-byte loads when in range)
+template <typename T>
+__device__ __forceinline__ void vt_load(const typename KeyOf<T>::K* __restrict__ keys, int64_t c, int64_t j0,
+                                        typename KeyOf<T>::K (&kv)[kCumPer]) {
+    using K = typename KeyOf<T>::K;
+    if (j0 + kCumPer <= c) {
+        using V = typename std::conditional<sizeof(K) == 4, uint4, ulonglong2>::type;
+        constexpr int E = 16 / sizeof(K);
+        const V* vp = reinterpret_cast<const V*>(keys + j0);
+#pragma unroll
+        for (int w = 0; w < kCumPer / E; ++w) {
+            const V x = vp[w];
+            const K* xe = reinterpret_cast<const K*>(&x);
+#pragma unroll
+            for (int e = 0; e < E; ++e) kv[w * E + e] = xe[e];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kCumPer; ++i) kv[i] = j0 + i < c ? keys[j0 + i] : (K)0;
+    }
+}
+
+// x / u rounded to nearest (a tie counted as m and flagged) for the active
+// keys [p, q1); returns the thread's saturated total
+template <typename T>
+__device__ __forceinline__ long long vt_round(const typename KeyOf<T>::K (&kv)[kCumPer], int64_t j0, int64_t p,
+                                              int64_t q1, double inv_u, long long (&r)[kCumPer],
+                                              bool (&tie)[kCumPer], int& ntie) {
+    using KO = KeyOf<T>;
+    constexpr long long LIM = 1ll << CumBits<T>::P;
+    long long loc = 0;
+    ntie = 0;
+#pragma unroll
+    for (int i = 0; i < kCumPer; ++i) {
+        const int64_t j = j0 + i;
+        r[i] = 0;
+        tie[i] = false;
+        if (j >= p && j < q1) {
+            const double q = (double)KO::val(kv[i]) * inv_u;  // exact (power-of-two scale)
+            if (!(q < (double)LIM)) {
+                r[i] = LIM;  // (this step alone leaves the binade)
+            } else {
+                const double m = floor(q), f = q - m;
+                tie[i] = f == 0.5;
+                r[i] = (long long)m + (f > 0.5 ? 1 : 0);
+            }
+        }
+        loc = sat_add(loc, r[i], LIM);
+        ntie += tie[i] ? 1 : 0;
+    }
+    return loc;
+}
+
+// chunk sums in double (block 0: the head; block b + 1: chunk b)
+template <typename T>
+__global__ __launch_bounds__(kCumThreads) void vt_chunk_sum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
+                                                                   const int* __restrict__ count,
+                                                                   VtChunk* __restrict__ ch,
+                                                                   const LoopCtl* __restrict__ ctl) {
+    using KO = KeyOf<T>;
+    __shared__ double ws[kCumThreads / 64];
+    if (ctl && ctl->done) return;
+    const int64_t c = *count;
+    const int64_t lo = blockIdx.x == 0 ? 0 : kCumHead + (int64_t)(blockIdx.x - 1) * kCumChunk;
+    const int64_t hi = blockIdx.x == 0 ? (c < kCumHead ? c : kCumHead) : (lo + kCumChunk < c ? lo + kCumChunk : c);
+    if (lo >= hi) return;
+    double v = 0.0;
+    for (int64_t j = lo + threadIdx.x; j < hi; j += kCumThreads) v += (double)KO::val(keys[j]);
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kCumThreads / 64; ++w) t += ws[w];
+        ch[blockIdx.x].sum = t;
+    }
+}
+
+// per chunk: the guessed binade, the integer total and the ties under it
+template <typename T>
+__global__ __launch_bounds__(kCumThreads) void vt_chunk_prep_kernel(const typename KeyOf<T>::K* __restrict__ keys,
+                                                                    const int* __restrict__ count,
+                                                                    VtChunk* __restrict__ ch, int* __restrict__ t_idx,
+                                                                    long long* __restrict__ t_pb,
+                                                                    long long* __restrict__ t_m,
+                                                                    const LoopCtl* __restrict__ ctl) {
+    using K = typename KeyOf<T>::K;
+    constexpr int P = CumBits<T>::P;
+    constexpr long long LIM = 1ll << P;
+    __shared__ long long wsum[kCumThreads / 64];
+    __shared__ double s_approx;
+    if (ctl && ctl->done) return;
+    const int64_t c = *count;
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int64_t lo = kCumHead + (int64_t)b * kCumChunk;
+    if (lo >= c) return;
+    const int64_t hi = lo + kCumChunk < c ? lo + kCumChunk : c;
+    if (t == 0) {
+        double a = 0.0;  // the head and every earlier chunk (an estimate of the running sum)
+        for (int i = 0; i <= b; ++i) a += ch[i].sum;
+        s_approx = a;
+    }
+    __syncthreads();
+    const int e = CumBits<T>::binade((T)s_approx);
+    const double inv_u = ldexp(1.0, P - 1 - e);
+    const int64_t j0 = lo + (int64_t)t * kCumPer;
+    K kv[kCumPer];
+    vt_load<T>(keys, c, j0, kv);
+    long long r[kCumPer];
+    bool tie[kCumPer];
+    int ntie;
+    const long long loc = vt_round<T>(kv, j0, lo, hi, inv_u, r, tie, ntie);
+    long long tot, tt;
+    const long long base = cum_block_scan(loc, LIM, wsum, tot);
+    const long long tbase = cum_block_scan((long long)ntie, LIM, wsum, tt);
+    if (tt <= kFastTies) {
+        long long run = base;
+        int k = b * kFastTies + (int)tbase;
+#pragma unroll
+        for (int i = 0; i < kCumPer; ++i) {
+            if (tie[i]) {
+                t_idx[k] = t * kCumPer + i;
+                t_pb[k] = run;
+                t_m[k] = r[i];
+                ++k;
+            }
+            run = sat_add(run, r[i], LIM);
+        }
+    }
+    if (t == 0) {
+        VtChunk& q = ch[b + 1];
+        q.P = tot;
+        q.e = e;
+        q.nt = tt <= kFastTies ? (int)tt : kFastTies + 1;
+        q.ok = 0;
+    }
+}
+
+// the fast chunks' sums: S0 + P_j + C_j in units of the chunk's binade
+template <typename T>
+__global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typename KeyOf<T>::K* __restrict__ keys,
+                                                                     const int* __restrict__ count,
+                                                                     const VtChunk* __restrict__ ch,
+                                                                     const int* __restrict__ t_idx,
+                                                                     const int* __restrict__ t_c, T* __restrict__ cum,
+                                                                     const LoopCtl* __restrict__ ctl) {
+    using K = typename KeyOf<T>::K;
+    constexpr int P = CumBits<T>::P;
+    constexpr long long LIM = 1ll << P;
+    __shared__ long long wsum[kCumThreads / 64];
+    __shared__ int l_idx[kFastTies];
+    __shared__ int l_c[kFastTies];
+    if (ctl && ctl->done) return;
+    const int64_t c = *count;
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int64_t lo = kCumHead + (int64_t)b * kCumChunk;
+    if (lo >= c) return;
+    const VtChunk q = ch[b + 1];
+    if (!q.ok) return;  // (uniform: the passes wrote this chunk)
+    const int64_t hi = lo + kCumChunk < c ? lo + kCumChunk : c;
+    const int nt = q.nt;
+    for (int k = t; k < nt; k += kCumThreads) {
+        l_idx[k] = t_idx[b * kFastTies + k];
+        l_c[k] = t_c[b * kFastTies + k];
+    }
+    const double inv_u = ldexp(1.0, P - 1 - q.e), u = ldexp(1.0, q.e - (P - 1));
+    const long long S0 = CumBits<T>::units((T)q.S0);
+    const int64_t j0 = lo + (int64_t)t * kCumPer;
+    K kv[kCumPer];
+    vt_load<T>(keys, c, j0, kv);
+    long long r[kCumPer];
+    bool tie[kCumPer];
+    int ntie;
+    const long long loc = vt_round<T>(kv, j0, lo, hi, inv_u, r, tie, ntie);
+    long long tot;
+    long long run = cum_block_scan(loc, LIM, wsum, tot);  // (its barriers also publish l_idx / l_c)
+    int kt = 0;
+    {
+        int lo2 = 0, hi2 = nt;  // first tie at a local index >= t * kCumPer
+        while (lo2 < hi2) {
+            const int mid = (lo2 + hi2) >> 1;
+            if (l_idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
+        }
+        kt = lo2;
+    }
+#pragma unroll
+    for (int i = 0; i < kCumPer; ++i) {
+        run = sat_add(run, r[i], LIM);
+        if (kt < nt && l_idx[kt] == t * kCumPer + i) ++kt;
+        const long long C = kt > 0 ? (long long)l_c[kt - 1] : 0ll;
+        const int64_t j = j0 + i;
+        if (j < hi) cum[j] = (T)((double)(S0 + run + C) * u);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
                                                                 const int* __restrict__ count, T* __restrict__ cum,
+                                                                VtChunk* __restrict__ ch,
+                                                                const int* __restrict__ t_idx,
+                                                                const long long* __restrict__ t_pb,
+                                                                const long long* __restrict__ t_m,
+                                                                int* __restrict__ t_c,
                                                                 const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
     constexpr int P = CumBits<T>::P;
@@ -496,18 +726,16 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     __shared__ long long tie_m[kCumMaxTies];
     __shared__ int tie_c[kCumMaxTies];          // rounded-up ties up to and including this one
     __shared__ int s_cross;
+    __shared__ int s_fast;
     __shared__ T s_run;                         // the running sum after the chunk
     if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     const int64_t c = *count;
     if (c <= 0) return;
-    // The head sequentially: there the running sum is still of the keys'
-    // size and leaves its binade every few keys (a chunk pass per crossing)
-    // (keys staged in LDS by the whole block: the one summing thread then
-    // waits on no global load)
-    constexpr int kHead = 4096;
-    __shared__ typename KO::K s_head[kHead];
-    const int ph = c < kHead ? (int)c : kHead;
+    // the head sequentially (keys staged in LDS by the whole block: the one
+    // summing thread then waits on no global load)
+    __shared__ typename KO::K s_head[kCumHead];
+    const int ph = c < kCumHead ? (int)c : kCumHead;
     for (int j = t; j < ph; j += kCumThreads) s_head[j] = keys[j];
     __syncthreads();
     if (t == 0) {
@@ -522,157 +750,166 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     }
     __syncthreads();
     T s = s_run;
-    int64_t p = ph;
     __syncthreads();
-    while (p < c) {  // (uniform)
-        const int eb = CumBits<T>::binade(s);
-        const double inv_u = ldexp(1.0, P - 1 - eb);  // 1 / ulp(2^eb)
-        const double u = ldexp(1.0, eb - (P - 1));
-        const long long S0 = CumBits<T>::units(s);  // in [2^(P-1), 2^P)
-        // the chunk starts at p rounded down to a multiple of kCumPer (each
-        // thread's keys then come in 16-byte vector loads); keys below p are
-        // inactive (contribute 0, written by an earlier chunk)
-        const int64_t jb = p & ~(int64_t)(kCumPer - 1);
-        const int64_t q1 = jb + (int64_t)kCumThreads * kCumPer < c ? jb + (int64_t)kCumThreads * kCumPer : c;
-        const int64_t j0 = jb + (int64_t)t * kCumPer;
-        using K = typename KO::K;
-        K kv[kCumPer];
-        if (j0 + kCumPer <= c) {
-            using V = typename std::conditional<sizeof(K) == 4, uint4, ulonglong2>::type;
-            constexpr int E = 16 / sizeof(K);
-            const V* vp = reinterpret_cast<const V*>(keys + j0);
-#pragma unroll
-            for (int w = 0; w < kCumPer / E; ++w) {
-                const V x = vp[w];
-                const K* xe = reinterpret_cast<const K*>(&x);
-#pragma unroll
-                for (int e = 0; e < E; ++e) kv[w * E + e] = xe[e];
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < kCumPer; ++i) kv[i] = j0 + i < c ? keys[j0 + i] : (K)0;
+    for (int64_t lo = ph, b = 0; lo < c; lo += kCumChunk, ++b) {  // (uniform)
+        const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
+        {  // the chunk's ties into LDS (the deciding thread then reads no global memory)
+            const int ntq = ch[b + 1].nt;
+            if (ntq <= kFastTies)
+                for (int k = t; k < ntq; k += kCumThreads) {
+                    tie_pb[k] = t_pb[b * kFastTies + k];
+                    tie_m[k] = t_m[b * kFastTies + k];
+                }
+            __syncthreads();
         }
-        long long r[kCumPer];
-        bool tie[kCumPer];
-        long long loc = 0;
-        int ntie = 0;
-#pragma unroll
-        for (int i = 0; i < kCumPer; ++i) {
-            const int64_t j = j0 + i;
-            r[i] = 0;
-            tie[i] = false;
-            if (j >= p && j < q1) {
-                const double q = (double)KO::val(kv[i]) * inv_u;  // exact (power-of-two scale)
-                if (!(q < (double)LIM)) {
-                    r[i] = LIM;  // (this step alone leaves the binade)
+        if (t == 0) {
+            // a fast chunk: the guessed binade is the running sum's, few ties,
+            // and the chunk's last sum stays below the next binade
+            VtChunk& q = ch[b + 1];
+            int fast = q.nt <= kFastTies && CumBits<T>::binade(s) == q.e && q.P < LIM;
+            if (fast) {
+                const long long S0 = CumBits<T>::units(s);
+                int up = 0;
+                for (int k = 0; k < q.nt; ++k) {
+                    const long long before = S0 + tie_pb[k] + up;
+                    up += ((before + tie_m[k]) & 1ll) ? 1 : 0;
+                    t_c[b * kFastTies + k] = up;
+                }
+                const long long fin = S0 + q.P + up;
+                if (fin < LIM) {
+                    q.S0 = (double)s;
+                    q.ok = 1;
+                    s_run = (T)((double)fin * ldexp(1.0, q.e - (P - 1)));
                 } else {
-                    const double m = floor(q), f = q - m;
-                    tie[i] = f == 0.5;
-                    r[i] = (long long)m + (f > 0.5 ? 1 : 0);
+                    fast = 0;
                 }
             }
-            loc = sat_add(loc, r[i], LIM);
-            ntie += tie[i] ? 1 : 0;
-        }
-        long long tot;
-        const long long base = cum_block_scan(loc, LIM, wsum, tot);
-        // the ties, in element order, with the P before each
-        long long tt;
-        const long long tbase = cum_block_scan((long long)ntie, LIM, wsum, tt);
-        if (t == 0) s_nt = (int)tt;
-        if (tt <= kCumMaxTies) {
-            long long run = base;
-            int k = (int)tbase;
-#pragma unroll
-            for (int i = 0; i < kCumPer; ++i) {
-                if (tie[i]) {
-                    tie_idx[k] = t * kCumPer + i;
-                    tie_pb[k] = run;
-                    tie_m[k] = r[i];
-                    ++k;
-                }
-                run = sat_add(run, r[i], LIM);
-            }
+            s_fast = fast;
         }
         __syncthreads();
-        const int nt = s_nt;
-        if (nt > kCumMaxTies) {
-            // (many ties: this chunk sequentially, exactly as partial_sum)
-            if (t == 0) {
-                T acc = s;
-                for (int64_t j = p; j < q1; ++j) {
-                    acc = acc + KO::val(keys[j]);
-                    cum[j] = acc;
-                }
-                s_run = acc;
-            }
-            __syncthreads();
+        if (s_fast) {
             s = s_run;
-            p = q1;
             __syncthreads();
             continue;
         }
-        if (t == 0) {
-            int up = 0;
-            for (int k = 0; k < nt; ++k) {
-                const long long before = S0 + tie_pb[k] + up;  // (saturated P: the crossing is before it)
-                up += ((before + tie_m[k]) & 1ll) ? 1 : 0;
-                tie_c[k] = up;
-            }
-            s_cross = 0x7fffffff;
-        }
-        __syncthreads();
-        // every element's sum in units of u; the first that leaves the binade
-        long long run = base;
-        int first = 0x7fffffff;
-        int kt = 0;  // ties at chunk-local index <= the element: binary search over tie_idx
-        {
-            int lo = 0, hi = nt;  // first tie with index >= t * kCumPer
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (tie_idx[mid] < t * kCumPer) lo = mid + 1; else hi = mid;
-            }
-            kt = lo;
-        }
-        long long Sv[kCumPer];
+        int64_t p = lo;
+        while (p < cend) {  // (uniform) passes over [p, cend)
+            const int eb = CumBits<T>::binade(s);
+            const double inv_u = ldexp(1.0, P - 1 - eb);  // 1 / ulp(2^eb)
+            const double u = ldexp(1.0, eb - (P - 1));
+            const long long S0 = CumBits<T>::units(s);  // in [2^(P-1), 2^P)
+            // the pass starts at p rounded down to a multiple of kCumPer (each
+            // thread's keys then come in 16-byte vector loads); keys below p
+            // are inactive (contribute 0, written earlier)
+            const int64_t jb = p & ~(int64_t)(kCumPer - 1);
+            const int64_t q1 = jb + (int64_t)kCumChunk < cend ? jb + (int64_t)kCumChunk : cend;
+            const int64_t j0 = jb + (int64_t)t * kCumPer;
+            typename KO::K kv[kCumPer];
+            vt_load<T>(keys, c, j0, kv);
+            long long r[kCumPer];
+            bool tie[kCumPer];
+            int ntie;
+            const long long loc = vt_round<T>(kv, j0, p, q1, inv_u, r, tie, ntie);
+            long long tot;
+            const long long base = cum_block_scan(loc, LIM, wsum, tot);
+            // the ties, in element order, with the P before each
+            long long tt;
+            const long long tbase = cum_block_scan((long long)ntie, LIM, wsum, tt);
+            if (t == 0) s_nt = (int)tt;
+            if (tt <= kCumMaxTies) {
+                long long run = base;
+                int k = (int)tbase;
 #pragma unroll
-        for (int i = 0; i < kCumPer; ++i) {
-            run = sat_add(run, r[i], LIM);
-            const int li = t * kCumPer + i;
-            if (kt < nt && tie_idx[kt] == li) ++kt;
-            const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
-            Sv[i] = S0 + run + C;
-            if (j0 + i >= p && j0 + i < q1 && Sv[i] >= LIM && first == 0x7fffffff) first = li;
-        }
-        if (first != 0x7fffffff) atomicMin(&s_cross, first);
-        __syncthreads();
-        const int cross = s_cross;
-#pragma unroll
-        for (int i = 0; i < kCumPer; ++i) {
-            const int li = t * kCumPer + i;
-            const int64_t j = j0 + i;
-            if (j >= p && j < q1 && li < cross) cum[j] = (T)((double)Sv[i] * u);
-            // the running sum: before the crossing, or after the whole chunk
-            if (j >= p && ((cross != 0x7fffffff && li == cross - 1) || (cross == 0x7fffffff && j == q1 - 1)))
-                s_run = (T)((double)Sv[i] * u);
-        }
-        __syncthreads();
-        if (cross == 0x7fffffff) {
-            s = s_run;
-            p = q1;
-        } else {
-            // the crossing step as a plain T addition, then the next binade
-            if (t == 0) {
-                const T prev = jb + cross == p ? s : s_run;  // (the crossing is the chunk's first active key)
-                const T nv = prev + KO::val(keys[jb + cross]);
-                cum[jb + cross] = nv;
-                s_run = nv;
+                for (int i = 0; i < kCumPer; ++i) {
+                    if (tie[i]) {
+                        tie_idx[k] = t * kCumPer + i;
+                        tie_pb[k] = run;
+                        tie_m[k] = r[i];
+                        ++k;
+                    }
+                    run = sat_add(run, r[i], LIM);
+                }
             }
             __syncthreads();
-            s = s_run;
-            p = jb + cross + 1;
+            const int nt = s_nt;
+            if (nt > kCumMaxTies) {
+                // (many ties: this pass sequentially, exactly as partial_sum)
+                if (t == 0) {
+                    T acc = s;
+                    for (int64_t j = p; j < q1; ++j) {
+                        acc = acc + KO::val(keys[j]);
+                        cum[j] = acc;
+                    }
+                    s_run = acc;
+                }
+                __syncthreads();
+                s = s_run;
+                p = q1;
+                __syncthreads();
+                continue;
+            }
+            if (t == 0) {
+                int up = 0;
+                for (int k = 0; k < nt; ++k) {
+                    const long long before = S0 + tie_pb[k] + up;  // (saturated P: the crossing is before it)
+                    up += ((before + tie_m[k]) & 1ll) ? 1 : 0;
+                    tie_c[k] = up;
+                }
+                s_cross = 0x7fffffff;
+            }
+            __syncthreads();
+            // every element's sum in units of u; the first that leaves the binade
+            long long run = base;
+            int first = 0x7fffffff;
+            int kt = 0;  // ties at chunk-local index <= the element: binary search over tie_idx
+            {
+                int lo2 = 0, hi2 = nt;  // first tie with index >= t * kCumPer
+                while (lo2 < hi2) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (tie_idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
+                }
+                kt = lo2;
+            }
+            long long Sv[kCumPer];
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                run = sat_add(run, r[i], LIM);
+                const int li = t * kCumPer + i;
+                if (kt < nt && tie_idx[kt] == li) ++kt;
+                const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
+                Sv[i] = S0 + run + C;
+                if (j0 + i >= p && j0 + i < q1 && Sv[i] >= LIM && first == 0x7fffffff) first = li;
+            }
+            if (first != 0x7fffffff) atomicMin(&s_cross, first);
+            __syncthreads();
+            const int cross = s_cross;
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                const int li = t * kCumPer + i;
+                const int64_t j = j0 + i;
+                if (j >= p && j < q1 && li < cross) cum[j] = (T)((double)Sv[i] * u);
+                // the running sum: before the crossing, or after the whole pass
+                if (j >= p && ((cross != 0x7fffffff && li == cross - 1) || (cross == 0x7fffffff && j == q1 - 1)))
+                    s_run = (T)((double)Sv[i] * u);
+            }
+            __syncthreads();
+            if (cross == 0x7fffffff) {
+                s = s_run;
+                p = q1;
+            } else {
+                // the crossing step as a plain T addition, then the next binade
+                if (t == 0) {
+                    const T prev = jb + cross == p ? s : s_run;  // (the crossing is the pass's first active key)
+                    const T nv = prev + KO::val(keys[jb + cross]);
+                    cum[jb + cross] = nv;
+                    s_run = nv;
+                }
+                __syncthreads();
+                s = s_run;
+                p = jb + cross + 1;
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
@@ -790,6 +1027,14 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     uint32_t* offsets = reinterpret_cast<uint32_t*>(p);
     p += al256(4 * 256 * tiles);
     void* scan_temp = p;  // hipcub's scan scratch (the digit counts' exclusive scan)
+    p += al256(rs_scan_temp_bytes(256 * tiles));
+    const int64_t nch = vt_chunks(n);
+    VtChunk* ch = reinterpret_cast<VtChunk*>(p);
+    p += al256(sizeof(VtChunk) * (nch + 1));
+    long long* t_pb = reinterpret_cast<long long*>(p);
+    long long* t_m = t_pb + kFastTies * nch;
+    int* t_idx = reinterpret_cast<int*>(t_m + kFastTies * nch);
+    int* t_c = t_idx + kFastTies * nch;
 
     (void)hipMemsetAsync(hdr, 0, 256, s);
     if (n > 0)
@@ -809,7 +1054,16 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
         src = dst;
         dst = tmp;
     }
-    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ctl);
+    if (nch > 0) {
+        hipLaunchKernelGGL(vt_chunk_sum_kernel<T>, dim3((unsigned)(nch + 1)), dim3(kCumThreads), 0, s, src, hdr, ch, ctl);
+        hipLaunchKernelGGL(vt_chunk_prep_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, t_idx,
+                           t_pb, t_m, ctl);
+    }
+    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ch, t_idx, t_pb, t_m, t_c,
+                       ctl);
+    if (nch > 0)
+        hipLaunchKernelGGL(vt_chunk_write_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, t_idx,
+                           t_c, cum, ctl);
     const int minEl = (int)std::floor(minRatio * (T)points_nbr);
     const int maxEl = (int)std::floor(maxRatio * (T)points_nbr);
     // (the radix sort's count / offset scratch, >= 2 KB each, holds the argmin partials)

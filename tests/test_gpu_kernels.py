@@ -238,17 +238,20 @@ def _grid_clouds(n_side, dtype, rng):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("data", ["surface", "dyadic"])
+@pytest.mark.parametrize("data", ["surface", "surface1m", "dyadic"])
 def test_vartrimmed_parallel_partial_sum(oracle, dtype, data):
     """VarTrimmed's std::partial_sum in T runs as a binade-segmented integer
-    scan (pmx_select.hip vt_cumsum_kernel): bit-identical to the sequential
-    sum, so the optimised ratio and the weights equal the oracle's — at
-    300k matches, and on dyadic data whose equal distances make the rounding
+    scan over chunks (pmx_select.hip vt_chunk_prep / vt_cumsum /
+    vt_chunk_write kernels): bit-identical to the sequential sum, so the
+    optimised ratio and the weights equal the oracle's — at 300k and 1M
+    matches, and on dyadic data whose equal distances make the rounding
     of every step a tie."""
     rng = np.random.default_rng(11)
-    if data == "surface":
-        ref, nrm = reference_cloud(300000, dtype)
-        rd = reading_cloud(300000, dtype)
+    if data.startswith("surface"):
+        # (1M: about 60 chunks of the parallel partial sum, most on its fast path)
+        size = 1000000 if data == "surface1m" else 300000
+        ref, nrm = reference_cloud(size, dtype)
+        rd = reading_cloud(size, dtype)
     else:
         ref, rd = _grid_clouds(48, dtype, rng)
     filters = [("VarTrimmedDistOutlierFilter", {"minRatio": 0.05, "maxRatio": 0.99, "lambda": 2.35})]
