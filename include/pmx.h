@@ -124,6 +124,15 @@ int pmx_comm_size(const pmx_ctx* ctx, int* nranks, int* rank, int* kind);
  * quantile was resolved inside the exchanged key window issues two: the
  * window segments' all-gather and the normal equations' all-reduce. */
 int pmx_comm_stats(const pmx_ctx* ctx, uint64_t* allreduces, uint64_t* allgathers);
+/* How a sharded device loop synchronised (no reference counterpart: the
+ * reference has one process, ICP.cpp:371-430).  verdict_syncs: iterations
+ * whose window verdict the host read back (one stream synchronisation each;
+ * only while the window is settling: after a miss, until two hits in a row);
+ * async_iterations: iterations enqueued without reading it (zero host
+ * synchronisations: a miss stalls the device loop); stalls: those misses,
+ * each replayed at the next batch check (its radix passes and histogram
+ * all-reduces, then the rest of the iteration). */
+int pmx_comm_loop_stats(const pmx_ctx* ctx, uint64_t* verdict_syncs, uint64_t* async_iterations, uint64_t* stalls);
 
 /* ------------------------------------------------------------ clouds --- */
 /* feat: rows x M column-major (point-major) T array, rows = D + 1 with the

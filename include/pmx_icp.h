@@ -109,6 +109,10 @@ int pmx_icp_timing_read(pmx_icp* icp, double* match_ms, int64_t* match_launches)
  * was resolved inside the match's key window, and iterations that ran the
  * radix passes.  Diagnostics only (no reference counterpart). */
 int pmx_icp_select_stats(pmx_icp* icp, uint64_t* window_hits, uint64_t* window_misses);
+/* multi-rank: the context's collectives and loop synchronisations since
+ * creation (pmx_comm_stats, pmx_comm_loop_stats).  Diagnostics only. */
+int pmx_icp_comm_stats(pmx_icp* icp, uint64_t* allreduces, uint64_t* allgathers, uint64_t* verdict_syncs,
+                       uint64_t* async_iterations, uint64_t* stalls);
 
 /* ICPSequence (PointMatcher.h:730-764, ICP.cpp:455-609).  set_map replaces
  * ICPSequence::setMap: the map is centred on its mean, filtered by the
@@ -120,12 +124,14 @@ int pmx_icp_select_stats(pmx_icp* icp, uint64_t* window_hits, uint64_t* window_m
  * no map T_out is the identity.  sequence_prepare is its first phase
  * (prepared = 0 without a map), followed by pmx_icp_iterate / pmx_icp_finish.
  * get_map: the prefiltered map in global coordinates (ICP.cpp:543-554),
- * rows x n features, point-major; features NULL returns n only.  A
- * load_yaml / set_default re-indexes a held map (ICP.cpp:520-539). */
+ * rows x n features, point-major, into `features` of `capacity` values;
+ * features NULL returns n and rows only, a capacity below n * rows is
+ * PMX_ICP_INVALID_PARAMETER (nothing written).  A load_yaml / set_default
+ * re-indexes a held map (ICP.cpp:520-539). */
 int pmx_icp_set_map(pmx_icp* icp, const void* map, int rows, int64_t M, const void* normals, int* accepted);
 int pmx_icp_clear_map(pmx_icp* icp);
 int pmx_icp_has_map(const pmx_icp* icp, int* has);
-int pmx_icp_get_map(pmx_icp* icp, void* features, int64_t* n);
+int pmx_icp_get_map(pmx_icp* icp, void* features, int64_t capacity, int64_t* n, int* rows);
 int pmx_icp_sequence_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init,
                              int* prepared);
 int pmx_icp_sequence_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init,

@@ -128,10 +128,14 @@ void set_map_impl(pmx_icp* icp, const void* map, int rows, int64_t M, const void
 }
 
 template <typename T>
-void get_map_impl(pmx_icp* icp, void* feat, int64_t* n) {
+void get_map_impl(pmx_icp* icp, void* feat, int64_t capacity, int64_t* n, int* rows) {
     const auto g = get<T>(icp).getPrefilteredMap();
     if (n) *n = g.n;
-    if (feat) std::memcpy(feat, g.features.data(), sizeof(T) * g.features.size());
+    if (rows) *rows = g.rows;
+    if (!feat) return;
+    if (capacity < 0 || (uint64_t)capacity < (uint64_t)g.features.size())
+        throw InvalidParameter("pmx_icp_get_map: capacity below n * rows");
+    std::memcpy(feat, g.features.data(), sizeof(T) * g.features.size());
 }
 
 // 1: prepared (iterate / finish follow), 0: no map (T_out = identity)
@@ -296,15 +300,20 @@ int pmx_icp_has_map(const pmx_icp* icp, int* has) {
     return PMX_ICP_OK;
 }
 
-int pmx_icp_get_map(pmx_icp* icp, void* features, int64_t* n) {
+int pmx_icp_get_map(pmx_icp* icp, void* features, int64_t capacity, int64_t* n, int* rows) {
     if (!icp) return PMX_ICP_INVALID_PARAMETER;
-    return guarded(icp, [&] { BOTH(icp, get_map_impl<float>(icp, features, n), get_map_impl<double>(icp, features, n)); });
+    return guarded(icp, [&] {
+        BOTH(icp, get_map_impl<float>(icp, features, capacity, n, rows),
+             get_map_impl<double>(icp, features, capacity, n, rows));
+    });
 }
 
 int pmx_icp_sequence_prepare(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init, int* prepared) {
     if (!icp) return PMX_ICP_INVALID_PARAMETER;
     return guarded(icp, [&] {
-        if (!reading && N > 0) throw InvalidParameter("pmx_icp_sequence_prepare: null reading");
+        // (the pmx_icp_set_map checks: make_cloud reads rows - 1 coordinates per point)
+        if ((!reading && N > 0) || N < 0 || (rows != 3 && rows != 4))
+            throw InvalidParameter("pmx_icp_sequence_prepare: bad arguments");
         const int p = BOTH(icp, seq_prepare_impl<float>(icp, reading, rows, N, T_init),
                            seq_prepare_impl<double>(icp, reading, rows, N, T_init));
         if (prepared) *prepared = p;
@@ -314,6 +323,10 @@ int pmx_icp_sequence_prepare(pmx_icp* icp, const void* reading, int rows, int64_
 int pmx_icp_sequence_compute(pmx_icp* icp, const void* reading, int rows, int64_t N, const void* T_init,
                              void* T_out) {
     if (!icp || !T_out) return PMX_ICP_INVALID_PARAMETER;
+    if ((!reading && N > 0) || N < 0 || (rows != 3 && rows != 4)) {  // (before the identity is written)
+        icp->err = "pmx_icp_sequence_compute: bad arguments";
+        return PMX_ICP_INVALID_PARAMETER;
+    }
     int prepared = 0;
     int rc = pmx_icp_sequence_prepare(icp, reading, rows, N, T_init, &prepared);
     if (rc) return rc;
@@ -386,6 +399,18 @@ int pmx_icp_select_stats(pmx_icp* icp, uint64_t* hits, uint64_t* misses) {
         Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
         dev.ensure();
         dev.check(pmx_loop_select_stats(dev.ctx, hits, misses));
+    });
+}
+
+int pmx_icp_comm_stats(pmx_icp* icp, uint64_t* allreduces, uint64_t* allgathers, uint64_t* verdict_syncs,
+                       uint64_t* async_iterations, uint64_t* stalls) {
+    if (!icp || !allreduces || !allgathers || !verdict_syncs || !async_iterations || !stalls)
+        return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] {
+        Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
+        dev.ensure();
+        dev.check(pmx_comm_stats(dev.ctx, allreduces, allgathers));
+        dev.check(pmx_comm_loop_stats(dev.ctx, verdict_syncs, async_iterations, stalls));
     });
 }
 

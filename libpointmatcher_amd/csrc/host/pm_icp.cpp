@@ -1345,8 +1345,8 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
         for (int64_t j = 0; j < M; ++j) reference.features[j * dim + r] = reference.features[j * dim + r] - mean;
     }
     dev.ensure();
+    mapIndexed_ = false;            // (an ICPSequence map is no longer the device's reference, even if init throws)
     matcher->init(dev, reference);  // ICP.cpp:302
-    mapIndexed_ = false;            // (an ICPSequence map is no longer the device's reference)
     referencePreprocessingDuration = since<T>(t);
     prefilteredReferencePtsCount = M;
     prepareReading(readingIn, T_init);
@@ -1432,24 +1432,30 @@ bool PointMatcher<T>::ICP::setMap(const DataPoints& inputCloud) {
             if (f->usesRandState())
                 throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
                                          "the reading shards of a multi-rank ICP");
-    map_ = inputCloud;
+    // the new map is built in locals and committed only once it is indexed:
+    // a filter or Matcher::init that throws leaves the previous map (or none),
+    // and mapIndexed_ false — the device reference may be half replaced
+    mapIndexed_ = false;
+    DataPoints map(inputCloud);
     // the mean of the map BEFORE the reference filters (ICP.cpp:490-497; ICP::compute
     // filters first), sequential sums in T as prepare
-    T_map_.assign((size_t)dim * dim, (T)0);
-    for (int i = 0; i < dim; ++i) T_map_[i * dim + i] = 1;
+    TransformationParameters T_map((size_t)dim * dim, (T)0);
+    for (int i = 0; i < dim; ++i) T_map[i * dim + i] = 1;
     for (int r = 0; r < dim - 1; ++r) {
         T s = 0;
-        for (int64_t j = 0; j < ptCount; ++j) s = s + map_.features[j * dim + r];
+        for (int64_t j = 0; j < ptCount; ++j) s = s + map.features[j * dim + r];
         const T mean = s / (T)ptCount;
-        T_map_[r * dim + dim - 1] = mean;
-        for (int64_t j = 0; j < ptCount; ++j) map_.features[j * dim + r] = map_.features[j * dim + r] - mean;
+        T_map[r * dim + dim - 1] = mean;
+        for (int64_t j = 0; j < ptCount; ++j) map.features[j * dim + r] = map.features[j * dim + r] - mean;
     }
     for (auto& f : referenceDataPointsFilters) f->device = dev.device;
     referenceDataPointsFilters.init();
-    referenceDataPointsFilters.apply(map_);
-    if (map_.n <= 0) throw ConvergenceError("empty reference");
+    referenceDataPointsFilters.apply(map);
+    if (map.n <= 0) throw ConvergenceError("empty reference");
     dev.ensure();
-    matcher->init(dev, map_);  // ICP.cpp:503 (the grid stays on the device)
+    matcher->init(dev, map);  // ICP.cpp:503 (the grid stays on the device)
+    map_ = std::move(map);
+    T_map_ = std::move(T_map);
     mapIndexed_ = true;
     referencePreprocessingDuration = since<T>(t);  // (SetMapDuration)
     prefilteredReferencePtsCount = map_.n;

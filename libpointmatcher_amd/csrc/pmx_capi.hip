@@ -18,6 +18,7 @@ size_t tsize(const pmx_ctx* c) { return c->dtype == PMX_F64 ? 8 : 4; }
 
 // the device loop's control word while iterations are being enqueued
 const LoopCtl* loop_ctl(const pmx_ctx* c) { return c->loop_on ? c->d_ctl : nullptr; }
+LoopCtl* loop_on_ctl(pmx_ctx* c) { return c->loop_on ? c->d_ctl : nullptr; }
 
 int ensure(pmx_ctx* c, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes && *p) return PMX_OK;
@@ -169,6 +170,16 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
+    // test hook: device-loop iterations (0-based, comma separated) whose
+    // sharded window pick is forced to miss (the stall-and-replay path)
+    if (const char* e = std::getenv("PMX_DEBUG_FORCE_MISS"))
+        for (const char* p = e; *p;) {
+            char* end = nullptr;
+            const long long v = std::strtoll(p, &end, 10);
+            if (end == p) break;
+            c->debug_force_miss.push_back((int64_t)v);
+            p = *end == ',' ? end + 1 : end;
+        }
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
@@ -298,6 +309,14 @@ int pmx_comm_stats(const pmx_ctx* c, uint64_t* allreduces, uint64_t* allgathers)
     if (!c || !allreduces || !allgathers) return PMX_E_BAD_PARAM;
     *allreduces = c->n_allreduce;
     *allgathers = c->n_allgather;
+    return PMX_OK;
+}
+
+int pmx_comm_loop_stats(const pmx_ctx* c, uint64_t* verdict_syncs, uint64_t* async_iterations, uint64_t* stalls) {
+    if (!c || !verdict_syncs || !async_iterations || !stalls) return PMX_E_BAD_PARAM;
+    *verdict_syncs = c->n_verdict_sync;
+    *async_iterations = c->n_async;
+    *stalls = c->n_stall;
     return PMX_OK;
 }
 

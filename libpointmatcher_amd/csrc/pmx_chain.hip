@@ -511,7 +511,10 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
             int rc = coll_allgather(c, xseg, xseg + kSpecXStride, kSpecXStride * sizeof(unsigned long long));
             if (rc) return rc;
-            launch_spec_pick<T>(xseg + kSpecXStride, c->nranks, spec, c->d_sel, loop_ctl(c), c->stream);
+            const bool force = c->enq_iter >= 0 && std::find(c->debug_force_miss.begin(), c->debug_force_miss.end(),
+                                                             c->enq_iter) != c->debug_force_miss.end();
+            launch_spec_pick<T>(xseg + kSpecXStride, c->nranks, spec, c->d_sel, loop_on_ctl(c), c->shard_async ? 1 : 0,
+                                force ? 1 : 0, c->stream);
             c->spec_exchanged = true;
         }
         c->safe_valid = ru.mode != 0;
@@ -544,6 +547,7 @@ int sharded_window_resolved(pmx_ctx* c, SpecSel* spec) {
     const LoopCtl* ctl = loop_ctl(c);
     if (ctl) HIPCHK(c, hipMemcpyAsync(c->h_flags + 1, &ctl->done, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    ++c->n_verdict_sync;
     if (c->h_flags[1]) c->shard_done_seen = true;  // (the loop's later iterations are not enqueued)
     return c->h_flags[0] != 0 || c->h_flags[1] != 0 ? 1 : 0;
 }
@@ -555,9 +559,21 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
     const int passes = select_passes<T>();
     if (spec && c->spec_exchanged && sharded(c)) {
         c->spec_exchanged = false;
-        const int r = sharded_window_resolved(c, spec);
-        if (r < 0) return r;
-        if (r == 1) return PMX_OK;  // (the pass kernels would return at spec->hit; no histogram exchange)
+        if (c->shard_replay || c->spec_fresh) {
+            // a known miss (the stalled pick missed, or the window is still
+            // empty): the passes below, no verdict to read
+            c->spec_fresh = false;
+            c->shard_hit_streak = 0;
+        } else if (c->shard_async) {
+            // verdict not read back: on a miss spec_pick_kernel stalled the
+            // loop, and the host replays this iteration (pmx_loop_capi.hip)
+            return PMX_OK;
+        } else {
+            const int r = sharded_window_resolved(c, spec);
+            if (r < 0) return r;
+            c->shard_hit_streak = r == 1 ? c->shard_hit_streak + 1 : 0;
+            if (r == 1) return PMX_OK;  // (the pass kernels would return at spec->hit; no histogram exchange)
+        }
     }
     if (!sharded(c)) {
         // every pass in one launch (a no-op launch when the window resolved it)

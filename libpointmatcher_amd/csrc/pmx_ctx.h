@@ -204,6 +204,18 @@ struct pmx_ctx {
     bool spec_exchanged = false;  // this match all-gathered the window segments and picked
     bool shard_done_seen = false; // a sharded loop read back its stop flag: no more iterations to enqueue
     uint64_t n_allreduce = 0, n_allgather = 0;  // collectives issued (pmx_comm_stats)
+    // Stall-and-replay of a sharded device loop (pmx_loop_capi.hip): the host
+    // reads the window verdict back (a stream synchronisation per iteration)
+    // only until kAsyncAfterHits hits in a row; after that it enqueues whole
+    // iterations without reading it, a miss stalls the loop on the device
+    // (kCtlStalled) and the batch check replays the stalled iteration.
+    int shard_hit_streak = 0;
+    bool shard_async = false;     // the iteration being enqueued does not read its verdict back
+    bool shard_replay = false;    // the iteration being enqueued replays a stalled one (its match ran)
+    bool spec_fresh = false;      // the window is empty (a loop's first iteration): a known miss
+    int64_t enq_iter = -1;        // loop iteration being enqueued (-1: not in a loop)
+    uint64_t n_verdict_sync = 0, n_async = 0, n_stall = 0;  // pmx_comm_loop_stats
+    std::vector<int64_t> debug_force_miss;  // PMX_DEBUG_FORCE_MISS: loop iterations whose window pick misses
     size_t h_stage_cap = 0;
     unsigned long long* d_specx = nullptr;  // quantile window exchange: own segment, then nranks gathered
 
@@ -269,6 +281,7 @@ int fail(pmx_ctx* c, int code, const std::string& msg);
 size_t tsize(const pmx_ctx* c);
 // the device loop's control word while iterations are being enqueued
 const LoopCtl* loop_ctl(const pmx_ctx* c);
+LoopCtl* loop_on_ctl(pmx_ctx* c);  // (the same, writable: the kernels that stop the loop)
 int ensure(pmx_ctx* c, void** p, size_t* cap, size_t bytes);
 
 // embed a rows x rows host transform (row-major T) into a 4x4 (see pmx_internal.h)

@@ -458,17 +458,22 @@ __global__ __launch_bounds__(kVSlots) void counter_sum_kernel(unsigned long long
 // (pmx_spec.h).  Every rank runs it on the same segments and writes the same
 // limit; a miss leaves the radix passes (with their histogram all-reduce) to
 // resolve it.
+// stall (the host enqueued the rest of the iteration without reading the
+// verdict): a miss stops the loop with done = kCtlStalled, so every kernel
+// enqueued after it returns at once, until the host replays the iteration's
+// radix passes (pmx_loop_capi.hip).  Every rank picks from the same union, so
+// every rank stalls at the same iteration.
 template <typename T>
 __global__ __launch_bounds__(kVSlots) void spec_pick_kernel(const unsigned long long* __restrict__ segs, int nseg,
                                                             SpecSel* __restrict__ spec,
                                                             SelectState* __restrict__ st,
-                                                            const LoopCtl* __restrict__ ctl) {
+                                                            LoopCtl* __restrict__ ctl, int stall, int force_miss) {
     __shared__ uint32_t lh[2048];
     __shared__ unsigned long long part[kVSlots];
     __shared__ unsigned long long bc[2];
     if (ctl && ctl->done) return;
     unsigned long long fin = 0, below = 0, nk = 0;
-    bool overflow = false;
+    bool overflow = force_miss != 0;  // (an overflowing segment makes the pick miss)
     for (int s = 0; s < nseg; ++s) {  // (uniform; a handful of segments)
         const unsigned long long* g = segs + (size_t)s * kSpecXStride;
         fin += g[0];
@@ -479,17 +484,19 @@ __global__ __launch_bounds__(kVSlots) void spec_pick_kernel(const unsigned long 
     SpecKeys<T> src;
     src.segs = segs;
     src.nseg = nseg;
-    spec_pick<T, kVSlots>(spec, st, fin, below, nk, overflow, src, lh, part, bc);
+    const bool hit = spec_pick<T, kVSlots>(spec, st, fin, below, nk, overflow, src, lh, part, bc);
+    if (!hit && stall && ctl && threadIdx.x == 0) ctl->done = kCtlStalled;
 }
 
 template <typename T>
-void launch_spec_pick(const unsigned long long* segs, int nseg, SpecSel* spec, SelectState* st, const LoopCtl* ctl,
-                      hipStream_t s) {
-    hipLaunchKernelGGL(spec_pick_kernel<T>, dim3(1), dim3(kVSlots), 0, s, segs, nseg, spec, st, ctl);
+void launch_spec_pick(const unsigned long long* segs, int nseg, SpecSel* spec, SelectState* st, LoopCtl* ctl,
+                      int stall, int force_miss, hipStream_t s) {
+    hipLaunchKernelGGL(spec_pick_kernel<T>, dim3(1), dim3(kVSlots), 0, s, segs, nseg, spec, st, ctl, stall,
+                       force_miss);
 }
-template void launch_spec_pick<float>(const unsigned long long*, int, SpecSel*, SelectState*, const LoopCtl*,
+template void launch_spec_pick<float>(const unsigned long long*, int, SpecSel*, SelectState*, LoopCtl*, int, int,
                                       hipStream_t);
-template void launch_spec_pick<double>(const unsigned long long*, int, SpecSel*, SelectState*, const LoopCtl*,
+template void launch_spec_pick<double>(const unsigned long long*, int, SpecSel*, SelectState*, LoopCtl*, int, int,
                                        hipStream_t);
 
 // counters: 0 pairs, 1 full-search fallbacks, 2 finite distances, 3 below the quantile window

@@ -146,6 +146,11 @@ struct GridDesc {
 // kernels of the iterations enqueued past convergence return at once; T is
 // the step transform (embedded 4x4, T values) and level the grid level of
 // this iteration's match, both written by the previous iteration's step.
+// A sharded loop that enqueues iterations without reading the window verdict
+// back (pmx_loop_capi.hip) marks a window miss done = kCtlStalled: the rest of
+// the enqueued iterations return at once (every kernel tests done != 0), and
+// the host replays the stalled iteration's radix passes at its batch check.
+constexpr int kCtlStalled = 2;
 struct LoopCtl {
     int done;
     int level;
@@ -196,10 +201,13 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
                        unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end, hipStream_t s);
 // several ranks: the quantile window's pick over the all-gathered segments
-// (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum
+// (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum.
+// stall: a miss sets ctl->done = kCtlStalled (the host did not read the
+// verdict; it replays the iteration).  force_miss: treat the window as
+// missed (test hook, PMX_DEBUG_FORCE_MISS).
 template <typename T>
-void launch_spec_pick(const unsigned long long* segs, int nseg, SpecSel* spec, SelectState* st, const LoopCtl* ctl,
-                      hipStream_t s);
+void launch_spec_pick(const unsigned long long* segs, int nseg, SpecSel* spec, SelectState* st, LoopCtl* ctl,
+                      int stall, int force_miss, hipStream_t s);
 // ---- once-per-compute setup on the device (pmx_setup.hip) ----
 // a uniform grid shape as the host sizes it (cells = g0 * g1 * g2)
 struct SetupShape {

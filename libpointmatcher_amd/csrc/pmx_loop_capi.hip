@@ -116,6 +116,9 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     c->loop_iters = 0;
     c->loop_done = false;
     c->shard_done_seen = false;
+    c->shard_hit_streak = 0;
+    c->shard_replay = false;
+    c->spec_fresh = c->spec_on && sharded(c);  // (the first pick of an empty window misses)
     c->loop_begun = true;
     return PMX_OK;
 }
@@ -139,6 +142,12 @@ int loop_trace_room(pmx_ctx* c, int64_t iters) {
     return PMX_OK;
 }
 
+// Sharded loops read the window verdict back (one stream synchronisation per
+// iteration) while the quantile is still moving: after a miss, until this
+// many hits in a row.  Past that the iterations are enqueued blind (stall and
+// replay, loop_run_impl).
+constexpr int kAsyncAfterHits = 2;
+
 // one ICP iteration, device-driven (transform and level from LoopCtl)
 template <typename T>
 int loop_enqueue_iteration(pmx_ctx* c) {
@@ -147,13 +156,28 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     T Ir[16];  // (placeholder: in loop mode the kernels read the step transform from LoopCtl.T)
     for (int i = 0; i < c->rows * c->rows; ++i) Ir[i] = (i % (c->rows + 1) == 0) ? (T)1 : (T)0;
     // the match's counter phase merged into the quantile's select launch
-    // (point-to-plane: its reduction zeroes the spread counters afterwards)
+    // (point-to-plane: its reduction zeroes the spread counters afterwards).
+    // Sharded: the counter phase packs the window segment the all-gather
+    // sends, so it stays a launch of its own before the collective.
     const int k0 = cfg.n_filters > 0 ? cfg.filter_kind[0] : -1;
     c->merge_counter = c->spec_on && !sharded(c) && cfg.minimizer == 0 && c->grid_mode >= 1 && c->N > 0 &&
                        cfg.knn <= kLaneMaxK && (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
     c->vpart_dirty = false;
-    int rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr);
-    if (rc) return rc;
+    c->shard_async = c->spec_on && sharded(c) && !c->shard_replay && !c->spec_fresh &&
+                     c->shard_hit_streak >= kAsyncAfterHits;
+    int rc;
+    if (c->shard_replay) {
+        // the stalled iteration: its match and window exchange ran (the
+        // outputs are intact: every kernel enqueued after the stall returned
+        // at once); its quantile from the radix passes, then the rest
+        c->spec_exchanged = true;
+        c->chain_n = 0;
+        c->w_valid = false;
+    } else {
+        if (c->shard_async) ++c->n_async;
+        rc = match_impl<T>(c, Ir, cfg.knn, cfg.max_dist, nullptr);
+        if (rc) return rc;
+    }
     if (cfg.n_filters == 0) {
         if ((rc = outlier_impl<T>(c, 0, 0, 0, 0, 0))) return rc;
     }
@@ -165,6 +189,7 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
                         (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, c->stream);
     HIPCHK(c, hipGetLastError());
+    c->shard_replay = false;
     return PMX_OK;
 }
 
@@ -173,18 +198,24 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
     if (!c->loop_begun) return fail(c, PMX_E_STATE, "pmx_loop_begin must be called first");
     if (n < 0) return fail(c, PMX_E_BAD_PARAM, "negative iteration count");
     int rc = PMX_OK;
-    int issued = 0, slot = 0, last_slot = -1;
+    // (iterations issued by this call: c->loop_issued - start; a stall
+    // winds loop_issued back to the stalled iteration)
+    const int64_t start = c->loop_issued;
+    int slot = 0, last_slot = -1;
     int fly[2], nfly = 0, head = 0;
     bool stop = c->loop_done;
     c->loop_on = true;
     while (!stop && rc == PMX_OK) {
-        while (issued < n && nfly < 2 && rc == PMX_OK) {
-            const int b = std::min(kLoopBatch, n - issued);
+        while (c->loop_issued - start < n && nfly < 2 && rc == PMX_OK) {
+            const int b = (int)std::min<int64_t>(kLoopBatch, n - (c->loop_issued - start));
             if (c->loop_cfg.keep_trace && (rc = loop_trace_room<T>(c, c->loop_issued + b))) break;
-            for (int i = 0; i < b && rc == PMX_OK; ++i) rc = loop_enqueue_iteration<T>(c);
+            for (int i = 0; i < b && rc == PMX_OK; ++i) {
+                c->enq_iter = c->loop_issued + i;
+                rc = loop_enqueue_iteration<T>(c);
+            }
+            c->enq_iter = -1;
             if (rc) break;
             c->loop_issued += b;
-            issued += b;
             // the whole status block (state, control word, iteration block):
             // the stop flag of this batch, and the final status if it is the last
             hipError_t e = hipMemcpyAsync((char*)c->h_loop + (size_t)slot * kStatBytes, c->d_result, kStatBytes,
@@ -204,8 +235,34 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
         head = (head + 1) % 2;
         --nfly;
         const hipError_t e = hipEventSynchronize(c->loop_ev[s]);
-        if (e != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
-        if (((const LoopState<T>*)(stat_slot(c, s) + kStatLoop))->done) stop = true;
+        if (e != hipSuccess) {
+            rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e));
+            break;
+        }
+        const LoopState<T>* Sb = (const LoopState<T>*)(stat_slot(c, s) + kStatLoop);
+        if (Sb->done) {
+            stop = true;
+        } else if (((const LoopCtl*)(stat_slot(c, s) + kStatCtl))->done == kCtlStalled) {
+            // A sharded window pick missed in an iteration whose verdict was
+            // not read: every kernel after it returned at once (the
+            // collectives were still issued, identically on every rank).  Let
+            // the later batch drain, then replay from the stalled iteration:
+            // its radix passes and the rest of it (loop_enqueue_iteration),
+            // then the iterations that were skipped.
+            while (rc == PMX_OK && nfly > 0) {
+                const hipError_t e2 = hipEventSynchronize(c->loop_ev[fly[head]]);
+                if (e2 != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop batch: ") + hipGetErrorString(e2));
+                head = (head + 1) % 2;
+                --nfly;
+            }
+            if (rc) break;
+            c->loop_issued = Sb->iter;  // (the stalled iteration: matched, not yet filtered / minimised)
+            c->shard_replay = true;
+            c->shard_hit_streak = 0;
+            ++c->n_stall;
+            hipError_t e3 = hipMemsetAsync(&c->d_ctl->done, 0, sizeof(int), c->stream);
+            if (e3 != hipSuccess) rc = fail(c, PMX_E_HIP, std::string("loop replay: ") + hipGetErrorString(e3));
+        }
     }
     // drain: the last issued batch's copy is the final status
     while (rc == PMX_OK && nfly > 0) {

@@ -88,10 +88,11 @@ def lib():
         l.pmx_icp_timing.argtypes = [C.c_void_p, C.c_int]
         l.pmx_icp_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         l.pmx_icp_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        l.pmx_icp_comm_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 5
         l.pmx_icp_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.POINTER(C.c_int)]
         l.pmx_icp_clear_map.argtypes = [C.c_void_p]
         l.pmx_icp_has_map.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
-        l.pmx_icp_get_map.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)]
+        l.pmx_icp_get_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
         l.pmx_icp_sequence_prepare.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
                                                C.POINTER(C.c_int)]
         l.pmx_icp_sequence_compute.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p]
@@ -268,6 +269,14 @@ class ICP:
         self._chk(self._l.pmx_icp_select_stats(self.h, C.byref(h), C.byref(m)))
         return h.value, m.value
 
+    def comm_stats(self):
+        """Multi-rank diagnostics since creation: {allreduces, allgathers, verdict_syncs,
+        async_iterations, stalls} (pmx_icp_comm_stats)."""
+        v = [C.c_uint64() for _ in range(5)]
+        self._chk(self._l.pmx_icp_comm_stats(self.h, *[C.byref(x) for x in v]))
+        keys = ("allreduces", "allgathers", "verdict_syncs", "async_iterations", "stalls")
+        return dict(zip(keys, (x.value for x in v)))
+
     def timing_read(self):
         ms = C.c_double()
         n = C.c_int64()
@@ -286,7 +295,6 @@ class ICPSequence(ICP):
         nrm = np.ascontiguousarray(normals, dtype=self.dtype) if normals is not None else None
         ok = C.c_int(0)
         self._chk(self._l.pmx_icp_set_map(self.h, _p(m), m.shape[1], m.shape[0], _p(nrm), C.byref(ok)))
-        self.rows = m.shape[1]
         return bool(ok.value)
 
     def clear_map(self):
@@ -300,9 +308,10 @@ class ICPSequence(ICP):
     def get_map(self):
         """The prefiltered map in global coordinates (getPrefilteredMap), (n, rows)."""
         n = C.c_int64(0)
-        self._chk(self._l.pmx_icp_get_map(self.h, None, C.byref(n)))
-        out = np.zeros((n.value, self.rows or 4), self.dtype)
-        self._chk(self._l.pmx_icp_get_map(self.h, _p(out), C.byref(n)))
+        rows = C.c_int(0)
+        self._chk(self._l.pmx_icp_get_map(self.h, None, 0, C.byref(n), C.byref(rows)))
+        out = np.zeros((n.value, rows.value), self.dtype)  # (sized by the library: the held map's rows)
+        self._chk(self._l.pmx_icp_get_map(self.h, _p(out), out.size, C.byref(n), C.byref(rows)))
         return out
 
     def _rd(self, reading, T_init):

@@ -100,3 +100,36 @@ def test_map_accessors_and_reload():
     assert not seq.has_map()
     np.testing.assert_array_equal(seq.compute(rd), np.eye(4, dtype=dtype))
     seq.close()
+
+
+def test_map_kept_when_set_map_fails_and_get_map_sized_by_library():
+    """get_map sizes its buffer from the held map's rows (not from
+    the last reading's), and a set_map whose reference filter throws leaves
+    the previous map indexed (pm_icp.cpp setMap commits after Matcher::init)."""
+    dtype = np.float32
+    ref, nrm = reference_cloud(30_000, dtype)
+    rd = reading_cloud(8_000, dtype)
+    yaml = chain_yaml(filters=FILTERS, maxit=20, differential=DIFF)
+    # DistanceLimit on z: valid for 3-D clouds (D = 3), throws for 2-D ones (DistanceLimit.cpp:68-70)
+    yaml = ("referenceDataPointsFilters:\n  - DistanceLimitDataPointsFilter:\n      dim: 2\n      dist: 100\n"
+            "      removeInside: 1\n" + yaml)
+    seq = ICPSequence(dtype)
+    seq.load_yaml(yaml)
+    assert seq.set_map(ref, nrm)
+    T1 = seq.compute(rd)
+    assert not seq.set_map(np.zeros((0, 3), dtype))  # ignored
+    with pytest.raises(Exception):
+        seq.set_map(np.ascontiguousarray(ref[:, [0, 1, 3]]))  # a 2-D map: the filter throws
+    assert seq.has_map()
+    g = seq.get_map()
+    assert g.shape == ref.shape
+    np.testing.assert_array_equal(seq.compute(rd), T1)  # the previous map, still indexed
+    # a 2-D ICP on the same object (3-row clouds) replaces the device reference
+    # only (the chain without the reference filter, which would throw on 2-D)
+    seq.load_yaml(chain_yaml(filters=FILTERS, maxit=20, differential=DIFF))
+    T1 = seq.compute(rd)  # (the same filtered map: no point has z > 100)
+    r2 = np.ascontiguousarray(ref[::3][:, [0, 1, 3]])
+    seq.compute_with_reference(np.ascontiguousarray(rd[:, [0, 1, 3]]), r2, np.ascontiguousarray(nrm[::3][:, :2]))
+    assert seq.get_map().shape == ref.shape
+    np.testing.assert_array_equal(seq.compute(rd), T1)
+    seq.close()

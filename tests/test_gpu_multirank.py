@@ -88,6 +88,9 @@ def _worker(rank, world, port, outdir, env):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    # MR_LOOP_ONLY: the device loop and the window ICP chains only (the
+    # forced-miss replay run)
+    loop_only = os.environ.get("MR_LOOP_ONLY") == "1"
     try:
         from libpointmatcher_amd import _capi
         from libpointmatcher_amd.icp import ICP
@@ -106,36 +109,43 @@ def _worker(rank, world, port, outdir, env):
             assert ctx.comm_size() == (world, rank, 2)
             ctx.set_reference(ref, nrm)
             ctx.set_reading(shard)
-            ctx.match(I, knn=1)
-            ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
-            A, b, st = ctx.p2plane_system()
-            res[f"{dn}_trim"] = np.concatenate([A.ravel(), b, [st.limit, st.kept, st.n_total]])
-            ctx.match(I, knn=1)
-            ctx.outlier("VarTrimmedDistOutlierFilter", 0, **VT)
-            A, b, st = ctx.p2plane_system()
-            res[f"{dn}_vt"] = np.concatenate([A.ravel(), b, [st.limit, st.kept]])
-            # RobustOutlierFilter: MAD (two sharded selects) and std (all-reduced moments)
-            for tag, fct, mode in (("rmad", "cauchy", _capi.RS_MAD), ("rstd", "welsch", _capi.RS_STD)):
-                ctx.match(I, knn=2)
-                ctx.outlier_robust(0, fct, 0.8, np.inf, mode, 0.0)
+            if not loop_only:
+                ctx.match(I, knn=1)
+                ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
                 A, b, st = ctx.p2plane_system()
-                res[f"{dn}_{tag}"] = np.concatenate([A.ravel(), b, [ctx.robust_scale(0), st.kept, st.sum_w]])
+                res[f"{dn}_trim"] = np.concatenate([A.ravel(), b, [st.limit, st.kept, st.n_total]])
+                ctx.match(I, knn=1)
+                ctx.outlier("VarTrimmedDistOutlierFilter", 0, **VT)
+                A, b, st = ctx.p2plane_system()
+                res[f"{dn}_vt"] = np.concatenate([A.ravel(), b, [st.limit, st.kept]])
+                # RobustOutlierFilter: MAD (two sharded selects) and std (all-reduced moments)
+                for tag, fct, mode in (("rmad", "cauchy", _capi.RS_MAD), ("rstd", "welsch", _capi.RS_STD)):
+                    ctx.match(I, knn=2)
+                    ctx.outlier_robust(0, fct, 0.8, np.inf, mode, 0.0)
+                    A, b, st = ctx.p2plane_system()
+                    res[f"{dn}_{tag}"] = np.concatenate([A.ravel(), b, [ctx.robust_scale(0), st.kept, st.sum_w]])
+                ctx.set_reading(shard)
             # the device loop on the context: quantile window exchanged as segments
-            ctx.set_reading(shard)
             ctx.loop_begin(filters=[("TrimmedDistOutlierFilter", 0.85)], checkers=[("CounterTransformationChecker", 25)])
             ar0, ag0 = ctx.comm_stats()
+            sy0 = ctx.comm_loop_stats()
             cb0 = dict(comm.calls)
             ls = ctx.loop_run(25)
             hits, misses = ctx.loop_select_stats()
             ar1, ag1 = ctx.comm_stats()
+            sy1 = ctx.comm_loop_stats()
             res[f"{dn}_loop"] = np.concatenate([np.asarray(ls.T_iter[:16]), [ls.iterations, ls.last.kept, hits,
                                                                               misses]])
             # the collectives of the loop: native counter, and the transport's own count
             res[f"{dn}_coll"] = np.array([ar1 - ar0, ag1 - ag0, comm.calls["allreduce"] - cb0["allreduce"],
                                           comm.calls["allgather"] - cb0["allgather"], ls.iterations, hits, misses])
+            # how the loop synchronised: verdict reads, blind iterations, stalls replayed
+            res[f"{dn}_sync"] = np.array([b - a for a, b in zip(sy0, sy1)])
             ctx.close()
             # whole ICPs through the host chain (pmx_icp_comm_init_host)
             for tag, knn, filters, minimizer, maxit, diff, with_n in ICP_RUNS:
+                if loop_only and tag not in ("trim", "med"):
+                    continue
                 icp = ICP(dtype)
                 icp.comm_init_host(comm)
                 icp.load_yaml(chain_yaml(knn=knn, filters=filters, minimizer=minimizer, maxit=maxit,
@@ -266,12 +276,21 @@ def test_sharded_hit_iterations_two_collectives(two_ranks, two_ranks_radix, dn):
     passes = 3 if dn == "float32" else 6
     for r in (two_ranks[0], two_ranks[1]):
         ar, ag, cb_ar, cb_ag, iters, hits, misses = (int(v) for v in r[f"{dn}_coll"])
-        print(f"{dn}: {iters} iterations, {hits} hits / {misses} misses: {ar} all-reduces, {ag} all-gathers")
+        syncs, blind, stalls = (int(v) for v in r[f"{dn}_sync"])
+        print(f"{dn}: {iters} iterations, {hits} hits / {misses} misses: {ar} all-reduces, {ag} all-gathers; "
+              f"{syncs} verdict syncs, {blind} blind iterations, {stalls} stalls")
         assert (ar, ag) == (cb_ar, cb_ag)  # every collective the library counts reached the transport
         assert hits > 0 and hits + misses <= ag
-        # per enqueued iteration: one all-gather + the system's all-reduce, and the passes on a miss
-        assert ar == ag + passes * misses
-        assert ag <= iters + 1
+        # per enqueued iteration: one all-gather + the system's all-reduce, the
+        # passes on a miss, and a stalled iteration's replayed system
+        assert ar == ag + passes * misses + stalls
+        assert ag <= iters + 1 + 2 * 4 * stalls  # (a stall wastes at most the two batches in flight)
+        # the verdict is read back only while the window settles: after the
+        # first (known) miss and every later miss, until two hits in a row
+        assert syncs <= 3 * misses + 2
+        assert blind >= hits - 2 * (misses + 1)
+        assert blind > 0
+        assert syncs + blind <= ag
     # the radix path: every iteration runs the passes
     ar, ag, _, _, iters, hits, _ = (int(v) for v in two_ranks_radix[0][f"{dn}_coll"])
     assert hits == 0 and ag == 0 and ar % (1 + passes) == 0 and ar // (1 + passes) >= iters
@@ -313,3 +332,30 @@ def test_rccl_one_rank_is_bit_identical(oracle, dn, monkeypatch):
         assert o[2] == out[0][2] and o[4] == out[0][4]
         np.testing.assert_array_equal(o[3], out[0][3])
         assert o[5] > 0
+
+
+@pytest.fixture(scope="module")
+def two_ranks_forced_miss(tmp_path_factory):
+    # misses forced at loop iterations 10 and 17 (past the settling
+    # iterations: enqueued blind, so they stall the device loop and replay)
+    return _run_two_ranks(tmp_path_factory.mktemp("mr_gpu_miss"), {"PMX_DEBUG_FORCE_MISS": "10,17",
+                                                                   "MR_LOOP_ONLY": "1"})
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dn", ["float32", "float64"])
+def test_sharded_stall_replay_bit_identical(two_ranks, two_ranks_forced_miss, dn):
+    """A window miss in an iteration enqueued without reading its verdict
+    stalls the device loop; the host replays it at the batch check (its radix
+    passes with their histogram all-reduces, then the rest).  Forced misses
+    mid-batch must leave every result bit-identical to the run without them
+    (which itself equals the oracle, test_sharded_icp_vs_oracle)."""
+    f, r = two_ranks_forced_miss, two_ranks
+    np.testing.assert_array_equal(f[0][f"{dn}_loop"], f[1][f"{dn}_loop"])
+    np.testing.assert_array_equal(f[0][f"{dn}_loop"][:18], r[0][f"{dn}_loop"][:18])  # T_iter, iterations, kept
+    syncs, blind, stalls = (int(v) for v in f[0][f"{dn}_sync"])
+    print(f"{dn}: forced misses -> {stalls} stalls, {syncs} verdict syncs, {blind} blind iterations")
+    assert stalls >= 1
+    for tag in ("trim", "med"):
+        np.testing.assert_array_equal(f[0][f"{dn}_icp_{tag}"], r[0][f"{dn}_icp_{tag}"])
+        np.testing.assert_array_equal(f[1][f"{dn}_icp_{tag}"], r[1][f"{dn}_icp_{tag}"])
