@@ -352,6 +352,7 @@ def main():
     if args.warmup > 0:
         icp.iterate(args.warmup)
 
+    cs0 = icp.comm_stats() if dist else None
     barrier()
     t0 = time.perf_counter()
     icp.iterate(args.steps)   # each batch ends with the status copy-back: device is synchronised
@@ -359,6 +360,9 @@ def main():
     barrier()
     elapsed = max_over_ranks(t1 - t0)
     st = icp.stats()
+    # collectives and host synchronisations of the timed iterations (sharded
+    # runs: stall-and-replay)
+    comm = ({k: v - cs0[k] for k, v in icp.comm_stats().items()} if dist else None)
     # Roofline pass: the same ICP again (prepare resets the pose and the
     # match history), now with HIP events around every match launch on the
     # context stream.  The events are kept out of the timed region above: each
@@ -433,6 +437,7 @@ def main():
                    "matcher": f"KDTreeMatcher searchType={search_type} ({args.matcher}, exact)",
                    "reading_global": N_global, "reading_per_gpu": N, "reference": M, "parallelism": par},
         "icp_iterations_per_s": args.steps / elapsed,
+        "comm_timed": comm,
         "kept_pairs_last_iter": st.kept,
         "whole_icp": whole,
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

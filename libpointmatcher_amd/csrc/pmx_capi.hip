@@ -233,6 +233,8 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (hipMalloc(&c->d_selx, selx_bytes()) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_selx, 0, selx_bytes());
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
+    if (hipMalloc((void**)&c->d_ticket, 256) != hipSuccess) return bad(PMX_E_HIP);
+    (void)hipMemset(c->d_ticket, 0, 256);
     if (hipHostMalloc((void**)&c->h_result, kBlkBytes, hipHostMallocDefault) != hipSuccess) return bad(PMX_E_HIP);
     *out = c;
     return PMX_OK;
@@ -247,7 +249,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
-                    c->d_rob, c->d_rdev, c->d_radii};
+                    c->d_rob, c->d_rdev, c->d_radii, c->d_ticket};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();

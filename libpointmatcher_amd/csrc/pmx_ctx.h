@@ -11,6 +11,7 @@
 #pragma once
 
 #include "pmx_internal.h"
+#include "pmx_p2plane.h"
 #include "pmx_spec.h"
 
 #include <rccl/rccl.h>
@@ -186,6 +187,7 @@ struct pmx_ctx {
 
     // reductions
     double* d_partials = nullptr;
+    unsigned* d_ticket = nullptr;  // the reductions' in-launch finalize ticket (RedTail; zero between launches)
     double* d_result = nullptr;  // [0..63] system, [64..127] second pass
     void* d_means = nullptr;
     double* h_result = nullptr;  // pinned

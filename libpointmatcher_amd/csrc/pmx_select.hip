@@ -433,6 +433,7 @@ struct CumBits;
 template <>
 struct CumBits<float> {
     static constexpr int P = 24;  // significand bits
+    static __device__ __forceinline__ float min_normal() { return 1.17549435e-38f; }
     static __device__ __forceinline__ int binade(float s) { return (int)((__float_as_uint(s) >> 23) & 0xffu) - 127; }
     // s / ulp(2^binade): the significand with its hidden bit (s normal)
     static __device__ __forceinline__ long long units(float s) {
@@ -442,6 +443,7 @@ struct CumBits<float> {
 template <>
 struct CumBits<double> {
     static constexpr int P = 53;
+    static __device__ __forceinline__ double min_normal() { return 2.2250738585072014e-308; }
     static __device__ __forceinline__ int binade(double s) {
         return (int)(((unsigned long long)__double_as_longlong(s) >> 52) & 0x7ffull) - 1023;
     }
@@ -766,7 +768,9 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
             // a fast chunk: the guessed binade is the running sum's, few ties,
             // and the chunk's last sum stays below the next binade
             VtChunk& q = ch[b + 1];
-            int fast = q.nt <= kFastTies && CumBits<T>::binade(s) == q.e && q.P < LIM;
+            // (s normal: units() adds the hidden bit)
+            int fast = q.nt <= kFastTies && s >= CumBits<T>::min_normal() && CumBits<T>::binade(s) == q.e &&
+                       q.P < LIM;
             if (fast) {
                 const long long S0 = CumBits<T>::units(s);
                 int up = 0;
@@ -803,6 +807,24 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
             // are inactive (contribute 0, written earlier)
             const int64_t jb = p & ~(int64_t)(kCumPer - 1);
             const int64_t q1 = jb + (int64_t)kCumChunk < cend ? jb + (int64_t)kCumChunk : cend;
+            if (!(s >= CumBits<T>::min_normal())) {
+                // a subnormal running sum (every key so far below the
+                // smallest normal): units() would add a hidden bit s does not
+                // have — this pass sequentially, exactly as partial_sum
+                if (t == 0) {
+                    T acc = s;
+                    for (int64_t j = p; j < q1; ++j) {
+                        acc = acc + KO::val(keys[j]);
+                        cum[j] = acc;
+                    }
+                    s_run = acc;
+                }
+                __syncthreads();
+                s = s_run;
+                p = q1;
+                __syncthreads();
+                continue;
+            }
             const int64_t j0 = jb + (int64_t)t * kCumPer;
             typename KO::K kv[kCumPer];
             vt_load<T>(keys, c, j0, kv);

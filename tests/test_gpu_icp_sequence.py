@@ -112,7 +112,7 @@ def test_map_kept_when_set_map_fails_and_get_map_sized_by_library():
     yaml = chain_yaml(filters=FILTERS, maxit=20, differential=DIFF)
     # DistanceLimit on z: valid for 3-D clouds (D = 3), throws for 2-D ones (DistanceLimit.cpp:68-70)
     yaml = ("referenceDataPointsFilters:\n  - DistanceLimitDataPointsFilter:\n      dim: 2\n      dist: 100\n"
-            "      removeInside: 1\n" + yaml)
+            "      removeInside: 0\n" + yaml)
     seq = ICPSequence(dtype)
     seq.load_yaml(yaml)
     assert seq.set_map(ref, nrm)
@@ -127,7 +127,7 @@ def test_map_kept_when_set_map_fails_and_get_map_sized_by_library():
     # a 2-D ICP on the same object (3-row clouds) replaces the device reference
     # only (the chain without the reference filter, which would throw on 2-D)
     seq.load_yaml(chain_yaml(filters=FILTERS, maxit=20, differential=DIFF))
-    T1 = seq.compute(rd)  # (the same filtered map: no point has z > 100)
+    T1 = seq.compute(rd)  # (the same filtered map: every point has z < 100)
     r2 = np.ascontiguousarray(ref[::3][:, [0, 1, 3]])
     seq.compute_with_reference(np.ascontiguousarray(rd[:, [0, 1, 3]]), r2, np.ascontiguousarray(nrm[::3][:, :2]))
     assert seq.get_map().shape == ref.shape

@@ -237,8 +237,25 @@ def _grid_clouds(n_side, dtype, rng):
     return ref, rd
 
 
+def _subnormal_clouds(n_side, dtype, rng):
+    """Twin points: the reading is the reference moved by a tiny offset, a
+    third of them so tiny that their squared distances are subnormal in T —
+    VarTrimmed's running sum stays subnormal well past the sequential head
+    (the partial sum's subnormal guard), then turns normal."""
+    if dtype == np.float32:
+        scale, tiny, big = 1e-18, 1e-22, 1e-19
+    else:
+        scale, tiny, big = 1e-147, 1e-158, 1e-151
+    g = np.stack(np.meshgrid(*[np.arange(n_side)] * 3, indexing="ij"), -1).reshape(-1, 3).astype(np.float64) * scale
+    mag = np.where(rng.random(len(g)) < 1 / 3, tiny, big)[:, None]
+    off = rng.uniform(0.5, 1.0, size=g.shape) * mag
+    ref = np.hstack([g, np.ones((len(g), 1))]).astype(dtype)
+    rd = np.hstack([g + off, np.ones((len(g), 1))]).astype(dtype)
+    return ref, rd
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("data", ["surface", "surface1m", "dyadic"])
+@pytest.mark.parametrize("data", ["surface", "surface1m", "dyadic", "subnormal"])
 def test_vartrimmed_parallel_partial_sum(oracle, dtype, data):
     """VarTrimmed's std::partial_sum in T runs as a binade-segmented integer
     scan over chunks (pmx_select.hip vt_chunk_prep / vt_cumsum /
@@ -252,10 +269,14 @@ def test_vartrimmed_parallel_partial_sum(oracle, dtype, data):
         size = 1000000 if data == "surface1m" else 300000
         ref, nrm = reference_cloud(size, dtype)
         rd = reading_cloud(size, dtype)
+    elif data == "subnormal":
+        ref, rd = _subnormal_clouds(58, dtype, rng)
     else:
         ref, rd = _grid_clouds(48, dtype, rng)
     filters = [("VarTrimmedDistOutlierFilter", {"minRatio": 0.05, "maxRatio": 0.99, "lambda": 2.35})]
     ctx = P.Context(0, dtype)
+    if data == "subnormal":
+        ctx.set_search(0)  # (brute force: the grid is not built for 1e-147-sized clouds)
     ctx.set_reference(ref)
     ctx.set_reading(rd)
     ctx.match(np.eye(4, dtype=dtype), knn=1)
