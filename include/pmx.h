@@ -158,7 +158,9 @@ int pmx_set_reading_radii(pmx_ctx* ctx, const void* radii);
  * lowest-index tie rule).  Takes effect at the next pmx_match. */
 int pmx_set_search(pmx_ctx* ctx, int search_type);
 
-/* T_iter: rows x rows row-major T.  knn >= 1 (<= 16 on this path),
+/* T_iter: rows x rows row-major T.  knn >= 1 (KDTreeMatcher's bound,
+ * MatchersImpl.h:83; k > 16 on the wave-per-query search, lists past 1024
+ * entries in chunks of 1024; N * knn entries must fit in device memory),
  * maxDist: radius (inclusive, squared in T; +inf = none), epsilon: the
  * search is exact, so any epsilon >= 0 is satisfied.  visited (may be NULL)
  * receives the pair evaluations of this call when they are known at launch
@@ -285,7 +287,7 @@ int pmx_loop_select_stats(pmx_ctx* ctx, uint64_t* window_hits, uint64_t* window_
  * Standalone (a temporary context on `device`); pmx_last_error(NULL) has the
  * message of a failed call.
  *   feat: rows x n point-major T (dtype PMX_F32 / PMX_F64), rows = D + 1
- *   knn in [1, 16], maxDist: neighbour radius (+inf = none)
+ *   knn >= 1 (SurfaceNormal.h:68), maxDist: neighbour radius (+inf = none)
  *   outputs (point-major T, each may be NULL): normals D x n, densities n,
  *   eig_values D x n (ascending), eig_vectors D*D x n (serializeEigVec,
  *   row-major; column j = eigenvector of eig_values[j], largest component

@@ -404,7 +404,7 @@ template <typename T>
 int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
     if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
     if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
-    if (knn < 1 || knn > kMaxKnn) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 256] on the GPU path");
+    if (knn < 1) return fail(c, PMX_E_BAD_PARAM, "knn must be >= 1");
     if (!(maxDist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
     const int64_t n = c->N * knn;
     size_t cap = (size_t)c->match_cap * tsize(c);

@@ -17,8 +17,8 @@ int surface_normals_impl(int device, const T* feat, int rows, int64_t n, int knn
         g_err = "SurfaceNormalDataPointsFilter: clouds must be 2-D or 3-D (3 or 4 homogeneous rows)";
         return PMX_E_BAD_PARAM;
     }
-    if (knn < 1 || knn > 16) {
-        g_err = "SurfaceNormalDataPointsFilter: knn must be in [1, 16] on the GPU path";
+    if (knn < 1) {  // (SurfaceNormal.h:68: min 1; k > 16 on the wave-per-query search)
+        g_err = "SurfaceNormalDataPointsFilter: knn must be >= 1";
         return PMX_E_BAD_PARAM;
     }
     if (degenerate) *degenerate = 0;

@@ -176,8 +176,7 @@ __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
 // k-NN for k > kLaneMaxK (pmx_knn_wide.hip): one wave per query, the k-list
 // spread over the wave.  start == null: brute force over pts[0, M) (ids are
 // indices); otherwise a grid level (ids are positions), G its geometry.
-constexpr int kLaneMaxK = 16;   // the per-lane searches' largest k-list
-constexpr int kMaxKnn = 256;    // the wide search's
+constexpr int kLaneMaxK = 16;   // the per-lane searches' largest k-list (wider: the wave-per-query search)
 template <typename T>
 void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* start, const GridGeom* G, int64_t M,
                      const P4<T>* rd, int64_t N, const Mat4<T>& Tm, int k, T maxR2, const T* radii, T* out_d,

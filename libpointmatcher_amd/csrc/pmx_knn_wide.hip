@@ -1,4 +1,5 @@
-// pmx_knn_wide.hip — exact k-NN for k > 16 (KDTreeMatcher knn up to 256).
+// pmx_knn_wide.hip — exact k-NN for k > 16 (KDTreeMatcher knn: any k >= 1,
+// MatchersImpl.h:83; lists past 1024 entries in chunks of 1024).
 //
 // Same contract as pmx_grid.hip / pmx_match.hip (MatchersImpl.cpp:85-101
 // with libnabo's exact search): distances are ((dx*dx + dy*dy) + dz*dz) in T
@@ -30,6 +31,7 @@ namespace pmx {
 namespace {
 
 constexpr int32_t kNone = 0x7fffffff;  // empty entry (sorts after every real index)
+constexpr int kWideChunk = 1024;       // the largest k-list one wave holds (16 entries per lane)
 
 template <typename T>
 __device__ __forceinline__ T wsqd(T qx, T qy, T qz, const P4<T>& r) {
@@ -121,11 +123,13 @@ __device__ __forceinline__ void wl_insert(WideList<T, E>& L, T d, int32_t o, int
 }
 
 // Evaluate the points of the lanes' ranges [a0, b0) + [a1, b1) against the
-// list; wd / wo: the current entry k - 1 (updated)
+// list; wd / wo: the current entry k - 1 (updated).  ld / lo: the chunk's
+// lower bound — only points sorting after (ld, lo) compete (chunked k-lists)
 template <typename T, int E>
 __device__ __forceinline__ void wl_scan(const P4<T>* __restrict__ pts, const int32_t* __restrict__ gidx, uint32_t a0,
                                         uint32_t b0, uint32_t a1, uint32_t b1, T qx, T qy, T qz, int k,
-                                        WideList<T, E>& L, T& wd, int32_t& wo, uint32_t& visits) {
+                                        WideList<T, E>& L, T& wd, int32_t& wo, uint32_t& visits, T ld,
+                                        int32_t lo) {
     const int lane = threadIdx.x & 63;
     const uint32_t l0 = b0 - a0, len = l0 + (b1 - a1);
     uint32_t inc = len;
@@ -155,11 +159,11 @@ __device__ __forceinline__ void wl_scan(const P4<T>* __restrict__ pts, const int
             d = wsqd(qx, qy, qz, gld32(pts, pos));
             ++visits;
         }
-        bool pass = act && d <= wd;
+        bool pass = act && d <= wd && d >= ld;
         int32_t o = kNone;
         if (pass) {
             o = gidx ? gld32(gidx, pos) : (int32_t)pos;
-            pass = before(d, o, wd, wo);
+            pass = before(d, o, wd, wo) && before(ld, lo, d, o);
         }
         unsigned long long m = __ballot(pass);
         while (m) {  // (uniform) in lane order; each re-checked against the moved k-th entry
@@ -189,12 +193,17 @@ __device__ __forceinline__ int wcell_x(const GridGeom& G, double v) {
 // One wave per query (4 per block).  gidx / start null: brute force over
 // pts[0, M) (ids are indices).  Loop mode (ctl): transform and level from the
 // device, as the per-lane kernel.
+// Chunked k-lists (k > 64 E: KDTreeMatcher's knn is bounded only by int,
+// MatchersImpl.h:83): this launch finds entries [c0, c0 + k) of the query's
+// list of kstride entries — the k smallest (distance, index) pairs after
+// entry c0 - 1, which the previous launch wrote — with the same search and
+// certificate; the launches run in stream order.
 template <typename T, int E>
 __global__ __launch_bounds__(256) void knn_wide_kernel(const P4<T>* __restrict__ pts, const int32_t* __restrict__ gidx,
                                                        const uint32_t* __restrict__ start, GridGeom G, int64_t M,
                                                        const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
-                                                       T maxR2, const T* __restrict__ radii, T* __restrict__ out_d,
-                                                       int32_t* __restrict__ out_i,
+                                                       int c0, int kstride, T maxR2, const T* __restrict__ radii,
+                                                       T* __restrict__ out_d, int32_t* __restrict__ out_i,
                                                        unsigned long long* __restrict__ visited,
                                                        const LoopCtl* __restrict__ ctl,
                                                        const GridDesc<T>* __restrict__ gd, SpecSel* __restrict__ spec) {
@@ -211,6 +220,16 @@ __global__ __launch_bounds__(256) void knn_wide_kernel(const P4<T>* __restrict__
     const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (j >= N) return;  // (whole wave)
     const T r2 = radii ? radii[j] * radii[j] : maxR2;
+    // the chunk's lower bound: the previous chunk's last entry
+    T ld = -(T)__builtin_huge_val();
+    int32_t lo = -1;
+    bool none = false;  // (the previous chunk already ran out of points: padding only)
+    if (c0 > 0) {
+        const int32_t pp = out_i[j * kstride + c0 - 1];
+        ld = out_d[j * kstride + c0 - 1];
+        none = pp < 0;
+        lo = none ? -1 : (gidx ? gld32(gidx, (uint32_t)pp) : (int32_t)pp);
+    }
     T qx, qy, qz;
     {
         const P4<T> p = gld(rd, j);
@@ -224,11 +243,12 @@ __global__ __launch_bounds__(256) void knn_wide_kernel(const P4<T>* __restrict__
     int32_t wo = kNone;
     uint32_t visits = 0;
     const double q[3] = {(double)qx, (double)qy, (double)qz};
-    bool qnan = !(q[0] == q[0]) || !(q[1] == q[1]) || !(q[2] == q[2]);
+    bool qnan = !(q[0] == q[0]) || !(q[1] == q[1]) || !(q[2] == q[2]) || none;
     if (!start) {
         // brute force: lane 0 holds the one range
         if (!qnan)
-            wl_scan<T, E>(pts, nullptr, 0u, lane == 0 ? (uint32_t)M : 0u, 0u, 0u, qx, qy, qz, k, L, wd, wo, visits);
+            wl_scan<T, E>(pts, nullptr, 0u, lane == 0 ? (uint32_t)M : 0u, 0u, 0u, qx, qy, qz, k, L, wd, wo, visits,
+                          ld, lo);
     } else if (!qnan) {
         const double margin = 1.0 - 1e-5;
         int c[3];
@@ -291,7 +311,7 @@ __global__ __launch_bounds__(256) void knn_wide_kernel(const P4<T>* __restrict__
                         }
                     }
                 }
-                wl_scan<T, E>(pts, gidx, a0, b0, a1, b1, qx, qy, qz, k, L, wd, wo, visits);
+                wl_scan<T, E>(pts, gidx, a0, b0, a1, b1, qx, qy, qz, k, L, wd, wo, visits, ld, lo);
             }
             // the lower bound on every unvisited cell (uniform)
             double lb = 1e300;
@@ -327,8 +347,8 @@ __global__ __launch_bounds__(256) void knn_wide_kernel(const P4<T>* __restrict__
                 d = (T)__builtin_huge_val();
                 id = -1;
             }
-            out_d[j * k + s] = d;
-            out_i[j * k + s] = id;
+            out_d[j * kstride + c0 + s] = d;
+            out_i[j * kstride + c0 + s] = id;
             if (sa.on) spec_acc<T>(sa, d);
         }
     }
@@ -356,15 +376,19 @@ void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* star
     GridGeom g{};
     if (G) g = *G;
     const dim3 grid((unsigned)((N + 3) / 4));
-#define PMX_WIDE(E)                                                                                                   \
-    hipLaunchKernelGGL((knn_wide_kernel<T, E>), grid, dim3(256), 0, s, pts, gidx, start, g, M, rd, N, Tm, k, maxR2,   \
-                       radii, out_d, out_i, visited, ctl, gd, spec)
+#define PMX_WIDE(E, KC, C0)                                                                                          \
+    hipLaunchKernelGGL((knn_wide_kernel<T, E>), grid, dim3(256), 0, s, pts, gidx, start, g, M, rd, N, Tm, KC, C0, k, \
+                       maxR2, radii, out_d, out_i, visited, ctl, gd, spec)
     if (k <= 64)
-        PMX_WIDE(1);
+        PMX_WIDE(1, k, 0);
     else if (k <= 128)
-        PMX_WIDE(2);
+        PMX_WIDE(2, k, 0);
+    else if (k <= 256)
+        PMX_WIDE(4, k, 0);
+    else if (k <= 512)
+        PMX_WIDE(8, k, 0);
     else
-        PMX_WIDE(4);
+        for (int c0 = 0; c0 < k; c0 += kWideChunk) PMX_WIDE(16, std::min(kWideChunk, k - c0), c0);
 #undef PMX_WIDE
 }
 

@@ -23,7 +23,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     if (!c->d_rd && c->N > 0) return fail(c, PMX_E_STATE, "no reading");
     if (c->search_type == 0 || !c->grid_ready || c->grid_mode == 0)
         return fail(c, PMX_E_BAD_PARAM, "device loop: needs the per-lane grid matcher (searchType 1 or 2)");
-    if (cfg->knn < 1 || cfg->knn > kMaxKnn) return fail(c, PMX_E_BAD_PARAM, "knn must be in [1, 256] on the GPU path");
+    if (cfg->knn < 1) return fail(c, PMX_E_BAD_PARAM, "knn must be >= 1");
     if (!(cfg->max_dist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
     if (cfg->n_filters < 0 || cfg->n_filters > kMaxChain)
         return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 outlier filters");

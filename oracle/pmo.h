@@ -68,7 +68,7 @@ typedef struct pmo_robust {
 
 enum { PMO_MIN_P2PLANE = 0, PMO_MIN_P2POINT = 1 };
 enum { PMO_KNN_BRUTE = 0, PMO_KNN_KDTREE = 1 };
-#define PMO_KNN_MAX 256  /* largest k of pmo_knn / the ICP's matcher (the GPU path's bound) */
+#define PMO_KNN_MAX (1 << 20)  /* largest k of pmo_knn / the ICP's matcher (k-lists past 256 on the heap) */
 /* accumulation mode of the minimizer sums:
  *   0 = T-precision products accumulated in double (the build's semantics)
  *   1 = T-precision products accumulated sequentially in T (reference-like,

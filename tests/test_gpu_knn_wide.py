@@ -1,4 +1,4 @@
-"""k-NN for k > 16 (KDTreeMatcher knn up to 256; pmx_knn_wide.hip): the
+"""k-NN for k > 16 (KDTreeMatcher knn: any k >= 1; pmx_knn_wide.hip): the
 wave-per-query search over the grid and over the whole reference (brute
 force) against the oracle's kd-tree, bit for bit (distances and ids, ties by
 original index), on the geometries of test_gpu_grid.py: surface density,
@@ -35,7 +35,7 @@ def check(oracle, ref, rd, T, k, max_dist=np.inf, dtype=np.float32):
         np.testing.assert_array_equal(g[0], o[0], err_msg=f"dists, search {search}, k {k}")
 
 
-@pytest.mark.parametrize("k", [17, 32, 64, 100, 256])
+@pytest.mark.parametrize("k", [17, 32, 64, 100, 256, 512, 1024, 1500])
 def test_surface_density(oracle, k):
     ref, _ = reference_cloud(40_000)
     rd = reading_cloud(3_000)
@@ -69,6 +69,15 @@ def test_fewer_points_than_k(oracle):
         ref = random_cloud(M, seed=9)
         rd = random_cloud(300, seed=10, scale=3.0)
         check(oracle, ref, rd, np.eye(4, dtype=np.float32), 64)
+    # chunked lists (k > 1024): the reference runs out inside the first and the second chunk
+    for M in (700, 1800):
+        ref = random_cloud(M, seed=11)
+        rd = random_cloud(200, seed=12, scale=2.0)
+        check(oracle, ref, rd, np.eye(4, dtype=np.float32), 2100)
+    # ... and with a radius that ends the list early
+    ref = random_cloud(5_000, seed=13, dtype=np.float64)
+    rd = random_cloud(300, seed=14, dtype=np.float64)
+    check(oracle, ref, rd, np.eye(4), 1300, max_dist=0.3, dtype=np.float64)
 
 
 def test_transformed_reading(oracle):
@@ -86,30 +95,32 @@ def test_knn_bounds():
     ctx.set_reference(random_cloud(100, seed=1))
     ctx.set_reading(random_cloud(10, seed=2))
     with pytest.raises(P.InvalidParameter):
-        ctx.match(np.eye(4, dtype=np.float32), knn=257)
+        ctx.match(np.eye(4, dtype=np.float32), knn=0)
     ctx.close()
 
 
-@pytest.mark.parametrize("dn", ["float32", "float64"])
-def test_icp_knn32_vs_oracle(oracle, dn):
-    """Whole ICP with knn = 32 (TrimmedDist over the N x 32 distances,
+@pytest.mark.parametrize("dn,knn", [("float32", 32), ("float64", 32), ("float32", 512)])
+def test_icp_knn32_vs_oracle(oracle, dn, knn):
+    """Whole ICP with knn = 32 and 512 (TrimmedDist over the N x k distances,
     point-to-plane over every kept pair): the host chain (device loop) against
-    the oracle ICP, equal iterations, T within 1e-5 (f32) / 1e-12 (f64)."""
+    the oracle ICP, equal iterations, T within 1e-5 (f32) / 1e-12 (f64).
+    (knn = 512 on smaller clouds: the oracle's kd-tree inserts into a
+    512-entry list.)"""
     from helpers import chain_yaml
     from libpointmatcher_amd.icp import ICP
 
     dtype = np.dtype(dn)
-    ref, nrm = reference_cloud(30_000, dtype)
-    rd = reading_cloud(6_000, dtype)
+    ref, nrm = reference_cloud(30_000 if knn <= 64 else 12_000, dtype)
+    rd = reading_cloud(6_000 if knn <= 64 else 1_200, dtype)
     diff = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
     icp = ICP(dtype)
-    icp.load_yaml(chain_yaml(knn=32, filters=(("TrimmedDistOutlierFilter", {"ratio": 0.8}),), maxit=20,
+    icp.load_yaml(chain_yaml(knn=knn, filters=(("TrimmedDistOutlierFilter", {"ratio": 0.8}),), maxit=20,
                              differential=diff))
     T = icp.compute(rd, ref, nrm)
     s = icp.stats()
     icp.close()
-    cfg = oracle.make_cfg(knn=32, filters=(("TrimmedDistOutlierFilter", {"ratio": 0.8}),), counter_max=20,
-                          differential=diff)
+    cfg = oracle.make_cfg(knn=knn, filters=(("TrimmedDistOutlierFilter", {"ratio": 0.8}),), counter_max=20,
+                          differential=diff, threads=8)
     rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm)
     assert rc == 0
     frob = np.linalg.norm(T.astype(np.float64) - To.astype(np.float64))

@@ -36,7 +36,7 @@ def compare(g, o, dtype):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("k", [3, 5, 10, 16])
+@pytest.mark.parametrize("k", [3, 5, 10, 16, 32])
 def test_surface_normals_equal_oracle(oracle, dtype, k):
     ref, nrm = reference_cloud(30000, dtype)
     g = _capi.surface_normals(ref, knn=k)
@@ -67,10 +67,14 @@ def test_surface_normals_radius_2d_degenerate_smooth(oracle):
     np.testing.assert_allclose(g["normals"], o["normals"], rtol=0, atol=1e-4)
 
 
-def test_surface_normals_bad_knn():
-    ref, _ = reference_cloud(1000, np.float32)
+def test_surface_normals_wide_knn_and_bounds(oracle):
+    """knn past the per-lane lists (the wave-per-query self-match): 64 and
+    100 neighbours (SurfaceNormal.h:68 bounds knn only from below)."""
+    ref, _ = reference_cloud(8000, np.float64)
+    for k in (64, 100):
+        compare(_capi.surface_normals(ref, knn=k), oracle.surface_normals(ref, k=k), np.float64)
     with pytest.raises(_capi.InvalidParameter):
-        _capi.surface_normals(ref, knn=17)
+        _capi.surface_normals(ref, knn=0)
 
 
 CHAIN = """

@@ -17,7 +17,7 @@ DIFF = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
 
 # --------------------------------------------------------------------- kNN --
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("k", [1, 3, 64, 256])
+@pytest.mark.parametrize("k", [1, 3, 64, 256, 700])
 def test_knn_kdtree_equals_brute_and_scipy(oracle, dtype, k):
     from scipy.spatial import cKDTree
 
@@ -36,8 +36,14 @@ def test_knn_kdtree_equals_brute_and_scipy(oracle, dtype, k):
 
 
 def test_knn_k_bound(oracle):
+    """k-lists past 256 entries live on the heap (any k up to PMO_KNN_MAX);
+    k larger than the reference pads with (+inf, -1); k < 1 is refused."""
     ref = hom(np.random.default_rng(2).uniform(-1, 1, (300, 3)), np.float32)
-    assert oracle.knn(ref, ref[:10], k=257)[2] == -1  # (PMO_KNN_MAX: refused, never past the list)
+    d, i, t = oracle.knn(ref, ref[:10], k=400)
+    assert t > 0 and np.all(i[:, 300:] == -1) and np.all(np.isinf(d[:, 300:]))
+    assert np.array_equal(np.sort(i[:, :300], axis=1), np.tile(np.arange(300), (10, 1)))
+    assert np.all(np.diff(d[:, :300], axis=1) >= 0)
+    assert oracle.knn(ref, ref[:10], k=0)[2] == -1
 
 
 def test_knn_ties_and_radius(oracle):
