@@ -232,13 +232,16 @@ int pmx_sync(pmx_ctx* ctx);
  * enqueued back to back and the host synchronises once per pmx_loop_run.
  * Requirements: a grid matcher (pmx_set_search 1/2, per-lane kernel), filters
  * among default / Null / MaxDist / MinDist / MedianDist / TrimmedDist /
- * VarTrimmedDist,
- * PointToPlane (no force2D / force4DOF) or PointToPoint, checkers among
- * Counter / Differential (smoothLength < 64) / Bound.  Otherwise pmx_loop_begin
- * returns PMX_E_BAD_PARAM and the caller keeps the per-module calls. */
+ * VarTrimmedDist / Robust (at most one; with PointToPoint only its
+ * point2point distance), PointToPlane (no force2D / force4DOF) or
+ * PointToPoint, checkers among Counter / Differential (smoothLength < 64) /
+ * Bound.  Otherwise pmx_loop_begin returns PMX_E_BAD_PARAM and the caller
+ * keeps the per-module calls. */
 enum { PMX_CHECK_COUNTER = 0, PMX_CHECK_DIFFERENTIAL = 1, PMX_CHECK_BOUND = 2 };
 enum { PMX_FILTER_DEFAULT = 0, PMX_FILTER_NULL = 1, PMX_FILTER_MAXDIST = 2, PMX_FILTER_MINDIST = 3,
-       PMX_FILTER_MEDIANDIST = 4, PMX_FILTER_TRIMMED = 5, PMX_FILTER_VARTRIMMED = 6 };
+       PMX_FILTER_MEDIANDIST = 4, PMX_FILTER_TRIMMED = 5, PMX_FILTER_VARTRIMMED = 6, PMX_FILTER_ROBUST = 7 };
+/* RobustOutlierFilter's scale estimator in a loop configuration */
+enum { PMX_RSE_NONE = 0, PMX_RSE_MAD = 1, PMX_RSE_STD = 2, PMX_RSE_BERG = 3 };
 typedef struct pmx_loop_cfg {
     int knn;
     double max_dist;
@@ -250,6 +253,19 @@ typedef struct pmx_loop_cfg {
     int checker_kind[8];        /* PMX_CHECK_* */
     double checker_p[8][3];     /* Counter: max; Differential: rot, trans, smoothLength; Bound: rot, trans */
     int keep_trace;             /* record T_iter of every iteration (pmx_loop_trace) */
+    /* PMX_FILTER_ROBUST (OutlierFiltersImpl.cpp:380-598): the filter's
+     * parameters and its call counter at the loop's start.  The scale of
+     * iteration i is recomputed while robust_first_call + i <=
+     * robust_nb_iter_for_scale (or always when that is 0), berg's first
+     * computation at call 1 — robustFiltering's schedule (:500-531). */
+    int robust_fct;             /* PMX_RF_* */
+    int robust_estimator;       /* PMX_RSE_* */
+    int robust_p2pl;            /* distanceType point2plane */
+    int robust_nb_iter_for_scale;
+    int robust_first_call;      /* the filter's iteration counter before the loop (1: never called) */
+    double robust_tuning;       /* after berg's tuning substitution (:419-433) */
+    double robust_approx;       /* approximation (inf: none) */
+    double robust_berg_target;  /* berg: the target scale */
 } pmx_loop_cfg;
 typedef struct pmx_loop_status {
     int iterations;             /* iterations completed (IterationsCount) */

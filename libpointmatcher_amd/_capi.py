@@ -68,7 +68,11 @@ class LoopCfg(C.Structure):
     _fields_ = [("knn", C.c_int), ("max_dist", C.c_double), ("n_filters", C.c_int),
                 ("filter_kind", C.c_int * 8), ("filter_p", (C.c_double * 3) * 8), ("minimizer", C.c_int),
                 ("n_checkers", C.c_int), ("checker_kind", C.c_int * 8), ("checker_p", (C.c_double * 3) * 8),
-                ("keep_trace", C.c_int)]
+                ("keep_trace", C.c_int),
+                # PMX_FILTER_ROBUST (include/pmx.h)
+                ("robust_fct", C.c_int), ("robust_estimator", C.c_int), ("robust_p2pl", C.c_int),
+                ("robust_nb_iter_for_scale", C.c_int), ("robust_first_call", C.c_int),
+                ("robust_tuning", C.c_double), ("robust_approx", C.c_double), ("robust_berg_target", C.c_double)]
 
 
 class LoopStatus(C.Structure):

@@ -330,8 +330,9 @@ struct VarTrimmedDistOF : PM<T>::OutlierFilter {
 // RobustOutlierFilter (OutlierFiltersImpl.h:220-260, OutlierFiltersImpl.cpp:380-598):
 // the parameters and the filter's state (iteration, berg target, tuning
 // substitution) stay here as in the reference object; the scale and the
-// weights are computed on the device (pmx_outlier_robust).  It has no
-// device-loop form: a chain holding it runs the per-module calls.
+// weights are computed on the device (pmx_outlier_robust).  In the device
+// loop the same schedule runs from the loop's iteration index (loopConfig
+// hands over the call counter; loopAdvance counts the iterations that ran).
 template <typename T>
 struct RobustOF : PM<T>::OutlierFilter {
     std::string robustFctName, scaleEstimator, distanceType;
@@ -389,6 +390,22 @@ struct RobustOF : PM<T>::OutlierFilter {
         d.check(pmx_outlier_robust(d.ctx, pos, robustFctId, (double)tuning, (double)approximation, mode,
                                    (double)berg_target_scale, distanceType == "point2plane" ? 1 : 0));
     }
+    bool loopConfig(pmx_loop_cfg& cfg, int pos) const override {
+        cfg.filter_kind[pos] = PMX_FILTER_ROBUST;
+        cfg.robust_fct = robustFctId;
+        cfg.robust_estimator = scaleEstimator == "mad"   ? PMX_RSE_MAD
+                               : scaleEstimator == "std" ? PMX_RSE_STD
+                               : scaleEstimator == "berg" ? PMX_RSE_BERG
+                                                          : PMX_RSE_NONE;
+        cfg.robust_p2pl = distanceType == "point2plane" ? 1 : 0;
+        cfg.robust_nb_iter_for_scale = nbIterationForScale;
+        cfg.robust_first_call = iteration;
+        cfg.robust_tuning = (double)tuning;
+        cfg.robust_approx = (double)approximation;
+        cfg.robust_berg_target = (double)berg_target_scale;
+        return true;
+    }
+    void loopAdvance(int64_t iterations) override { iteration += (int)iterations; }
 };
 
 // ---- error minimisers -----------------------------------------------------
@@ -1583,6 +1600,7 @@ bool PointMatcher<T>::ICP::iterate(int n) {
             trace.emplace_back(buf.begin() + i * dim * dim, buf.begin() + (i + 1) * dim * dim);
     }
     iterationCount += fresh;
+    for (auto& f : outlierFilters) f->loopAdvance(fresh);
     loopIters_ = st.iterations;
     matcher->visitCounter += (uint64_t)(st.point_count_touched - loopTouched_);  // MatchersImpl.cpp:98
     loopTouched_ = st.point_count_touched;

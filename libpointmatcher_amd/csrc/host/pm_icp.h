@@ -89,6 +89,9 @@ struct PointMatcher {
         // (chain_pos 0 assigns) — OutlierFilter.cpp:90-99
         virtual void compute(Device& dev, const Matches& m, int chain_pos) = 0;
         virtual bool loopConfig(pmx_loop_cfg&, int /*chain_pos*/) const { return false; }
+        // the device loop ran `iterations` more calls of this filter (its
+        // per-call state, as the per-module calls would have left it)
+        virtual void loopAdvance(int64_t /*iterations*/) {}
     };
     struct OutlierFilters : std::vector<std::shared_ptr<OutlierFilter>> {
         void compute(Device& dev, const Matches& m);  // OutlierFilter.cpp:63-103

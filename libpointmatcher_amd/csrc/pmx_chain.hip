@@ -838,32 +838,32 @@ int outlier_robust_impl(pmx_ctx* c, int pos, int fct, double tuning, double appr
     case kRSMad:  // Matches::getMedianAbsDeviation (Matches.cpp:88-122)
         if ((rc = quantile_select<T>(c, d, n, kRatioMedianIndex, nullptr, slot))) return rc;
         if ((rc = ensure(c, &c->d_rdev, &c->rdev_bytes, sizeof(T) * (size_t)(n > 0 ? n : 1)))) return rc;
-        launch_abs_dev<T>(d, n, slot, (T*)c->d_rdev, c->stream);
+        launch_abs_dev<T>(d, n, slot, (T*)c->d_rdev, loop_ctl(c), c->stream);
         if ((rc = quantile_select<T>(c, (const T*)c->d_rdev, n, kRatioMedianIndex, nullptr, c->rob_sel()))) return rc;
-        launch_robust_scale<T>(kRSMad, c->rob_sel(), nullptr, 0, 0.0, scale, c->stream);
+        launch_robust_scale<T>(kRSMad, c->rob_sel(), nullptr, 0, 0.0, scale, loop_ctl(c), c->stream);
         smode = -1;
         break;
     case kRSStd: {  // Matches::getStandardDeviation (Matches.cpp:124-129) over all k x N
         double* sums = c->rob_sums();
         const int64_t nt = c->N_total * c->knn;  // (the mean over every rank's distances)
-        launch_moment<T>(d, n, 0, sums, c->d_partials, nt, c->stream);
+        launch_moment<T>(d, n, 0, sums, c->d_partials, nt, loop_ctl(c), c->stream);
         launch_finalize(c->d_partials, kRedBlocks, 1, sums, loop_ctl(c), c->stream);
         if ((rc = allreduce_f64(c, sums, 1))) return rc;
-        launch_moment<T>(d, n, 1, sums, c->d_partials, nt, c->stream);
+        launch_moment<T>(d, n, 1, sums, c->d_partials, nt, loop_ctl(c), c->stream);
         launch_finalize(c->d_partials, kRedBlocks, 1, sums + 1, loop_ctl(c), c->stream);
         if ((rc = allreduce_f64(c, sums + 1, 1))) return rc;
-        launch_robust_scale<T>(kRSStd, nullptr, sums, c->N_total * c->knn, 0.0, scale, c->stream);
+        launch_robust_scale<T>(kRSStd, nullptr, sums, c->N_total * c->knn, 0.0, scale, loop_ctl(c), c->stream);
         smode = -1;
         break;
     }
     case kRSBergFirst:  // 1.9 sqrt(getDistsQuantile(0.5))
         if ((rc = quantile_select<T>(c, d, n, 0.5, nullptr, slot))) return rc;
-        launch_robust_scale<T>(kRSBergFirst, slot, nullptr, 0, 0.0, scale, c->stream);
+        launch_robust_scale<T>(kRSBergFirst, slot, nullptr, 0, 0.0, scale, loop_ctl(c), c->stream);
         smode = -1;
         break;
     default: break;
     }
-    if (smode >= 0) launch_robust_scale<T>(smode, nullptr, nullptr, 0, target, scale, c->stream);
+    if (smode >= 0) launch_robust_scale<T>(smode, nullptr, nullptr, 0, target, scale, loop_ctl(c), c->stream);
     chain_set(c, pos, kWPRobust, 0.0);
     c->rb_pos = pos;
     c->rb_fct = fct;
@@ -977,13 +977,10 @@ int p2plane_enqueue(pmx_ctx* c) {
     const WChain<T> chain = chain_of<T>(c);
     const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
-    // (0/1 weights: the launch's last block sums the partials itself; the
-    // robust kernel keeps the finalize launch)
+    // (the launch's last block sums the partials itself)
     RedTail tail;
-    if (!chain.robust) {
-        tail.ticket = c->d_ticket;
-        tail.out = c->d_result;
-    }
+    tail.ticket = c->d_ticket;
+    tail.out = c->d_result;
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
                               match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
                               loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->vpart_dirty ? c->d_vpart : nullptr,
@@ -1139,6 +1136,7 @@ int get_weights_impl(pmx_ctx* c, void* w) {
     template int set_reading_impl<T>(pmx_ctx*, const T*, int, int64_t, const T*);            \
     template int match_impl<T>(pmx_ctx*, const T*, int, double, uint64_t*);                  \
     template int outlier_impl<T>(pmx_ctx*, int, int, double, double, double);               \
+    template int outlier_robust_impl<T>(pmx_ctx*, int, int, double, double, int, double, int); \
     template int p2plane_enqueue<T>(pmx_ctx*);                                              \
     template int p2point_enqueue<T>(pmx_ctx*);                                              \
     template int get_matches_impl<T>(pmx_ctx*, void*, int32_t*);                            \

@@ -333,6 +333,9 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
 template <typename T>
 int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, double p2);
 template <typename T>
+int outlier_robust_impl(pmx_ctx* c, int pos, int fct, double tuning, double approx, int mode, double target,
+                        int p2pl);
+template <typename T>
 int p2plane_enqueue(pmx_ctx* c);
 template <typename T>
 int p2point_enqueue(pmx_ctx* c);

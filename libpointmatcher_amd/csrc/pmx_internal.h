@@ -387,16 +387,16 @@ constexpr double kRatioMedianIndex = 2.0;
 enum RobustScaleMode { kRSNone = 0, kRSMad = 1, kRSStd = 2, kRSBergFirst = 3, kRSBergNext = 4, kRSKeep = 5 };
 // dev[i] = |d[i] - median| for finite d (median: st->limit), +inf otherwise
 template <typename T>
-void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, hipStream_t s);
+void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, const LoopCtl* ctl, hipStream_t s);
 // sum of d (pass 0) / of (d - mean)^2 with mean = (T)(sum / n) (pass 1) into
 // partials (kRedBlocks x 1), summed by launch_finalize
 template <typename T>
 void launch_moment(const T* d, int64_t n, int pass, const double* sum, double* partials, int64_t n_total,
-                   hipStream_t s);
+                   const LoopCtl* ctl, hipStream_t s);
 // the scale (a T value stored as double) of the iteration, from the mode
 template <typename T>
 void launch_robust_scale(int mode, const SelectState* st, const double* sums, int64_t n, double target,
-                         double* scale, hipStream_t s);
+                         double* scale, const LoopCtl* ctl, hipStream_t s);
 
 // ---- quantile / weights (pmx_select.hip) ----
 // one radix-select pass: histogram of digit `pass` among keys matching the

@@ -29,6 +29,7 @@ struct Mat4d {
 struct LoopCfg {
     int rows;       // 3 (2-D) or 4 (3-D)
     int minimizer;  // 0 point-to-plane, 1 point-to-point
+    int full;       // point-to-plane: the weighted reduction's layout (full A; a RobustOutlierFilter chain)
     int n_checkers;
     int checker_kind[kMaxCheckers];
     double checker_p[kMaxCheckers][3];

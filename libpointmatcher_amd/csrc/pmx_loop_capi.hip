@@ -27,11 +27,22 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     if (!(cfg->max_dist >= 0)) return fail(c, PMX_E_BAD_PARAM, "maxDist must be >= 0");
     if (cfg->n_filters < 0 || cfg->n_filters > kMaxChain)
         return fail(c, PMX_E_BAD_PARAM, "device loop: at most 8 outlier filters");
+    int n_robust = 0;
     for (int i = 0; i < cfg->n_filters; ++i) {
         const int k = cfg->filter_kind[i];
         const double* p = cfg->filter_p[i];
-        if (k < PMX_FILTER_DEFAULT || k > PMX_FILTER_VARTRIMMED || (k == PMX_FILTER_DEFAULT && i != 0))
+        if (k < PMX_FILTER_DEFAULT || k > PMX_FILTER_ROBUST || (k == PMX_FILTER_DEFAULT && i != 0))
             return fail(c, PMX_E_BAD_PARAM, "device loop: unknown outlier filter");
+        if (k == PMX_FILTER_ROBUST) {
+            ++n_robust;
+            if (cfg->robust_fct < PMX_RF_CAUCHY || cfg->robust_fct > PMX_RF_STUDENT ||
+                cfg->robust_estimator < PMX_RSE_NONE || cfg->robust_estimator > PMX_RSE_BERG)
+                return fail(c, PMX_E_BAD_PARAM, "device loop: bad RobustOutlierFilter parameters");
+            // (the point-to-point kernels carry no normals: the point2plane
+            // distance's weights are materialised on the module path)
+            if (cfg->robust_p2pl && (cfg->minimizer != 0 || c->dim != 3))
+                return fail(c, PMX_E_BAD_PARAM, "device loop: RobustOutlierFilter point2plane needs PointToPlane, 3-D");
+        }
         if ((k == PMX_FILTER_MAXDIST || k == PMX_FILTER_MINDIST) && !(p[0] >= 1e-7))
             return fail(c, PMX_E_BAD_PARAM, "device loop: distance threshold < 1e-7");
         if (k == PMX_FILTER_TRIMMED && !(p[0] >= 1e-7 && p[0] <= 1.0))
@@ -39,6 +50,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
         if (k == PMX_FILTER_VARTRIMMED && !((T)p[0] < (T)p[1]))
             return fail(c, PMX_E_BAD_PARAM, "VarTrimmedDistOutlierFilter: minRatio should be smaller than maxRatio");
     }
+    if (n_robust > 1) return fail(c, PMX_E_BAD_PARAM, "device loop: one RobustOutlierFilter per chain");
     if (cfg->minimizer != 0 && cfg->minimizer != 1) return fail(c, PMX_E_BAD_PARAM, "device loop: unknown minimizer");
     if (cfg->minimizer == 0 && !c->has_normals)
         return fail(c, PMX_E_BAD_PARAM, "PointToPlaneErrorMinimizer requires \"normals\" on the reference");
@@ -56,6 +68,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     LoopCfg d{};
     d.rows = c->rows;
     d.minimizer = cfg->minimizer;
+    d.full = n_robust > 0 ? 1 : 0;  // (point-to-plane: the weighted system's full A layout)
     d.n_checkers = cfg->n_checkers;
     for (int i = 0; i < cfg->n_checkers; ++i) {
         d.checker_kind[i] = cfg->checker_kind[i];
@@ -183,6 +196,22 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     }
     for (int i = 0; i < cfg.n_filters; ++i) {
         const double* p = cfg.filter_p[i];
+        if (cfg.filter_kind[i] == PMX_FILTER_ROBUST) {
+            // RobustOutlierFilter::robustFiltering's scale schedule for this
+            // loop iteration (OutlierFiltersImpl.cpp:500-531; the host module
+            // counts the iterations that ran, pm_icp.cpp RobustOF)
+            const int64_t call = (int64_t)cfg.robust_first_call + c->enq_iter;
+            const bool recompute = cfg.robust_nb_iter_for_scale == 0 || call <= cfg.robust_nb_iter_for_scale;
+            int mode = PMX_RS_NONE;
+            if (cfg.robust_estimator == PMX_RSE_MAD) mode = recompute ? PMX_RS_MAD : PMX_RS_KEEP;
+            else if (cfg.robust_estimator == PMX_RSE_STD) mode = recompute ? PMX_RS_STD : PMX_RS_KEEP;
+            else if (cfg.robust_estimator == PMX_RSE_BERG)
+                mode = !recompute ? PMX_RS_KEEP : (call == 1 ? PMX_RS_BERG_FIRST : PMX_RS_BERG_NEXT);
+            if ((rc = outlier_robust_impl<T>(c, i, cfg.robust_fct, cfg.robust_tuning, cfg.robust_approx, mode,
+                                             cfg.robust_berg_target, cfg.robust_p2pl)))
+                return rc;
+            continue;
+        }
         if ((rc = outlier_impl<T>(c, cfg.filter_kind[i], i, p[0], p[1], p[2]))) return rc;
     }
     if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c))) return rc;

@@ -109,7 +109,16 @@ __global__ __launch_bounds__(256) void p2plane_weighted_kernel(const P4<T>* __re
                                                                const P4<T>* __restrict__ nrm, int rs,
                                                                const T* __restrict__ d,
                                                                const int32_t* __restrict__ ids, WChain<T> chain,
-                                                               int k, int64_t N, double* __restrict__ partials) {
+                                                               int k, int64_t N, double* __restrict__ partials,
+                                                               const LoopCtl* __restrict__ ctl,
+                                                               const GridDesc<T>* __restrict__ gd, RedTail tail) {
+    if (ctl) {  // device loop (a robust chain): transform and level from the device
+        if (ctl->done) return;
+        ctl_transform(ctl, Tm);
+        ref = gd[ctl->level].gpn;
+        nrm = ref + 1;
+        rs = 2;
+    }
     constexpr int NF = DIM == 3 ? 6 : 3;
     constexpr int NS = NF * NF;  // (full A)
     constexpr int NV = NS + NF + 5;
@@ -150,7 +159,12 @@ __global__ __launch_bounds__(256) void p2plane_weighted_kernel(const P4<T>* __re
         }
         if (!exist) acc[NS + NF + 3] += 1.0;
     }
-    block_store<NV>(acc, partials);
+    if (!tail.ticket) {
+        block_store<NV>(acc, partials);
+        return;
+    }
+    block_store<NV, true>(acc, partials);
+    (void)reduce_tail<NV>(partials, tail);
 }
 
 template <typename T>
@@ -158,13 +172,13 @@ void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
                             const RedTail& tail, hipStream_t s) {
-    if (chain.robust) {  // (never in the device loop: a robust chain runs the module calls)
+    if (chain.robust) {  // real-valued weights: the full asymmetric A
         if (dim == 3)
             hipLaunchKernelGGL((p2plane_weighted_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
-                               rs, d, ids, chain, k, N, partials);
+                               rs, d, ids, chain, k, N, partials, ctl, gd, tail);
         else
             hipLaunchKernelGGL((p2plane_weighted_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
-                               rs, d, ids, chain, k, N, partials);
+                               rs, d, ids, chain, k, N, partials, ctl, gd, tail);
         return;
     }
     if (dim == 3)

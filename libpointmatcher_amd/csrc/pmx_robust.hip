@@ -16,9 +16,12 @@
 
 namespace pmx {
 
+// ctl (device loop, may be null): every kernel returns at once once the loop
+// has stopped or stalled, as the other kernels of an iteration
 template <typename T>
 __global__ void abs_dev_kernel(const T* __restrict__ d, int64_t n, const SelectState* __restrict__ st,
-                               T* __restrict__ dev) {
+                               T* __restrict__ dev, const LoopCtl* __restrict__ ctl) {
+    if (ctl && ctl->done) return;
     const T med = (T)st->limit;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -28,11 +31,11 @@ __global__ void abs_dev_kernel(const T* __restrict__ d, int64_t n, const SelectS
 }
 
 template <typename T>
-void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, hipStream_t s) {
+void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, const LoopCtl* ctl, hipStream_t s) {
     if (n <= 0) return;
     int64_t g = (n + 1023) / 1024;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(abs_dev_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, n, st, dev);
+    hipLaunchKernelGGL(abs_dev_kernel<T>, dim3((unsigned)g), dim3(256), 0, s, d, n, st, dev, ctl);
 }
 
 // pass 0: sum d; pass 1: sum (d - mean)^2, mean = (T)(sum / n_total) (T
@@ -40,8 +43,9 @@ void launch_abs_dev(const T* d, int64_t n, const SelectState* st, T* dev, hipStr
 template <typename T>
 __global__ __launch_bounds__(256) void moment_kernel(const T* __restrict__ d, int64_t n, int pass,
                                                      const double* __restrict__ sum, double* __restrict__ partials,
-                                                     int64_t n_total) {
+                                                     int64_t n_total, const LoopCtl* __restrict__ ctl) {
     __shared__ double red[4];
+    if (ctl && ctl->done) return;
     const T mean = pass ? (T)(*sum / (double)n_total) : (T)0;
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -62,14 +66,15 @@ __global__ __launch_bounds__(256) void moment_kernel(const T* __restrict__ d, in
 
 template <typename T>
 void launch_moment(const T* d, int64_t n, int pass, const double* sum, double* partials, int64_t n_total,
-                   hipStream_t s) {
-    hipLaunchKernelGGL(moment_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, d, n, pass, sum, partials, n_total);
+                   const LoopCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(moment_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, d, n, pass, sum, partials, n_total, ctl);
 }
 
 template <typename T>
 __global__ void robust_scale_kernel(int mode, const SelectState* __restrict__ st, const double* __restrict__ sums,
-                                    int64_t n, double target, double* __restrict__ scale) {
-    if (threadIdx.x != 0) return;
+                                    int64_t n, double target, double* __restrict__ scale,
+                                    const LoopCtl* __restrict__ ctl) {
+    if (threadIdx.x != 0 || (ctl && ctl->done)) return;
     T sc = (T)*scale;
     switch (mode) {
     case kRSNone: sc = (T)1; break;
@@ -92,15 +97,16 @@ __global__ void robust_scale_kernel(int mode, const SelectState* __restrict__ st
 
 template <typename T>
 void launch_robust_scale(int mode, const SelectState* st, const double* sums, int64_t n, double target,
-                         double* scale, hipStream_t s) {
-    hipLaunchKernelGGL(robust_scale_kernel<T>, dim3(1), dim3(64), 0, s, mode, st, sums, n, target, scale);
+                         double* scale, const LoopCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(robust_scale_kernel<T>, dim3(1), dim3(64), 0, s, mode, st, sums, n, target, scale, ctl);
 }
 
-#define PMX_ROBUST_INST(T)                                                                                  \
-    template void launch_abs_dev<T>(const T*, int64_t, const SelectState*, T*, hipStream_t);               \
-    template void launch_moment<T>(const T*, int64_t, int, const double*, double*, int64_t, hipStream_t);  \
-    template void launch_robust_scale<T>(int, const SelectState*, const double*, int64_t, double, double*, \
-                                         hipStream_t);
+#define PMX_ROBUST_INST(T)                                                                                        \
+    template void launch_abs_dev<T>(const T*, int64_t, const SelectState*, T*, const LoopCtl*, hipStream_t);      \
+    template void launch_moment<T>(const T*, int64_t, int, const double*, double*, int64_t, const LoopCtl*,       \
+                                   hipStream_t);                                                                  \
+    template void launch_robust_scale<T>(int, const SelectState*, const double*, int64_t, double, double*,       \
+                                         const LoopCtl*, hipStream_t);
 PMX_ROBUST_INST(float)
 PMX_ROBUST_INST(double)
 #undef PMX_ROBUST_INST

@@ -71,9 +71,14 @@ __device__ __forceinline__ void p2plane_system_of(const double* __restrict__ res
 // Rank-deficient point-to-plane system: rare, kept out of line so that its
 // dynamically indexed work arrays do not push the hot path's into scratch.
 template <typename T, int NF>
-__device__ __noinline__ void loop_solve_rank_deficient(const double* __restrict__ res, T* __restrict__ xout) {
+__device__ __noinline__ void loop_solve_rank_deficient(const double* __restrict__ res, int full, T* __restrict__ xout) {
     T A[36], b[6], x[6];
-    p2plane_system_of<T, NF>(res, A, b);
+    if (full) {
+        for (int i = 0; i < NF * NF; ++i) A[i] = (T)res[i];
+        for (int i = 0; i < NF; ++i) b[i] = (T)(-res[NF * NF + i]);
+    } else {
+        p2plane_system_of<T, NF>(res, A, b);
+    }
     solve_rank_deficient(A, b, NF, x);
     for (int i = 0; i < NF; ++i) xout[i] = x[i];
 }
@@ -149,7 +154,7 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
     // statistics of the iteration (ErrorElements, ErrorMinimizer.cpp:133-192)
     double kept, nz, rejM, rejP, sw;
     if (MIN == 0) {
-        const int NF = D == 3 ? 6 : 3, o = NF * (NF + 1) / 2 + NF;
+        const int NF = D == 3 ? 6 : 3, o = (cfg.full ? NF * NF : NF * (NF + 1) / 2) + NF;
         kept = res[o];
         nz = res[o + 1];
         rejM = res[o + 2];
@@ -188,7 +193,14 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
     if constexpr (MIN == 0) {
         constexpr int NF = D == 3 ? 6 : 3;
         T A[NF * NF], b[NF], x[NF], L[NF * NF];
-        p2plane_system_of<T, NF>(res, A, b);
+        if (cfg.full) {  // (a robust chain: (w F_r) F_c in T, the reference's asymmetric wF * F^T)
+#pragma unroll
+            for (int i = 0; i < NF * NF; ++i) A[i] = (T)res[i];
+#pragma unroll
+            for (int i = 0; i < NF; ++i) b[i] = (T)(-res[NF * NF + i]);
+        } else {
+            p2plane_system_of<T, NF>(res, A, b);
+        }
         // solve_full_rank: FullPivQR(A).isInvertible() -> LLT solve.  The
         // QR's rank test is skipped when the LLT factor proves A far from
         // rank-deficient (well_conditioned below): its answer is then known.
@@ -202,7 +214,7 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
         if (full) {
             llt_solve(L, NF, b, x);
         } else {
-            loop_solve_rank_deficient<T, NF>(res, S->xsolve);
+            loop_solve_rank_deficient<T, NF>(res, cfg.full, S->xsolve);
             for (int i = 0; i < NF; ++i) x[i] = S->xsolve[i];
         }
         p2plane_transform(rows, x, dT);

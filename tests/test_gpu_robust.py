@@ -180,3 +180,51 @@ def test_icp_robust_equals_oracle(golden, oracle, dtype):
     print(f"robust {np.dtype(dtype).name}: iterations {icp.stats().iterations}/{so.iterations} |dT|={frob:.3g}")
     assert icp.stats().iterations == so.iterations
     assert frob <= (1e-5 if dtype == np.float32 else 1e-12)
+
+
+ROBUST_LOOP_CASES = [
+    # (robust params, minimizer, with normals)
+    ({"robustFct": "cauchy", "scaleEstimator": "mad", "tuning": 1}, "PointToPointErrorMinimizer", False),
+    ({"robustFct": "huber", "scaleEstimator": "berg", "tuning": 0.05}, "PointToPointErrorMinimizer", False),
+    ({"robustFct": "welsch", "scaleEstimator": "std", "tuning": 1.5, "nbIterationForScale": 3},
+     "PointToPlaneErrorMinimizer", True),
+    ({"robustFct": "tukey", "scaleEstimator": "mad", "tuning": 4, "distanceType": "point2plane",
+      "nbIterationForScale": 5}, "PointToPlaneErrorMinimizer", True),
+]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("case", range(len(ROBUST_LOOP_CASES)))
+def test_robust_device_loop_equals_modules(monkeypatch, oracle, dtype, case):
+    """RobustOutlierFilter chains on the device loop (pmx_loop_*: the scale
+    schedule from the loop's iteration index, the weighted reductions and the
+    full-A step on the device) against the per-module calls (PMX_DEVICE_LOOP=0)
+    and the oracle ICP: same iteration count, |dT|_F within 1e-5 / 1e-12."""
+    from helpers import chain_yaml
+
+    params, minimizer, with_n = ROBUST_LOOP_CASES[case]
+    ref, nrm = reference_cloud(40_000, dtype)
+    rd = reading_cloud(20_000, dtype)
+    diff = dict(minDiffRotErr=0.001, minDiffTransErr=0.01, smoothLength=4)
+    filters = (("RobustOutlierFilter", params),)
+    yaml = chain_yaml(knn=2, filters=filters, minimizer=minimizer, maxit=25, differential=diff)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PMX_DEVICE_LOOP", mode)
+        icp = ICP(dtype)
+        icp.load_yaml(yaml)
+        T = icp.compute(rd, ref, nrm if with_n else None)
+        out[mode] = (T, icp.stats())
+        icp.close()
+    (Tl, sl), (Tm, sm) = out["1"], out["0"]
+    cfg = oracle.make_cfg(knn=2, filters=filters, minimizer=minimizer, counter_max=25, differential=diff, threads=8)
+    rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm if with_n else None)
+    assert rc == 0
+    tol = 1e-5 if dtype == np.float32 else 1e-12
+    fl = np.linalg.norm(Tl.astype(np.float64) - To.astype(np.float64))
+    fm = np.linalg.norm(Tm.astype(np.float64) - To.astype(np.float64))
+    print(f"{np.dtype(dtype).name} {params['robustFct']}/{params['scaleEstimator']}: iterations loop {sl.iterations} "
+          f"modules {sm.iterations} oracle {so.iterations}; |dT| loop {fl:.3g} modules {fm:.3g}")
+    assert sl.iterations == sm.iterations == so.iterations
+    assert sl.kept == sm.kept
+    assert fl <= tol and fm <= tol
