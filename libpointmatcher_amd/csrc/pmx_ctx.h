@@ -188,6 +188,7 @@ struct pmx_ctx {
     // reductions
     double* d_partials = nullptr;
     unsigned* d_ticket = nullptr;  // the reductions' in-launch finalize ticket (RedTail; zero between launches)
+    bool red_tail = true;          // in-launch finalize (PMX_RED_TAIL=0: a finalize launch instead)
     double* d_result = nullptr;  // [0..63] system, [64..127] second pass
     void* d_means = nullptr;
     double* h_result = nullptr;  // pinned
