@@ -140,6 +140,12 @@ int pmx_comm_loop_stats(const pmx_ctx* ctx, uint64_t* verdict_syncs, uint64_t* a
  * reference (ICP.cpp:299).  normals: D x M (point-major) or NULL.  Copied
  * to HBM once and kept resident across iterations and ICP calls. */
 int pmx_set_reference(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const void* normals);
+/* The same with the centring done on the device: offset = the D reference
+ * means (T values, ICP.cpp:291-292), subtracted from every point in T as
+ * ICP.cpp:299 does (features.topRows(dim - 1) -= mean).  The caller then
+ * needs no centred host copy of the reference. */
+int pmx_set_reference_centred(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const void* normals,
+                              const void* offset);
 /* reading shard: rows x N.  T0 (rows x rows, row-major T) is applied once on
  * the device (T_refMean_dataIn, ICP.cpp:345-347). */
 int pmx_set_reading(pmx_ctx* ctx, const void* feat, int rows, int64_t N, const void* T0);

@@ -102,11 +102,14 @@ using PM = PointMatcher<T>;
 // Matcher::init of both kd-tree matchers: the reference (and its normals,
 // for the point-to-plane minimiser) to HBM, the search structure built there
 template <typename T>
-void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType) {
+void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType, const T* centre) {
     dev.ensure();
     std::vector<T> nrm;
     const T* np = nullptr;
-    if (ref.descriptorExists("normals")) {
+    if (ref.descriptorLabels.size() == 1 && ref.descriptorLabels[0].text == "normals" &&
+        ref.descriptorLabels[0].span == ref.rows - 1) {
+        np = ref.descriptors.data();  // (the only descriptor: already the dense D x n block, no copy)
+    } else if (ref.descriptorExists("normals")) {
         int span = 0;
         nrm = ref.descriptor("normals", &span);
         if (span < ref.rows - 1) throw InvalidElement("normals descriptor has fewer rows than the dimension");
@@ -119,7 +122,10 @@ void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType) {
         np = nrm.data();
     }
     dev.check(pmx_set_search(dev.ctx, searchType));  // 0: brute force, 1/2: exact grid search
-    dev.check(pmx_set_reference(dev.ctx, ref.features.data(), ref.rows, ref.n, np));
+    if (centre)
+        dev.check(pmx_set_reference_centred(dev.ctx, ref.features.data(), ref.rows, ref.n, np, centre));
+    else
+        dev.check(pmx_set_reference(dev.ctx, ref.features.data(), ref.rows, ref.n, np));
 }
 template <typename T>
 typename PM<T>::Matches device_matches(Device& dev, int knn) {
@@ -156,7 +162,9 @@ struct KDTreeMatcherGPU : PM<T>::Matcher {
           searchType(this->template get<int>("searchType")),
           maxDist(this->template get<T>("maxDist")) {}
 
-    void init(Device& dev, const DataPoints<T>& ref) override { matcher_init<T>(dev, ref, searchType); }
+    void init(Device& dev, const DataPoints<T>& ref, const T* centre) override {
+        matcher_init<T>(dev, ref, searchType, centre);
+    }
     Matches findClosests(Device& dev, const std::vector<T>& T_iter) override {
         // PointCountTouched is added from the minimiser's pmx_stats.visited
         // once the (asynchronous) match has completed, see ICP::step
@@ -196,7 +204,9 @@ struct KDTreeVarDistMatcherGPU : PM<T>::Matcher {
           epsilon(this->template get<T>("epsilon")),
           searchType(this->template get<int>("searchType")),
           maxDistField(this->template get<std::string>("maxDistField")) {}
-    void init(Device& dev, const DataPoints<T>& ref) override { matcher_init<T>(dev, ref, searchType); }
+    void init(Device& dev, const DataPoints<T>& ref, const T* centre) override {
+        matcher_init<T>(dev, ref, searchType, centre);
+    }
     void initReading(Device& dev, const DataPoints<T>& reading) override {
         // getDescriptorViewByName(maxDistField).transpose(): one radius per point
         int span = 0;
@@ -1344,26 +1354,45 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
                 if (f->usesRandState())
                     throw ConfigurationError(f->className + " draws from the process's rand() state: it cannot run on "
                                              "the reading shards of a multi-rank ICP");
-    DataPoints reference(referenceIn);
     for (auto& f : referenceDataPointsFilters) f->device = dev.device;
     for (auto& f : readingDataPointsFilters) f->device = dev.device;
-    referenceDataPointsFilters.init();
-    referenceDataPointsFilters.apply(reference);
+    // (no reference filters: the caller's cloud is uploaded as it is and
+    // centred on the device — no host copy of the reference)
+    const bool filtered = !referenceDataPointsFilters.empty();
+    DataPoints refCopy;
+    if (filtered) {
+        refCopy = referenceIn;
+        referenceDataPointsFilters.init();
+        referenceDataPointsFilters.apply(refCopy);
+    }
+    const DataPoints& reference = filtered ? refCopy : referenceIn;
     const int64_t M = reference.n;
     if (M <= 0) throw ConvergenceError("empty reference");
-    // mean of the reference columns in T (sequential), ICP.cpp:291-292
+    // mean of the reference columns in T, ICP.cpp:291-292: each coordinate's
+    // sum sequential in point order (the three sums in one pass)
     T_refIn_refMean_.assign((size_t)dim * dim, (T)0);
     for (int i = 0; i < dim; ++i) T_refIn_refMean_[i * dim + i] = 1;
+    T sum[3] = {0, 0, 0}, mean[3] = {0, 0, 0};
+    const T* f = reference.features.data();
+    if (dim == 4) {
+        for (int64_t j = 0; j < M; ++j) {
+            sum[0] = sum[0] + f[j * 4];
+            sum[1] = sum[1] + f[j * 4 + 1];
+            sum[2] = sum[2] + f[j * 4 + 2];
+        }
+    } else {
+        for (int64_t j = 0; j < M; ++j) {
+            sum[0] = sum[0] + f[j * 3];
+            sum[1] = sum[1] + f[j * 3 + 1];
+        }
+    }
     for (int r = 0; r < dim - 1; ++r) {
-        T s = 0;
-        for (int64_t j = 0; j < M; ++j) s = s + reference.features[j * dim + r];
-        const T mean = s / (T)M;
-        T_refIn_refMean_[r * dim + dim - 1] = mean;
-        for (int64_t j = 0; j < M; ++j) reference.features[j * dim + r] = reference.features[j * dim + r] - mean;
+        mean[r] = sum[r] / (T)M;
+        T_refIn_refMean_[r * dim + dim - 1] = mean[r];
     }
     dev.ensure();
-    mapIndexed_ = false;            // (an ICPSequence map is no longer the device's reference, even if init throws)
-    matcher->init(dev, reference);  // ICP.cpp:302
+    mapIndexed_ = false;                  // (an ICPSequence map is no longer the device's reference, even if init throws)
+    matcher->init(dev, reference, mean);  // ICP.cpp:302 (features - mean, ICP.cpp:299, on the device)
     referencePreprocessingDuration = since<T>(t);
     prefilteredReferencePtsCount = M;
     prepareReading(readingIn, T_init);
@@ -1379,9 +1408,14 @@ void PointMatcher<T>::ICP::prepareReading(const DataPoints& readingIn, const Tra
                                  "rows in the read/reference scans.");
     if (readingIn.rows != dim) throw std::runtime_error("reading and reference dimensions differ");
     const auto t = std::chrono::steady_clock::now();
-    DataPoints reading(readingIn);
-    readingDataPointsFilters.init();
-    readingDataPointsFilters.apply(reading);
+    // (no reading filters: the caller's cloud directly, no host copy)
+    DataPoints readCopy;
+    if (!readingDataPointsFilters.empty()) {
+        readCopy = readingIn;
+        readingDataPointsFilters.init();
+        readingDataPointsFilters.apply(readCopy);
+    }
+    const DataPoints& reading = readingDataPointsFilters.empty() ? readingIn : readCopy;
     // T_refMean_dataIn = T_refIn_refMean^-1 * T_init (the inverse of a pure
     // translation is exact), ICP.cpp:345-346
     TransformationParameters inv((size_t)dim * dim, (T)0);

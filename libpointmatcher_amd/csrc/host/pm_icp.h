@@ -70,7 +70,9 @@ struct PointMatcher {
         virtual ~Matcher() {}
         void resetVisitCount() { visitCounter = 0; }
         uint64_t getVisitCount() const { return visitCounter; }
-        virtual void init(Device& dev, const DataPoints& filteredReference) = 0;
+        // centre (may be null): rows - 1 values the matcher subtracts per axis
+        // in T (ICP.cpp:299's centring done with the upload, on the device)
+        virtual void init(Device& dev, const DataPoints& filteredReference, const T* centre = nullptr) = 0;
         // the reading's inputs of the match, once per compute after the
         // reading upload (KDTreeVarDistMatcher: its per-point radii)
         virtual void initReading(Device&, const DataPoints&) {}

@@ -250,7 +250,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
-                    c->d_rob, c->d_rdev, c->d_radii, c->d_ticket};
+                    c->d_rob, c->d_rdev, c->d_radii, c->d_ticket, c->d_rd_p4, c->d_rd_sorted};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();

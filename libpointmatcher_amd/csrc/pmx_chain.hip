@@ -143,8 +143,14 @@ int build_grid(pmx_ctx* c, int64_t M) {
         dim = std::min(3.0, std::max(1.0, dim));
         ppc1 = (double)valid / (double)o1;
     }
-    for (auto& L : c->levels) L.release();
-    c->levels.clear();
+    // (the level buffers are kept: reused when the new shapes fit)
+    if (c->levels.size() > c->level_ppc.size()) {
+        for (size_t l = c->level_ppc.size(); l < c->levels.size(); ++l) c->levels[l].release();
+        c->levels.resize(c->level_ppc.size());
+    }
+    std::vector<GridLevel> keep;
+    keep.swap(c->levels);
+    keep.resize(c->level_ppc.size());
     c->level = 0;
     c->match_count = 0;
     c->level_cells.assign(c->level_ppc.size(), 0.0);
@@ -165,17 +171,27 @@ int build_grid(pmx_ctx* c, int64_t M) {
     }
     if ((rc = setup_room(c, M, max_cells))) return rc;
     const int64_t np = std::max<int64_t>(valid, 1);
+    auto room = [](void** p, size_t* cap, size_t bytes) -> bool {
+        if (*p && *cap >= bytes) return true;
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        if (hipMalloc(p, bytes) != hipSuccess) return false;
+        *cap = bytes;
+        return true;
+    };
     for (size_t l = 0; l < shapes.size(); ++l) {
         const SetupShape& s = shapes[l];
-        GridLevel L;
+        GridLevel L = keep[l];
+        keep[l] = GridLevel{};
         auto bad = [&](int r) {
             L.release();
+            for (auto& K : keep) K.release();
             return r;
         };
-        if (hipMalloc(&L.gpts, sizeof(P4<T>) * np) != hipSuccess ||
-            hipMalloc((void**)&L.gidx, sizeof(int32_t) * np) != hipSuccess ||
-            hipMalloc((void**)&L.gstart, sizeof(uint32_t) * (size_t)(s.cells + 1)) != hipSuccess ||
-            (nrm && hipMalloc(&L.gpn, 2 * sizeof(P4<T>) * np) != hipSuccess))
+        if (!room(&L.gpts, &L.cap_pts, sizeof(P4<T>) * np) || !room((void**)&L.gidx, &L.cap_idx, sizeof(int32_t) * np) ||
+            !room((void**)&L.gstart, &L.cap_start, sizeof(uint32_t) * (size_t)(s.cells + 1)) ||
+            (nrm && !room(&L.gpn, &L.cap_gpn, 2 * sizeof(P4<T>) * np)))
             return bad(fail(c, PMX_E_HIP, "grid level allocation failed"));
         const int r = build_level_device<T>(pts, M, nrm, s, valid, c->setup, (P4<T>*)L.gpts, (P4<T>*)L.gpn, L.gidx,
                                             L.gstart, c->stream);
@@ -204,9 +220,8 @@ int build_grid(pmx_ctx* c, int64_t M) {
         D.G.h = L.h;
         D.G.inv_h = 1.0 / L.h;
     }
-    if (c->d_gdesc) (void)hipFree(c->d_gdesc);
-    c->d_gdesc = nullptr;
-    HIPCHK(c, hipMalloc(&c->d_gdesc, sizeof(GridDesc<T>) * std::max<size_t>(tab.size(), 1)));
+    if (!c->d_gdesc) HIPCHK(c, hipMalloc(&c->d_gdesc, sizeof(GridDesc<T>) * kMaxLevels));
+    if (tab.size() > (size_t)kMaxLevels) return fail(c, PMX_E_BAD_PARAM, "at most 8 grid levels");
     HIPCHK(c, hipMemcpyAsync(c->d_gdesc, tab.data(), sizeof(GridDesc<T>) * tab.size(), hipMemcpyHostToDevice,
                              c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -264,7 +279,7 @@ int host_order(pmx_ctx* c) {
 
 // ------------------------------------------------------------------ clouds --
 template <typename T>
-int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals) {
+int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals, const T* offset) {
     if (rows != 3 && rows != 4) return fail(c, PMX_E_BAD_PARAM, "reference must have 3 (2-D) or 4 (3-D) rows");
     if (M <= 0) return fail(c, PMX_E_BAD_PARAM, "empty reference");
     if (M > (int64_t)0x7fffffff - kTile) return fail(c, PMX_E_BAD_PARAM, "reference larger than int32 ids");
@@ -274,16 +289,13 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     const int D = rows - 1;
     const int64_t M_pad = ((M + kTile - 1) / kTile) * kTile;
     int rc;
-    if (c->d_ref) (void)hipFree(c->d_ref);
-    c->d_ref = nullptr;
-    HIPCHK(c, hipMalloc(&c->d_ref, sizeof(P4<T>) * M_pad));
+    // (buffers kept across references; the stream orders a previous user's reads first)
+    if ((rc = ensure(c, &c->d_ref, &c->ref_bytes, sizeof(P4<T>) * M_pad))) return rc;
     if ((rc = upload_raw(c, feat, sizeof(T) * (size_t)rows * M))) return rc;
-    launch_pack_p4<T>((const T*)c->d_raw, rows, M, M_pad, (P4<T>*)c->d_ref, c->stream);
-    if (c->d_nrm) (void)hipFree(c->d_nrm);
-    c->d_nrm = nullptr;
+    launch_pack_p4<T>((const T*)c->d_raw, rows, M, M_pad, (P4<T>*)c->d_ref, c->stream, offset);
     c->has_normals = normals != nullptr;
     if (normals) {
-        HIPCHK(c, hipMalloc(&c->d_nrm, sizeof(P4<T>) * M));
+        if ((rc = ensure(c, &c->d_nrm, &c->nrm_bytes, sizeof(P4<T>) * M))) return rc;
         // (the raw buffer is reused: the copy is ordered after the pack on the stream)
         if ((rc = upload_raw(c, normals, sizeof(T) * (size_t)D * M))) return rc;
         launch_pack_nrm<T>((const T*)c->d_raw, D, M, (P4<T>*)c->d_nrm, c->stream);
@@ -311,14 +323,13 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     const int64_t n1 = std::max<int64_t>(N, 1);
     c->has_radii = false;  // (a new reading: its radii, if any, follow)
     // raw P4 reading (pack), then the slot order, then T_refMean_dataIn
-    void* d_p4 = nullptr;
-    HIPCHK(c, hipMalloc(&d_p4, sizeof(P4<T>) * n1));
-    std::unique_ptr<void, void (*)(void*)> free_p4(d_p4, [](void* p) { (void)hipFree(p); });
+    // (scratch and the resident reading kept across readings: ICPSequence
+    // scans pay no allocation)
+    if ((rc = ensure(c, &c->d_rd_p4, &c->rd_p4_bytes, sizeof(P4<T>) * n1))) return rc;
+    void* d_p4 = c->d_rd_p4;
     if ((rc = upload_raw(c, feat, sizeof(T) * (size_t)rows * N))) return rc;
     launch_pack_p4<T>((const T*)c->d_raw, rows, N, N, (P4<T>*)d_p4, c->stream);
-    if (c->d_rd) (void)hipFree(c->d_rd);
-    c->d_rd = nullptr;
-    HIPCHK(c, hipMalloc(&c->d_rd, sizeof(P4<T>) * n1));
+    if ((rc = ensure(c, &c->d_rd, &c->rd_bytes, sizeof(P4<T>) * n1))) return rc;
     if (c->d_waves) (void)hipFree(c->d_waves);
     c->d_waves = nullptr;
     c->n_waves = 0;
@@ -337,9 +348,8 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
         s.cells = (int64_t)s.g[0] * s.g[1] * s.g[2];
         const bool morton = s.g[0] <= (1 << 21) && s.g[1] <= (1 << 21) && s.g[2] <= (1 << 21);
         if ((rc = setup_room(c, N, std::max<int64_t>(c->setup_cells, 1)))) return rc;
-        void* d_sorted = nullptr;
-        HIPCHK(c, hipMalloc(&d_sorted, sizeof(P4<T>) * n1));
-        std::unique_ptr<void, void (*)(void*)> free_sorted(d_sorted, [](void* p) { (void)hipFree(p); });
+        if ((rc = ensure(c, &c->d_rd_sorted, &c->rd_sorted_bytes, sizeof(P4<T>) * n1))) return rc;
+        void* d_sorted = c->d_rd_sorted;
         const int r = reading_order_device<T>((const P4<T>*)d_p4, N, M0, s, morton, c->setup, (P4<T>*)d_sorted,
                                               c->stream);
         if (r) return fail(c, PMX_E_HIP, "reading order failed (" + std::to_string(r) + ")");
@@ -362,7 +372,6 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
             c->n_waves = (int64_t)waves.size() - 1;
         }
         HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipStreamSynchronize(c->stream));  // (d_sorted is freed on return)
     } else if (N > 0) {
         launch_transform<T>((const P4<T>*)d_p4, (P4<T>*)c->d_rd, N, M0, c->stream);
         HIPCHK(c, hipGetLastError());
@@ -1138,7 +1147,7 @@ int get_weights_impl(pmx_ctx* c, void* w) {
 
 // ---- instantiations used by the other translation units (pmx_ctx.h) ----
 #define PMX_INST(T)                                                                          \
-    template int set_reference_impl<T>(pmx_ctx*, const T*, int, int64_t, const T*);          \
+    template int set_reference_impl<T>(pmx_ctx*, const T*, int, int64_t, const T*, const T*); \
     template int set_reading_impl<T>(pmx_ctx*, const T*, int, int64_t, const T*);            \
     template int match_impl<T>(pmx_ctx*, const T*, int, double, uint64_t*);                  \
     template int outlier_impl<T>(pmx_ctx*, int, int, double, double, double);               \
@@ -1164,6 +1173,17 @@ int pmx_set_reference(pmx_ctx* c, const void* feat, int rows, int64_t M, const v
     (void)hipSetDevice(c->device);
     return DISPATCH(c, set_reference_impl<float>(c, (const float*)feat, rows, M, (const float*)normals),
                     set_reference_impl<double>(c, (const double*)feat, rows, M, (const double*)normals));
+}
+
+int pmx_set_reference_centred(pmx_ctx* c, const void* feat, int rows, int64_t M, const void* normals,
+                              const void* offset) {
+    if (!c || !feat || !offset) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c,
+                    set_reference_impl<float>(c, (const float*)feat, rows, M, (const float*)normals,
+                                              (const float*)offset),
+                    set_reference_impl<double>(c, (const double*)feat, rows, M, (const double*)normals,
+                                               (const double*)offset));
 }
 
 int pmx_set_reading(pmx_ctx* c, const void* feat, int rows, int64_t N, const void* T0) {

@@ -59,12 +59,16 @@ struct GridLevel {
     double h = 1.0;
     int dim[3] = {1, 1, 1};
     double ppc = 0.0;
+    // allocated capacities (a new reference reuses the buffers when it fits:
+    // hipMalloc / hipFree of 4 buffers x 6 levels was a large part of setup)
+    size_t cap_pts = 0, cap_gpn = 0, cap_idx = 0, cap_start = 0;
     void release() {
         for (void* b : {gpts, gpn, (void*)gidx, (void*)gstart})
             if (b) (void)hipFree(b);
         gpts = gpn = nullptr;
         gidx = nullptr;
         gstart = nullptr;
+        cap_pts = cap_gpn = cap_idx = cap_start = 0;
     }
 };
 
@@ -80,6 +84,7 @@ struct pmx_ctx {
     int64_t M = 0, M_pad = 0;
     void* d_ref = nullptr;
     void* d_nrm = nullptr;
+    size_t ref_bytes = 0, nrm_bytes = 0;  // (capacities: kept across references)
     bool has_normals = false;
 
     // uniform grid over the reference (exact shell search, pmx_grid.hip)
@@ -129,6 +134,10 @@ struct pmx_ctx {
     // reading shard
     int64_t N = 0, N_total = 0, N_max = 0;
     void* d_rd = nullptr;
+    size_t rd_bytes = 0;
+    void* d_rd_p4 = nullptr;       // set_reading scratch: the packed reading before / after the slot sort
+    void* d_rd_sorted = nullptr;
+    size_t rd_p4_bytes = 0, rd_sorted_bytes = 0;
     // KDTreeVarDistMatcher: per-point search radii in slot order (pmx_set_reading_radii)
     void* d_radii = nullptr;
     size_t radii_bytes = 0;
@@ -326,7 +335,7 @@ double host_limit(const pmx_ctx* c);
 void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double rm, double rp, double sw,
                 double limit);
 template <typename T>
-int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals);
+int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals, const T* offset = nullptr);
 template <typename T>
 int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0);
 template <typename T>

@@ -228,7 +228,14 @@ struct SetupScratch {
     size_t temp_bytes = 0;
 };
 template <typename T>
-void launch_pack_p4(const T* raw, int rows, int64_t n, int64_t n_pad, P4<T>* out, hipStream_t s);
+struct Off3 {
+    T v[3];
+    int on;
+};
+// offset (may be null): rows - 1 values subtracted per axis in T (centring)
+template <typename T>
+void launch_pack_p4(const T* raw, int rows, int64_t n, int64_t n_pad, P4<T>* out, hipStream_t s,
+                    const T* offset = nullptr);
 template <typename T>
 void launch_pack_nrm(const T* raw, int D, int64_t n, P4<T>* out, hipStream_t s);
 template <typename T>

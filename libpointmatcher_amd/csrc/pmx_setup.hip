@@ -34,8 +34,11 @@
 namespace pmx {
 
 // ------------------------------------------------------------------ pack --
+// off (may be null): subtracted per axis in T — the centring of ICP.cpp:299
+// (features.topRows(dim - 1) -= mean), the same one rounding per coordinate
 template <typename T>
-__global__ void pack_p4_kernel(const T* __restrict__ raw, int rows, int64_t n, int64_t n_pad, P4<T>* __restrict__ out) {
+__global__ void pack_p4_kernel(const T* __restrict__ raw, int rows, int64_t n, int64_t n_pad, P4<T>* __restrict__ out,
+                               Off3<T> off) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_pad) return;
     if (i >= n) {
@@ -44,7 +47,13 @@ __global__ void pack_p4_kernel(const T* __restrict__ raw, int rows, int64_t n, i
         return;
     }
     const T* p = raw + i * rows;
-    out[i] = rows == 4 ? P4<T>{p[0], p[1], p[2], p[3]} : P4<T>{p[0], p[1], (T)0, p[2]};
+    P4<T> q = rows == 4 ? P4<T>{p[0], p[1], p[2], p[3]} : P4<T>{p[0], p[1], (T)0, p[2]};
+    if (off.on) {
+        q.x = q.x - off.v[0];
+        q.y = q.y - off.v[1];
+        if (rows == 4) q.z = q.z - off.v[2];
+    }
+    out[i] = q;
 }
 
 template <typename T>
@@ -58,9 +67,14 @@ __global__ void pack_nrm_kernel(const T* __restrict__ raw, int D, int64_t n, P4<
 static unsigned blocks_for(int64_t n, int per = 256) { return (unsigned)((n + per - 1) / per > 0 ? (n + per - 1) / per : 1); }
 
 template <typename T>
-void launch_pack_p4(const T* raw, int rows, int64_t n, int64_t n_pad, P4<T>* out, hipStream_t s) {
+void launch_pack_p4(const T* raw, int rows, int64_t n, int64_t n_pad, P4<T>* out, hipStream_t s, const T* offset) {
     if (n_pad <= 0) return;
-    hipLaunchKernelGGL(pack_p4_kernel<T>, dim3(blocks_for(n_pad)), dim3(256), 0, s, raw, rows, n, n_pad, out);
+    Off3<T> off{};
+    if (offset) {
+        off.on = 1;
+        for (int a = 0; a < rows - 1; ++a) off.v[a] = offset[a];
+    }
+    hipLaunchKernelGGL(pack_p4_kernel<T>, dim3(blocks_for(n_pad)), dim3(256), 0, s, raw, rows, n, n_pad, out, off);
 }
 template <typename T>
 void launch_pack_nrm(const T* raw, int D, int64_t n, P4<T>* out, hipStream_t s) {
@@ -111,18 +125,36 @@ __global__ __launch_bounds__(256) void bbox_kernel(const P4<T>* __restrict__ p, 
     if (t < 7) part[blockIdx.x * 8 + t] = red[t][0];
 }
 
+// (min / max are order-free and the count is an exact integer in double:
+// the block tree gives the same result as a sequential walk)
 __global__ __launch_bounds__(256) void bbox_final_kernel(const double* __restrict__ part, int nb,
                                                          double* __restrict__ out) {
-    if (threadIdx.x != 0) return;
+    __shared__ double red[7][256];
+    const int t = threadIdx.x;
     double v[7] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300, 0.0};
-    for (int b = 0; b < nb; ++b) {
+    for (int b = t; b < nb; b += 256) {
+#pragma unroll
         for (int a = 0; a < 3; ++a) {
             v[a] = fmin(v[a], part[b * 8 + a]);
             v[3 + a] = fmax(v[3 + a], part[b * 8 + 3 + a]);
         }
         v[6] += part[b * 8 + 6];
     }
-    for (int k = 0; k < 7; ++k) out[k] = v[k];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) red[k][t] = v[k];
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if (t < off) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                red[a][t] = fmin(red[a][t], red[a][t + off]);
+                red[3 + a][t] = fmax(red[3 + a][t], red[3 + a][t + off]);
+            }
+            red[6][t] += red[6][t + off];
+        }
+        __syncthreads();
+    }
+    if (t < 7) out[t] = red[t][0];
 }
 
 // out[7]: lo xyz, hi xyz, finite count; scratch: kBBoxBlocks * 8 doubles
@@ -151,24 +183,49 @@ __device__ __forceinline__ int64_t dcell_of(const SetupShape& s, double x, doubl
     return (ci[2] * s.g[1] + ci[1]) * s.g[0] + ci[0];
 }
 
-// distinct cells: one bit per cell, the first setter counts it
+// distinct cells: one bit per cell, the first setter counts it.  Neighbouring
+// points (clouds are often spatially ordered) hit the same bitmap word: the
+// lanes of a wave are grouped by word first — one atomicOr per distinct word
+// with the OR of the group's bits, the new bits counted from its return
+// (per-lane atomics on one word serialised: ~300 us at 1M points)
 template <typename T>
 __global__ void occupancy_kernel(const P4<T>* __restrict__ p, int64_t n, SetupShape s, uint32_t* __restrict__ bits,
                                  unsigned long long* __restrict__ count) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
     uint32_t mine = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const P4<T> q = p[i];
-        if (!dfinite(q)) continue;
-        int64_t ci[3];
-        const int64_t c = dcell_of(s, (double)q.x, (double)q.y, (double)q.z, ci);
-        const uint32_t b = 1u << (uint32_t)(c & 31);
-        const uint32_t old = atomicOr(&bits[c >> 5], b);
-        mine += (old & b) ? 0u : 1u;
+    // (uniform trip count: every lane of the wave runs every round)
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+        const int64_t i = i0 + threadIdx.x;
+        int64_t w = -1;
+        uint32_t b = 0;
+        if (i < n) {
+            const P4<T> q = p[i];
+            if (dfinite(q)) {
+                int64_t ci[3];
+                const int64_t c = dcell_of(s, (double)q.x, (double)q.y, (double)q.z, ci);
+                w = c >> 5;
+                b = 1u << (uint32_t)(c & 31);
+            }
+        }
+        unsigned long long todo = __ballot(w >= 0);
+        while (todo) {  // (uniform) one distinct word per round
+            const int lead = __ffsll((long long)todo) - 1;
+            const long long lw = __shfl(w, lead);
+            const bool in = w == lw;
+            uint32_t ob = in ? b : 0u;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) ob |= __shfl_xor(ob, off);
+            todo &= ~__ballot(in);
+            if (lane == lead) {
+                const uint32_t old = atomicOr(&bits[lw], ob);
+                mine += (uint32_t)__popc(ob & ~old);
+            }
+        }
     }
     unsigned long long v = mine;
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(count, v);
+    if (lane == 0 && v) atomicAdd(count, v);
 }
 
 template <typename T>
@@ -379,7 +436,7 @@ void launch_apply_radii(T* dists, int32_t* ids, const T* radii, int64_t N, int k
 }
 
 #define PMX_SETUP_INST(T)                                                                                            \
-    template void launch_pack_p4<T>(const T*, int, int64_t, int64_t, P4<T>*, hipStream_t);                          \
+    template void launch_pack_p4<T>(const T*, int, int64_t, int64_t, P4<T>*, hipStream_t, const T*);                \
     template void launch_pack_nrm<T>(const T*, int, int64_t, P4<T>*, hipStream_t);                                  \
     template void launch_bbox<T>(const P4<T>*, int64_t, double*, double*, hipStream_t);                             \
     template void launch_occupancy<T>(const P4<T>*, int64_t, const SetupShape&, uint32_t*, unsigned long long*,    \
