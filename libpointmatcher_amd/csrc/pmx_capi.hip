@@ -72,7 +72,8 @@ int coll_allreduce(pmx_ctx* c, void* dbuf, int64_t count, int type, int op) {
     return PMX_OK;
 }
 
-// all-gather `bytes` per rank: recv holds nranks blocks in rank order
+// all-gather `bytes` per rank: recv holds nranks blocks in rank order (send
+// may be this rank's block of recv: in place)
 int coll_allgather(pmx_ctx* c, const void* dsend, void* drecv, size_t bytes) {
     if (!sharded(c)) {
         if (drecv != dsend) HIPCHK(c, hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, c->stream));

@@ -508,7 +508,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // the segments are all-gathered and every rank picks from the union
         SpecSel* spec = c->spec_now();
         c->spec_exchanged = false;
-        unsigned long long* xseg = spec && sharded(c) ? c->d_specx : nullptr;
+        // (this rank's segment is its block of the gathered array: an in-place all-gather)
+        unsigned long long* xseg = spec && sharded(c) ? c->d_specx + (size_t)kSpecXStride * c->rank : nullptr;
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->d_vpart, c->merge_counter ? nullptr : c->d_visited,
@@ -518,11 +519,11 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
-            int rc = coll_allgather(c, xseg, xseg + kSpecXStride, kSpecXStride * sizeof(unsigned long long));
+            int rc = coll_allgather(c, xseg, c->d_specx, kSpecXStride * sizeof(unsigned long long));
             if (rc) return rc;
             const bool force = c->enq_iter >= 0 && std::find(c->debug_force_miss.begin(), c->debug_force_miss.end(),
                                                              c->enq_iter) != c->debug_force_miss.end();
-            launch_spec_pick<T>(xseg + kSpecXStride, c->nranks, spec, c->d_sel, loop_on_ctl(c), c->shard_async ? 1 : 0,
+            launch_spec_pick<T>(c->d_specx, c->nranks, spec, c->d_sel, loop_on_ctl(c), c->shard_async ? 1 : 0,
                                 force ? 1 : 0, c->stream);
             c->spec_exchanged = true;
         }

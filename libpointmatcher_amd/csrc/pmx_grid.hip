@@ -484,6 +484,24 @@ __global__ __launch_bounds__(kVSlots) void spec_pick_kernel(const unsigned long 
     SpecKeys<T> src;
     src.segs = segs;
     src.nseg = nseg;
+    // the union's keys into LDS once when they fit (every radix round of the
+    // pick reads them all; the segments are global memory)
+    using K = typename KeyOf<T>::K;
+    constexpr unsigned kPickLds = 4096;
+    __shared__ K lkeys[kPickLds];
+    if (!overflow && nk <= kPickLds && spec->valid) {
+        unsigned o = 0;
+        for (int s = 0; s < nseg; ++s) {  // (uniform)
+            const unsigned ns = src.n(s);
+            for (unsigned i = threadIdx.x; i < ns; i += kVSlots) lkeys[o + i] = (K)segs[(size_t)s * kSpecXStride + kSpecXHdr + i];
+            o += ns;
+        }
+        __syncthreads();
+        src = SpecKeys<T>();
+        src.local = lkeys;
+        src.n_local = o;
+        src.lds = lkeys;
+    }
     const bool hit = spec_pick<T, kVSlots>(spec, st, fin, below, nk, overflow, src, lh, part, bc);
     if (!hit && stall && ctl && threadIdx.x == 0) ctl->done = kCtlStalled;
 }
