@@ -666,8 +666,10 @@ struct LaneQ {
 // XCD-aware block order of the per-lane kernel (pmx_internal.h xcd_block:
 // adjacent slot ranges gather through one L2; match HBM traffic 75.3 -> 66.5
 // MB per launch at C3)
-template <typename T, int KT, int Q>
-__global__ __launch_bounds__(256, 4) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
+// OCC: waves per SIMD the register budget is cut for (launch bounds; 4 =
+// the natural fit; 5 / 6 spill in the full-search path — PMX_LANE_OCC)
+template <typename T, int KT, int Q, int OCC = 4>
+__global__ __launch_bounds__(256, OCC) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
@@ -802,6 +804,8 @@ __global__ __launch_bounds__(256, 4) void grid_lane_kernel(const P4<T>* __restri
 // ------------------------------------------------------------ tile kernel --
 #include "pmx_grid_tile.inc"
 
+int g_lane_occ = 4;  // (PMX_LANE_OCC, read at context creation)
+
 template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
@@ -815,9 +819,17 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
-        hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
-                           rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
-                           ctl, gd, spec, radii);
+#define PMX_LANE(OCC)                                                                                                 \
+    hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q, OCC>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G, \
+                       rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev, ctl,  \
+                       gd, spec, radii)
+        if (KT <= 2 && g_lane_occ == 5)
+            PMX_LANE(5);
+        else if (KT <= 2 && g_lane_occ == 6)
+            PMX_LANE(6);
+        else
+            PMX_LANE(4);
+#undef PMX_LANE
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
