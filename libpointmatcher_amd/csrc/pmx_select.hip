@@ -285,129 +285,52 @@ static unsigned grid_for(int64_t n) {
 // ============================================================ VarTrimmed ==
 // scratch layout (bytes, 256-aligned pieces):
 //   [hdr: 64 B]   int count, int err
-//   keysA[n], keysB[n]   sort ping-pong (K)
+//   keysA[n], keysB[n]   the keys, then sorted (K)
 //   cum[n]               sequential partial sums (T)
-//   counts[256 * tiles], offsets[256 * tiles]  (uint32)
+//   argmin partials      (kFrmsBlocks values + indices)
+//   hipcub's sort scratch, the partial sum's chunk tables
 // deno: host-computed table pow(id / points_nbr, lambda) in T (the same libm
 // call as the reference's Eigen pow, OutlierFiltersImpl.cpp:209)
-constexpr int kRsItems = 16;
-constexpr int kRsTile = 256 * kRsItems;
-
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static size_t rs_scan_temp_bytes(int64_t items) {
-    size_t tb = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)items);
-    return tb;
-}
 
 
-// the finite positive distances as keys (OutlierFiltersImpl.cpp:186-188), in
-// any order (sorted next).  One append atomic per block of kCmpPer * 256
-// distances: the compiler already merges a wave's same-address atomics, and
-// the wave-level appends (16 K at C3) serialised at one L2 address for 180 us.
-constexpr int kCmpPer = 16;
+// The finite positive distances (OutlierFiltersImpl.cpp:186-188) as sort
+// keys in place, every other distance as the all-ones key (sorted after every
+// finite positive float's bits); the count of the kept ones.  hipcub's radix
+// sort then orders all n keys — the kept ones first — in one call (it
+// replaced a four-pass LSD sort of the compacted keys: 4 x (count, scan,
+// scatter) launches).
 template <typename T>
-__global__ __launch_bounds__(256) void vt_compact_kernel(const T* __restrict__ d, int64_t n,
-                                                         typename KeyOf<T>::K* __restrict__ keys,
-                                                         int* __restrict__ count, const LoopCtl* __restrict__ ctl) {
+__global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, int64_t n,
+                                                      typename KeyOf<T>::K* __restrict__ keys, int* __restrict__ count,
+                                                      const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
+    using K = typename KO::K;
     __shared__ int wtot[4];
-    __shared__ int s_base;
     if (ctl && ctl->done) return;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kCmpPer;
-    T v[kCmpPer];
     int c = 0;
-#pragma unroll
-    for (int u = 0; u < kCmpPer; ++u) {
-        v[u] = i0 + u < n ? d[i0 + u] : (T)0;
-        c += (v[u] != (T)__builtin_huge_val() && v[u] > (T)0) ? 1 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const T v = d[i];
+        const bool keep = v != (T)__builtin_huge_val() && v > (T)0;
+        keys[i] = keep ? KO::key(v) : ~(K)0;
+        c += keep ? 1 : 0;
     }
-    int incl = c;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wtot[wave] = incl;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int tot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-        s_base = tot ? atomicAdd(count, tot) : 0;
+        const int tot = (wtot[0] + wtot[1]) + (wtot[2] + wtot[3]);
+        if (tot) atomicAdd(count, tot);
     }
-    __syncthreads();
-    int pos = s_base + incl - c;
-    for (int w = 0; w < wave; ++w) pos += wtot[w];
-#pragma unroll
-    for (int u = 0; u < kCmpPer; ++u)
-        if (v[u] != (T)__builtin_huge_val() && v[u] > (T)0) keys[pos++] = KO::key(v[u]);
 }
-
 template <typename K>
-__global__ __launch_bounds__(256) void rs_count_kernel(const K* __restrict__ keys, const int* __restrict__ count,
-                                                       int shift, int tiles, uint32_t* __restrict__ counts,
-                                                       const LoopCtl* __restrict__ ctl) {
-    __shared__ uint32_t lc[256];
-    if (ctl && ctl->done) return;
-    lc[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t c = *count;
-    const int64_t base = (int64_t)blockIdx.x * kRsTile;
-    for (int it = 0; it < kRsItems; ++it) {
-        const int64_t i = base + it * 256 + threadIdx.x;
-        if (i < c) atomicAdd(&lc[(uint32_t)(keys[i] >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    counts[(int64_t)threadIdx.x * tiles + blockIdx.x] = lc[threadIdx.x];
-}
-
-// stable scatter: keys of a tile are ranked in index order (round-major,
-// then lane) with wave ballots; per-digit running offsets live in LDS
-template <typename K>
-__global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ in, K* __restrict__ out,
-                                                         const int* __restrict__ count, int shift, int tiles,
-                                                         const uint32_t* __restrict__ offsets,
-                                                         const LoopCtl* __restrict__ ctl) {
-    __shared__ uint32_t run[256];
-    if (ctl && ctl->done) return;
-    __shared__ uint32_t wcnt[4][256];
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wave = t >> 6;
-    run[t] = offsets[(int64_t)t * tiles + blockIdx.x];
-    for (int w = 0; w < 4; ++w) wcnt[w][t] = 0;
-    __syncthreads();
-    const int64_t c = *count;
-    const int64_t base = (int64_t)blockIdx.x * kRsTile;
-    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int it = 0; it < kRsItems; ++it) {
-        const int64_t i = base + it * 256 + t;
-        const bool valid = i < c;
-        K key = valid ? in[i] : (K)0;
-        const uint32_t dg = (uint32_t)(key >> shift) & 255u;
-        unsigned long long peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const unsigned long long bb = __ballot(valid && ((dg >> b) & 1u));
-            peers &= ((dg >> b) & 1u) ? bb : ~bb;
-        }
-        const int rank = __popcll(peers & lt);
-        if (valid && rank == 0) wcnt[wave][dg] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = run[dg] + (uint32_t)rank;
-            for (int w = 0; w < wave; ++w) pos += wcnt[w][dg];
-            out[pos] = key;
-        }
-        __syncthreads();
-        run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-        wcnt[0][t] = 0;
-        wcnt[1][t] = 0;
-        wcnt[2][t] = 0;
-        wcnt[3][t] = 0;
-        __syncthreads();
-    }
+static size_t vt_sort_temp_bytes(int64_t n) {
+    size_t t = 0;
+    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, t, (const K*)nullptr, (K*)nullptr, (int)std::max<int64_t>(n, 1),
+                                            0, (int)(8 * sizeof(K)));
+    return t;
 }
 
 // std::partial_sum in T with the sequential rounding, computed in parallel.
@@ -507,10 +430,9 @@ static int64_t vt_chunks(int64_t n) { return n > kCumHead ? (n - kCumHead + kCum
 template <typename T>
 size_t vartrim_scratch_bytes(int64_t n) {
     using K = typename KeyOf<T>::K;
-    const int64_t tiles = (n + kRsTile - 1) / kRsTile + 1;
     const int64_t nch = vt_chunks(n);
-    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(4 * 256 * tiles) +
-           al256(rs_scan_temp_bytes(256 * tiles)) + al256(sizeof(VtChunk) * (nch + 1)) +
+    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(8 * 256) +
+           al256(vt_sort_temp_bytes<K>(n)) + al256(sizeof(VtChunk) * (nch + 1)) +
            al256((size_t)kFastTies * nch * (2 * sizeof(int) + 2 * sizeof(long long)));
 }
 
@@ -1043,13 +965,13 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     p += al256(sizeof(K) * n);
     T* cum = reinterpret_cast<T*>(p);
     p += al256(sizeof(T) * n);
-    const int64_t tiles = (n + kRsTile - 1) / kRsTile + 1;
-    uint32_t* counts = reinterpret_cast<uint32_t*>(p);
-    p += al256(4 * 256 * tiles);
-    uint32_t* offsets = reinterpret_cast<uint32_t*>(p);
-    p += al256(4 * 256 * tiles);
-    void* scan_temp = p;  // hipcub's scan scratch (the digit counts' exclusive scan)
-    p += al256(rs_scan_temp_bytes(256 * tiles));
+    T* part_v = reinterpret_cast<T*>(p);  // (the FRMS argmin's block partials)
+    p += al256(8 * 256);
+    int* part_i = reinterpret_cast<int*>(p);
+    p += al256(8 * 256);
+    void* sort_temp = p;  // hipcub's radix sort scratch
+    const size_t sort_tb = vt_sort_temp_bytes<K>(n);
+    p += al256(sort_tb);
     const int64_t nch = vt_chunks(n);
     VtChunk* ch = reinterpret_cast<VtChunk*>(p);
     p += al256(sizeof(VtChunk) * (nch + 1));
@@ -1059,22 +981,11 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     int* t_c = t_idx + kFastTies * nch;
 
     (void)hipMemsetAsync(hdr, 0, 256, s);
-    if (n > 0)
-        hipLaunchKernelGGL(vt_compact_kernel<T>, dim3((unsigned)((n + 256 * kCmpPer - 1) / (256 * kCmpPer))), dim3(256), 0,
-                           s, d, n, keysA, hdr, ctl);
-    const int key_bits = KeyOf<T>::bits;
-    K* src = keysA;
-    K* dst = keysB;
-    for (int shift = 0; shift < key_bits; shift += 8) {
-        hipLaunchKernelGGL(rs_count_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, hdr, shift, (int)tiles,
-                           counts, ctl);
-        size_t tb = rs_scan_temp_bytes(256 * tiles);
-        (void)hipcub::DeviceScan::ExclusiveSum(scan_temp, tb, counts, offsets, (int)(256 * tiles), s);
-        hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3((unsigned)tiles), dim3(256), 0, s, src, dst, hdr, shift,
-                           (int)tiles, offsets, ctl);
-        K* tmp = src;
-        src = dst;
-        dst = tmp;
+    K* src = keysB;  // (the sorted keys: the kept ones first)
+    if (n > 0) {
+        hipLaunchKernelGGL(vt_keys_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl);
+        size_t tb = sort_tb;
+        (void)hipcub::DeviceRadixSort::SortKeys(sort_temp, tb, keysA, keysB, (int)n, 0, KeyOf<T>::bits, s);
     }
     if (nch > 0) {
         hipLaunchKernelGGL(vt_chunk_sum_kernel<T>, dim3((unsigned)(nch + 1)), dim3(kCumThreads), 0, s, src, hdr, ch, ctl);
@@ -1088,9 +999,6 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
                            t_c, cum, ctl);
     const int minEl = (int)std::floor(minRatio * (T)points_nbr);
     const int maxEl = (int)std::floor(maxRatio * (T)points_nbr);
-    // (the radix sort's count / offset scratch, >= 2 KB each, holds the argmin partials)
-    T* part_v = reinterpret_cast<T*>(counts);
-    int* part_i = reinterpret_cast<int*>(offsets);
     hipLaunchKernelGGL(vt_frms_part_kernel<T>, dim3(kFrmsBlocks), dim3(256), 0, s, cum, hdr, deno, minEl, maxEl, part_v,
                        part_i, ctl);
     hipLaunchKernelGGL(vt_frms_final_kernel<T>, dim3(1), dim3(256), 0, s, part_v, part_i, hdr, minEl, maxEl,
