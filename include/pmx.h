@@ -221,6 +221,11 @@ int pmx_p2point_system(pmx_ctx* ctx, double* mean_p, double* mean_q, double* m, 
 /* dists: k x N T (point-major), ids: k x N int32 (this rank's shard) */
 int pmx_get_matches(pmx_ctx* ctx, void* dists, int32_t* ids);
 int pmx_get_weights(pmx_ctx* ctx, void* w);
+/* The last VarTrimmedDist filter's partial sums (OutlierFiltersImpl.cpp:
+ * 196-198: std::partial_sum in T over the sorted finite positive distances):
+ * *count of them, copied into out when out != NULL and capacity suffices.
+ * Diagnostic (the sequential rounding the device reproduces in parallel). */
+int pmx_vartrim_partial_sums(pmx_ctx* ctx, void* out, int64_t capacity, int64_t* count);
 /* shape of the current match arrays */
 int pmx_get_shape(const pmx_ctx* ctx, int64_t* n_local, int* knn);
 

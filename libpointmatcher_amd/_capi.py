@@ -153,7 +153,7 @@ EXPORTS = [
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed", "pmx_outlier_robust",
     "pmx_robust_scale", "pmx_set_reading_radii",
-    "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights",
+    "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights", "pmx_vartrim_partial_sums",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
     "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_surface_normals",
     "pmx_sampling_surface_normals", "pmx_voxel_grid",
@@ -197,6 +197,7 @@ def lib():
                                          C.POINTER(Stats)]
         l.pmx_get_matches.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         l.pmx_get_weights.argtypes = [C.c_void_p, C.c_void_p]
+        l.pmx_vartrim_partial_sums.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
         l.pmx_get_shape.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
         l.pmx_timing_enable.argtypes = [C.c_void_p, C.c_int]
         l.pmx_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
@@ -494,6 +495,14 @@ class Context:
         w = np.empty((self.N, self.knn), self.dtype)
         self._chk(self._l.pmx_get_weights(self.h, _ptr(w)))
         return w
+
+    def vartrim_partial_sums(self):
+        """The last VarTrimmedDist filter's partial sums (diagnostic)."""
+        n = C.c_int64(0)
+        self._chk(self._l.pmx_vartrim_partial_sums(self.h, None, 0, C.byref(n)))
+        out = np.empty(n.value, self.dtype)
+        self._chk(self._l.pmx_vartrim_partial_sums(self.h, _ptr(out), out.size, C.byref(n)))
+        return out
 
     # --- timing
     def timing(self, on=True):

@@ -803,6 +803,7 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
         }
         const size_t need = vartrim_scratch_bytes<T>(nsrc);
         if ((rc = ensure(c, &c->d_vt, &c->vt_bytes, need))) return rc;
+        c->vt_n = nsrc;
         launch_vartrim<T>(dsrc, nsrc, points_nbr, minR, maxR, (const T*)c->d_deno, c->d_vt, c->vt_bytes, c->d_ratio,
                           c->d_iter_err, loop_ctl(c), c->stream);
         HIPCHK(c, hipGetLastError());
@@ -1244,6 +1245,25 @@ int pmx_robust_scale(pmx_ctx* c, int pos, double* scale) {
     if (!c || !scale) return fail(c, PMX_E_BAD_PARAM, "null argument");
     return DISPATCH(c, robust_scale_impl<float>(c, pos, scale), robust_scale_impl<double>(c, pos, scale));
 }
+int pmx_vartrim_partial_sums(pmx_ctx* c, void* out, int64_t capacity, int64_t* count) {
+    if (!c || !count) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    if (c->vt_n < 0 || !c->d_vt) return fail(c, PMX_E_STATE, "no VarTrimmedDist filter has run");
+    // scratch layout of launch_vartrim: the 256-byte header (count), two key
+    // arrays, then the partial sums
+    const size_t ksz = c->dtype == PMX_F64 ? 8 : 4;
+    const auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    int cnt = 0;
+    HIPCHK(c, hipMemcpyAsync(&cnt, c->d_vt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *count = cnt;
+    if (!out) return PMX_OK;
+    if (capacity < cnt) return fail(c, PMX_E_BAD_PARAM, "capacity below the partial-sum count");
+    const char* cum = (const char*)c->d_vt + 256 + 2 * al(ksz * (size_t)c->vt_n);
+    HIPCHK(c, hipMemcpyAsync(out, cum, ksz * (size_t)cnt, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PMX_OK;
+}
+
 int pmx_get_weights(pmx_ctx* c, void* w) {
     if (!c || !w) return fail(c, PMX_E_BAD_PARAM, "null argument");
     return DISPATCH(c, get_weights_impl<float>(c, w), get_weights_impl<double>(c, w));

@@ -187,6 +187,7 @@ struct pmx_ctx {
     // VarTrimmed scratch + cached pow table
     void* d_vt = nullptr;
     size_t vt_bytes = 0;
+    int64_t vt_n = -1;  // distances the last VarTrimmed launch sorted (its scratch layout; -1: none)
     void* d_deno = nullptr;
     size_t deno_bytes = 0;
     int deno_pts = -1, deno_min = -1, deno_max = -1;

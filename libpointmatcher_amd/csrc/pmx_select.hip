@@ -402,27 +402,51 @@ __device__ __forceinline__ long long cum_block_scan(long long v, long long lim, 
 
 // The head (the first kCumHead keys, where the running sum leaves its binade
 // every few keys) is summed sequentially; the rest is cut into chunks of
-// kCumChunk keys.  A chunk that starts and ends in one binade with few ties
-// is the fast case: given its start sum S0 (exact), its sums are S0 + P_j +
-// C_j with P_j independent of S0, so vt_chunk_prep_kernel computes P for
-// every chunk in parallel under the binade GUESSED from a double prefix of
-// the chunk sums, vt_cumsum_kernel walks the chunks in order with the exact
-// running sum (a fast chunk: the guess checked, its ties resolved by one
-// thread, its end sum in O(ties); any other chunk: the passes below, which
-// write its sums), and vt_chunk_write_kernel writes the fast chunks' sums in
-// parallel.  A wrong guess only sends a chunk to the passes.
+// kCumChunk keys.  vt_chunk_prep_kernel prepares every chunk in parallel
+// under the binade e GUESSED from a double prefix of the chunk sums, and under
+// e + 1: the integer prefixes P_e[j], P_e+1[j] of rnd(x / u) (stored), the
+// ties of both binades, and for binade e the ties' rounding already resolved
+// for an even and for an odd start: the parity of S0 / u decides every tie of
+// the chunk (the units before tie k are S0 + pb_k + up_k-1, so their parity
+// is that of S0 plus integers known beforehand).  vt_cumsum_kernel then walks
+// the chunks in order with the exact running sum S:
+//   fast   S in binade e, S / u + P_e + C_e[parity] < 2^P: the chunk's end
+//          sum in O(1) from the chunk table (preloaded in LDS);
+//   cross  the sum leaves binade e inside the chunk: the crossing step (the
+//          first j whose units reach 2^P, found by the whole block over the
+//          stored P_e) is a plain T addition, and when it lands in binade
+//          e + 1 and the rest of the chunk stays there, the rest's sums are
+//          the e + 1 prefix from there (its few ties resolved in order);
+//   slow   anything else (a wrong guess, many ties, two crossings, a
+//          subnormal sum): the passes below, which write the chunk's sums.
+// vt_chunk_write_kernel writes the fast and crossing chunks' sums in
+// parallel.  Every path computes the sequential loop's bits.
 constexpr int kCumChunk = kCumThreads * kCumPer;
 constexpr int kCumHead = 4096;
 constexpr int kFastTies = 256;
+constexpr int kChunkLds = 512;  // chunk-table entries the walk preloads into LDS
 
 struct VtChunk {
-    double sum;   // double sum of the chunk's keys (the guess)
-    long long P;  // integer prefix total under the guessed binade (saturated)
-    double S0;    // exact start sum (T value), fast chunks
-    int e;        // guessed binade
-    int nt;       // ties (kFastTies + 1: too many)
-    int ok;       // 1: a fast chunk (vt_chunk_write_kernel writes it)
-    int pad;
+    double sum;       // double sum of the chunk's keys (the guess)
+    long long P[2];   // integer totals under binades e and e + 1
+    long long C[2];   // binade e: ties rounded up over the chunk, for an even / odd start
+    double S0;        // exact start sum (T value): fast and crossing chunks
+    double S1;        // crossing: the sum after the crossing step
+    int e;            // guessed binade
+    int nt[2];        // ties under e, e + 1 (kFastTies + 1: too many)
+    int ok;           // 0: the passes wrote it; 1 fast; 2 crossing
+    int par;          // parity of S0 / u
+    int jc;           // crossing: chunk-local index of the crossing step
+};
+
+// the per-chunk arrays of the prepared chunks (launch_vartrim lays them out)
+struct VtPrep {
+    long long* P[2];  // inclusive prefixes, index j - kCumHead
+    int* t_idx[2];    // ties: chunk-local index, by chunk (kFastTies each)
+    long long* t_m[2];
+    long long* t_pb[2];  // prefix before the tie (ties counted as m)
+    int* t_c0[2];        // binade e: rounded-up ties up to and including tie k, even / odd start
+    int* t_c1;           // binade e + 1: the same after a crossing (written by the walk)
 };
 
 static int64_t vt_chunks(int64_t n) { return n > kCumHead ? (n - kCumHead + kCumChunk - 1) / kCumChunk : 0; }
@@ -432,8 +456,8 @@ size_t vartrim_scratch_bytes(int64_t n) {
     using K = typename KeyOf<T>::K;
     const int64_t nch = vt_chunks(n);
     return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(8 * 256) +
-           al256(vt_sort_temp_bytes<K>(n)) + al256(sizeof(VtChunk) * (nch + 1)) +
-           al256((size_t)kFastTies * nch * (2 * sizeof(int) + 2 * sizeof(long long)));
+           al256(vt_sort_temp_bytes<K>(n)) + al256(sizeof(VtChunk) * (nch + 1)) + 2 * al256(8 * (size_t)n) +
+           al256((size_t)kFastTies * nch * (4 * sizeof(long long) + 5 * sizeof(int)));
 }
 
 // this thread's kCumPer keys from j0 (16-byte loads when in range)
@@ -514,19 +538,41 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_sum_kernel(const typenam
     }
 }
 
-// per chunk: the guessed binade, the integer total and the ties under it
+// exclusive scan of int64 values over the block (no saturation: the chunk
+// totals stay below 2^38); wsum: kCumThreads / 64 entries
+__device__ __forceinline__ long long block_excl_scan_ll(long long v, long long* wsum, long long& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    long long incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const long long u = __shfl_up(incl, off);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    long long before = 0;
+    total = 0;
+    for (int w = 0; w < kCumThreads / 64; ++w) {
+        before += w < wave ? wsum[w] : 0ll;
+        total += wsum[w];
+    }
+    __syncthreads();
+    return before + (incl - v);
+}
+
+// per chunk: the guessed binade e; under e and e + 1 the inclusive prefixes,
+// the totals and the ties; binade e's ties resolved for both start parities
 template <typename T>
 __global__ __launch_bounds__(kCumThreads) void vt_chunk_prep_kernel(const typename KeyOf<T>::K* __restrict__ keys,
                                                                     const int* __restrict__ count,
-                                                                    VtChunk* __restrict__ ch, int* __restrict__ t_idx,
-                                                                    long long* __restrict__ t_pb,
-                                                                    long long* __restrict__ t_m,
+                                                                    VtChunk* __restrict__ ch, VtPrep pr,
                                                                     const LoopCtl* __restrict__ ctl) {
     using K = typename KeyOf<T>::K;
     constexpr int P = CumBits<T>::P;
-    constexpr long long LIM = 1ll << P;
     __shared__ long long wsum[kCumThreads / 64];
     __shared__ double s_approx;
+    __shared__ int l_idx[kFastTies];
+    __shared__ long long l_pb[kFastTies], l_m[kFastTies];
     if (ctl && ctl->done) return;
     const int64_t c = *count;
     const int b = blockIdx.x, t = threadIdx.x;
@@ -540,54 +586,74 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_prep_kernel(const typena
     }
     __syncthreads();
     const int e = CumBits<T>::binade((T)s_approx);
-    const double inv_u = ldexp(1.0, P - 1 - e);
     const int64_t j0 = lo + (int64_t)t * kCumPer;
     K kv[kCumPer];
     vt_load<T>(keys, c, j0, kv);
-    long long r[kCumPer];
-    bool tie[kCumPer];
-    int ntie;
-    const long long loc = vt_round<T>(kv, j0, lo, hi, inv_u, r, tie, ntie);
-    long long tot, tt;
-    const long long base = cum_block_scan(loc, LIM, wsum, tot);
-    const long long tbase = cum_block_scan((long long)ntie, LIM, wsum, tt);
-    if (tt <= kFastTies) {
-        long long run = base;
-        int k = b * kFastTies + (int)tbase;
+    for (int v = 0; v < 2; ++v) {  // (uniform) binade e, then e + 1
+        const double inv_u = ldexp(1.0, P - 1 - (e + v));
+        long long r[kCumPer];
+        bool tie[kCumPer];
+        int ntie;
+        (void)vt_round<T>(kv, j0, lo, hi, inv_u, r, tie, ntie);
+        long long loc = 0;  // (exact: each r <= 2^P)
+#pragma unroll
+        for (int i = 0; i < kCumPer; ++i) loc += r[i];
+        long long tot, tt;
+        long long run = block_excl_scan_ll(loc, wsum, tot);
+        const long long tbase = block_excl_scan_ll((long long)ntie, wsum, tt);
+        int k = (int)tbase;
 #pragma unroll
         for (int i = 0; i < kCumPer; ++i) {
-            if (tie[i]) {
-                t_idx[k] = t * kCumPer + i;
-                t_pb[k] = run;
-                t_m[k] = r[i];
+            if (tie[i] && tt <= kFastTies) {
+                l_idx[k] = t * kCumPer + i;
+                l_pb[k] = run;
+                l_m[k] = r[i];
                 ++k;
             }
-            run = sat_add(run, r[i], LIM);
+            run += r[i];
+            const int64_t j = j0 + i;
+            if (j < hi) pr.P[v][j - kCumHead] = run;
         }
+        __syncthreads();
+        const int nt = tt <= kFastTies ? (int)tt : kFastTies + 1;
+        if (nt <= kFastTies) {
+            for (int q = t; q < nt; q += kCumThreads) {
+                pr.t_idx[v][b * kFastTies + q] = l_idx[q];
+                pr.t_pb[v][b * kFastTies + q] = l_pb[q];
+                pr.t_m[v][b * kFastTies + q] = l_m[q];
+            }
+            if (v == 0 && t < 2) {  // binade e: every tie's rounding for an even (t = 0) / odd (t = 1) start
+                int up = 0;
+                for (int q = 0; q < nt; ++q) {
+                    up += ((t + l_pb[q] + up + l_m[q]) & 1ll) ? 1 : 0;
+                    pr.t_c0[t][b * kFastTies + q] = up;
+                }
+                ch[b + 1].C[t] = up;
+            }
+        }
+        if (t == 0) {
+            ch[b + 1].P[v] = tot;
+            ch[b + 1].nt[v] = nt;
+        }
+        __syncthreads();  // (the LDS tie list is rewritten for e + 1)
     }
     if (t == 0) {
-        VtChunk& q = ch[b + 1];
-        q.P = tot;
-        q.e = e;
-        q.nt = tt <= kFastTies ? (int)tt : kFastTies + 1;
-        q.ok = 0;
+        ch[b + 1].e = e;
+        ch[b + 1].ok = 0;
     }
 }
 
-// the fast chunks' sums: S0 + P_j + C_j in units of the chunk's binade
+// the fast and crossing chunks' sums: S0 + P_j + C_j in units of binade e,
+// then after a crossing S1 + (P'_j - P'_jc) + C'_j in units of binade e + 1
 template <typename T>
 __global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typename KeyOf<T>::K* __restrict__ keys,
                                                                      const int* __restrict__ count,
-                                                                     const VtChunk* __restrict__ ch,
-                                                                     const int* __restrict__ t_idx,
-                                                                     const int* __restrict__ t_c, T* __restrict__ cum,
+                                                                     const VtChunk* __restrict__ ch, VtPrep pr,
+                                                                     T* __restrict__ cum,
                                                                      const LoopCtl* __restrict__ ctl) {
-    using K = typename KeyOf<T>::K;
     constexpr int P = CumBits<T>::P;
-    constexpr long long LIM = 1ll << P;
-    __shared__ long long wsum[kCumThreads / 64];
-    __shared__ int l_idx[kFastTies];
-    __shared__ int l_c[kFastTies];
+    __shared__ int l_idx[kFastTies], l_c[kFastTies];
+    __shared__ int l1_idx[kFastTies], l1_c[kFastTies];
     if (ctl && ctl->done) return;
     const int64_t c = *count;
     const int b = blockIdx.x, t = threadIdx.x;
@@ -596,49 +662,55 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typen
     const VtChunk q = ch[b + 1];
     if (!q.ok) return;  // (uniform: the passes wrote this chunk)
     const int64_t hi = lo + kCumChunk < c ? lo + kCumChunk : c;
-    const int nt = q.nt;
-    for (int k = t; k < nt; k += kCumThreads) {
-        l_idx[k] = t_idx[b * kFastTies + k];
-        l_c[k] = t_c[b * kFastTies + k];
+    const int nt0 = q.nt[0], nt1 = q.ok == 2 ? q.nt[1] : 0, jc = q.ok == 2 ? q.jc : 0x7fffffff;
+    for (int k = t; k < nt0; k += kCumThreads) {
+        l_idx[k] = pr.t_idx[0][b * kFastTies + k];
+        l_c[k] = pr.t_c0[q.par][b * kFastTies + k];
     }
-    const double inv_u = ldexp(1.0, P - 1 - q.e), u = ldexp(1.0, q.e - (P - 1));
-    const long long S0 = CumBits<T>::units((T)q.S0);
-    const int64_t j0 = lo + (int64_t)t * kCumPer;
-    K kv[kCumPer];
-    vt_load<T>(keys, c, j0, kv);
-    long long r[kCumPer];
-    bool tie[kCumPer];
-    int ntie;
-    const long long loc = vt_round<T>(kv, j0, lo, hi, inv_u, r, tie, ntie);
-    long long tot;
-    long long run = cum_block_scan(loc, LIM, wsum, tot);  // (its barriers also publish l_idx / l_c)
-    int kt = 0;
-    {
-        int lo2 = 0, hi2 = nt;  // first tie at a local index >= t * kCumPer
+    for (int k = t; k < nt1; k += kCumThreads) {
+        l1_idx[k] = pr.t_idx[1][b * kFastTies + k];
+        l1_c[k] = l1_idx[k] > jc ? pr.t_c1[b * kFastTies + k] : 0;
+    }
+    __syncthreads();
+    const double u0 = ldexp(1.0, q.e - (P - 1)), u1 = ldexp(1.0, q.e + 1 - (P - 1));
+    const long long U0 = CumBits<T>::units((T)q.S0);
+    const long long U1 = q.ok == 2 ? CumBits<T>::units((T)q.S1) : 0;
+    const long long P1jc = q.ok == 2 ? pr.P[1][lo + jc - kCumHead] : 0;
+    // the ties at local indices below this thread's first key
+    auto first_at = [&](const int* idx, int n) {
+        int lo2 = 0, hi2 = n;
         while (lo2 < hi2) {
             const int mid = (lo2 + hi2) >> 1;
-            if (l_idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
+            if (idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
         }
-        kt = lo2;
-    }
+        return lo2;
+    };
+    int kt0 = first_at(l_idx, nt0), kt1 = first_at(l1_idx, nt1);
 #pragma unroll
     for (int i = 0; i < kCumPer; ++i) {
-        run = sat_add(run, r[i], LIM);
-        if (kt < nt && l_idx[kt] == t * kCumPer + i) ++kt;
-        const long long C = kt > 0 ? (long long)l_c[kt - 1] : 0ll;
-        const int64_t j = j0 + i;
-        if (j < hi) cum[j] = (T)((double)(S0 + run + C) * u);
+        const int li = t * kCumPer + i;
+        const int64_t j = lo + li;
+        if (kt0 < nt0 && l_idx[kt0] == li) ++kt0;
+        if (kt1 < nt1 && l1_idx[kt1] == li) ++kt1;
+        if (j >= hi) continue;
+        T v;
+        if (li < jc) {
+            const long long C = kt0 > 0 ? (long long)l_c[kt0 - 1] : 0ll;
+            v = (T)((double)(U0 + pr.P[0][j - kCumHead] + C) * u0);
+        } else if (li == jc) {
+            v = (T)q.S1;
+        } else {
+            const long long C = kt1 > 0 ? (long long)l1_c[kt1 - 1] : 0ll;  // (0 for ties at or before jc)
+            v = (T)((double)(U1 + (pr.P[1][j - kCumHead] - P1jc) + C) * u1);
+        }
+        cum[j] = v;
     }
 }
 
 template <typename T>
 __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
                                                                 const int* __restrict__ count, T* __restrict__ cum,
-                                                                VtChunk* __restrict__ ch,
-                                                                const int* __restrict__ t_idx,
-                                                                const long long* __restrict__ t_pb,
-                                                                const long long* __restrict__ t_m,
-                                                                int* __restrict__ t_c,
+                                                                VtChunk* __restrict__ ch, VtPrep pr, int nch,
                                                                 const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
     constexpr int P = CumBits<T>::P;
@@ -650,12 +722,27 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     __shared__ long long tie_m[kCumMaxTies];
     __shared__ int tie_c[kCumMaxTies];          // rounded-up ties up to and including this one
     __shared__ int s_cross;
-    __shared__ int s_fast;
+    __shared__ int s_mode;
+    __shared__ long long s_U0;
+    __shared__ int s_par;
     __shared__ T s_run;                         // the running sum after the chunk
+    // the chunk table of the fast test (the walk's per-chunk decision then
+    // reads no global memory)
+    __shared__ long long c_P0[kChunkLds], c_C[2][kChunkLds];
+    __shared__ int c_e[kChunkLds], c_nt0[kChunkLds];
     if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     const int64_t c = *count;
     if (c <= 0) return;
+    const int nchl = nch < kChunkLds ? nch : kChunkLds;
+    for (int i = t; i < nchl; i += kCumThreads) {
+        const VtChunk& q = ch[i + 1];
+        c_P0[i] = q.P[0];
+        c_C[0][i] = q.C[0];
+        c_C[1][i] = q.C[1];
+        c_e[i] = q.e;
+        c_nt0[i] = q.nt[0];
+    }
     // the head sequentially (keys staged in LDS by the whole block: the one
     // summing thread then waits on no global load)
     __shared__ typename KO::K s_head[kCumHead];
@@ -677,46 +764,118 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     __syncthreads();
     for (int64_t lo = ph, b = 0; lo < c; lo += kCumChunk, ++b) {  // (uniform)
         const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
-        {  // the chunk's ties into LDS (the deciding thread then reads no global memory)
-            const int ntq = ch[b + 1].nt;
-            if (ntq <= kFastTies)
-                for (int k = t; k < ntq; k += kCumThreads) {
-                    tie_pb[k] = t_pb[b * kFastTies + k];
-                    tie_m[k] = t_m[b * kFastTies + k];
-                }
-            __syncthreads();
-        }
         if (t == 0) {
-            // a fast chunk: the guessed binade is the running sum's, few ties,
-            // and the chunk's last sum stays below the next binade
-            VtChunk& q = ch[b + 1];
+            // 1 fast: the guessed binade is the running sum's, few ties, and
+            // the chunk's last sum stays below the next binade (O(1): the
+            // ties were resolved for both parities of the start);
+            // 2 a crossing to examine; 0 the passes
+            const bool inl = b < kChunkLds;
+            const int e = inl ? c_e[b] : ch[b + 1].e;
+            const int nt0 = inl ? c_nt0[b] : ch[b + 1].nt[0];
+            int mode = 0;
             // (s normal: units() adds the hidden bit)
-            int fast = q.nt <= kFastTies && s >= CumBits<T>::min_normal() && CumBits<T>::binade(s) == q.e &&
-                       q.P < LIM;
-            if (fast) {
-                const long long S0 = CumBits<T>::units(s);
-                int up = 0;
-                for (int k = 0; k < q.nt; ++k) {
-                    const long long before = S0 + tie_pb[k] + up;
-                    up += ((before + tie_m[k]) & 1ll) ? 1 : 0;
-                    t_c[b * kFastTies + k] = up;
-                }
-                const long long fin = S0 + q.P + up;
+            if (nt0 <= kFastTies && s >= CumBits<T>::min_normal() && CumBits<T>::binade(s) == e) {
+                const long long U0 = CumBits<T>::units(s);
+                const int par = (int)(U0 & 1ll);
+                const long long fin = U0 + (inl ? c_P0[b] : ch[b + 1].P[0]) + (inl ? c_C[par][b] : ch[b + 1].C[par]);
+                VtChunk& q = ch[b + 1];
                 if (fin < LIM) {
                     q.S0 = (double)s;
+                    q.par = par;
                     q.ok = 1;
-                    s_run = (T)((double)fin * ldexp(1.0, q.e - (P - 1)));
-                } else {
-                    fast = 0;
+                    s_run = (T)((double)fin * ldexp(1.0, e - (P - 1)));
+                    mode = 1;
+                } else if (q.nt[1] <= kFastTies) {
+                    s_U0 = U0;
+                    s_par = par;
+                    mode = 2;
                 }
             }
-            s_fast = fast;
+            s_mode = mode;
+            s_cross = 0x7fffffff;
         }
         __syncthreads();
-        if (s_fast) {
+        if (s_mode == 1) {
             s = s_run;
             __syncthreads();
             continue;
+        }
+        if (s_mode == 2) {
+            // the first step whose units reach 2^P: every thread over its
+            // keys' stored prefix, with the ties' rounding for this start
+            const long long U0 = s_U0;
+            const int par = s_par;
+            const int nt0 = ch[b + 1].nt[0];
+            for (int k = t; k < nt0; k += kCumThreads) {
+                tie_idx[k] = pr.t_idx[0][b * kFastTies + k];
+                tie_c[k] = pr.t_c0[par][b * kFastTies + k];
+            }
+            __syncthreads();
+            int kt = 0;
+            {
+                int lo2 = 0, hi2 = nt0;  // first tie at a local index >= t * kCumPer
+                while (lo2 < hi2) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (tie_idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
+                }
+                kt = lo2;
+            }
+            int first = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                const int li = t * kCumPer + i;
+                if (kt < nt0 && tie_idx[kt] == li) ++kt;
+                const int64_t j = lo + li;
+                if (j >= cend || first != 0x7fffffff) continue;
+                const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
+                if (U0 + pr.P[0][j - kCumHead] + C >= LIM) first = li;
+            }
+            if (first != 0x7fffffff) atomicMin(&s_cross, first);
+            __syncthreads();
+            if (t == 0) {
+                VtChunk& q = ch[b + 1];
+                const int jc = s_cross;  // (exists: the chunk's last sum reaches 2^P)
+                const int e = q.e;
+                T before = s;
+                if (jc > 0) {
+                    int n0 = 0;  // ties at local indices <= jc - 1
+                    while (n0 < nt0 && tie_idx[n0] <= jc - 1) ++n0;
+                    const long long C = n0 > 0 ? (long long)tie_c[n0 - 1] : 0ll;
+                    before = (T)((double)(U0 + pr.P[0][lo + jc - 1 - kCumHead] + C) * ldexp(1.0, e - (P - 1)));
+                }
+                const T S1 = before + KO::val(keys[lo + jc]);  // the crossing step, in T
+                int mode = 0;
+                if (S1 >= CumBits<T>::min_normal() && CumBits<T>::binade(S1) == e + 1) {
+                    // the rest of the chunk in binade e + 1: its ties in order
+                    const long long U1 = CumBits<T>::units(S1);
+                    const long long P1jc = pr.P[1][lo + jc - kCumHead];
+                    const int nt1 = q.nt[1];
+                    int up = 0;
+                    for (int k = 0; k < nt1; ++k) {
+                        if (pr.t_idx[1][b * kFastTies + k] <= jc) continue;
+                        const long long bf = U1 + (pr.t_pb[1][b * kFastTies + k] - P1jc) + up;
+                        up += ((bf + pr.t_m[1][b * kFastTies + k]) & 1ll) ? 1 : 0;
+                        pr.t_c1[b * kFastTies + k] = up;
+                    }
+                    const long long fin = U1 + (q.P[1] - P1jc) + up;
+                    if (fin < LIM) {
+                        q.S0 = (double)s;
+                        q.par = par;
+                        q.jc = jc;
+                        q.S1 = (double)S1;
+                        q.ok = 2;
+                        s_run = (T)((double)fin * ldexp(1.0, e + 1 - (P - 1)));
+                        mode = 3;
+                    }
+                }
+                s_mode = mode;
+            }
+            __syncthreads();
+            if (s_mode == 3) {
+                s = s_run;
+                __syncthreads();
+                continue;
+            }
         }
         int64_t p = lo;
         while (p < cend) {  // (uniform) passes over [p, cend)
@@ -975,10 +1134,25 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     const int64_t nch = vt_chunks(n);
     VtChunk* ch = reinterpret_cast<VtChunk*>(p);
     p += al256(sizeof(VtChunk) * (nch + 1));
-    long long* t_pb = reinterpret_cast<long long*>(p);
-    long long* t_m = t_pb + kFastTies * nch;
-    int* t_idx = reinterpret_cast<int*>(t_m + kFastTies * nch);
-    int* t_c = t_idx + kFastTies * nch;
+    VtPrep pr;
+    for (int v = 0; v < 2; ++v) {
+        pr.P[v] = reinterpret_cast<long long*>(p);
+        p += al256(8 * (size_t)n);
+    }
+    {
+        const size_t F = (size_t)kFastTies * (size_t)nch;
+        long long* ll = reinterpret_cast<long long*>(p);
+        pr.t_m[0] = ll;
+        pr.t_m[1] = ll + F;
+        pr.t_pb[0] = ll + 2 * F;
+        pr.t_pb[1] = ll + 3 * F;
+        int* ii = reinterpret_cast<int*>(ll + 4 * F);
+        pr.t_idx[0] = ii;
+        pr.t_idx[1] = ii + F;
+        pr.t_c0[0] = ii + 2 * F;
+        pr.t_c0[1] = ii + 3 * F;
+        pr.t_c1 = ii + 4 * F;
+    }
 
     (void)hipMemsetAsync(hdr, 0, 256, s);
     K* src = keysB;  // (the sorted keys: the kept ones first)
@@ -989,14 +1163,13 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     }
     if (nch > 0) {
         hipLaunchKernelGGL(vt_chunk_sum_kernel<T>, dim3((unsigned)(nch + 1)), dim3(kCumThreads), 0, s, src, hdr, ch, ctl);
-        hipLaunchKernelGGL(vt_chunk_prep_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, t_idx,
-                           t_pb, t_m, ctl);
+        hipLaunchKernelGGL(vt_chunk_prep_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
+                           ctl);
     }
-    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ch, t_idx, t_pb, t_m, t_c,
-                       ctl);
+    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ch, pr, (int)nch, ctl);
     if (nch > 0)
-        hipLaunchKernelGGL(vt_chunk_write_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, t_idx,
-                           t_c, cum, ctl);
+        hipLaunchKernelGGL(vt_chunk_write_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
+                           cum, ctl);
     const int minEl = (int)std::floor(minRatio * (T)points_nbr);
     const int maxEl = (int)std::floor(maxRatio * (T)points_nbr);
     hipLaunchKernelGGL(vt_frms_part_kernel<T>, dim3(kFrmsBlocks), dim3(256), 0, s, cum, hdr, deno, minEl, maxEl, part_v,

@@ -283,7 +283,17 @@ def test_vartrimmed_parallel_partial_sum(oracle, dtype, data):
     ctx.outlier(filters[0][0], 0, **filters[0][1])
     w = ctx.get_weights()
     d, _ = ctx.get_matches()
+    cum = ctx.vartrim_partial_sums()
     ctx.close()
     rc, ow = oracle.outlier_chain(filters, d)
     assert rc == 0
     assert np.array_equal(w, ow)
+    # the partial sums themselves, bit for bit: numpy's cumsum in T is the
+    # sequential loop (add.accumulate), std::partial_sum's rounding
+    keys = np.sort(d[np.isfinite(d) & (d > 0)].astype(dtype))
+    ref_cum = np.cumsum(keys, dtype=dtype)
+    assert cum.shape == ref_cum.shape
+    bad = np.flatnonzero(cum.view(np.uint32 if dtype == np.float32 else np.uint64) !=
+                         ref_cum.view(np.uint32 if dtype == np.float32 else np.uint64))
+    assert bad.size == 0, f"{bad.size} partial sums differ, first at {bad[:5]}"
+
