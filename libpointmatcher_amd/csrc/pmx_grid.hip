@@ -808,12 +808,11 @@ __global__ __launch_bounds__(256, 4) void grid_lane_kernel(const P4<T>* __restri
 //                        high occupancy, the gathers of many more waves in
 //                        flight); its block's misses, compacted in slot order,
 //                        go to the block's segment of `miss` with their count;
-//   grid_search_kernel   the full searches of those misses, kSearchSpan
-//                        certify blocks per search block (a block with no
-//                        misses returns at once).
+//   grid_search_kernel   the full searches of those misses, `span` certify
+//                        blocks per search block (a block with no misses
+//                        returns at once; PMX_SEARCH_SPAN, default 4).
 // Results, visits and the quantile window's counters are those of the single
 // kernel: only the launch a query's work runs in changes.
-constexpr int kSearchSpan = 4;
 
 template <typename T, int KT>
 __global__ __launch_bounds__(256) void grid_certify_kernel(const P4<T>* __restrict__ gpts,
@@ -914,7 +913,8 @@ __global__ __launch_bounds__(256, 4) void grid_search_kernel(const P4<T>* __rest
                                                           const GridDesc<T>* __restrict__ gd,
                                                           SpecSel* __restrict__ spec, const T* __restrict__ radii,
                                                           const uint16_t* __restrict__ miss,
-                                                          const int* __restrict__ miss_cnt, int64_t nblk, int all) {
+                                                          const int* __restrict__ miss_cnt, int64_t nblk, int all,
+                                                          int span) {
     if (ctl) {
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -928,8 +928,8 @@ __global__ __launch_bounds__(256, 4) void grid_search_kernel(const P4<T>* __rest
     uint32_t visits = 0, searched = 0;
     SpecAcc<T> sa;
     spec_acc_init<T>(sa, spec);
-    for (int s2 = 0; s2 < kSearchSpan; ++s2) {  // (uniform)
-        const int64_t cb = (int64_t)blockIdx.x * kSearchSpan + s2;
+    for (int s2 = 0; s2 < span; ++s2) {  // (uniform)
+        const int64_t cb = (int64_t)blockIdx.x * span + s2;
         if (cb >= nblk) break;
         const int64_t base = cb * 256;
         const int cnt = all ? (int)min((int64_t)256, N - base) : miss_cnt[cb];
@@ -949,7 +949,8 @@ __global__ __launch_bounds__(256, 4) void grid_search_kernel(const P4<T>* __rest
 // ------------------------------------------------------------ tile kernel --
 #include "pmx_grid_tile.inc"
 
-int g_lane_split = 1;  // (PMX_LANE_SPLIT: the certify / search launches)
+int g_lane_split = 1;   // (PMX_LANE_SPLIT: the certify / search launches)
+int g_search_span = 4;  // (PMX_SEARCH_SPAN: certify blocks per search block)
 
 template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
@@ -971,10 +972,11 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
             hipLaunchKernelGGL((grid_certify_kernel<T, KT>), dim3((unsigned)nblk), dim3(256), 0, s, gpts, rd, N, Tm,
                                knn, maxR2, dists, ids, visited, ru.mode, ru.safe, ru.Tprev, ctl, gd, spec, radii,
                                ru.miss, ru.miss_cnt, gidx);
-        const int64_t nsb = (nblk + kSearchSpan - 1) / kSearchSpan;
+        const int span = g_search_span > 0 ? g_search_span : 4;
+        const int64_t nsb = (nblk + span - 1) / span;
         hipLaunchKernelGGL((grid_search_kernel<T, KT>), dim3((unsigned)nsb), dim3(256), 0, s, gpts, gidx, start, G, rd,
                            N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode != 0 ? 1 : 0, ru.safe,
-                           ctl, gd, spec, radii, ru.miss, ru.miss_cnt, nblk, certify ? 0 : 1);
+                           ctl, gd, spec, radii, ru.miss, ru.miss_cnt, nblk, certify ? 0 : 1, span);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
