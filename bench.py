@@ -47,6 +47,7 @@ CONFIGS = {
             [("VarTrimmedDistOutlierFilter", {"minRatio": 0.05, "maxRatio": 0.99, "lambda": 2.35})],
             "PointToPlaneErrorMinimizer"),
 }
+BASELINE_CONFIGS = ("c2", "c3", "c4", "c5")
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 FP32_VALU_TFLOPS = 157.3   # MI355X FP32 vector peak (spec)
 FP64_VALU_TFLOPS = 78.6
@@ -349,6 +350,31 @@ def main():
                       f"first_matches_us: device time of each of the first matches (separate run, HIP events)",
              "device_warmup": f"{n_warm} untimed whole ICPs ({args.device_warmup:.2f} s) before every measured region"}
 
+    # ---- ICPSequence (before the driver region: the last dispatches of the
+    # command are the timed pass and the roofline pass, tools/pmc_phases.py)
+    seq_ms, seq_note = None, None
+    if not dist:
+        # ICPSequence (ICP.cpp:455-609): the map set once, then each scan pays
+        # only the reading side (upload, slot order) and its iterations
+        from libpointmatcher_amd.icp import ICPSequence
+
+        seq = ICPSequence(dtype, device=local_rank)
+        seq.load_yaml(chain_yaml(knn, filters, minimizer, search_type, args.cpu_iters))
+        seq.set_map(reference, nrm_in)
+        seq.compute(reading)  # (warm)
+        scans = []
+        for _ in range(3):
+            t_q = time.perf_counter()
+            seq.prepare(reading)
+            t_p = time.perf_counter()
+            seq.iterate(args.cpu_iters)
+            t_e = time.perf_counter()
+            scans.append((1e3 * (t_p - t_q), 1e3 * (t_e - t_q)))
+        seq.close()
+        seq_ms = min(x[1] for x in scans)
+        seq_note = (f"ICPSequence: map set once; per scan the reading-side setup "
+                    f"({min(x[0] for x in scans):.2f} ms) + {args.cpu_iters} iterations from the initial pose; best of 3")
+
     # ---- the driver's region: W untimed iterations, then exactly K timed
     icp.load_yaml(chain_yaml(knn, filters, minimizer, search_type, total_it))
     icp.prepare(reading, reference, nrm_in)
@@ -399,7 +425,8 @@ def main():
     # null for other configurations
     traffic, traffic_src = None, None
     if args.config == "c3" and args.matcher == "grid" and world == 1:
-        for src in (os.path.join("profiles", "r03", "pmc_c3_driver.json"),
+        for src in (os.path.join("profiles", "r04", "pmc_c3_driver.json"),
+                    os.path.join("profiles", "r03", "pmc_c3_driver.json"),
                     os.path.join("profiles", "r02", "pmc_c3_driver.json")):
             try:
                 with open(os.path.join(ROOT, src)) as f:
@@ -435,7 +462,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32" if esz == 4 else "f64",
         "data": "synthetic (box+sphere surface, seeds 1/2, sigma 0.01, SURVEY.md §8(d))",
-        "config": {"workload": f"BASELINE {args.config}: {N_global}->{M} {'float' if esz == 4 else 'double'}, "
+        "config": {"workload": f"{'BASELINE ' + args.config if args.config in BASELINE_CONFIGS else args.config + ' (not a BASELINE config: C3 with VarTrimmedDist)'}: {N_global}->{M} {'float' if esz == 4 else 'double'}, "
                                f"k={knn}, {', '.join(f[0] for f in filters) or 'no outlier filter'}, {minimizer}",
                    "matcher": f"KDTreeMatcher searchType={search_type} ({args.matcher}, exact)",
                    "reading_global": N_global, "reading_per_gpu": N, "reference": M, "parallelism": par},
@@ -448,6 +475,10 @@ def main():
                      "traffic_unit": "bytes per launch past L2 (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,
                      "kernel": "match (k-NN + fused transform)", "avg_launch_ms": avg_match_s * 1e3,
+                     "launches": (f"the {args.steps} matches of a repeat of the timed region (prepare, {args.warmup} "
+                                  f"untimed, then {args.steps} iterations with HIP events on the context stream around "
+                                  f"each match: grid_certify_kernel + grid_search_kernel, or grid_lane_kernel; "
+                                  f"tools/pmc_phases.py 'roofline' phase = the same launches in the rocprof trace)"),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "note": "steady-state launches certify most k-lists from the previous iteration (exact temporal "
                              "reuse, DESIGN.md §5); the ~70 MB C3 working set fits the 256 MB Infinity Cache, so "
@@ -463,29 +494,10 @@ def main():
         result["compute_roofline"]["note"] = ("grid search: FLOP counts only the pairs actually evaluated; the kernel "
                                               "is gather-latency-bound, neither VALU- nor HBM-bandwidth-bound")
     result["setup_ms"] = setup_s * 1e3
+    if seq_ms is not None:
+        result["sequence_scan_ms"] = seq_ms
+        result["sequence_scan_note"] = seq_note
     result["setup_parts"] = setup_parts
-    if not dist:
-        # ICPSequence (ICP.cpp:455-609): the map set once, then each scan pays
-        # only the reading side (upload, slot order) and its iterations
-        from libpointmatcher_amd.icp import ICPSequence
-
-        seq = ICPSequence(dtype, device=local_rank)
-        seq.load_yaml(chain_yaml(knn, filters, minimizer, search_type, args.cpu_iters))
-        seq.set_map(reference, nrm_in)
-        seq.compute(reading)  # (warm)
-        scans = []
-        for _ in range(3):
-            t_q = time.perf_counter()
-            seq.prepare(reading)
-            t_p = time.perf_counter()
-            seq.iterate(args.cpu_iters)
-            t_e = time.perf_counter()
-            scans.append((1e3 * (t_p - t_q), 1e3 * (t_e - t_q)))
-        seq.close()
-        result["sequence_scan_ms"] = min(x[1] for x in scans)
-        result["sequence_scan_note"] = (f"ICPSequence: map set once; per scan the reading-side setup "
-                                        f"({min(x[0] for x in scans):.2f} ms) + {args.cpu_iters} iterations from the "
-                                        f"initial pose; best of 3")
     result["first_prepare_ms"] = first_prepare_s * 1e3
     result["setup_note"] = ("ICP::compute setup before the first iteration, on a live device context: reference "
                             "filters + mean + centring (host, T-sequential), Matcher::init (reference upload, grid "
