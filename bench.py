@@ -477,7 +477,7 @@ def main():
                      "kernel": "match (k-NN + fused transform)", "avg_launch_ms": avg_match_s * 1e3,
                      "launches": (f"the {args.steps} matches of a repeat of the timed region (prepare, {args.warmup} "
                                   f"untimed, then {args.steps} iterations with HIP events on the context stream around "
-                                  f"each match: grid_certify_kernel + grid_search_kernel, or grid_lane_kernel; "
+                                  f"each match: grid_lane_kernel; "
                                   f"tools/pmc_phases.py 'roofline' phase = the same launches in the rocprof trace)"),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "note": "steady-state launches certify most k-lists from the previous iteration (exact temporal "

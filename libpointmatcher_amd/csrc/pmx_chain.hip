@@ -504,15 +504,6 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             ru.safe = (T*)c->d_safe;
             for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
         }
-        if (c->grid_mode >= 1 && knn <= kLaneMaxK && c->N > 0) {  // (the certify / search split's miss lists)
-            const int64_t nblk = (c->N + 255) / 256;
-            int rc;
-            if ((rc = ensure(c, (void**)&c->d_miss, &c->miss_bytes, sizeof(uint16_t) * 256 * (size_t)nblk)) ||
-                (rc = ensure(c, (void**)&c->d_miss_cnt, &c->miss_cnt_bytes, sizeof(int) * (size_t)nblk)))
-                return rc;
-            ru.miss = c->d_miss;
-            ru.miss_cnt = c->d_miss_cnt;
-        }
         // several ranks: the counter sum packs this rank's window segment,
         // the segments are all-gathered and every rank picks from the union
         SpecSel* spec = c->spec_now();

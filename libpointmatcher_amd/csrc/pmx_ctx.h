@@ -108,9 +108,6 @@ struct pmx_ctx {
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
     void* d_safe = nullptr;       // T[N]: safe radius per query
-    uint16_t* d_miss = nullptr;   // certify / search split: each block's missed slots (pmx_grid.hip)
-    int* d_miss_cnt = nullptr;
-    size_t miss_bytes = 0, miss_cnt_bytes = 0;
     int64_t safe_cap = 0;
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }

@@ -799,158 +799,8 @@ __global__ __launch_bounds__(256, 4) void grid_lane_kernel(const P4<T>* __restri
     if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
 }
 
-// ------------------------------------------- certify / search split --
-// The per-lane kernel above holds both the certificate and the full shell
-// search, and the search's registers set the occupancy of the whole launch
-// (4 waves per SIMD; the double form spills).  Once the pose has settled
-// nearly every query is certified, so the match runs as two launches:
-//   grid_certify_kernel  one slot per thread: the certificate only (light:
-//                        high occupancy, the gathers of many more waves in
-//                        flight); its block's misses, compacted in slot order,
-//                        go to the block's segment of `miss` with their count;
-//   grid_search_kernel   the full searches of those misses, `span` certify
-//                        blocks per search block (a block with no misses
-//                        returns at once; PMX_SEARCH_SPAN, default 4).
-// Results, visits and the quantile window's counters are those of the single
-// kernel: only the launch a query's work runs in changes.
-
-template <typename T, int KT>
-__global__ __launch_bounds__(256) void grid_certify_kernel(const P4<T>* __restrict__ gpts,
-                                                           const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm,
-                                                           int k, T maxR2, T* __restrict__ out_d,
-                                                           int32_t* __restrict__ out_i,
-                                                           unsigned long long* __restrict__ visited, int reuse,
-                                                           T* __restrict__ safe, Mat4<T> Tprev,
-                                                           const LoopCtl* __restrict__ ctl,
-                                                           const GridDesc<T>* __restrict__ gd,
-                                                           SpecSel* __restrict__ spec, const T* __restrict__ radii,
-                                                           uint16_t* __restrict__ miss, int* __restrict__ miss_cnt,
-                                                           const int32_t* __restrict__ gidx) {
-    if (ctl) {  // device loop: transform, level and reuse state from the device
-        if (ctl->done) return;
-        const GridDesc<T>& D = gd[ctl->level];
-        gpts = D.gpts;
-        gidx = D.gidx;
-        ctl_transform(ctl, Tm);
-        reuse = ctl->prev_level == ctl->level ? 2 : 1;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) Tprev.m[i] = (T)ctl->Tprev[i];
-    }
-    __shared__ int wave_cnt[4];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    bool missed = j < N;
-    uint32_t visits = 0;
-    SpecAcc<T> sa;
-    spec_acc_init<T>(sa, spec);
-    if (reuse == 2 && missed) {
-        // the certificate (reuse_query's rule); a list kept for reuse holds
-        // k <= KT - 1 entries (room for the (k+1)-th: the safe radius)
-        constexpr int KR = KT > 1 ? KT - 1 : 1;
-        const P4<T> p = gld(rd, j);
-        const T rs = safe[j];
-        const T dkp = out_d[j * k + k - 1];
-        int32_t id[KR];
-#pragma unroll
-        for (int s2 = 0; s2 < KR; ++s2) id[s2] = s2 < k ? out_i[j * k + s2] : 0;
-        T qx, qy, qz;
-        gxform(Tm, p, qx, qy, qz);
-        bool o = k <= KR && rs > (T)0 && dkp < (T)__builtin_huge_val();
-#pragma unroll
-        for (int s2 = 0; s2 < KR; ++s2) o = o && id[s2] >= 0;
-        T ox, oy, oz;
-        gxform(Tprev, p, ox, oy, oz);
-        const double ex = (double)qx - (double)ox, ey = (double)qy - (double)oy, ez = (double)qz - (double)oz;
-        const double delta = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + kReuseMargin);
-        const double av = sqrt((double)dkp) * (1.0 + kReuseMargin) + delta;
-        const double bq = (double)rs * (1.0 - kReuseMargin) - delta;
-        if (o && av < bq) {
-            P4<T> r[KR];
-#pragma unroll
-            for (int s2 = 0; s2 < KR; ++s2) r[s2] = gld32(gpts, s2 < k ? (uint32_t)id[s2] : 0u);
-            // the same k points: new distances, sorted as a full search sorts them
-            T kd[KT];
-            int32_t ki[KT];
-#pragma unroll
-            for (int s2 = 0; s2 < KT; ++s2) {
-                kd[s2] = (T)__builtin_huge_val();
-                ki[s2] = kNoPos;
-            }
-#pragma unroll
-            for (int s2 = 0; s2 < KR; ++s2)
-                if (s2 < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx, qy, qz, r[s2]), id[s2]);
-            visits += (uint32_t)k;
-            write_out<T, KT>(j, k, qr2(radii, j, maxR2), kd, ki, out_d, out_i, sa);
-            safe[j] = (T)(bq * (1.0 - 1e-6));
-            missed = false;
-        }
-    }
-    // the block's misses, compacted in slot order into its segment
-    const unsigned long long mq = __ballot(missed);
-    if (lane == 0) wave_cnt[wave] = __popcll(mq);
-    __syncthreads();
-    int off = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        off += w < wave ? wave_cnt[w] : 0;
-        total += wave_cnt[w];
-    }
-    if (missed) miss[(size_t)blockIdx.x * 256 + off + __popcll(mq & ((1ull << lane) - 1))] = (uint16_t)threadIdx.x;
-    if (threadIdx.x == 0) miss_cnt[blockIdx.x] = total;
-    add_visits(visits, visited);
-    if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
-}
-
-template <typename T, int KT>
-__global__ __launch_bounds__(256, 4) void grid_search_kernel(const P4<T>* __restrict__ gpts,
-                                                          const int32_t* __restrict__ gidx,
-                                                          const uint32_t* __restrict__ start, GridGeom G,
-                                                          const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
-                                                          T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                                          unsigned long long* __restrict__ visited, int oct,
-                                                          int reuse, T* __restrict__ safe,
-                                                          const LoopCtl* __restrict__ ctl,
-                                                          const GridDesc<T>* __restrict__ gd,
-                                                          SpecSel* __restrict__ spec, const T* __restrict__ radii,
-                                                          const uint16_t* __restrict__ miss,
-                                                          const int* __restrict__ miss_cnt, int64_t nblk, int all,
-                                                          int span) {
-    if (ctl) {
-        if (ctl->done) return;
-        const GridDesc<T>& D = gd[ctl->level];
-        gpts = D.gpts;
-        gidx = D.gidx;
-        start = D.start;
-        G = D.G;
-        ctl_transform(ctl, Tm);
-    }
-    if (!reuse) safe = nullptr;
-    uint32_t visits = 0, searched = 0;
-    SpecAcc<T> sa;
-    spec_acc_init<T>(sa, spec);
-    for (int s2 = 0; s2 < span; ++s2) {  // (uniform)
-        const int64_t cb = (int64_t)blockIdx.x * span + s2;
-        if (cb >= nblk) break;
-        const int64_t base = cb * 256;
-        const int cnt = all ? (int)min((int64_t)256, N - base) : miss_cnt[cb];
-        searched += (uint32_t)cnt;
-        if (threadIdx.x < cnt) {
-            const int64_t j = base + (all ? (int)threadIdx.x : (int)miss[(size_t)cb * 256 + threadIdx.x]);
-            full_query<T, KT>(gpts, gidx, start, G, rd, j, Tm, k, qr2(radii, j, maxR2), oct, out_d, out_i, safe,
-                              visits, sa);
-        }
-    }
-    add_visits(visits, visited);
-    // queries that took the full search (the "fallback" counter the level choice reads)
-    if (threadIdx.x == 0 && visited && searched && reuse) atomicAdd(vslot(visited, 1), (unsigned long long)searched);
-    if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
-}
-
 // ------------------------------------------------------------ tile kernel --
 #include "pmx_grid_tile.inc"
-
-int g_lane_split = 1;   // (PMX_LANE_SPLIT: the certify / search launches)
-int g_search_span = 4;  // (PMX_SEARCH_SPAN: certify blocks per search block)
 
 template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
@@ -962,21 +812,6 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
                            G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
                            ctl, gd, spec, ru.safe);
-    } else if (mode >= 1 && g_lane_split && ru.miss) {  // certify, then the misses' full searches
-        const int64_t nblk = (N + 255) / 256;
-        // the certificate runs when a previous match may be reused: in the
-        // device loop whenever reuse is on (the device decides), on the module
-        // path when the host knows the previous match is at this level
-        const bool certify = ctl ? ru.mode != 0 : ru.mode == 2;
-        if (certify)
-            hipLaunchKernelGGL((grid_certify_kernel<T, KT>), dim3((unsigned)nblk), dim3(256), 0, s, gpts, rd, N, Tm,
-                               knn, maxR2, dists, ids, visited, ru.mode, ru.safe, ru.Tprev, ctl, gd, spec, radii,
-                               ru.miss, ru.miss_cnt, gidx);
-        const int span = g_search_span > 0 ? g_search_span : 4;
-        const int64_t nsb = (nblk + span - 1) / span;
-        hipLaunchKernelGGL((grid_search_kernel<T, KT>), dim3((unsigned)nsb), dim3(256), 0, s, gpts, gidx, start, G, rd,
-                           N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode != 0 ? 1 : 0, ru.safe,
-                           ctl, gd, spec, radii, ru.miss, ru.miss_cnt, nblk, certify ? 0 : 1, span);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);

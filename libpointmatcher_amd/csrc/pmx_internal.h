@@ -166,10 +166,6 @@ struct GridReuse {
     int mode = 0;
     T* safe = nullptr;
     Mat4<T> Tprev{};
-    // the certify / search split of the per-lane match (pmx_grid.hip): each
-    // certify block's missed slots (block-local offsets) and their count
-    uint16_t* miss = nullptr;
-    int* miss_cnt = nullptr;
 };
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
@@ -203,8 +199,6 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
                        unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end, hipStream_t s);
-extern int g_lane_split;   // the match as certify + search launches (PMX_LANE_SPLIT=0: one launch)
-extern int g_search_span;  // certify blocks per search block (PMX_SEARCH_SPAN)
 // several ranks: the quantile window's pick over the all-gathered segments
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum.
 // stall: a miss sets ctl->done = kCtlStalled (the host did not read the

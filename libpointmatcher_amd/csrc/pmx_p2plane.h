@@ -100,6 +100,7 @@ struct RedTail {
     double* out = nullptr;
     void* means = nullptr;       // point-to-point pass 1: the means in T (p2point_means_kernel), when not sharded
 };
+constexpr int kTailChunk = 16;
 template <int NV>
 __device__ __forceinline__ bool reduce_tail(const double* __restrict__ partials, const RedTail& rt,
                                             const double** vals = nullptr) {
@@ -115,18 +116,26 @@ __device__ __forceinline__ bool reduce_tail(const double* __restrict__ partials,
     __syncthreads();
     if (!last) return false;
     const int t = threadIdx.x, wave = t >> 6;
-    double s[NV];
+    // (kTailChunk values at a time: all NV in flight at once would raise the
+    // kernel's VGPR count for its main loop too — 158 -> 213, 3 -> 2 waves
+    // per SIMD for the point-to-plane kernel)
+    constexpr int C = NV < kTailChunk ? NV : kTailChunk;
+#pragma unroll 1
+    for (int v0 = 0; v0 < NV; v0 += C) {
+        double s[C];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double* p = partials + (size_t)v * kRedBlocks;
-        const double a = __hip_atomic_load(p + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double b = __hip_atomic_load(p + t + 256, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s[v] = (0.0 + a) + b;
-    }
+        for (int j = 0; j < C; ++j) {
+            const int v = v0 + j < NV ? v0 + j : NV - 1;
+            const double* p = partials + (size_t)v * kRedBlocks;
+            const double a = __hip_atomic_load(p + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double b = __hip_atomic_load(p + t + 256, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s[j] = (0.0 + a) + b;
+        }
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        const double w = wave_sum(s[v]);
-        if ((t & 63) == 0) red[v][wave] = w;
+        for (int j = 0; j < C; ++j) {
+            const double w = wave_sum(s[j]);
+            if ((t & 63) == 0 && v0 + j < NV) red[v0 + j][wave] = w;
+        }
     }
     __shared__ double fin[NV];
     __syncthreads();

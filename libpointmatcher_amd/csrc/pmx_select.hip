@@ -482,11 +482,22 @@ __device__ __forceinline__ void vt_load(const typename KeyOf<T>::K* __restrict__
     }
 }
 
+// 1 / u = 2^sh as two finite factors: in double's lowest binades sh reaches
+// 1075 (u = 2^-1074), beyond the largest double power of two; x * a * b is
+// still exact (power-of-two scalings of a value that stays in range)
+struct UScale {
+    double a, b;
+};
+__device__ __forceinline__ UScale uscale(int sh) {
+    const int h = sh > 1000 ? 1000 : sh;
+    return {ldexp(1.0, h), ldexp(1.0, sh - h)};
+}
+
 // x / u rounded to nearest (a tie counted as m and flagged) for the active
 // keys [p, q1); returns the thread's saturated total
 template <typename T>
 __device__ __forceinline__ long long vt_round(const typename KeyOf<T>::K (&kv)[kCumPer], int64_t j0, int64_t p,
-                                              int64_t q1, double inv_u, long long (&r)[kCumPer],
+                                              int64_t q1, UScale inv_u, long long (&r)[kCumPer],
                                               bool (&tie)[kCumPer], int& ntie) {
     using KO = KeyOf<T>;
     constexpr long long LIM = 1ll << CumBits<T>::P;
@@ -498,7 +509,7 @@ __device__ __forceinline__ long long vt_round(const typename KeyOf<T>::K (&kv)[k
         r[i] = 0;
         tie[i] = false;
         if (j >= p && j < q1) {
-            const double q = (double)KO::val(kv[i]) * inv_u;  // exact (power-of-two scale)
+            const double q = ((double)KO::val(kv[i]) * inv_u.a) * inv_u.b;  // exact (power-of-two scales)
             if (!(q < (double)LIM)) {
                 r[i] = LIM;  // (this step alone leaves the binade)
             } else {
@@ -590,7 +601,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_prep_kernel(const typena
     K kv[kCumPer];
     vt_load<T>(keys, c, j0, kv);
     for (int v = 0; v < 2; ++v) {  // (uniform) binade e, then e + 1
-        const double inv_u = ldexp(1.0, P - 1 - (e + v));
+        const UScale inv_u = uscale(P - 1 - (e + v));
         long long r[kCumPer];
         bool tie[kCumPer];
         int ntie;
@@ -880,7 +891,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         int64_t p = lo;
         while (p < cend) {  // (uniform) passes over [p, cend)
             const int eb = CumBits<T>::binade(s);
-            const double inv_u = ldexp(1.0, P - 1 - eb);  // 1 / ulp(2^eb)
+            const UScale inv_u = uscale(P - 1 - eb);  // 1 / ulp(2^eb)
             const double u = ldexp(1.0, eb - (P - 1));
             const long long S0 = CumBits<T>::units(s);  // in [2^(P-1), 2^P)
             // the pass starts at p rounded down to a multiple of kCumPer (each

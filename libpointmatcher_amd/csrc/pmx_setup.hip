@@ -183,58 +183,60 @@ __device__ __forceinline__ int64_t dcell_of(const SetupShape& s, double x, doubl
     return (ci[2] * s.g[1] + ci[1]) * s.g[0] + ci[0];
 }
 
-// distinct cells: one bit per cell, the first setter counts it.  Neighbouring
-// points (clouds are often spatially ordered) hit the same bitmap word: the
-// lanes of a wave are grouped by word first — one atomicOr per distinct word
-// with the OR of the group's bits, the new bits counted from its return
-// (per-lane atomics on one word serialised: ~300 us at 1M points)
+// distinct occupied cells of a trial grid: every finite point sets its
+// cell's bit with a non-returning atomicOr (fire-and-forget: a wave never
+// waits on one), a wave whose points all fall in one word sets it once; the
+// count is then the popcount of the bitmap (occupancy_count_kernel).  (The
+// count taken from the atomics' return values serialised every wave on
+// round trips to contended words: ~600 us at 1M points.)
 template <typename T>
-__global__ void occupancy_kernel(const P4<T>* __restrict__ p, int64_t n, SetupShape s, uint32_t* __restrict__ bits,
-                                 unsigned long long* __restrict__ count) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    uint32_t mine = 0;
-    // (uniform trip count: every lane of the wave runs every round)
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
-        const int64_t i = i0 + threadIdx.x;
-        int64_t w = -1;
-        uint32_t b = 0;
-        if (i < n) {
-            const P4<T> q = p[i];
-            if (dfinite(q)) {
-                int64_t ci[3];
-                const int64_t c = dcell_of(s, (double)q.x, (double)q.y, (double)q.z, ci);
-                w = c >> 5;
-                b = 1u << (uint32_t)(c & 31);
-            }
-        }
-        unsigned long long todo = __ballot(w >= 0);
-        while (todo) {  // (uniform) one distinct word per round
-            const int lead = __ffsll((long long)todo) - 1;
-            const long long lw = __shfl(w, lead);
-            const bool in = w == lw;
-            uint32_t ob = in ? b : 0u;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) ob |= __shfl_xor(ob, off);
-            todo &= ~__ballot(in);
-            if (lane == lead) {
-                const uint32_t old = atomicOr(&bits[lw], ob);
-                mine += (uint32_t)__popc(ob & ~old);
-            }
+__global__ void occupancy_kernel(const P4<T>* __restrict__ p, int64_t n, SetupShape s, uint32_t* __restrict__ bits) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t w = -1;
+    uint32_t b = 0;
+    if (i < n) {
+        const P4<T> q = p[i];
+        if (dfinite(q)) {
+            int64_t ci[3];
+            const int64_t c = dcell_of(s, (double)q.x, (double)q.y, (double)q.z, ci);
+            w = c >> 5;
+            b = 1u << (uint32_t)(c & 31);
         }
     }
-    unsigned long long v = mine;
+    const long long w0 = __shfl(w, 0);
+    if (__all(w == w0 || w < 0) && w0 >= 0) {
+        uint32_t ob = b;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) ob |= __shfl_xor(ob, off);
+        if ((threadIdx.x & 63) == 0) atomicOr(&bits[w0], ob);
+    } else if (w >= 0) {
+        atomicOr(&bits[w], b);
+    }
+}
+
+__global__ void occupancy_count_kernel(const uint32_t* __restrict__ bits, int64_t words,
+                                       unsigned long long* __restrict__ count) {
+    __shared__ unsigned long long part[4];
+    unsigned long long v = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
+        v += (unsigned)__popc(bits[i]);
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (lane == 0 && v) atomicAdd(count, v);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t = part[0] + part[1] + part[2] + part[3];
+        if (t) atomicAdd(count, t);
+    }
 }
 
 template <typename T>
 void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, uint32_t* bits, unsigned long long* count,
                       hipStream_t st) {
-    int64_t nb = (n + 255) / 256;
-    if (nb > 2048) nb = 2048;
-    if (nb < 1) nb = 1;
-    hipLaunchKernelGGL(occupancy_kernel<T>, dim3((unsigned)nb), dim3(256), 0, st, p, n, s, bits, count);
+    const int64_t nb = std::max<int64_t>(1, (n + 255) / 256);
+    hipLaunchKernelGGL(occupancy_kernel<T>, dim3((unsigned)nb), dim3(256), 0, st, p, n, s, bits);
+    const int64_t words = (s.cells + 31) / 32;
+    const int64_t cb = std::min<int64_t>(1024, std::max<int64_t>(1, (words + 255) / 256));
+    hipLaunchKernelGGL(occupancy_count_kernel, dim3((unsigned)cb), dim3(256), 0, st, bits, words, count);
 }
 
 // cell key of every point (non-finite: the sentinel C, sorted last) and the
