@@ -112,31 +112,31 @@ int build_grid(pmx_ctx* c, int64_t M) {
         maxe = std::max(maxe, ext[a]);
     }
     if (!(maxe > 0)) maxe = 1;
-    // distinct occupied cells at a trial size (device bitmap)
-    auto occupied = [&](double h, int64_t& occ) -> int {
-        const SetupShape s = grid_shape(lo, ext, h);
-        occ = -1;
-        if (s.cells > ((int64_t)1 << 28)) return PMX_OK;
-        // bitmap, then the 8-byte counter on its own aligned line (a 64-bit
-        // atomic must be naturally aligned)
-        const size_t words = (size_t)((s.cells + 31) / 32);
-        const size_t cnt_off = (sizeof(uint32_t) * words + 255) & ~(size_t)255;
-        int r = ensure(c, &c->d_occ, &c->occ_bytes, cnt_off + 256);
+    // distinct occupied cells at two trial sizes (device bitmaps; one host sync)
+    auto occupied = [&](double ha, double hb, int64_t& oa, int64_t& ob) -> int {
+        const SetupShape sa = grid_shape(lo, ext, ha), sb = grid_shape(lo, ext, hb);
+        // (the count, then the per-slice bitmaps: pmx_setup.hip; cells <= 129^3 at these sizes)
+        const size_t ba = (occupancy_bytes(sa.cells) + 255) & ~(size_t)255;
+        int r = ensure(c, &c->d_occ, &c->occ_bytes, ba + occupancy_bytes(sb.cells));
         if (r) return r;
-        unsigned long long* cnt = (unsigned long long*)((char*)c->d_occ + cnt_off);
-        HIPCHK(c, hipMemsetAsync(c->d_occ, 0, cnt_off + 8, c->stream));
-        launch_occupancy<T>(pts, M, s, (uint32_t*)c->d_occ, cnt, c->stream);
-        unsigned long long v = 0;
-        HIPCHK(c, hipMemcpyAsync(&v, cnt, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+        char* base = (char*)c->d_occ;
+        HIPCHK(c, hipMemsetAsync(base, 0, 8, c->stream));
+        HIPCHK(c, hipMemsetAsync(base + ba, 0, 8, c->stream));
+        launch_occupancy<T>(pts, M, sa, base, c->stream);
+        launch_occupancy<T>(pts, M, sb, base + ba, c->stream);
+        unsigned long long v[2] = {0, 0};
+        HIPCHK(c, hipMemcpyAsync(&v[0], base, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&v[1], base + ba, 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        occ = (int64_t)v;
+        oa = (int64_t)v[0];
+        ob = (int64_t)v[1];
         return PMX_OK;
     };
     double dim = 3.0, ppc1 = 1.0, h1 = maxe / 128.0;
     if (valid > 0) {
         const double h0 = maxe / 64.0;
         int64_t o0 = 0, o1 = 0;
-        if ((rc = occupied(h0, o0)) || (rc = occupied(h1, o1))) return rc;
+        if ((rc = occupied(h0, h1, o0, o1))) return rc;
         o0 = std::max<int64_t>(1, o0);
         o1 = std::max<int64_t>(1, o1);
         dim = std::log2((double)o1 / (double)o0);

@@ -242,8 +242,8 @@ template <typename T>
 void launch_bbox(const P4<T>* p, int64_t n, double* scratch, double* out, hipStream_t s);
 size_t bbox_scratch_bytes();
 template <typename T>
-void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, uint32_t* bits, unsigned long long* count,
-                      hipStream_t st);
+void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, void* scratch, hipStream_t st);
+size_t occupancy_bytes(int64_t cells);  // the scratch of launch_occupancy (count first)
 template <typename T>
 int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const SetupShape& s, int64_t valid,
                        const SetupScratch& sc, P4<T>* gp, P4<T>* gpn, int32_t* gi, uint32_t* gstart, hipStream_t st);

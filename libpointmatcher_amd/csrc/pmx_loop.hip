@@ -47,10 +47,14 @@ __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl
 template <typename T>
 __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S, LoopCfg cfg,
                                  const T* __restrict__ T0, int level, int prev_level, Mat4d Tprev) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    // (the state zeroed by the whole wave, word by word: a LoopState<T> z = {}
+    // copied by one lane went through scratch, ~60 us)
+    static_assert(sizeof(LoopState<T>) % 4 == 0, "LoopState: whole words");
+    uint32_t* sw = reinterpret_cast<uint32_t*>(S);
+    for (int i = threadIdx.x; i < (int)(sizeof(LoopState<T>) / 4); i += blockDim.x) sw[i] = 0u;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     const int rows = cfg.rows, D = rows - 1;
-    LoopState<T> z = {};
-    *S = z;
     for (int i = 0; i < rows * rows; ++i) S->Titer[i] = T0[i];
     for (int ci = 0; ci < cfg.n_checkers; ++ci) {
         if (cfg.checker_kind[ci] == kCheckDifferential) {

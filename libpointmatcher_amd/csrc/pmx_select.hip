@@ -19,6 +19,7 @@
 // in T (one wave, bit-identical to the CPU), the FRMS curve and a first-index
 // argmin, then the same radix select with the optimised ratio.
 #include "pmx_internal.h"
+#include "pmx_sort.h"
 #include "pmx_spec.h"
 #include "pmx_selectall.h"
 
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, i
 template <typename K>
 static size_t vt_sort_temp_bytes(int64_t n) {
     size_t t = 0;
-    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, t, (const K*)nullptr, (K*)nullptr, (int)std::max<int64_t>(n, 1),
+    (void)pmx_sort_keys(nullptr, t, (const K*)nullptr, (K*)nullptr, (int)std::max<int64_t>(n, 1),
                                             0, (int)(8 * sizeof(K)));
     return t;
 }
@@ -1170,7 +1171,7 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     if (n > 0) {
         hipLaunchKernelGGL(vt_keys_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl);
         size_t tb = sort_tb;
-        (void)hipcub::DeviceRadixSort::SortKeys(sort_temp, tb, keysA, keysB, (int)n, 0, KeyOf<T>::bits, s);
+        (void)pmx_sort_keys(sort_temp, tb, keysA, keysB, (int)n, 0, KeyOf<T>::bits, s);
     }
     if (nch > 0) {
         hipLaunchKernelGGL(vt_chunk_sum_kernel<T>, dim3((unsigned)(nch + 1)), dim3(kCumThreads), 0, s, src, hdr, ch, ctl);

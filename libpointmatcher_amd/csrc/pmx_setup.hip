@@ -30,6 +30,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "pmx_internal.h"
+#include "pmx_sort.h"
 
 namespace pmx {
 
@@ -183,43 +184,51 @@ __device__ __forceinline__ int64_t dcell_of(const SetupShape& s, double x, doubl
     return (ci[2] * s.g[1] + ci[1]) * s.g[0] + ci[0];
 }
 
-// distinct occupied cells of a trial grid: every finite point sets its
-// cell's bit with a non-returning atomicOr (fire-and-forget: a wave never
-// waits on one), a wave whose points all fall in one word sets it once; the
-// count is then the popcount of the bitmap (occupancy_count_kernel).  (The
-// count taken from the atomics' return values serialised every wave on
-// round trips to contended words: ~600 us at 1M points.)
+// distinct occupied cells of a trial grid, with no global atomics: block
+// (slice, part) sets, in an LDS bitmap, the bits of the cells of its slice of
+// the points that fall in its part of the bitmap (kOccWords words), and
+// writes that part to its own slice of `slices`; occupancy_count_kernel ORs
+// the slices word by word and counts the bits.  (Global atomicOr on a shared
+// bitmap serialised on contended words: 300 us non-returning, 600 us with the
+// returned bits counted, at 1M points.)
+constexpr int kOccWords = 32768;  // 128 KB of LDS
+constexpr int kOccSlices = 32;
+size_t occupancy_bytes(int64_t cells) { return 256 + sizeof(uint32_t) * (size_t)kOccSlices * (size_t)((cells + 31) / 32); }
+
 template <typename T>
-__global__ void occupancy_kernel(const P4<T>* __restrict__ p, int64_t n, SetupShape s, uint32_t* __restrict__ bits) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t w = -1;
-    uint32_t b = 0;
-    if (i < n) {
+__global__ __launch_bounds__(1024) void occupancy_kernel(const P4<T>* __restrict__ p, int64_t n, SetupShape s,
+                                                         int64_t words, uint32_t* __restrict__ slices) {
+    __shared__ uint32_t bm[kOccWords];
+    const int64_t w0 = (int64_t)blockIdx.y * kOccWords;
+    const int nw = (int)(words - w0 < kOccWords ? words - w0 : kOccWords);
+    for (int i = threadIdx.x; i < nw; i += 1024) bm[i] = 0;
+    __syncthreads();
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t a = (int64_t)blockIdx.x * per, b = a + per < n ? a + per : n;
+    for (int64_t i = a + threadIdx.x; i < b; i += 1024) {
         const P4<T> q = p[i];
         if (dfinite(q)) {
             int64_t ci[3];
             const int64_t c = dcell_of(s, (double)q.x, (double)q.y, (double)q.z, ci);
-            w = c >> 5;
-            b = 1u << (uint32_t)(c & 31);
+            const int64_t w = (c >> 5) - w0;
+            if (w >= 0 && w < nw) atomicOr(&bm[w], 1u << (uint32_t)(c & 31));
         }
     }
-    const long long w0 = __shfl(w, 0);
-    if (__all(w == w0 || w < 0) && w0 >= 0) {
-        uint32_t ob = b;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) ob |= __shfl_xor(ob, off);
-        if ((threadIdx.x & 63) == 0) atomicOr(&bits[w0], ob);
-    } else if (w >= 0) {
-        atomicOr(&bits[w], b);
-    }
+    __syncthreads();
+    uint32_t* out = slices + (int64_t)blockIdx.x * words + w0;
+    for (int i = threadIdx.x; i < nw; i += 1024) out[i] = bm[i];
 }
 
-__global__ void occupancy_count_kernel(const uint32_t* __restrict__ bits, int64_t words,
-                                       unsigned long long* __restrict__ count) {
+__global__ __launch_bounds__(256) void occupancy_count_kernel(const uint32_t* __restrict__ slices, int64_t words,
+                                                              unsigned long long* __restrict__ count) {
     __shared__ unsigned long long part[4];
     unsigned long long v = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
-        v += (unsigned)__popc(bits[i]);
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t o = 0;
+#pragma unroll 8
+        for (int sl = 0; sl < kOccSlices; ++sl) o |= slices[(int64_t)sl * words + w];
+        v += (unsigned)__popc(o);
+    }
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
     __syncthreads();
@@ -229,14 +238,17 @@ __global__ void occupancy_count_kernel(const uint32_t* __restrict__ bits, int64_
     }
 }
 
+// scratch: occupancy_bytes(s.cells) at `scratch`; the count (zeroed by the
+// caller) in its first 8 bytes
 template <typename T>
-void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, uint32_t* bits, unsigned long long* count,
-                      hipStream_t st) {
-    const int64_t nb = std::max<int64_t>(1, (n + 255) / 256);
-    hipLaunchKernelGGL(occupancy_kernel<T>, dim3((unsigned)nb), dim3(256), 0, st, p, n, s, bits);
+void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, void* scratch, hipStream_t st) {
     const int64_t words = (s.cells + 31) / 32;
+    unsigned long long* count = (unsigned long long*)scratch;
+    uint32_t* slices = (uint32_t*)((char*)scratch + 256);
+    const unsigned parts = (unsigned)((words + kOccWords - 1) / kOccWords);
+    hipLaunchKernelGGL(occupancy_kernel<T>, dim3(kOccSlices, parts), dim3(1024), 0, st, p, n, s, words, slices);
     const int64_t cb = std::min<int64_t>(1024, std::max<int64_t>(1, (words + 255) / 256));
-    hipLaunchKernelGGL(occupancy_count_kernel, dim3((unsigned)cb), dim3(256), 0, st, bits, words, count);
+    hipLaunchKernelGGL(occupancy_count_kernel, dim3((unsigned)cb), dim3(256), 0, st, slices, words, count);
 }
 
 // cell key of every point (non-finite: the sentinel C, sorted last) and the
@@ -286,7 +298,7 @@ static int bits_for(uint64_t v) {
 template <typename K>
 static size_t sort_temp_bytes(int64_t n) {
     size_t t = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const K*)nullptr, (K*)nullptr, (const int32_t*)nullptr,
+    (void)pmx_sort_pairs(nullptr, t, (const K*)nullptr, (K*)nullptr, (const int32_t*)nullptr,
                                              (int32_t*)nullptr, (int)n, 0, (int)(8 * sizeof(K)));
     return t;
 }
@@ -307,7 +319,7 @@ int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const Setu
         hipLaunchKernelGGL(cell_keys_kernel<T>, dim3(blocks_for(M)), dim3(256), 0, st, pts, M, s, sc.keys32,
                            sc.idx, sc.counts);
         size_t tb = sc.temp_bytes;
-        e = hipcub::DeviceRadixSort::SortPairs(sc.temp, tb, sc.keys32, sc.keys32_out, sc.idx, sc.idx_out, (int)M, 0,
+        e = pmx_sort_pairs(sc.temp, tb, sc.keys32, sc.keys32_out, sc.idx, sc.idx_out, (int)M, 0,
                                                bits_for((uint64_t)C), st);
         if (e != hipSuccess) return -2;
     }
@@ -376,7 +388,7 @@ int reading_order_device(const P4<T>* raw, int64_t n, const Mat4<T>& M0, const S
     hipLaunchKernelGGL(morton_keys_kernel<T>, dim3(blocks_for(n)), dim3(256), 0, st, raw, n, M0, s, morton ? 1 : 0,
                        sc.keys64, sc.idx);
     size_t tb = sc.temp_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(sc.temp, tb, sc.keys64, sc.keys64_out, sc.idx, sc.idx_out,
+    hipError_t e = pmx_sort_pairs(sc.temp, tb, sc.keys64, sc.keys64_out, sc.idx, sc.idx_out,
                                                       (int)n, 0, 64, st);
     if (e != hipSuccess) return -2;
     hipLaunchKernelGGL(slot_gather_kernel<T>, dim3(blocks_for(n)), dim3(256), 0, st, raw, sc.idx_out, n, sorted);
@@ -441,7 +453,7 @@ void launch_apply_radii(T* dists, int32_t* ids, const T* radii, int64_t N, int k
     template void launch_pack_p4<T>(const T*, int, int64_t, int64_t, P4<T>*, hipStream_t, const T*);                \
     template void launch_pack_nrm<T>(const T*, int, int64_t, P4<T>*, hipStream_t);                                  \
     template void launch_bbox<T>(const P4<T>*, int64_t, double*, double*, hipStream_t);                             \
-    template void launch_occupancy<T>(const P4<T>*, int64_t, const SetupShape&, uint32_t*, unsigned long long*,    \
+    template void launch_occupancy<T>(const P4<T>*, int64_t, const SetupShape&, void*,                             \
                                       hipStream_t);                                                                 \
     template int build_level_device<T>(const P4<T>*, int64_t, const P4<T>*, const SetupShape&, int64_t,           \
                                        const SetupScratch&, P4<T>*, P4<T>*, int32_t*, uint32_t*, hipStream_t);      \

@@ -39,6 +39,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "pmx_internal.h"
+#include "pmx_sort.h"
 
 #include "common/pmx_dense.h"
 
@@ -356,7 +357,7 @@ int ssn_run(const P4<T>* d_pts, int D, int64_t n, int knn, T max_box, bool want_
     }
     int32_t* base = m.get<int32_t>(nb_max + 1);
     size_t tsort = 0, tscan = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, keys, keys2, idx, idx2, (int)n, 0, 64, st);
+    (void)pmx_sort_pairs(nullptr, tsort, keys, keys2, idx, idx2, (int)n, 0, 64, st);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tscan, B[0].nchild, base, (int)(nb_max + 1), st);
     const size_t tbytes = std::max(tsort, tscan);
     void* temp = m.get<char>(tbytes);
@@ -373,7 +374,7 @@ int ssn_run(const P4<T>* d_pts, int D, int64_t n, int knn, T max_box, bool want_
     for (int a = 0; a < D; ++a) {
         hipLaunchKernelGGL(axis_keys_kernel<T>, dim3(nblk(n)), dim3(256), 0, st, d_pts, n, a, keys, idx);
         size_t tb = tbytes;
-        if (hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys2, idx, idx2, (int)n, 0,
+        if (pmx_sort_pairs(temp, tb, keys, keys2, idx, idx2, (int)n, 0,
                                                sizeof(T) == 4 ? 32 : 64, st) != hipSuccess)
             return fail_hip("axis sort");
         hipLaunchKernelGGL(rank_scatter_kernel, dim3(nblk(n)), dim3(256), 0, st, idx2, n, rank + (size_t)a * n);
@@ -386,7 +387,7 @@ int ssn_run(const P4<T>* d_pts, int D, int64_t n, int knn, T max_box, bool want_
         for (int a = 0; a < D; ++a) {
             hipLaunchKernelGGL(axis_keys_kernel<T>, dim3(nblk(n)), dim3(256), 0, st, d_pts, n, a, keys, idx);
             size_t tb = tbytes;
-            if (hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys2, idx, idx2, (int)n, 0,
+            if (pmx_sort_pairs(temp, tb, keys, keys2, idx, idx2, (int)n, 0,
                                                    sizeof(T) == 4 ? 32 : 64, st) != hipSuccess)
                 return fail_hip("bounds sort");
             int32_t e[2];
@@ -437,7 +438,7 @@ int ssn_run(const P4<T>* d_pts, int D, int64_t n, int knn, T max_box, bool want_
         // every box sorted along its own cut axis
         hipLaunchKernelGGL(level_keys_kernel, dim3(nblk(n)), dim3(256), 0, st, boxof, b.cut, rank, perm, n, keys);
         tb = tbytes;
-        if (hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys2, perm, perm2, (int)n, 0,
+        if (pmx_sort_pairs(temp, tb, keys, keys2, perm, perm2, (int)n, 0,
                                                32 + bits_of((uint64_t)nbox), st) != hipSuccess)
             return fail_hip("level sort");
         std::swap(perm, perm2);
@@ -452,7 +453,7 @@ int ssn_run(const P4<T>* d_pts, int D, int64_t n, int knn, T max_box, bool want_
     // leaves in index order
     hipLaunchKernelGGL(leaf_index_keys_kernel, dim3(nblk(n)), dim3(256), 0, st, boxof, perm, n, keys);
     size_t tb = tbytes;
-    if (hipcub::DeviceRadixSort::SortPairs(temp, tb, keys, keys2, perm, perm2, (int)n, 0, 32 + bits_of((uint64_t)nbox),
+    if (pmx_sort_pairs(temp, tb, keys, keys2, perm, perm2, (int)n, 0, 32 + bits_of((uint64_t)nbox),
                                            st) != hipSuccess)
         return fail_hip("leaf sort");
     std::swap(perm, perm2);

@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "pmx_internal.h"
+#include "pmx_sort.h"
 
 #include "../../include/pmx.h"
 
@@ -244,9 +245,9 @@ int voxel_run(const T* d_f, int rows, int64_t n, const T* d_desc, int desc_dim, 
     int64_t* nsel = nullptr;
     void* temp = nullptr;
     size_t tsort = 0, tsel = 0, tsort2 = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, key, key2, idx, idx2, (int)n, 0, 32, st);
+    (void)pmx_sort_pairs(nullptr, tsort, key, key2, idx, idx2, (int)n, 0, 32, st);
     (void)hipcub::DeviceSelect::Flagged(nullptr, tsel, idx, head, segs, nsel, (int)n, st);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tsort2, key, key2, idx, idx2, (int)n, 0, 32, st);
+    (void)pmx_sort_pairs(nullptr, tsort2, key, key2, idx, idx2, (int)n, 0, 32, st);
     const size_t tb = std::max(std::max(tsort, tsel), tsort2);
     const size_t words = (size_t)n;
     char* buf = nullptr;
@@ -269,7 +270,7 @@ int voxel_run(const T* d_f, int rows, int64_t n, const T* d_desc, int desc_dim, 
     const unsigned G = vox_grid(n);
     hipLaunchKernelGGL(vox_key_kernel<T>, dim3(G), dim3(256), 0, st, d_f, n, g, key, idx);
     size_t t = tb;
-    if (hipcub::DeviceRadixSort::SortPairs(temp, t, key, key2, idx, idx2, (int)n, 0, 32, st) != hipSuccess)
+    if (pmx_sort_pairs(temp, t, key, key2, idx, idx2, (int)n, 0, 32, st) != hipSuccess)
         return PMX_E_HIP;
     hipLaunchKernelGGL(vox_heads_kernel, dim3(G), dim3(256), 0, st, key2, n, head);
     // segment starts: the positions whose head flag is set (the positions are the iota in key)
@@ -284,7 +285,7 @@ int voxel_run(const T* d_f, int rows, int64_t n, const T* d_desc, int desc_dim, 
     hipLaunchKernelGGL(vox_record_kernel<T>, dim3(vox_grid(nseg)), dim3(256), 0, st, d_f, d_desc, desc_dim, key2, idx2,
                        segs, nseg, n, g, centroid ? 1 : 0, avg ? 1 : 0, rf, rdsc, key, head);
     t = tb;  // (first points -> idx, scratch; voxel slots in that order -> segs)
-    if (hipcub::DeviceRadixSort::SortPairs(temp, t, key, idx, head, segs, (int)nseg, 0, 32, st) != hipSuccess)
+    if (pmx_sort_pairs(temp, t, key, idx, head, segs, (int)nseg, 0, 32, st) != hipSuccess)
         return PMX_E_HIP;
     hipLaunchKernelGGL(vox_gather_kernel<T>, dim3(vox_grid(nseg)), dim3(256), 0, st, rf, rdsc, rows, desc_dim, segs,
                        nseg, d_of, d_od);
