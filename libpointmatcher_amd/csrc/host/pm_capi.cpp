@@ -59,12 +59,16 @@ DataPoints<T> make_cloud(const void* feat, int rows, int64_t n, const void* norm
     DataPoints<T> c;
     c.rows = rows;
     c.n = n;
-    const T* p = static_cast<const T*>(feat);
-    c.features.assign(p, p + (size_t)rows * n);
+    // (borrowed: the caller's arrays stay valid for the call; DataPoints copies own their data)
+    c.ext = static_cast<const T*>(feat);
     const char* xyz[] = {"x", "y", "z"};
     for (int r = 0; r < rows - 1; ++r) c.featureLabels.push_back({xyz[r], 1});
     c.featureLabels.push_back({"pad", 1});
-    if (normals) c.addDescriptor("normals", rows - 1, static_cast<const T*>(normals));
+    if (normals) {
+        c.descriptorLabels.push_back({"normals", rows - 1});
+        c.descDim = rows - 1;
+        c.extDesc = static_cast<const T*>(normals);
+    }
     return c;
 }
 

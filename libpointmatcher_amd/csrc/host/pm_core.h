@@ -177,6 +177,44 @@ struct DataPoints {
     std::vector<Label> descriptorLabels;
     int descDim = 0;
     std::vector<T> descriptors;  // point-major: descriptors[i * descDim + r]
+    // A borrowed cloud (the C ABI's prepare / setMap with the caller's arrays,
+    // pm_capi.cpp): the features / descriptors are read in place, not copied
+    // (1M points: 44 MB of host copies and first-touch page faults, ~3 ms of
+    // setup).  Any copy of a DataPoints owns its data (the filter chains
+    // mutate copies), and every mutator materialises first; read through
+    // feat() / desc().
+    const T* ext = nullptr;
+    const T* extDesc = nullptr;
+
+    DataPoints() = default;
+    DataPoints(DataPoints&&) = default;
+    DataPoints& operator=(DataPoints&&) = default;
+    DataPoints(const DataPoints& o) { *this = o; }
+    DataPoints& operator=(const DataPoints& o) {
+        if (this == &o) return *this;
+        rows = o.rows;
+        n = o.n;
+        featureLabels = o.featureLabels;
+        descriptorLabels = o.descriptorLabels;
+        descDim = o.descDim;
+        if (o.ext)
+            features.assign(o.ext, o.ext + (size_t)rows * (size_t)n);
+        else
+            features = o.features;
+        if (o.extDesc)
+            descriptors.assign(o.extDesc, o.extDesc + (size_t)descDim * (size_t)n);
+        else
+            descriptors = o.descriptors;
+        ext = extDesc = nullptr;
+        return *this;
+    }
+    const T* feat() const { return ext ? ext : features.data(); }
+    const T* desc() const { return extDesc ? extDesc : descriptors.data(); }
+    void materialize() {
+        if (ext) features.assign(ext, ext + (size_t)rows * (size_t)n);
+        if (extDesc) descriptors.assign(extDesc, extDesc + (size_t)descDim * (size_t)n);
+        ext = extDesc = nullptr;
+    }
 
     int64_t getNbPoints() const { return n; }
     int getEuclideanDim() const { return rows - 1; }
@@ -192,8 +230,9 @@ struct DataPoints {
         for (auto& l : descriptorLabels) {
             if (l.text == name) {
                 std::vector<T> out((size_t)l.span * n);
+                const T* d = desc();
                 for (int64_t i = 0; i < n; ++i)
-                    for (int r = 0; r < l.span; ++r) out[i * l.span + r] = descriptors[i * descDim + off + r];
+                    for (int r = 0; r < l.span; ++r) out[i * l.span + r] = d[i * descDim + off + r];
                 if (span) *span = l.span;
                 return out;
             }
@@ -204,6 +243,7 @@ struct DataPoints {
     // allocateDescriptors + the view assignment of a data filter: overwrite an
     // existing label of the same span, else append (PointMatcher.h:281-296)
     void setDescriptor(const std::string& name, int span, const T* data) {
+        materialize();
         int off = 0;
         for (auto& l : descriptorLabels) {
             if (l.text == name && l.span == span) {
@@ -216,6 +256,7 @@ struct DataPoints {
         addDescriptor(name, span, data);
     }
     void addDescriptor(const std::string& name, int span, const T* data) {
+        materialize();
         std::vector<T> nd((size_t)(descDim + span) * n);
         for (int64_t i = 0; i < n; ++i) {
             for (int r = 0; r < descDim; ++r) nd[i * (descDim + span) + r] = descriptors[i * descDim + r];

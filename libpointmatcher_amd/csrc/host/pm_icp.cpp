@@ -108,7 +108,7 @@ void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType, const T
     const T* np = nullptr;
     if (ref.descriptorLabels.size() == 1 && ref.descriptorLabels[0].text == "normals" &&
         ref.descriptorLabels[0].span == ref.rows - 1) {
-        np = ref.descriptors.data();  // (the only descriptor: already the dense D x n block, no copy)
+        np = ref.desc();  // (the only descriptor: already the dense D x n block, no copy)
     } else if (ref.descriptorExists("normals")) {
         int span = 0;
         nrm = ref.descriptor("normals", &span);
@@ -123,9 +123,9 @@ void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType, const T
     }
     dev.check(pmx_set_search(dev.ctx, searchType));  // 0: brute force, 1/2: exact grid search
     if (centre)
-        dev.check(pmx_set_reference_centred(dev.ctx, ref.features.data(), ref.rows, ref.n, np, centre));
+        dev.check(pmx_set_reference_centred(dev.ctx, ref.feat(), ref.rows, ref.n, np, centre));
     else
-        dev.check(pmx_set_reference(dev.ctx, ref.features.data(), ref.rows, ref.n, np));
+        dev.check(pmx_set_reference(dev.ctx, ref.feat(), ref.rows, ref.n, np));
 }
 template <typename T>
 typename PM<T>::Matches device_matches(Device& dev, int knn) {
@@ -1373,7 +1373,7 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     T_refIn_refMean_.assign((size_t)dim * dim, (T)0);
     for (int i = 0; i < dim; ++i) T_refIn_refMean_[i * dim + i] = 1;
     T sum[3] = {0, 0, 0}, mean[3] = {0, 0, 0};
-    const T* f = reference.features.data();
+    const T* f = reference.feat();
     if (dim == 4) {
         for (int64_t j = 0; j < M; ++j) {
             sum[0] = sum[0] + f[j * 4];
@@ -1426,7 +1426,7 @@ void PointMatcher<T>::ICP::prepareReading(const DataPoints& readingIn, const Tra
     if (std::fabs((T)1 - dense::det_rot(T_refMean_dataIn_.data(), dim)) > (T)0.001)
         throw TransformationError("RigidTransformation: Error, rotation matrix is not orthogonal.");
     // transformations.apply(reading, T_refMean_dataIn): done on the device
-    dev.check(pmx_set_reading(dev.ctx, reading.features.data(), dim, reading.n, T_refMean_dataIn_.data()));
+    dev.check(pmx_set_reading(dev.ctx, reading.feat(), dim, reading.n, T_refMean_dataIn_.data()));
     matcher->initReading(dev, reading);  // (per-reading matcher inputs: KDTreeVarDistMatcher's radii)
     // readingStepDataPointsFilters (ICP.cpp:349-350, 373-377): the step
     // filters see the reading in <refMean> every iteration; keep that copy on
@@ -1437,7 +1437,7 @@ void PointMatcher<T>::ICP::prepareReading(const DataPoints& readingIn, const Tra
         stepBase_ = reading;
         const int D = dim - 1;
         for (int64_t j = 0; j < reading.n; ++j) {
-            const T* f = &reading.features[(size_t)j * dim];
+            const T* f = reading.feat() + (size_t)j * dim;
             T* o = &stepBase_.features[(size_t)j * dim];
             for (int r = 0; r < D; ++r) {
                 const T* m = &T_refMean_dataIn_[(size_t)r * dim];

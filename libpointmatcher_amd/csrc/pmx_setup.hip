@@ -354,14 +354,15 @@ __device__ __forceinline__ uint64_t dspread3(uint64_t v) {
 // non-finite points last
 template <typename T>
 __global__ void morton_keys_kernel(const P4<T>* __restrict__ p, int64_t n, Mat4<T> M0, SetupShape s, int morton,
-                                   unsigned long long* __restrict__ keys, int32_t* __restrict__ idx) {
+                                   unsigned long long sentinel, unsigned long long* __restrict__ keys,
+                                   int32_t* __restrict__ idx) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const P4<T> r = p[i];
     const double x = ((double)M0.m[0] * r.x + (double)M0.m[1] * r.y) + (double)M0.m[2] * r.z + (double)M0.m[3] * r.w;
     const double y = ((double)M0.m[4] * r.x + (double)M0.m[5] * r.y) + (double)M0.m[6] * r.z + (double)M0.m[7] * r.w;
     const double z = ((double)M0.m[8] * r.x + (double)M0.m[9] * r.y) + (double)M0.m[10] * r.z + (double)M0.m[11] * r.w;
-    unsigned long long k = ~0ull;
+    unsigned long long k = sentinel;
     if (isfinite(x) && isfinite(y) && isfinite(z)) {
         int64_t ci[3];
         const int64_t c = dcell_of(s, x, y, z, ci);
@@ -385,11 +386,17 @@ template <typename T>
 int reading_order_device(const P4<T>* raw, int64_t n, const Mat4<T>& M0, const SetupShape& s, bool morton,
                          const SetupScratch& sc, P4<T>* sorted, hipStream_t st) {
     if (n <= 0) return 0;
+    // the sort runs over the key bits in use only (one onesweep pass per 8):
+    // the Morton code of the largest cell coordinate, or the cell count, and
+    // one more bit for the non-finite points' key (past every finite key)
+    int gb = 1;
+    while (gb < 21 && (((int64_t)1 << gb) < (int64_t)std::max(s.g[0], std::max(s.g[1], s.g[2])))) ++gb;
+    const unsigned long long sentinel = morton ? (1ull << (3 * gb)) : (unsigned long long)s.cells;
+    const int end_bit = bits_for(sentinel);
     hipLaunchKernelGGL(morton_keys_kernel<T>, dim3(blocks_for(n)), dim3(256), 0, st, raw, n, M0, s, morton ? 1 : 0,
-                       sc.keys64, sc.idx);
+                       sentinel, sc.keys64, sc.idx);
     size_t tb = sc.temp_bytes;
-    hipError_t e = pmx_sort_pairs(sc.temp, tb, sc.keys64, sc.keys64_out, sc.idx, sc.idx_out,
-                                                      (int)n, 0, 64, st);
+    hipError_t e = pmx_sort_pairs(sc.temp, tb, sc.keys64, sc.keys64_out, sc.idx, sc.idx_out, (int)n, 0, end_bit, st);
     if (e != hipSuccess) return -2;
     hipLaunchKernelGGL(slot_gather_kernel<T>, dim3(blocks_for(n)), dim3(256), 0, st, raw, sc.idx_out, n, sorted);
     return hipGetLastError() == hipSuccess ? 0 : -4;
