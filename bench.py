@@ -424,10 +424,9 @@ def main():
     # WRITE_SIZE per launch, averaged over the launches of the timed steps);
     # null for other configurations
     traffic, traffic_src = None, None
-    if args.config == "c3" and args.matcher == "grid" and world == 1:
-        for src in (os.path.join("profiles", "r04", "pmc_c3_driver.json"),
-                    os.path.join("profiles", "r03", "pmc_c3_driver.json"),
-                    os.path.join("profiles", "r02", "pmc_c3_driver.json")):
+    if args.matcher == "grid" and world == 1:
+        for src in (os.path.join("profiles", "r04", f"pmc_{args.config}_driver.json"),
+                    os.path.join("profiles", "r03", f"pmc_{args.config}_driver.json")):
             try:
                 with open(os.path.join(ROOT, src)) as f:
                     pm = json.load(f)

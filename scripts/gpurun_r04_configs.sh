@@ -13,8 +13,7 @@ for c in $CFGS; do
   cap=100; [ "$c" = c5 ] && cap=30
   step bench_$c && timeout -k 10 420 python bench.py --config $c --steps 20 --warmup 5 --cpu-one-thread-cap $cap \
       > gpurun_out/bench_$c.json 2> gpurun_out/bench_$c.err || exit 1
-  step prof_$c && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$c" -o run \
-      --output-format csv -- python3 "$R/bench.py" --config $c --steps 20 --warmup 5 --no-cpu-baseline \
-      > "$R/gpurun_out/prof_$c.log" 2>&1) || exit 1
+  step pmc_$c && PMC_TAG=$c bash scripts/gpurun_r04_pmc.sh --config $c || exit 1
+  mkdir -p gpurun_out/prof_$c && cp gpurun_out/pmc_trace/run_kernel_stats.csv gpurun_out/prof_$c/ || exit 1
 done
 step "done"
