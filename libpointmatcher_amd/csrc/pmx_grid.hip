@@ -666,8 +666,20 @@ struct LaneQ {
 // XCD-aware block order of the per-lane kernel (pmx_internal.h xcd_block:
 // adjacent slot ranges gather through one L2; match HBM traffic 75.3 -> 66.5
 // MB per launch at C3)
+// waves per SIMD the per-lane kernel is built for (its VGPR budget: 512 /
+// waves).  The double and the wide (KT >= 8) forms spill at 128 VGPRs (C5:
+// 78 VGPRs to scratch inside the shell walk), so they take fewer waves and
+// no spills.
+#ifndef PMX_LANE_WAVES_WIDE
+#define PMX_LANE_WAVES_WIDE 2
+#endif
+template <typename T, int KT>
+struct LaneWaves {
+    static constexpr int value = (sizeof(T) == 8 || KT >= 8) ? PMX_LANE_WAVES_WIDE : 4;
+};
+
 template <typename T, int KT, int Q>
-__global__ __launch_bounds__(256, 4) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
+__global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
