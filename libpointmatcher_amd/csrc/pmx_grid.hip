@@ -666,16 +666,15 @@ struct LaneQ {
 // XCD-aware block order of the per-lane kernel (pmx_internal.h xcd_block:
 // adjacent slot ranges gather through one L2; match HBM traffic 75.3 -> 66.5
 // MB per launch at C3)
-// waves per SIMD the per-lane kernel is built for (its VGPR budget: 512 /
-// waves).  The double and the wide (KT >= 8) forms spill at 128 VGPRs (C5:
-// 78 VGPRs to scratch inside the shell walk), so they take fewer waves and
-// no spills.
-#ifndef PMX_LANE_WAVES_WIDE
-#define PMX_LANE_WAVES_WIDE 2
-#endif
+// waves per SIMD the per-lane and tile kernels are built for (their VGPR
+// budget: 512 / waves).  The double forms spill at 128 VGPRs (C5: 78 VGPRs to
+// scratch inside the shell walk), so they are built for 2 (the compiler then
+// takes 133-220 VGPRs, 2-3 waves, no spills): C5 1.79 -> 1.62 ms/iteration.
+// The float KT = 8 form spills 26 at 128 but measured faster that way than
+// unspilled at 3 waves (C4 0.202 vs 0.217 ms/iteration).
 template <typename T, int KT>
 struct LaneWaves {
-    static constexpr int value = (sizeof(T) == 8 || KT >= 8) ? PMX_LANE_WAVES_WIDE : 4;
+    static constexpr int value = sizeof(T) == 8 ? 2 : 4;
 };
 
 template <typename T, int KT, int Q>

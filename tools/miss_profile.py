@@ -27,6 +27,7 @@ ref, nrm = reference_cloud(M, dtype)
 rd = reading_cloud(N, dtype)
 icp = ICP(dtype)
 icp.load_yaml(bench.chain_yaml(knn, filters, minimizer, 1, iters))
+icp.keep_trace(True)
 icp.compute(rd, ref, nrm)
 tr = icp.trace()
 icp.close()
