@@ -804,10 +804,12 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
         const size_t need = vartrim_scratch_bytes<T>(nsrc);
         if ((rc = ensure(c, &c->d_vt, &c->vt_bytes, need))) return rc;
         c->vt_n = nsrc;
+        // (the quantile at the optimised ratio from the sorted keys: no radix
+        // passes, and on several ranks no histogram all-reduces — the sort
+        // covers the gathered distances)
         launch_vartrim<T>(dsrc, nsrc, points_nbr, minR, maxR, (const T*)c->d_deno, c->d_vt, c->vt_bytes, c->d_ratio,
-                          c->d_iter_err, loop_ctl(c), c->stream);
+                          c->d_iter_err, slot, loop_ctl(c), c->stream);
         HIPCHK(c, hipGetLastError());
-        if ((rc = quantile_select<T>(c, d, n, 0.0, c->d_ratio, slot))) return rc;
         chain_set(c, chain_pos, kWPState, 1.0);
         break;
     }

@@ -438,7 +438,7 @@ int select_bins(int pass, int key_bits);
 // VarTrimmed pieces
 template <typename T>
 void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRatio, const T* deno,
-                    void* scratch, size_t scratch_bytes, double* ratio_dev, int* err_dev,
+                    void* scratch, size_t scratch_bytes, double* ratio_dev, int* err_dev, SelectState* st,
                     const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 size_t vartrim_scratch_bytes(int64_t n);

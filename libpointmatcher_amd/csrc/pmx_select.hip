@@ -308,22 +308,31 @@ __global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, i
                                                       const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
-    __shared__ int wtot[4];
+    __shared__ int wtot[4], wz[4];
     if (ctl && ctl->done) return;
-    int c = 0;
+    int c = 0, z = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const T v = d[i];
         const bool keep = v != (T)__builtin_huge_val() && v > (T)0;
         keys[i] = keep ? KO::key(v) : ~(K)0;
         c += keep ? 1 : 0;
+        z += v == (T)0 ? 1 : 0;  // (finite, not kept: the quantile's population has them)
     }
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-    if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = c;
+    for (int off = 32; off > 0; off >>= 1) {
+        c += __shfl_xor(c, off);
+        z += __shfl_xor(z, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wtot[threadIdx.x >> 6] = c;
+        wz[threadIdx.x >> 6] = z;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         const int tot = (wtot[0] + wtot[1]) + (wtot[2] + wtot[3]);
+        const int zt = (wz[0] + wz[1]) + (wz[2] + wz[3]);
         if (tot) atomicAdd(count, tot);
+        if (zt) atomicAdd(count + 2, zt);
     }
 }
 template <typename K>
@@ -742,6 +751,8 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     // reads no global memory)
     __shared__ long long c_P0[kChunkLds], c_C[2][kChunkLds];
     __shared__ int c_e[kChunkLds], c_nt0[kChunkLds];
+    __shared__ int t1_idx[kFastTies];  // a crossing chunk's binade e + 1 ties
+    __shared__ long long t1_pb[kFastTies], t1_m[kFastTies];
     if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     const int64_t c = *count;
@@ -843,33 +854,45 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
                 if (U0 + pr.P[0][j - kCumHead] + C >= LIM) first = li;
             }
             if (first != 0x7fffffff) atomicMin(&s_cross, first);
+            // binade e + 1's ties into LDS by the whole block (the serial
+            // resolution below then waits on no global load: one round trip
+            // per tie made the crossing chunks most of the walk)
+            const int nt1 = ch[b + 1].nt[1];
+            for (int k = t; k < nt1; k += kCumThreads) {
+                t1_idx[k] = pr.t_idx[1][b * kFastTies + k];
+                t1_pb[k] = pr.t_pb[1][b * kFastTies + k];
+                t1_m[k] = pr.t_m[1][b * kFastTies + k];
+            }
             __syncthreads();
             if (t == 0) {
                 VtChunk& q = ch[b + 1];
                 const int jc = s_cross;  // (exists: the chunk's last sum reaches 2^P)
                 const int e = q.e;
+                // (the three independent loads first, together)
+                const long long P0b = jc > 0 ? pr.P[0][lo + jc - 1 - kCumHead] : 0ll;
+                const T xc = KO::val(keys[lo + jc]);
+                const long long P1jc = pr.P[1][lo + jc - kCumHead];
+                const long long P1t = q.P[1];
                 T before = s;
                 if (jc > 0) {
                     int n0 = 0;  // ties at local indices <= jc - 1
                     while (n0 < nt0 && tie_idx[n0] <= jc - 1) ++n0;
                     const long long C = n0 > 0 ? (long long)tie_c[n0 - 1] : 0ll;
-                    before = (T)((double)(U0 + pr.P[0][lo + jc - 1 - kCumHead] + C) * ldexp(1.0, e - (P - 1)));
+                    before = (T)((double)(U0 + P0b + C) * ldexp(1.0, e - (P - 1)));
                 }
-                const T S1 = before + KO::val(keys[lo + jc]);  // the crossing step, in T
+                const T S1 = before + xc;  // the crossing step, in T
                 int mode = 0;
                 if (S1 >= CumBits<T>::min_normal() && CumBits<T>::binade(S1) == e + 1) {
                     // the rest of the chunk in binade e + 1: its ties in order
                     const long long U1 = CumBits<T>::units(S1);
-                    const long long P1jc = pr.P[1][lo + jc - kCumHead];
-                    const int nt1 = q.nt[1];
                     int up = 0;
                     for (int k = 0; k < nt1; ++k) {
-                        if (pr.t_idx[1][b * kFastTies + k] <= jc) continue;
-                        const long long bf = U1 + (pr.t_pb[1][b * kFastTies + k] - P1jc) + up;
-                        up += ((bf + pr.t_m[1][b * kFastTies + k]) & 1ll) ? 1 : 0;
+                        if (t1_idx[k] <= jc) continue;
+                        const long long bf = U1 + (t1_pb[k] - P1jc) + up;
+                        up += ((bf + t1_m[k]) & 1ll) ? 1 : 0;
                         pr.t_c1[b * kFastTies + k] = up;
                     }
-                    const long long fin = U1 + (q.P[1] - P1jc) + up;
+                    const long long fin = U1 + (P1t - P1jc) + up;
                     if (fin < LIM) {
                         q.S0 = (double)s;
                         q.par = par;
@@ -1122,9 +1145,54 @@ __global__ __launch_bounds__(256) void vt_frms_final_kernel(const T* __restrict_
     }
 }
 
+// VarTrimmed's quantile at the optimised ratio (OutlierFiltersImpl.cpp:
+// 221-223, Matches::getDistsQuantile) straight from the sort: the radix
+// select over the same distances finds the same order statistic, and its
+// population — the finite distances — is the zeros (not sort keys: the
+// partial sum takes the positive ones only) followed by the sorted positive
+// keys.  The rank rule and the final select state are select_all_kernel's
+// (pick_phase, pass 0); one thread, one load instead of the radix passes.
+template <typename T>
+__global__ void vt_quantile_kernel(const typename KeyOf<T>::K* __restrict__ sorted, const int* __restrict__ hdr,
+                                   const double* __restrict__ ratio_dev, SelectState* __restrict__ st,
+                                   int* __restrict__ iter_err, const LoopCtl* __restrict__ ctl) {
+    using KO = KeyOf<T>;
+    using K = typename KO::K;
+    if (threadIdx.x != 0 || (ctl && ctl->done)) return;
+    const unsigned long long zeros = (unsigned)hdr[2];
+    const unsigned long long total = (unsigned long long)(unsigned)hdr[0] + zeros;
+    const T q = (T)(*ratio_dev);
+    unsigned long long rank = 0;
+    int err = 0;
+    if (total == 0) {
+        err = -2;  // PMX_E_EMPTY_QUANTILE: ConvergenceError("no outlier to filter")
+    } else if (q < (T)0 || q > (T)1) {
+        err = -3;  // ConvergenceError("quantile must be between 0 and 1")
+    } else if (q == (T)1) {
+        rank = total - 1;  // max_element
+    } else {
+        rank = (unsigned long long)((T)total * q);
+        if (rank >= total) rank = total - 1;
+    }
+    st->err = err;
+    st->count = total;
+    st->ratio = (double)q;
+    st->rank = 0;
+    if (err) {
+        st->prefix = 0;
+        st->limit = __builtin_nan("");
+        __hip_atomic_store(iter_err, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const K key = rank < zeros ? KO::key((T)0) : sorted[rank - zeros];
+    st->prefix = (unsigned long long)key;
+    st->limit = (double)KO::val(key);
+}
+
 template <typename T>
 void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRatio, const T* deno, void* scratch,
-                    size_t scratch_bytes, double* ratio_dev, int* err_dev, const LoopCtl* ctl, hipStream_t s) {
+                    size_t scratch_bytes, double* ratio_dev, int* err_dev, SelectState* st, const LoopCtl* ctl,
+                    hipStream_t s) {
     (void)scratch_bytes;
     using K = typename KeyOf<T>::K;
     char* p = static_cast<char*>(scratch);
@@ -1188,6 +1256,7 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
                        part_i, ctl);
     hipLaunchKernelGGL(vt_frms_final_kernel<T>, dim3(1), dim3(256), 0, s, part_v, part_i, hdr, minEl, maxEl,
                        points_nbr, ratio_dev, hdr + 1, err_dev, ctl);
+    hipLaunchKernelGGL(vt_quantile_kernel<T>, dim3(1), dim3(64), 0, s, src, hdr, ratio_dev, st, err_dev, ctl);
 }
 
 // explicit instantiations
@@ -1206,9 +1275,9 @@ template void launch_select_all<double>(const double*, int64_t, void*, SelectSta
                                         const LoopCtl*, SpecSel*, const unsigned long long*, unsigned long long*,
                                         hipStream_t);
 template void launch_vartrim<float>(const float*, int64_t, int, float, float, const float*, void*, size_t, double*,
-                                    int*, const LoopCtl*, hipStream_t);
+                                    int*, SelectState*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,
-                                     double*, int*, const LoopCtl*, hipStream_t);
+                                     double*, int*, SelectState*, const LoopCtl*, hipStream_t);
 template size_t vartrim_scratch_bytes<float>(int64_t);
 template size_t vartrim_scratch_bytes<double>(int64_t);
 
