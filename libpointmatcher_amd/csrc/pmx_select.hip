@@ -746,6 +746,8 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     __shared__ int s_mode;
     __shared__ long long s_U0;
     __shared__ int s_par;
+    __shared__ long long s_lo;                  // the walk's position (chunk start, chunk)
+    __shared__ int s_b;
     __shared__ T s_run;                         // the running sum after the chunk
     // the chunk table of the fast test (the walk's per-chunk decision then
     // reads no global memory)
@@ -785,44 +787,59 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     __syncthreads();
     T s = s_run;
     __syncthreads();
-    for (int64_t lo = ph, b = 0; lo < c; lo += kCumChunk, ++b) {  // (uniform)
-        const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
+    // The walk.  Thread 0 settles a run of fast chunks in one go (no block
+    // barrier between them: one per chunk made the ~50 fast chunks of a 1M
+    // sum most of the walk); the block then takes the first chunk that is
+    // not fast, as a crossing or through the passes.
+    int64_t lo = ph;
+    int b = 0;
+    while (lo < c) {  // (uniform)
         if (t == 0) {
             // 1 fast: the guessed binade is the running sum's, few ties, and
             // the chunk's last sum stays below the next binade (O(1): the
             // ties were resolved for both parities of the start);
             // 2 a crossing to examine; 0 the passes
-            const bool inl = b < kChunkLds;
-            const int e = inl ? c_e[b] : ch[b + 1].e;
-            const int nt0 = inl ? c_nt0[b] : ch[b + 1].nt[0];
+            T sr = s;
             int mode = 0;
-            // (s normal: units() adds the hidden bit)
-            if (nt0 <= kFastTies && s >= CumBits<T>::min_normal() && CumBits<T>::binade(s) == e) {
-                const long long U0 = CumBits<T>::units(s);
+            for (; lo < c; lo += kCumChunk, ++b) {
+                const bool inl = b < kChunkLds;
+                const int e = inl ? c_e[b] : ch[b + 1].e;
+                const int nt0 = inl ? c_nt0[b] : ch[b + 1].nt[0];
+                mode = 0;
+                // (sr normal: units() adds the hidden bit)
+                if (!(nt0 <= kFastTies && sr >= CumBits<T>::min_normal() && CumBits<T>::binade(sr) == e)) break;
+                const long long U0 = CumBits<T>::units(sr);
                 const int par = (int)(U0 & 1ll);
-                const long long fin = U0 + (inl ? c_P0[b] : ch[b + 1].P[0]) + (inl ? c_C[par][b] : ch[b + 1].C[par]);
+                const long long fin =
+                    U0 + (inl ? c_P0[b] : ch[b + 1].P[0]) + (inl ? c_C[par][b] : ch[b + 1].C[par]);
                 VtChunk& q = ch[b + 1];
                 if (fin < LIM) {
-                    q.S0 = (double)s;
+                    q.S0 = (double)sr;
                     q.par = par;
                     q.ok = 1;
-                    s_run = (T)((double)fin * ldexp(1.0, e - (P - 1)));
-                    mode = 1;
-                } else if (q.nt[1] <= kFastTies) {
+                    sr = (T)((double)fin * ldexp(1.0, e - (P - 1)));
+                    continue;
+                }
+                if (q.nt[1] <= kFastTies) {
                     s_U0 = U0;
                     s_par = par;
                     mode = 2;
                 }
+                break;
             }
+            s_run = sr;
+            s_lo = lo;
+            s_b = b;
             s_mode = mode;
             s_cross = 0x7fffffff;
         }
         __syncthreads();
-        if (s_mode == 1) {
-            s = s_run;
-            __syncthreads();
-            continue;
-        }
+        s = s_run;
+        lo = s_lo;
+        b = s_b;
+        __syncthreads();  // (read before thread 0 rewrites them)
+        if (lo >= c) break;
+        const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
         if (s_mode == 2) {
             // the first step whose units reach 2^P: every thread over its
             // keys' stored prefix, with the ties' rounding for this start
@@ -909,6 +926,8 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
             if (s_mode == 3) {
                 s = s_run;
                 __syncthreads();
+                lo += kCumChunk;
+                ++b;
                 continue;
             }
         }
@@ -1048,6 +1067,8 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
             }
             __syncthreads();
         }
+        lo += kCumChunk;
+        ++b;
     }
 }
 
