@@ -1263,6 +1263,17 @@ int pmx_vartrim_partial_sums(pmx_ctx* c, void* out, int64_t capacity, int64_t* c
     const char* cum = (const char*)c->d_vt + 256 + 2 * al(ksz * (size_t)c->vt_n);
     HIPCHK(c, hipMemcpyAsync(out, cum, ksz * (size_t)cnt, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (g_vt_trace) {  // (development trace of the last walk, PMX_VT_TRACE)
+        const int mx = vartrim_trace_max();
+        std::vector<unsigned long long> tr(2 * (size_t)mx + 1);
+        const size_t off = c->dtype == PMX_F64 ? vartrim_trace_offset<double>(c->vt_n) : vartrim_trace_offset<float>(c->vt_n);
+        HIPCHK(c, hipMemcpy(tr.data(), (const char*)c->d_vt + off, 8 * tr.size(), hipMemcpyDeviceToHost));
+        const int nm = (int)std::min<unsigned long long>(tr[2 * (size_t)mx], (unsigned long long)mx);
+        for (int i = 0; i < nm; ++i)
+            std::fprintf(stderr, "vt_trace %d t=%.2fus type=%llu chunk=%llu detail=%llu\n", i,
+                         (double)(tr[2 * i] - tr[0]) * 0.01, tr[2 * i + 1] >> 56, (tr[2 * i + 1] >> 24) & 0xffffffffull,
+                         tr[2 * i + 1] & 0xffffffull);
+    }
     return PMX_OK;
 }
 

@@ -436,6 +436,12 @@ void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, doubl
 int select_bins(int pass, int key_bits);
 
 // VarTrimmed pieces
+// development trace of the VarTrimmed walk (PMX_VT_TRACE=1): printed by
+// pmx_vartrim_partial_sums
+extern int g_vt_trace;
+template <typename T>
+size_t vartrim_trace_offset(int64_t n);
+int vartrim_trace_max();
 template <typename T>
 void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRatio, const T* deno,
                     void* scratch, size_t scratch_bytes, double* ratio_dev, int* err_dev, SelectState* st,

@@ -459,6 +459,8 @@ struct VtPrep {
     int* t_c1;           // binade e + 1: the same after a crossing (written by the walk)
 };
 
+constexpr int kVtTraceMax = 2048;  // (development trace of the walk: marks, then the count)
+
 static int64_t vt_chunks(int64_t n) { return n > kCumHead ? (n - kCumHead + kCumChunk - 1) / kCumChunk : 0; }
 
 template <typename T>
@@ -467,7 +469,8 @@ size_t vartrim_scratch_bytes(int64_t n) {
     const int64_t nch = vt_chunks(n);
     return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(8 * 256) +
            al256(vt_sort_temp_bytes<K>(n)) + al256(sizeof(VtChunk) * (nch + 1)) + 2 * al256(8 * (size_t)n) +
-           al256((size_t)kFastTies * nch * (4 * sizeof(long long) + 5 * sizeof(int)));
+           al256((size_t)kFastTies * nch * (4 * sizeof(long long) + 5 * sizeof(int))) +
+           al256(8 * (2 * (size_t)kVtTraceMax + 1));
 }
 
 // this thread's kCumPer keys from j0 (16-byte loads when in range)
@@ -728,12 +731,24 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typen
     }
 }
 
+int g_vt_trace = 0;
 template <typename T>
 __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
                                                                 const int* __restrict__ count, T* __restrict__ cum,
                                                                 VtChunk* __restrict__ ch, VtPrep pr, int nch,
-                                                                const LoopCtl* __restrict__ ctl) {
+                                                                const LoopCtl* __restrict__ ctl,
+                                                                unsigned long long* __restrict__ trace) {
     using KO = KeyOf<T>;
+    // (development trace, PMX_VT_TRACE: thread 0 stamps each step of the walk
+    // with the 100 MHz real-time counter; pmx_vartrim_partial_sums prints it)
+    int nmark = 0;
+#define VT_MARK(type, bb, detail)                                                                               \
+    if (trace && threadIdx.x == 0 && nmark < kVtTraceMax) {                                                     \
+        trace[2 * nmark] = __builtin_amdgcn_s_memrealtime();                                                    \
+        trace[2 * nmark + 1] = ((unsigned long long)(type) << 56) | ((unsigned long long)(unsigned)(bb) << 24) | \
+                               ((unsigned long long)(detail) & 0xffffffull);                                    \
+        ++nmark;                                                                                                \
+    }
     constexpr int P = CumBits<T>::P;
     constexpr long long LIM = 1ll << P;
     __shared__ long long wsum[kCumThreads / 64];
@@ -784,6 +799,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         }
         s_run = acc;
     }
+    VT_MARK(1, 0, ph);
     __syncthreads();
     T s = s_run;
     __syncthreads();
@@ -828,6 +844,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
                 break;
             }
             s_run = sr;
+            VT_MARK(2, b, mode);
             s_lo = lo;
             s_b = b;
             s_mode = mode;
@@ -923,6 +940,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
                 s_mode = mode;
             }
             __syncthreads();
+            VT_MARK(3, b, s_mode);
             if (s_mode == 3) {
                 s = s_run;
                 __syncthreads();
@@ -933,6 +951,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         }
         int64_t p = lo;
         while (p < cend) {  // (uniform) passes over [p, cend)
+            VT_MARK(4, b, p - lo);
             const int eb = CumBits<T>::binade(s);
             const UScale inv_u = uscale(P - 1 - eb);  // 1 / ulp(2^eb)
             const double u = ldexp(1.0, eb - (P - 1));
@@ -1070,6 +1089,9 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         lo += kCumChunk;
         ++b;
     }
+    VT_MARK(7, b, 0);
+    if (trace && threadIdx.x == 0) trace[2 * kVtTraceMax] = (unsigned long long)nmark;
+#undef VT_MARK
 }
 
 // FRMS_j = (cum[minEl+j] * (1/id)) * ((1/deno)^2), first argmin; writes the
@@ -1253,6 +1275,7 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
         pr.t_c0[0] = ii + 2 * F;
         pr.t_c0[1] = ii + 3 * F;
         pr.t_c1 = ii + 4 * F;
+        p += al256(F * (4 * sizeof(long long) + 5 * sizeof(int)));
     }
 
     (void)hipMemsetAsync(hdr, 0, 256, s);
@@ -1267,7 +1290,9 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
         hipLaunchKernelGGL(vt_chunk_prep_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
                            ctl);
     }
-    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ch, pr, (int)nch, ctl);
+    unsigned long long* trace = g_vt_trace ? reinterpret_cast<unsigned long long*>(p) : nullptr;
+    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ch, pr, (int)nch, ctl,
+                       trace);
     if (nch > 0)
         hipLaunchKernelGGL(vt_chunk_write_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
                            cum, ctl);
@@ -1299,6 +1324,13 @@ template void launch_vartrim<float>(const float*, int64_t, int, float, float, co
                                     int*, SelectState*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,
                                      double*, int*, SelectState*, const LoopCtl*, hipStream_t);
+template <typename T>
+size_t vartrim_trace_offset(int64_t n) {
+    return vartrim_scratch_bytes<T>(n) - al256(8 * (2 * (size_t)kVtTraceMax + 1));
+}
+int vartrim_trace_max() { return kVtTraceMax; }
+template size_t vartrim_trace_offset<float>(int64_t);
+template size_t vartrim_trace_offset<double>(int64_t);
 template size_t vartrim_scratch_bytes<float>(int64_t);
 template size_t vartrim_scratch_bytes<double>(int64_t);
 
