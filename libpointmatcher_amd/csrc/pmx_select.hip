@@ -862,10 +862,29 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
             // keys' stored prefix, with the ties' rounding for this start
             const long long U0 = s_U0;
             const int par = s_par;
-            const int nt0 = ch[b + 1].nt[0];
+            const int nt0 = ch[b + 1].nt[0], nt1 = ch[b + 1].nt[1];
+            // this thread's 16 stored prefixes, all loads issued before any
+            // is used (a use-then-load loop made them 16 dependent round
+            // trips: 12-18 us per crossing chunk)
+            const int64_t jt = lo + (int64_t)t * kCumPer;
+            long long pv[kCumPer];
+            if (jt + kCumPer <= cend) {
+#pragma unroll
+                for (int i = 0; i < kCumPer; ++i) pv[i] = pr.P[0][jt + i - kCumHead];
+            } else {
+#pragma unroll
+                for (int i = 0; i < kCumPer; ++i) pv[i] = jt + i < cend ? pr.P[0][jt + i - kCumHead] : 0ll;
+            }
+            // the ties of binades e and e + 1 into LDS by the whole block (the
+            // serial resolution below then waits on no global load)
             for (int k = t; k < nt0; k += kCumThreads) {
                 tie_idx[k] = pr.t_idx[0][b * kFastTies + k];
                 tie_c[k] = pr.t_c0[par][b * kFastTies + k];
+            }
+            for (int k = t; k < nt1; k += kCumThreads) {
+                t1_idx[k] = pr.t_idx[1][b * kFastTies + k];
+                t1_pb[k] = pr.t_pb[1][b * kFastTies + k];
+                t1_m[k] = pr.t_m[1][b * kFastTies + k];
             }
             __syncthreads();
             int kt = 0;
@@ -882,21 +901,10 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
             for (int i = 0; i < kCumPer; ++i) {
                 const int li = t * kCumPer + i;
                 if (kt < nt0 && tie_idx[kt] == li) ++kt;
-                const int64_t j = lo + li;
-                if (j >= cend || first != 0x7fffffff) continue;
                 const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
-                if (U0 + pr.P[0][j - kCumHead] + C >= LIM) first = li;
+                if (jt + i < cend && first == 0x7fffffff && U0 + pv[i] + C >= LIM) first = li;
             }
             if (first != 0x7fffffff) atomicMin(&s_cross, first);
-            // binade e + 1's ties into LDS by the whole block (the serial
-            // resolution below then waits on no global load: one round trip
-            // per tie made the crossing chunks most of the walk)
-            const int nt1 = ch[b + 1].nt[1];
-            for (int k = t; k < nt1; k += kCumThreads) {
-                t1_idx[k] = pr.t_idx[1][b * kFastTies + k];
-                t1_pb[k] = pr.t_pb[1][b * kFastTies + k];
-                t1_m[k] = pr.t_m[1][b * kFastTies + k];
-            }
             __syncthreads();
             if (t == 0) {
                 VtChunk& q = ch[b + 1];
@@ -1024,14 +1032,21 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
                 __syncthreads();
                 continue;
             }
-            if (t == 0) {
-                int up = 0;
-                for (int k = 0; k < nt; ++k) {
-                    const long long before = S0 + tie_pb[k] + up;  // (saturated P: the crossing is before it)
-                    up += ((before + tie_m[k]) & 1ll) ? 1 : 0;
-                    tie_c[k] = up;
-                }
-                s_cross = 0x7fffffff;
+            // the ties' rounding, in parallel: tie k rounds up iff the units
+            // before it plus m_k are odd, i.e. c_k ^ parity(up_(k-1)) with
+            // c_k = (S0 + pb_k + m_k) & 1 — and then parity(up_k) = c_k.  So
+            // tie k rounds up iff c_k != c_(k-1) (c_(-1) = 0), and up_k is a
+            // prefix sum of those (a serial loop over the ties before; past a
+            // crossing the saturated values are as meaningless either way)
+            {
+                static_assert(kCumMaxTies <= kCumThreads, "one tie per thread");
+                const int ck = t < nt ? (int)((S0 + tie_pb[t] + tie_m[t]) & 1ll) : 0;
+                const int cp = t > 0 && t - 1 < nt ? (int)((S0 + tie_pb[t - 1] + tie_m[t - 1]) & 1ll) : 0;
+                const long long inc = t < nt ? (long long)(ck ^ cp) : 0ll;
+                long long ttot;
+                const long long upx = block_excl_scan_ll(inc, wsum, ttot);
+                if (t < nt) tie_c[t] = (int)(upx + inc);
+                if (t == 0) s_cross = 0x7fffffff;
             }
             __syncthreads();
             // every element's sum in units of u; the first that leaves the binade
