@@ -767,6 +767,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     // the chunk table of the fast test (the walk's per-chunk decision then
     // reads no global memory)
     __shared__ long long c_P0[kChunkLds], c_C[2][kChunkLds];
+    __shared__ double c_sum[kChunkLds];
     __shared__ int c_e[kChunkLds], c_nt0[kChunkLds];
     __shared__ int t1_idx[kFastTies];  // a crossing chunk's binade e + 1 ties
     __shared__ long long t1_pb[kFastTies], t1_m[kFastTies];
@@ -782,6 +783,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         c_C[1][i] = q.C[1];
         c_e[i] = q.e;
         c_nt0[i] = q.nt[0];
+        c_sum[i] = q.sum;
     }
     // the head sequentially (keys staged in LDS by the whole block: the one
     // summing thread then waits on no global load)
@@ -822,6 +824,13 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
                 const int e = inl ? c_e[b] : ch[b + 1].e;
                 const int nt0 = inl ? c_nt0[b] : ch[b + 1].nt[0];
                 mode = 0;
+                // a chunk whose keys add up to 3 x the running sum or more
+                // crosses two binades or more: summed in order by thread 0
+                // (4) — one pass per crossing cost more (~19 us each)
+                if ((double)sr + (inl ? c_sum[b] : ch[b + 1].sum) >= 4.0 * (double)sr) {
+                    mode = 4;
+                    break;
+                }
                 // (sr normal: units() adds the hidden bit)
                 if (!(nt0 <= kFastTies && sr >= CumBits<T>::min_normal() && CumBits<T>::binade(sr) == e)) break;
                 const long long U0 = CumBits<T>::units(sr);
@@ -857,6 +866,30 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         __syncthreads();  // (read before thread 0 rewrites them)
         if (lo >= c) break;
         const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
+        if (s_mode == 4) {
+            // in order, from keys staged in LDS by the block (as the head)
+            T acc = s;
+            for (int64_t a0 = lo; a0 < cend; a0 += kCumHead) {  // (uniform)
+                const int nk = (int)(cend - a0 < kCumHead ? cend - a0 : kCumHead);
+                for (int j = t; j < nk; j += kCumThreads) s_head[j] = keys[a0 + j];
+                __syncthreads();
+                if (t == 0) {
+#pragma unroll 8
+                    for (int j = 0; j < nk; ++j) {
+                        acc = acc + KO::val(s_head[j]);
+                        cum[a0 + j] = acc;
+                    }
+                    s_run = acc;
+                }
+                __syncthreads();
+            }
+            s = s_run;
+            VT_MARK(5, b, 0);
+            __syncthreads();
+            lo += kCumChunk;
+            ++b;
+            continue;
+        }
         if (s_mode == 2) {
             // the first step whose units reach 2^P: every thread over its
             // keys' stored prefix, with the ties' rounding for this start
