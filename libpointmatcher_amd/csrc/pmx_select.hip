@@ -409,27 +409,19 @@ __device__ __forceinline__ long long cum_block_scan(long long v, long long lim, 
     return sat_add(before, incl - v, lim);
 }
 
-// The head (the first kCumHead keys, where the running sum leaves its binade
-// every few keys) is summed sequentially; the rest is cut into chunks of
-// kCumChunk keys.  vt_chunk_prep_kernel prepares every chunk in parallel
-// under the binade e GUESSED from a double prefix of the chunk sums, and under
-// e + 1: the integer prefixes P_e[j], P_e+1[j] of rnd(x / u) (stored), the
-// ties of both binades, and for binade e the ties' rounding already resolved
-// for an even and for an odd start: the parity of S0 / u decides every tie of
-// the chunk (the units before tie k are S0 + pb_k + up_k-1, so their parity
-// is that of S0 plus integers known beforehand).  vt_cumsum_kernel then walks
-// the chunks in order with the exact running sum S:
-//   fast   S in binade e, S / u + P_e + C_e[parity] < 2^P: the chunk's end
-//          sum in O(1) from the chunk table (preloaded in LDS);
-//   cross  the sum leaves binade e inside the chunk: the crossing step (the
-//          first j whose units reach 2^P, found by the whole block over the
-//          stored P_e) is a plain T addition, and when it lands in binade
-//          e + 1 and the rest of the chunk stays there, the rest's sums are
-//          the e + 1 prefix from there (its few ties resolved in order);
-//   slow   anything else (a wrong guess, many ties, two crossings, a
-//          subnormal sum): the passes below, which write the chunk's sums.
-// vt_chunk_write_kernel writes the fast and crossing chunks' sums in
-// parallel.  Every path computes the sequential loop's bits.
+// The keys are cut into the head (the first kCumHead keys, where the running
+// sum leaves its binade every few keys) and chunks of kCumChunk keys.
+// vt_chunk_prep_kernel prepares every chunk in parallel under the binade e
+// GUESSED from a double prefix of the chunk sums: the integer prefixes P_e[j]
+// of rnd(x / u) (stored), the chunk's ties, and their rounding resolved for an
+// even and for an odd start (the parity of S0 / u decides every tie of the
+// chunk).  vt_cumsum_kernel — one wave — then walks the chunks in order with
+// the exact running sum S: a chunk whose guess is S's binade, with few ties,
+// and whose last sum stays below the next binade is FAST (its end sum in O(1)
+// from the chunk table; vt_chunk_write_kernel writes its sums in parallel
+// afterwards); the head and every other chunk (a crossing, a wrong guess,
+// many ties, a subnormal sum) run through vt_wave_pass, which writes their
+// sums.  Every path computes the sequential loop's bits.
 constexpr int kCumChunk = kCumThreads * kCumPer;
 constexpr int kCumHead = 4096;
 constexpr int kFastTies = 256;
