@@ -170,7 +170,6 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_RED_TAIL")) c->red_tail = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_VT_TRACE")) g_vt_trace = std::atoi(e);
     if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
     // test hook: device-loop iterations (0-based, comma separated) whose
@@ -236,8 +235,6 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (hipMalloc(&c->d_selx, selx_bytes()) != hipSuccess) return bad(PMX_E_HIP);
     (void)hipMemset(c->d_selx, 0, selx_bytes());
     if (hipMalloc((void**)&c->d_partials, sizeof(double) * kRedBlocks * kNVMax) != hipSuccess) return bad(PMX_E_HIP);
-    if (hipMalloc((void**)&c->d_ticket, 256) != hipSuccess) return bad(PMX_E_HIP);
-    (void)hipMemset(c->d_ticket, 0, 256);
     if (hipHostMalloc((void**)&c->h_result, kBlkBytes, hipHostMallocDefault) != hipSuccess) return bad(PMX_E_HIP);
     *out = c;
     return PMX_OK;
@@ -252,7 +249,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_result, c->d_waves, c->d_vpart,
                     c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
-                    c->d_rob, c->d_rdev, c->d_radii, c->d_ticket, c->d_rd_p4, c->d_rd_sorted};
+                    c->d_rob, c->d_rdev, c->d_radii, c->d_rd_p4, c->d_rd_sorted};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();

@@ -990,18 +990,12 @@ int p2plane_enqueue(pmx_ctx* c) {
     const WChain<T> chain = chain_of<T>(c);
     const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
-    // (the launch's last block sums the partials itself)
-    RedTail tail;
-    if (c->red_tail) {
-        tail.ticket = c->d_ticket;
-        tail.out = c->d_result;
-    }
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
                               match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
                               loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->vpart_dirty ? c->d_vpart : nullptr,
-                              tail, c->stream);
+                              c->stream);
     c->vpart_dirty = false;
-    if (!tail.ticket) launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result, NV);
 }
@@ -1017,24 +1011,15 @@ int p2point_enqueue(pmx_ctx* c) {
         chain.w_arr = (const T*)c->d_w;
     }
     const GridDesc<T>* gd = (const GridDesc<T>*)c->d_gdesc;
-    // each pass's last block sums the partials (and, on one rank, pass 1's
-    // the means: the all-reduce of several ranks comes between)
-    RedTail t1, t2;
-    if (c->red_tail) {
-        t1.ticket = t2.ticket = c->d_ticket;
-        t1.out = c->d_result;
-        t2.out = c->d_result + 16;
-        if (!sharded(c)) t1.means = c->d_means;
-    }
     launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
-                            chain, c->knn, c->N, c->d_partials, loop_ctl(c), gd, t1, c->dim, c->stream);
-    if (!t1.ticket) launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, loop_ctl(c), c->stream);
+                            chain, c->knn, c->N, c->d_partials, loop_ctl(c), gd, c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, loop_ctl(c), c->stream);
     int rc = allreduce_f64(c, c->d_result, 11);
     if (rc) return rc;
-    if (!t1.means) launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, loop_ctl(c), c->stream);
+    launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, loop_ctl(c), c->stream);
     launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
-                            chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, loop_ctl(c), gd, t2, c->stream);
-    if (!t2.ticket) launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, loop_ctl(c), c->stream);
+                            chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, loop_ctl(c), gd, c->stream);
+    launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result + 16, 9);
 }

@@ -197,11 +197,6 @@ struct pmx_ctx {
 
     // reductions
     double* d_partials = nullptr;
-    unsigned* d_ticket = nullptr;  // the reductions' in-launch finalize ticket (RedTail; zero between launches)
-    // in-launch finalize (PMX_RED_TAIL=1) instead of the finalize launch: off,
-    // measured slower at C3 (0.078 vs 0.068 ms/iteration: the last block's
-    // ticket and write-through hand-off cost more than the kernel boundary)
-    bool red_tail = false;
     double* d_result = nullptr;  // [0..63] system, [64..127] second pass
     void* d_means = nullptr;
     double* h_result = nullptr;  // pinned

@@ -463,27 +463,22 @@ constexpr int p2plane_nv_full(int dim) { return dim == 3 ? 36 + 6 + 5 : 9 + 3 + 
 // interleaved point / normal records, ref = gpn, nrm = gpn + 1)
 // vzero (may be null): the match's spread counters, zeroed by block 0 (a
 // counter phase merged into the select launch read them)
-// tail (pmx_p2plane.h RedTail): ticket non-null = the launch's last block
-// sums the partials into tail.out itself (no launch_finalize), and point-to-
-// point pass 1 writes the means too when tail.means is set
-struct RedTail;
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
-                            const RedTail& tail, hipStream_t s);
+                            hipStream_t s);
 void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
                           const int32_t* ids, const WChain<T>& chain, int k, int64_t N, double* partials,
-                          const LoopCtl* ctl, const GridDesc<T>* gd, const RedTail& tail, int dim, hipStream_t s);
+                          const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 template <typename T>
 void launch_p2point_means(const double* sums, T* means_dev, int dim, const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
                           const int32_t* ids, const WChain<T>& chain, int k, int64_t N, const T* means_dev,
-                          double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, const RedTail& tail,
-                          hipStream_t s);
+                          double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 template <typename T>
 void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, const P4<T>* rd, const Mat4<T>& Tm,
                           const P4<T>* ref, const P4<T>* nrm, int rs, const int32_t* ids, int k, hipStream_t s);

@@ -85,70 +85,6 @@ __device__ __forceinline__ void block_store(double (&acc)[NV], double* __restric
     }
 }
 
-// In-launch finalize.  Every block stores its partials with agent-scope
-// (sc1) stores (block_store<NV, true>), waits for them, and one lane draws a
-// ticket; the block that draws the last one sums every block's partials —
-// with sc1 loads — in finalize_kernel's order (so the sums are bit-identical
-// to the separate launch it replaces: two blocks per thread, the wave
-// butterfly, then the four waves' tree) and writes out[0, NV).  Saves the
-// finalize launch and its kernel boundary; the ticket is reset by the last
-// block (zeroed once at allocation).  Returns true in that block (all its
-// threads); *vals then points at the NV sums in LDS (read them there: the
-// block's own global stores are not re-read through L1).
-struct RedTail {
-    unsigned* ticket = nullptr;  // null: no in-launch finalize (a finalize launch follows)
-    double* out = nullptr;
-    void* means = nullptr;       // point-to-point pass 1: the means in T (p2point_means_kernel), when not sharded
-};
-constexpr int kTailChunk = 16;
-template <int NV>
-__device__ __forceinline__ bool reduce_tail(const double* __restrict__ partials, const RedTail& rt,
-                                            const double** vals = nullptr) {
-    static_assert(kRedBlocks == 512, "reduce_tail assumes two partials per thread");
-    __shared__ int last;
-    __shared__ double red[NV][4];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's partial stores have completed)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(rt.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = prev == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return false;
-    const int t = threadIdx.x, wave = t >> 6;
-    // (kTailChunk values at a time: all NV in flight at once would raise the
-    // kernel's VGPR count for its main loop too — 158 -> 213, 3 -> 2 waves
-    // per SIMD for the point-to-plane kernel)
-    constexpr int C = NV < kTailChunk ? NV : kTailChunk;
-#pragma unroll 1
-    for (int v0 = 0; v0 < NV; v0 += C) {
-        double s[C];
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-            const int v = v0 + j < NV ? v0 + j : NV - 1;
-            const double* p = partials + (size_t)v * kRedBlocks;
-            const double a = __hip_atomic_load(p + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const double b = __hip_atomic_load(p + t + 256, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s[j] = (0.0 + a) + b;
-        }
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-            const double w = wave_sum(s[j]);
-            if ((t & 63) == 0 && v0 + j < NV) red[v0 + j][wave] = w;
-        }
-    }
-    __shared__ double fin[NV];
-    __syncthreads();
-    if (t < NV) {
-        const double f = (red[t][0] + red[t][1]) + (red[t][2] + red[t][3]);
-        fin[t] = f;
-        rt.out[t] = f;
-    }
-    if (t == 0) __hip_atomic_store(rt.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (vals) *vals = fin;
-    return true;
-}
 
 // one kept pair: F and dot in T exactly as PointToPlane.cpp:171-243, the
 // upper triangle of F F^T and F dot added in fp64
@@ -196,7 +132,7 @@ __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const
                                              const P4<T>* __restrict__ ref, const P4<T>* __restrict__ nrm, int rs,
                                              const T* __restrict__ d, const int32_t* __restrict__ ids,
                                              const WChain<T>& chain, int k, int64_t N,
-                                             double* __restrict__ partials, const RedTail& tail = RedTail()) {
+                                             double* __restrict__ partials) {
     constexpr int NF = DIM == 3 ? 6 : 3;
     constexpr int NS = NF * (NF + 1) / 2;
     constexpr int NV = NS + NF + 5;  // (the fifth counter, sum of w, is the kept count with 0/1 weights)
@@ -279,12 +215,7 @@ __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const
         }
         if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
     }
-    if (tail.ticket) {
-        block_store<NV, true>(acc, partials);
-        (void)reduce_tail<NV>(partials, tail);
-    } else {
-        block_store<NV, kCoherent>(acc, partials);
-    }
+    block_store<NV, kCoherent>(acc, partials);
 }
 
 }  // namespace pmx

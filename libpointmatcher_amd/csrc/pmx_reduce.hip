@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                                                               int k, int64_t N, double* __restrict__ partials,
                                                               const LoopCtl* __restrict__ ctl,
                                                               const GridDesc<T>* __restrict__ gd,
-                                                              unsigned long long* __restrict__ vzero, RedTail tail) {
+                                                              unsigned long long* __restrict__ vzero) {
     if (ctl) {  // device loop
         if (ctl->done) return;
         ctl_transform(ctl, Tm);
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
     }
     if (vzero && blockIdx.x == 0)  // (the spread counters the merged counter phase read, for the next match)
         for (int c = 0; c < 4; ++c) vzero[(size_t)(c * kVSlots + threadIdx.x) * kVStride] = 0ull;
-    p2plane_body<T, DIM>(rd, Tm, ref, nrm, rs, d, ids, chain, k, N, partials, tail);
+    p2plane_body<T, DIM>(rd, Tm, ref, nrm, rs, d, ids, chain, k, N, partials);
 }
 
 // Real-valued weights (a RobustOutlierFilter in the chain; per-module path):
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void p2plane_weighted_kernel(const P4<T>* __re
                                                                const int32_t* __restrict__ ids, WChain<T> chain,
                                                                int k, int64_t N, double* __restrict__ partials,
                                                                const LoopCtl* __restrict__ ctl,
-                                                               const GridDesc<T>* __restrict__ gd, RedTail tail) {
+                                                               const GridDesc<T>* __restrict__ gd) {
     if (ctl) {  // device loop (a robust chain): transform and level from the device
         if (ctl->done) return;
         ctl_transform(ctl, Tm);
@@ -159,34 +159,29 @@ __global__ __launch_bounds__(256) void p2plane_weighted_kernel(const P4<T>* __re
         }
         if (!exist) acc[NS + NF + 3] += 1.0;
     }
-    if (!tail.ticket) {
-        block_store<NV>(acc, partials);
-        return;
-    }
-    block_store<NV, true>(acc, partials);
-    (void)reduce_tail<NV>(partials, tail);
+    block_store<NV>(acc, partials);
 }
 
 template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
-                            const RedTail& tail, hipStream_t s) {
+                            hipStream_t s) {
     if (chain.robust) {  // real-valued weights: the full asymmetric A
         if (dim == 3)
             hipLaunchKernelGGL((p2plane_weighted_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
-                               rs, d, ids, chain, k, N, partials, ctl, gd, tail);
+                               rs, d, ids, chain, k, N, partials, ctl, gd);
         else
             hipLaunchKernelGGL((p2plane_weighted_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
-                               rs, d, ids, chain, k, N, partials, ctl, gd, tail);
+                               rs, d, ids, chain, k, N, partials, ctl, gd);
         return;
     }
     if (dim == 3)
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
-                           d, ids, chain, k, N, partials, ctl, gd, vzero, tail);
+                           d, ids, chain, k, N, partials, ctl, gd, vzero);
     else
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
-                           d, ids, chain, k, N, partials, ctl, gd, vzero, tail);
+                           d, ids, chain, k, N, partials, ctl, gd, vzero);
 }
 
 // Sum the per-block partials: one block per accumulator, each thread adds a
@@ -218,8 +213,7 @@ __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restr
                                                             const int32_t* __restrict__ ids, WChain<T> chain, int k,
                                                             int64_t N, double* __restrict__ partials,
                                                             const LoopCtl* __restrict__ ctl,
-                                                            const GridDesc<T>* __restrict__ gd, RedTail tail,
-                                                            int dim) {
+                                                            const GridDesc<T>* __restrict__ gd) {
     constexpr int NV = 11;
     if (ctl) {  // device loop
         if (ctl->done) return;
@@ -261,28 +255,15 @@ __global__ __launch_bounds__(256) void p2point_pass1_kernel(const P4<T>* __restr
         }
         if (!exist) acc[10] += 1.0;
     }
-    if (!tail.ticket) {
-        block_store<NV>(acc, partials);
-        return;
-    }
-    block_store<NV, true>(acc, partials);
-    const double* sums = nullptr;
-    if (!reduce_tail<NV>(partials, tail, &sums) || !tail.means || threadIdx.x != 0) return;
-    // (single rank: p2point_means_kernel's arithmetic on the final sums)
-    T* means = (T*)tail.means;
-    const T winv = (T)1 / (T)sums[0];
-    for (int r = 0; r < 3; ++r) {
-        means[r] = r < dim ? (T)sums[1 + r] * winv : (T)0;
-        means[3 + r] = r < dim ? (T)sums[4 + r] * winv : (T)0;
-    }
+    block_store<NV>(acc, partials);
 }
 
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
                           const WChain<T>& chain, int k, int64_t N, double* partials, const LoopCtl* ctl,
-                          const GridDesc<T>* gd, const RedTail& tail, int dim, hipStream_t s) {
+                          const GridDesc<T>* gd, hipStream_t s) {
     hipLaunchKernelGGL(p2point_pass1_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, chain, k, N,
-                       partials, ctl, gd, tail, dim);
+                       partials, ctl, gd);
 }
 
 // means in T: w_sum_inv = 1 / w.sum(); mean = sum * w_sum_inv (PointToPoint.cpp:67-72)
@@ -311,7 +292,7 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
                                                             int64_t N, const T* __restrict__ means,
                                                             double* __restrict__ partials,
                                                             const LoopCtl* __restrict__ ctl,
-                                                            const GridDesc<T>* __restrict__ gd, RedTail tail) {
+                                                            const GridDesc<T>* __restrict__ gd) {
     constexpr int NV = 9;
     if (ctl) {  // device loop
         if (ctl->done) return;
@@ -349,20 +330,15 @@ __global__ __launch_bounds__(256) void p2point_pass2_kernel(const P4<T>* __restr
             }
         }
     }
-    if (!tail.ticket) {
-        block_store<NV>(acc, partials);
-        return;
-    }
-    block_store<NV, true>(acc, partials);
-    (void)reduce_tail<NV>(partials, tail);
+    block_store<NV>(acc, partials);
 }
 
 template <typename T>
 void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
                           const WChain<T>& chain, int k, int64_t N, const T* means_dev, double* partials,
-                          const LoopCtl* ctl, const GridDesc<T>* gd, const RedTail& tail, hipStream_t s) {
+                          const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s) {
     hipLaunchKernelGGL(p2point_pass2_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, chain, k, N,
-                       means_dev, partials, ctl, gd, tail);
+                       means_dev, partials, ctl, gd);
 }
 
 // materialise the chain's weights (host mirror only); point-to-plane robust
@@ -406,15 +382,14 @@ void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, c
 #define PMX_INST(T)                                                                                                  \
     template void launch_p2plane_partial<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const P4<T>*, int, const T*, \
                                             const int32_t*, const WChain<T>&, int, int64_t, int, double*,           \
-                                            const LoopCtl*, const GridDesc<T>*, unsigned long long*, const RedTail&, \
-                                            hipStream_t);                                                            \
+                                            const LoopCtl*, const GridDesc<T>*, unsigned long long*, hipStream_t);    \
     template void launch_p2point_pass1<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
                                           const WChain<T>&, int, int64_t, double*, const LoopCtl*,                   \
-                                          const GridDesc<T>*, const RedTail&, int, hipStream_t);                     \
+                                          const GridDesc<T>*, hipStream_t);                                          \
     template void launch_p2point_means<T>(const double*, T*, int, const LoopCtl*, hipStream_t);                      \
     template void launch_p2point_pass2<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
                                           const WChain<T>&, int, int64_t, const T*, double*, const LoopCtl*,         \
-                                          const GridDesc<T>*, const RedTail&, hipStream_t);                          \
+                                          const GridDesc<T>*, hipStream_t);                                          \
     template void launch_weights_chain<T>(const T*, T*, int64_t, const WChain<T>&, const P4<T>*, const Mat4<T>&,     \
                                           const P4<T>*, const P4<T>*, int, const int32_t*, int, hipStream_t);
 PMX_INST(float)
