@@ -359,7 +359,12 @@ static size_t vt_sort_temp_bytes(int64_t n) {
 // summed sequentially.  One block of kCumThreads, chunks of kCumThreads *
 // kCumPer keys.
 constexpr int kCumThreads = 1024;
-constexpr int kCumPer = 16;
+// (4 keys per thread: 4 K-key chunks — a chunk then rarely holds two binade
+// crossings, and the preparation runs on 4x as many blocks; 16 K chunks put
+// the first ~5 crossings after the head into one chunk, walked with one
+// block-wide pass per crossing)
+constexpr int kCumPer = 4;
+constexpr int kCumMaxTies = 1024;
 template <typename T>
 struct CumBits;
 template <>
@@ -409,19 +414,27 @@ __device__ __forceinline__ long long cum_block_scan(long long v, long long lim, 
     return sat_add(before, incl - v, lim);
 }
 
-// The keys are cut into the head (the first kCumHead keys, where the running
-// sum leaves its binade every few keys) and chunks of kCumChunk keys.
-// vt_chunk_prep_kernel prepares every chunk in parallel under the binade e
-// GUESSED from a double prefix of the chunk sums: the integer prefixes P_e[j]
-// of rnd(x / u) (stored), the chunk's ties, and their rounding resolved for an
-// even and for an odd start (the parity of S0 / u decides every tie of the
-// chunk).  vt_cumsum_kernel — one wave — then walks the chunks in order with
-// the exact running sum S: a chunk whose guess is S's binade, with few ties,
-// and whose last sum stays below the next binade is FAST (its end sum in O(1)
-// from the chunk table; vt_chunk_write_kernel writes its sums in parallel
-// afterwards); the head and every other chunk (a crossing, a wrong guess,
-// many ties, a subnormal sum) run through vt_wave_pass, which writes their
-// sums.  Every path computes the sequential loop's bits.
+// The head (the first kCumHead keys, where the running sum leaves its binade
+// every few keys) is summed sequentially; the rest is cut into chunks of
+// kCumChunk keys.  vt_chunk_prep_kernel prepares every chunk in parallel
+// under the binade e GUESSED from a double prefix of the chunk sums, and under
+// e + 1: the integer prefixes P_e[j], P_e+1[j] of rnd(x / u) (stored), the
+// ties of both binades, and for binade e the ties' rounding already resolved
+// for an even and for an odd start: the parity of S0 / u decides every tie of
+// the chunk (the units before tie k are S0 + pb_k + up_k-1, so their parity
+// is that of S0 plus integers known beforehand).  vt_cumsum_kernel then walks
+// the chunks in order with the exact running sum S:
+//   fast   S in binade e, S / u + P_e + C_e[parity] < 2^P: the chunk's end
+//          sum in O(1) from the chunk table (preloaded in LDS);
+//   cross  the sum leaves binade e inside the chunk: the crossing step (the
+//          first j whose units reach 2^P, found by the whole block over the
+//          stored P_e) is a plain T addition, and when it lands in binade
+//          e + 1 and the rest of the chunk stays there, the rest's sums are
+//          the e + 1 prefix from there (its few ties resolved in order);
+//   slow   anything else (a wrong guess, many ties, two crossings, a
+//          subnormal sum): the passes below, which write the chunk's sums.
+// vt_chunk_write_kernel writes the fast and crossing chunks' sums in
+// parallel.  Every path computes the sequential loop's bits.
 constexpr int kCumChunk = kCumThreads * kCumPer;
 constexpr int kCumHead = 4096;
 constexpr int kFastTies = 256;
@@ -723,176 +736,14 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typen
 }
 
 int g_vt_trace = 0;
-
-// One wave's pass over keys [p, q_end) from the exact running sum s.  Tiles
-// of 64 x kWaveKeys keys in order (lane L holds the kWaveKeys keys from
-// p + L * kWaveKeys), each an integer prefix scan of rnd(x / u) in the running
-// sum's binade (wave shuffles), the ties resolved by the parity identity
-// (tie k rounds up iff c_k != c_(k-1), c_k = (S0 + pb_k + m_k) & 1: after a
-// tie the parity of the round-ups so far is c_k), the sums written up to the
-// first step that leaves the binade; that step is a plain T addition and the
-// next tile starts after it.  Wave-synchronous (no block barrier: the block-
-// wide passes this replaced cost ~19 us per crossing).  Returns the running
-// sum through q_end - 1, wave-uniform.
-constexpr int kWaveKeys = 16;
 template <typename T>
-__device__ T vt_wave_pass(const typename KeyOf<T>::K* __restrict__ keys, int64_t p, int64_t q_end, T s,
-                          T* __restrict__ cum) {
+__global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
+                                                                const int* __restrict__ count, T* __restrict__ cum,
+                                                                VtChunk* __restrict__ ch, VtPrep pr, int nch,
+                                                                const LoopCtl* __restrict__ ctl,
+                                                                unsigned long long* __restrict__ trace) {
     using KO = KeyOf<T>;
-    constexpr int P = CumBits<T>::P;
-    constexpr long long LIM = 1ll << P;
-    constexpr int64_t kTile = 64 * kWaveKeys;
-    const int lane = threadIdx.x & 63;
-    while (p < q_end) {  // (wave-uniform)
-        if (!(s >= CumBits<T>::min_normal())) {
-            // a subnormal running sum (units() would add a hidden bit s
-            // lacks): the next 64 keys in order
-            const int64_t e = p + 64 < q_end ? p + 64 : q_end;
-            T acc = s;
-            if (lane == 0)
-                for (int64_t j = p; j < e; ++j) {
-                    acc = acc + KO::val(keys[j]);
-                    cum[j] = acc;
-                }
-            s = __shfl(acc, 0);
-            p = e;
-            continue;
-        }
-        const int eb = CumBits<T>::binade(s);
-        const UScale inv_u = uscale(P - 1 - eb);  // 1 / ulp(2^eb)
-        const double u = ldexp(1.0, eb - (P - 1));
-        const long long S0 = CumBits<T>::units(s);  // in [2^(P-1), 2^P)
-        const int64_t j0 = p + (int64_t)lane * kWaveKeys;
-        T x[kWaveKeys];
-#pragma unroll
-        for (int i = 0; i < kWaveKeys; ++i) x[i] = j0 + i < q_end ? KO::val(keys[j0 + i]) : (T)0;
-        long long r[kWaveKeys];
-        bool tie[kWaveKeys];
-        long long loc = 0;
-#pragma unroll
-        for (int i = 0; i < kWaveKeys; ++i) {
-            r[i] = 0;
-            tie[i] = false;
-            if (j0 + i < q_end) {
-                const double q = ((double)x[i] * inv_u.a) * inv_u.b;  // exact (power-of-two scales)
-                if (!(q < (double)LIM)) {
-                    r[i] = LIM;  // (this step alone leaves the binade)
-                } else {
-                    const double m = floor(q), f = q - m;
-                    tie[i] = f == 0.5;
-                    r[i] = (long long)m + (f > 0.5 ? 1 : 0);
-                }
-            }
-            loc = sat_add(loc, r[i], LIM);
-        }
-        // the lanes' totals: saturating inclusive scan (exact below LIM)
-        long long incl = loc;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const long long v = __shfl_up(incl, off);
-            if (lane >= off) incl = sat_add(incl, v, LIM);
-        }
-        long long base = __shfl_up(incl, 1);
-        if (lane == 0) base = 0;
-        // the ties' parity bits c_k, the lane's first / last, its inner round-ups
-        int cb[kWaveKeys];
-        int cfirst = -1, clast = -1, inner = 0;
-        long long run = base;
-#pragma unroll
-        for (int i = 0; i < kWaveKeys; ++i) {
-            cb[i] = 0;
-            if (tie[i]) {
-                cb[i] = (int)((S0 + run + r[i]) & 1ll);  // (saturated run: past the crossing, unused)
-                if (cfirst < 0)
-                    cfirst = cb[i];
-                else
-                    inner += cb[i] ^ clast;
-                clast = cb[i];
-            }
-            run = sat_add(run, r[i], LIM);
-        }
-        // c of the last tie of the lanes before (0: none since the pass start)
-        int lv = clast;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(lv, off);
-            if (lane >= off && lv < 0) lv = v;
-        }
-        int cin = __shfl_up(lv, 1);
-        if (lane == 0 || cin < 0) cin = 0;
-        int ui = cfirst < 0 ? 0 : (cfirst ^ cin) + inner;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(ui, off);
-            if (lane >= off) ui += v;
-        }
-        int up = __shfl_up(ui, 1);
-        if (lane == 0) up = 0;
-        // every element's sum in units of u; the first that leaves the binade
-        long long Sv[kWaveKeys];
-        int cprev = cin, first = 0x7fffffff;
-        run = base;
-#pragma unroll
-        for (int i = 0; i < kWaveKeys; ++i) {
-            run = sat_add(run, r[i], LIM);
-            if (tie[i]) {
-                up += cb[i] ^ cprev;
-                cprev = cb[i];
-            }
-            Sv[i] = S0 + run + up;
-            if (j0 + i < q_end && Sv[i] >= LIM && first == 0x7fffffff) first = i;
-        }
-        const unsigned long long has = __ballot(first != 0x7fffffff);
-        int64_t jc = -1;
-        if (has) {
-            const int fl = __ffsll((long long)has) - 1;
-            jc = p + (int64_t)fl * kWaveKeys + __shfl(first, fl);
-        }
-#pragma unroll
-        for (int i = 0; i < kWaveKeys; ++i) {
-            const int64_t j = j0 + i;
-            if (j < q_end && (jc < 0 || j < jc)) cum[j] = (T)((double)Sv[i] * u);
-        }
-        // the sum through element `at` (>= p) of this tile, from its lane
-        auto sum_at = [&](int64_t at) -> T {
-            const int ll = (int)((at - p) / kWaveKeys), li = (int)((at - p) % kWaveKeys);
-            long long mine = 0;
-#pragma unroll
-            for (int i = 0; i < kWaveKeys; ++i)
-                if (i == li) mine = Sv[i];
-            return (T)((double)__shfl(mine, ll) * u);
-        };
-        if (jc < 0) {
-            const int64_t last = (q_end < p + kTile ? q_end : p + kTile) - 1;
-            s = sum_at(last);
-            p = last + 1;
-        } else {
-            const T before = jc > p ? sum_at(jc - 1) : s;
-            const T S1 = before + KO::val(keys[jc]);  // the crossing step, in T
-            if (lane == 0) cum[jc] = S1;
-            s = S1;
-            p = jc + 1;
-        }
-    }
-    return s;
-}
-
-// The walk (one wave).  The head and every chunk that is not fast run
-// through vt_wave_pass; lane 0 settles runs of fast chunks in O(1) each from
-// the chunk table (the guessed binade is the running sum's, few ties, and
-// the chunk's last sum stays below the next binade: its end sum is
-// S0 + u (P_e + C_e[parity of S0 / u])), and vt_chunk_write_kernel writes
-// those chunks' sums in parallel afterwards.
-template <typename T>
-__global__ __launch_bounds__(64) void vt_cumsum_kernel(const typename KeyOf<T>::K* __restrict__ keys,
-                                                       const int* __restrict__ count, T* __restrict__ cum,
-                                                       VtChunk* __restrict__ ch, int nch,
-                                                       const LoopCtl* __restrict__ ctl,
-                                                       unsigned long long* __restrict__ trace) {
-    using KO = KeyOf<T>;
-    constexpr int P = CumBits<T>::P;
-    constexpr long long LIM = 1ll << P;
-    // (development trace, PMX_VT_TRACE: lane 0 stamps each step of the walk
+    // (development trace, PMX_VT_TRACE: thread 0 stamps each step of the walk
     // with the 100 MHz real-time counter; pmx_vartrim_partial_sums prints it)
     int nmark = 0;
 #define VT_MARK(type, bb, detail)                                                                               \
@@ -902,14 +753,33 @@ __global__ __launch_bounds__(64) void vt_cumsum_kernel(const typename KeyOf<T>::
                                ((unsigned long long)(detail) & 0xffffffull);                                    \
         ++nmark;                                                                                                \
     }
+    constexpr int P = CumBits<T>::P;
+    constexpr long long LIM = 1ll << P;
+    __shared__ long long wsum[kCumThreads / 64];
+    __shared__ int s_nt;
+    __shared__ int tie_idx[kCumMaxTies];        // chunk-local index, in order
+    __shared__ long long tie_pb[kCumMaxTies];   // P before the tie (ties counted as m)
+    __shared__ long long tie_m[kCumMaxTies];
+    __shared__ int tie_c[kCumMaxTies];          // rounded-up ties up to and including this one
+    __shared__ int s_cross;
+    __shared__ int s_mode;
+    __shared__ long long s_U0;
+    __shared__ int s_par;
+    __shared__ long long s_lo;                  // the walk's position (chunk start, chunk)
+    __shared__ int s_b;
+    __shared__ T s_run;                         // the running sum after the chunk
+    // the chunk table of the fast test (the walk's per-chunk decision then
+    // reads no global memory)
     __shared__ long long c_P0[kChunkLds], c_C[2][kChunkLds];
     __shared__ int c_e[kChunkLds], c_nt0[kChunkLds];
+    __shared__ int t1_idx[kFastTies];  // a crossing chunk's binade e + 1 ties
+    __shared__ long long t1_pb[kFastTies], t1_m[kFastTies];
     if (ctl && ctl->done) return;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x;
     const int64_t c = *count;
     if (c <= 0) return;
     const int nchl = nch < kChunkLds ? nch : kChunkLds;
-    for (int i = lane; i < nchl; i += 64) {
+    for (int i = t; i < nchl; i += kCumThreads) {
         const VtChunk& q = ch[i + 1];
         c_P0[i] = q.P[0];
         c_C[0][i] = q.C[0];
@@ -917,46 +787,324 @@ __global__ __launch_bounds__(64) void vt_cumsum_kernel(const typename KeyOf<T>::
         c_e[i] = q.e;
         c_nt0[i] = q.nt[0];
     }
+    // the head sequentially (keys staged in LDS by the whole block: the one
+    // summing thread then waits on no global load)
+    __shared__ typename KO::K s_head[kCumHead];
+    const int ph = c < kCumHead ? (int)c : kCumHead;
+    for (int j = t; j < ph; j += kCumThreads) s_head[j] = keys[j];
     __syncthreads();
-    // the head: partial_sum's first output is the first element
-    T s = KO::val(keys[0]);
-    if (lane == 0) cum[0] = s;
-    const int64_t ph = c < kCumHead ? c : kCumHead;
-    s = vt_wave_pass<T>(keys, 1, ph, s, cum);
+    if (t == 0) {
+        T acc = KO::val(s_head[0]);  // partial_sum's first output is the first element
+        cum[0] = acc;
+#pragma unroll 8
+        for (int j = 1; j < ph; ++j) {
+            acc = acc + KO::val(s_head[j]);
+            cum[j] = acc;
+        }
+        s_run = acc;
+    }
     VT_MARK(1, 0, ph);
+    __syncthreads();
+    T s = s_run;
+    __syncthreads();
+    // The walk.  Thread 0 settles a run of fast chunks in one go (no block
+    // barrier between them: one per chunk made the ~50 fast chunks of a 1M
+    // sum most of the walk); the block then takes the first chunk that is
+    // not fast, as a crossing or through the passes.
     int64_t lo = ph;
     int b = 0;
-    while (lo < c) {  // (wave-uniform)
-        T sr = s;
-        int64_t lo2 = lo;
-        int b2 = b;
-        if (lane == 0) {
-            for (; lo2 < c; lo2 += kCumChunk, ++b2) {
-                const bool inl = b2 < kChunkLds;
-                const int e = inl ? c_e[b2] : ch[b2 + 1].e;
-                const int nt0 = inl ? c_nt0[b2] : ch[b2 + 1].nt[0];
+    while (lo < c) {  // (uniform)
+        if (t == 0) {
+            // 1 fast: the guessed binade is the running sum's, few ties, and
+            // the chunk's last sum stays below the next binade (O(1): the
+            // ties were resolved for both parities of the start);
+            // 2 a crossing to examine; 0 the passes
+            T sr = s;
+            int mode = 0;
+            for (; lo < c; lo += kCumChunk, ++b) {
+                const bool inl = b < kChunkLds;
+                const int e = inl ? c_e[b] : ch[b + 1].e;
+                const int nt0 = inl ? c_nt0[b] : ch[b + 1].nt[0];
+                mode = 0;
                 // (sr normal: units() adds the hidden bit)
                 if (!(nt0 <= kFastTies && sr >= CumBits<T>::min_normal() && CumBits<T>::binade(sr) == e)) break;
                 const long long U0 = CumBits<T>::units(sr);
                 const int par = (int)(U0 & 1ll);
                 const long long fin =
-                    U0 + (inl ? c_P0[b2] : ch[b2 + 1].P[0]) + (inl ? c_C[par][b2] : ch[b2 + 1].C[par]);
-                if (fin >= LIM) break;
-                VtChunk& q = ch[b2 + 1];
-                q.S0 = (double)sr;
-                q.par = par;
-                q.ok = 1;
-                sr = (T)((double)fin * ldexp(1.0, e - (P - 1)));
+                    U0 + (inl ? c_P0[b] : ch[b + 1].P[0]) + (inl ? c_C[par][b] : ch[b + 1].C[par]);
+                VtChunk& q = ch[b + 1];
+                if (fin < LIM) {
+                    q.S0 = (double)sr;
+                    q.par = par;
+                    q.ok = 1;
+                    sr = (T)((double)fin * ldexp(1.0, e - (P - 1)));
+                    continue;
+                }
+                if (q.nt[1] <= kFastTies) {
+                    s_U0 = U0;
+                    s_par = par;
+                    mode = 2;
+                }
+                break;
             }
+            s_run = sr;
+            VT_MARK(2, b, mode);
+            s_lo = lo;
+            s_b = b;
+            s_mode = mode;
+            s_cross = 0x7fffffff;
         }
-        s = __shfl(sr, 0);
-        lo = __shfl(lo2, 0);
-        b = __shfl(b2, 0);
-        VT_MARK(2, b, 0);
+        __syncthreads();
+        s = s_run;
+        lo = s_lo;
+        b = s_b;
+        __syncthreads();  // (read before thread 0 rewrites them)
         if (lo >= c) break;
         const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
-        s = vt_wave_pass<T>(keys, lo, cend, s, cum);
-        VT_MARK(4, b, 0);
+        if (s_mode == 2) {
+            // the first step whose units reach 2^P: every thread over its
+            // keys' stored prefix, with the ties' rounding for this start
+            const long long U0 = s_U0;
+            const int par = s_par;
+            const int nt0 = ch[b + 1].nt[0], nt1 = ch[b + 1].nt[1];
+            // this thread's 16 stored prefixes, all loads issued before any
+            // is used (a use-then-load loop made them 16 dependent round
+            // trips: 12-18 us per crossing chunk)
+            const int64_t jt = lo + (int64_t)t * kCumPer;
+            long long pv[kCumPer];
+            if (jt + kCumPer <= cend) {
+#pragma unroll
+                for (int i = 0; i < kCumPer; ++i) pv[i] = pr.P[0][jt + i - kCumHead];
+            } else {
+#pragma unroll
+                for (int i = 0; i < kCumPer; ++i) pv[i] = jt + i < cend ? pr.P[0][jt + i - kCumHead] : 0ll;
+            }
+            // the ties of binades e and e + 1 into LDS by the whole block (the
+            // serial resolution below then waits on no global load)
+            for (int k = t; k < nt0; k += kCumThreads) {
+                tie_idx[k] = pr.t_idx[0][b * kFastTies + k];
+                tie_c[k] = pr.t_c0[par][b * kFastTies + k];
+            }
+            for (int k = t; k < nt1; k += kCumThreads) {
+                t1_idx[k] = pr.t_idx[1][b * kFastTies + k];
+                t1_pb[k] = pr.t_pb[1][b * kFastTies + k];
+                t1_m[k] = pr.t_m[1][b * kFastTies + k];
+            }
+            __syncthreads();
+            int kt = 0;
+            {
+                int lo2 = 0, hi2 = nt0;  // first tie at a local index >= t * kCumPer
+                while (lo2 < hi2) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (tie_idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
+                }
+                kt = lo2;
+            }
+            int first = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                const int li = t * kCumPer + i;
+                if (kt < nt0 && tie_idx[kt] == li) ++kt;
+                const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
+                if (jt + i < cend && first == 0x7fffffff && U0 + pv[i] + C >= LIM) first = li;
+            }
+            if (first != 0x7fffffff) atomicMin(&s_cross, first);
+            __syncthreads();
+            if (t == 0) {
+                VtChunk& q = ch[b + 1];
+                const int jc = s_cross;  // (exists: the chunk's last sum reaches 2^P)
+                const int e = q.e;
+                // (the three independent loads first, together)
+                const long long P0b = jc > 0 ? pr.P[0][lo + jc - 1 - kCumHead] : 0ll;
+                const T xc = KO::val(keys[lo + jc]);
+                const long long P1jc = pr.P[1][lo + jc - kCumHead];
+                const long long P1t = q.P[1];
+                T before = s;
+                if (jc > 0) {
+                    int n0 = 0;  // ties at local indices <= jc - 1
+                    while (n0 < nt0 && tie_idx[n0] <= jc - 1) ++n0;
+                    const long long C = n0 > 0 ? (long long)tie_c[n0 - 1] : 0ll;
+                    before = (T)((double)(U0 + P0b + C) * ldexp(1.0, e - (P - 1)));
+                }
+                const T S1 = before + xc;  // the crossing step, in T
+                int mode = 0;
+                if (S1 >= CumBits<T>::min_normal() && CumBits<T>::binade(S1) == e + 1) {
+                    // the rest of the chunk in binade e + 1: its ties in order
+                    const long long U1 = CumBits<T>::units(S1);
+                    int up = 0;
+                    for (int k = 0; k < nt1; ++k) {
+                        if (t1_idx[k] <= jc) continue;
+                        const long long bf = U1 + (t1_pb[k] - P1jc) + up;
+                        up += ((bf + t1_m[k]) & 1ll) ? 1 : 0;
+                        pr.t_c1[b * kFastTies + k] = up;
+                    }
+                    const long long fin = U1 + (P1t - P1jc) + up;
+                    if (fin < LIM) {
+                        q.S0 = (double)s;
+                        q.par = par;
+                        q.jc = jc;
+                        q.S1 = (double)S1;
+                        q.ok = 2;
+                        s_run = (T)((double)fin * ldexp(1.0, e + 1 - (P - 1)));
+                        mode = 3;
+                    }
+                }
+                s_mode = mode;
+            }
+            __syncthreads();
+            VT_MARK(3, b, s_mode);
+            if (s_mode == 3) {
+                s = s_run;
+                __syncthreads();
+                lo += kCumChunk;
+                ++b;
+                continue;
+            }
+        }
+        int64_t p = lo;
+        while (p < cend) {  // (uniform) passes over [p, cend)
+            VT_MARK(4, b, p - lo);
+            const int eb = CumBits<T>::binade(s);
+            const UScale inv_u = uscale(P - 1 - eb);  // 1 / ulp(2^eb)
+            const double u = ldexp(1.0, eb - (P - 1));
+            const long long S0 = CumBits<T>::units(s);  // in [2^(P-1), 2^P)
+            // the pass starts at p rounded down to a multiple of kCumPer (each
+            // thread's keys then come in 16-byte vector loads); keys below p
+            // are inactive (contribute 0, written earlier)
+            const int64_t jb = p & ~(int64_t)(kCumPer - 1);
+            const int64_t q1 = jb + (int64_t)kCumChunk < cend ? jb + (int64_t)kCumChunk : cend;
+            if (!(s >= CumBits<T>::min_normal())) {
+                // a subnormal running sum (every key so far below the
+                // smallest normal): units() would add a hidden bit s does not
+                // have — this pass sequentially, exactly as partial_sum
+                if (t == 0) {
+                    T acc = s;
+                    for (int64_t j = p; j < q1; ++j) {
+                        acc = acc + KO::val(keys[j]);
+                        cum[j] = acc;
+                    }
+                    s_run = acc;
+                }
+                __syncthreads();
+                s = s_run;
+                p = q1;
+                __syncthreads();
+                continue;
+            }
+            const int64_t j0 = jb + (int64_t)t * kCumPer;
+            typename KO::K kv[kCumPer];
+            vt_load<T>(keys, c, j0, kv);
+            long long r[kCumPer];
+            bool tie[kCumPer];
+            int ntie;
+            const long long loc = vt_round<T>(kv, j0, p, q1, inv_u, r, tie, ntie);
+            long long tot;
+            const long long base = cum_block_scan(loc, LIM, wsum, tot);
+            // the ties, in element order, with the P before each
+            long long tt;
+            const long long tbase = cum_block_scan((long long)ntie, LIM, wsum, tt);
+            if (t == 0) s_nt = (int)tt;
+            if (tt <= kCumMaxTies) {
+                long long run = base;
+                int k = (int)tbase;
+#pragma unroll
+                for (int i = 0; i < kCumPer; ++i) {
+                    if (tie[i]) {
+                        tie_idx[k] = t * kCumPer + i;
+                        tie_pb[k] = run;
+                        tie_m[k] = r[i];
+                        ++k;
+                    }
+                    run = sat_add(run, r[i], LIM);
+                }
+            }
+            __syncthreads();
+            const int nt = s_nt;
+            if (nt > kCumMaxTies) {
+                // (many ties: this pass sequentially, exactly as partial_sum)
+                if (t == 0) {
+                    T acc = s;
+                    for (int64_t j = p; j < q1; ++j) {
+                        acc = acc + KO::val(keys[j]);
+                        cum[j] = acc;
+                    }
+                    s_run = acc;
+                }
+                __syncthreads();
+                s = s_run;
+                p = q1;
+                __syncthreads();
+                continue;
+            }
+            // the ties' rounding, in parallel: tie k rounds up iff the units
+            // before it plus m_k are odd, i.e. c_k ^ parity(up_(k-1)) with
+            // c_k = (S0 + pb_k + m_k) & 1 — and then parity(up_k) = c_k.  So
+            // tie k rounds up iff c_k != c_(k-1) (c_(-1) = 0), and up_k is a
+            // prefix sum of those (a serial loop over the ties before; past a
+            // crossing the saturated values are as meaningless either way)
+            {
+                static_assert(kCumMaxTies <= kCumThreads, "one tie per thread");
+                const int ck = t < nt ? (int)((S0 + tie_pb[t] + tie_m[t]) & 1ll) : 0;
+                const int cp = t > 0 && t - 1 < nt ? (int)((S0 + tie_pb[t - 1] + tie_m[t - 1]) & 1ll) : 0;
+                const long long inc = t < nt ? (long long)(ck ^ cp) : 0ll;
+                long long ttot;
+                const long long upx = block_excl_scan_ll(inc, wsum, ttot);
+                if (t < nt) tie_c[t] = (int)(upx + inc);
+                if (t == 0) s_cross = 0x7fffffff;
+            }
+            __syncthreads();
+            // every element's sum in units of u; the first that leaves the binade
+            long long run = base;
+            int first = 0x7fffffff;
+            int kt = 0;  // ties at chunk-local index <= the element: binary search over tie_idx
+            {
+                int lo2 = 0, hi2 = nt;  // first tie with index >= t * kCumPer
+                while (lo2 < hi2) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (tie_idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
+                }
+                kt = lo2;
+            }
+            long long Sv[kCumPer];
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                run = sat_add(run, r[i], LIM);
+                const int li = t * kCumPer + i;
+                if (kt < nt && tie_idx[kt] == li) ++kt;
+                const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
+                Sv[i] = S0 + run + C;
+                if (j0 + i >= p && j0 + i < q1 && Sv[i] >= LIM && first == 0x7fffffff) first = li;
+            }
+            if (first != 0x7fffffff) atomicMin(&s_cross, first);
+            __syncthreads();
+            const int cross = s_cross;
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                const int li = t * kCumPer + i;
+                const int64_t j = j0 + i;
+                if (j >= p && j < q1 && li < cross) cum[j] = (T)((double)Sv[i] * u);
+                // the running sum: before the crossing, or after the whole pass
+                if (j >= p && ((cross != 0x7fffffff && li == cross - 1) || (cross == 0x7fffffff && j == q1 - 1)))
+                    s_run = (T)((double)Sv[i] * u);
+            }
+            __syncthreads();
+            if (cross == 0x7fffffff) {
+                s = s_run;
+                p = q1;
+            } else {
+                // the crossing step as a plain T addition, then the next binade
+                if (t == 0) {
+                    const T prev = jb + cross == p ? s : s_run;  // (the crossing is the pass's first active key)
+                    const T nv = prev + KO::val(keys[jb + cross]);
+                    cum[jb + cross] = nv;
+                    s_run = nv;
+                }
+                __syncthreads();
+                s = s_run;
+                p = jb + cross + 1;
+            }
+            __syncthreads();
+        }
         lo += kCumChunk;
         ++b;
     }
@@ -1162,7 +1310,8 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
                            ctl);
     }
     unsigned long long* trace = g_vt_trace ? reinterpret_cast<unsigned long long*>(p) : nullptr;
-    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(64), 0, s, src, hdr, cum, ch, (int)nch, ctl, trace);
+    hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ch, pr, (int)nch, ctl,
+                       trace);
     if (nch > 0)
         hipLaunchKernelGGL(vt_chunk_write_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
                            cum, ctl);
