@@ -672,18 +672,13 @@ struct LaneQ {
 // takes 133-220 VGPRs, 2-3 waves, no spills): C5 1.79 -> 1.62 ms/iteration.
 // The float KT = 8 form spills 26 at 128 but measured faster that way than
 // unspilled at 3 waves (C4 0.202 vs 0.217 ms/iteration).
-#ifndef PMX_LANE_HOT_WAVES
-#define PMX_LANE_HOT_WAVES 8
-#endif
-constexpr int kLaneHotWaves = PMX_LANE_HOT_WAVES;
-int g_lane_hot = 0;  // (PMX_LANE_HOT: the certify-heavy build of the f32 k = 1 per-lane kernel)
 template <typename T, int KT>
 struct LaneWaves {
     static constexpr int value = sizeof(T) == 8 ? 2 : 4;
 };
 
-template <typename T, int KT, int Q, int W = LaneWaves<T, KT>::value>
-__global__ __launch_bounds__(256, W) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
+template <typename T, int KT, int Q>
+__global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
@@ -831,14 +826,9 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
-        if (sizeof(T) == 4 && KT <= 2 && g_lane_hot)  // (the certify-heavy build: more waves, the full search spills)
-            hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q, kLaneHotWaves>), dim3((unsigned)grid), dim3(256), 0, s, gpts,
-                               gidx, start, G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode,
-                               ru.safe, ru.Tprev, ctl, gd, spec, radii);
-        else
-            hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start,
-                               G, rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe,
-                               ru.Tprev, ctl, gd, spec, radii);
+        hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
+                           rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
+                           ctl, gd, spec, radii);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,

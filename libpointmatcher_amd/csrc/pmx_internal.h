@@ -104,7 +104,6 @@ struct SelectState {
     int pad;
 };
 
-extern int g_lane_hot;  // pmx_grid.hip (PMX_LANE_HOT)
 // ---- match (pmx_match.hip) ----
 template <typename T>
 void launch_match(const P4<T>* ref, int64_t M_pad, const P4<T>* rd, int64_t N, const Mat4<T>& Tm,
