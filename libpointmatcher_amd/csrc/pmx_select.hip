@@ -819,33 +819,51 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
             // the chunk's last sum stays below the next binade (O(1): the
             // ties were resolved for both parities of the start);
             // 2 a crossing to examine; 0 the passes
+            // (integer units along a run: the run stays in S's binade es,
+            // so each chunk's end units are the next chunk's start units —
+            // no float round trips between chunks; the table reads of a
+            // chunk do not wait on the running units)
             T sr = s;
             int mode = 0;
-            for (; lo < c; lo += kCumChunk, ++b) {
-                const bool inl = b < kChunkLds;
-                const int e = inl ? c_e[b] : ch[b + 1].e;
-                const int nt0 = inl ? c_nt0[b] : ch[b + 1].nt[0];
-                mode = 0;
-                // (sr normal: units() adds the hidden bit)
-                if (!(nt0 <= kFastTies && sr >= CumBits<T>::min_normal() && CumBits<T>::binade(sr) == e)) break;
-                const long long U0 = CumBits<T>::units(sr);
-                const int par = (int)(U0 & 1ll);
-                const long long fin =
-                    U0 + (inl ? c_P0[b] : ch[b + 1].P[0]) + (inl ? c_C[par][b] : ch[b + 1].C[par]);
-                VtChunk& q = ch[b + 1];
-                if (fin < LIM) {
-                    q.S0 = (double)sr;
+            if (sr >= CumBits<T>::min_normal()) {
+                const int es = CumBits<T>::binade(sr);
+                const double u = ldexp(1.0, es - (P - 1));
+                long long U = CumBits<T>::units(sr);
+                for (; lo < c; lo += kCumChunk, ++b) {
+                    int e, nt0;
+                    long long P0, C0, C1;
+                    if (b < kChunkLds) {
+                        e = c_e[b];
+                        nt0 = c_nt0[b];
+                        P0 = c_P0[b];
+                        C0 = c_C[0][b];
+                        C1 = c_C[1][b];
+                    } else {
+                        const VtChunk& g = ch[b + 1];
+                        e = g.e;
+                        nt0 = g.nt[0];
+                        P0 = g.P[0];
+                        C0 = g.C[0];
+                        C1 = g.C[1];
+                    }
+                    if (!(nt0 <= kFastTies && e == es)) break;
+                    const int par = (int)(U & 1ll);
+                    const long long fin = U + P0 + (par ? C1 : C0);
+                    VtChunk& q = ch[b + 1];
+                    if (fin >= LIM) {
+                        if (q.nt[1] <= kFastTies) {
+                            s_U0 = U;
+                            s_par = par;
+                            mode = 2;
+                        }
+                        break;
+                    }
+                    q.S0 = (double)U * u;  // (the T value of the start sum, exactly)
                     q.par = par;
                     q.ok = 1;
-                    sr = (T)((double)fin * ldexp(1.0, e - (P - 1)));
-                    continue;
+                    U = fin;
                 }
-                if (q.nt[1] <= kFastTies) {
-                    s_U0 = U0;
-                    s_par = par;
-                    mode = 2;
-                }
-                break;
+                sr = (T)((double)U * u);
             }
             s_run = sr;
             VT_MARK(2, b, mode);
