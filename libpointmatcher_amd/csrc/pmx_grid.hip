@@ -191,7 +191,7 @@ template <typename T, int KT>
 __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                                               const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy,
                                               T qz, const double q[3], const int c[3], T maxR2, int k, T (&kd)[KT],
-                                              int32_t (&ki)[KT], uint32_t& visits) {
+                                              int32_t (&ki)[KT], uint32_t& visits, double& lb_exit) {
     int b0[3], b1[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -246,6 +246,7 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
             any = true;
         }
     }
+    lb_exit = any ? lb : 1e300;  // (every point outside the block is at least lb away)
     if (!any) return true;  // the block is the whole grid
     if (lb > 0.0) {
         const double lb2 = lb * lb * (1.0 - 1e-5);
@@ -595,7 +596,7 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
     double lb_exit = -1.0;
     if (!qnan) {
         bool done = false;
-        if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits);
+        if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit);
         if (!done) {
 #pragma unroll
             for (int s = 0; s < KT; ++s) {  // (a k-list must not see the octant's points twice)
@@ -606,7 +607,9 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
         }
     }
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
-    if (safe) safe[j] = oct ? (T)0 : safe_radius<T, KT>(kd, ki, k, lb_exit);
+    // (a certified octant block bounds the rest by its interior faces, as a
+    // shell walk's exit does)
+    if (safe) safe[j] = safe_radius<T, KT>(kd, ki, k, lb_exit);
 }
 
 // the certificate for query j; true when the k-list was rewritten from the
