@@ -171,7 +171,6 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_VT_TRACE")) g_vt_trace = std::atoi(e);
-    if (const char* e = std::getenv("PMX_SEED")) g_seed = std::atoi(e);
     if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
     // test hook: device-loop iterations (0-based, comma separated) whose
     // sharded window pick is forced to miss (the stall-and-replay path)

@@ -307,7 +307,6 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     c->M_pad = M_pad;
     c->have_match = false;
     c->grid_ready = false;
-    c->next_dirty = true;  // (grid positions of the old reference)
     // a resident reading keeps its slot order (any permutation is correct;
     // it was only chosen for the previous grid's locality)
     return build_grid<T>(c, M);
@@ -406,7 +405,6 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
         c->N_max = (int64_t)hv[1];
     }
     c->have_match = false;
-    c->next_dirty = true;  // (another reading's queries)
     return PMX_OK;
 }
 
@@ -440,16 +438,9 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         c->d_safe = nullptr;
         size_t caps = 0;
         int rc;
-        // (the safe radii T[N], then the seeds' (k+1)-th points int32[N])
-        const int64_t n1 = std::max<int64_t>(c->N, 1);
-        if ((rc = ensure(c, &c->d_safe, &caps, safe_next_offset(c, n1) + sizeof(int32_t) * (size_t)n1))) return rc;
-        c->safe_cap = n1;
+        if ((rc = ensure(c, &c->d_safe, &caps, tsize(c) * (size_t)std::max<int64_t>(c->N, 1)))) return rc;
+        c->safe_cap = std::max<int64_t>(c->N, 1);
         c->safe_valid = false;
-        c->next_dirty = true;
-    }
-    if (c->reuse_on && c->next_dirty) {  // (no stale position may reach a seed: -1 = none)
-        HIPCHK(c, hipMemsetAsync(safe_next(c), 0xff, sizeof(int32_t) * (size_t)c->safe_cap, c->stream));
-        c->next_dirty = false;
     }
     const int64_t pe = match_part_elems<T>(c->N, c->M_pad, knn, c->cu_count);
     if (pe > c->part_cap) {
@@ -511,7 +502,6 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         if (c->reuse_on && c->grid_mode >= 1 && knn <= kLaneMaxK) {  // (the wide search keeps no safe radii)
             ru.mode = c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
-            ru.next = safe_next(c);
             for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
         }
         // several ranks: the counter sum packs this rank's window segment,

@@ -107,8 +107,7 @@ struct pmx_ctx {
     bool adaptive = true;
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
-    void* d_safe = nullptr;       // T[N]: safe radius per query, then int32[N]: the seeds' (k+1)-th points
-    bool next_dirty = true;       // the (k+1)-th points may be stale (new reading or grid): reset before the next match
+    void* d_safe = nullptr;       // T[N]: safe radius per query
     int64_t safe_cap = 0;
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }
@@ -291,11 +290,6 @@ int fail(pmx_ctx* c, int code, const std::string& msg);
     } while (0)
 
 size_t tsize(const pmx_ctx* c);
-// the seeds' (k+1)-th points after the safe radii in d_safe (256-aligned)
-inline size_t safe_next_offset(const pmx_ctx* c, int64_t n) { return (tsize(c) * (size_t)n + 255) & ~(size_t)255; }
-inline int32_t* safe_next(pmx_ctx* c) {
-    return c->d_safe ? (int32_t*)((char*)c->d_safe + safe_next_offset(c, c->safe_cap)) : nullptr;
-}
 // the device loop's control word while iterations are being enqueued
 const LoopCtl* loop_ctl(const pmx_ctx* c);
 LoopCtl* loop_on_ctl(pmx_ctx* c);  // (the same, writable: the kernels that stop the loop)

@@ -266,37 +266,23 @@ template <typename T, int KT>
 __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                             const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy, T qz,
                             const double q[3], const int c[3], T maxR2, int k, T (&kd)[KT], int32_t (&ki)[KT],
-                            uint32_t& visits, double& lb_exit, double seed_lim = 1e300) {
+                            uint32_t& visits, double& lb_exit) {
     const double margin = 1.0 - 1e-5;
     lb_exit = 1e300;
     {
         // phase 1: the whole 3x3x3 block (R = 0 and 1).  The nine row
         // bounds are loaded together from always-valid (clamped)
         // addresses and masked afterwards, then the rows are scanned.
-        // (seed_lim: a bound on the squared (k+1)-th distance known before
-        // the walk — rows and end cells farther than it are skipped, as the
-        // shells below skip them against the list)
         uint32_t ra[9], rb[9];
         const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
-        const bool sd = seed_lim < 1e300;
-        const double gxl = sd && x0 < c[0] ? axis_gap(G, 0, x0, q[0]) : 0.0;
-        const double gxr = sd && x1 > c[0] ? axis_gap(G, 0, x1, q[0]) : 0.0;
 #pragma unroll
         for (int r = 0; r < 9; ++r) {
             const int z = c[2] + r / 3 - 1, y = c[1] + r % 3 - 1;
-            bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
+            const bool ok = z >= 0 && z < G.g[2] && y >= 0 && y < G.g[1];
             const int zc = min(max(z, 0), G.g[2] - 1), yc = min(max(y, 0), G.g[1] - 1);
             const uint32_t row = ((uint32_t)zc * (uint32_t)G.g[1] + (uint32_t)yc) * (uint32_t)G.g[0];
-            int xa = x0, xb = x1;
-            if (sd) {
-                const double gz = axis_gap(G, 2, zc, q[2]), gy = axis_gap(G, 1, yc, q[1]);
-                const double g2 = gz * gz + gy * gy;
-                ok = ok && g2 <= seed_lim;
-                if (g2 + gxl * gxl > seed_lim) xa = c[0];
-                if (g2 + gxr * gxr > seed_lim) xb = c[0];
-            }
-            const uint32_t va = gld32(start, row + xa);
-            const uint32_t vb = gld32(start, row + xb + 1);
+            const uint32_t va = gld32(start, row + x0);
+            const uint32_t vb = gld32(start, row + x1 + 1);
             ra[r] = ok ? va : 0u;
             rb[r] = ok ? vb : 0u;
         }
@@ -351,7 +337,7 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
                 T dkT;
                 int32_t ikT;
                 kth(kd, ki, k < KT ? k + 1 : k, dkT, ikT);
-                const double lim = fmin(ikT == kNoPos ? 1e300 : (double)dkT / margin, seed_lim);
+                const double lim = ikT == kNoPos ? 1e300 : (double)dkT / margin;
                 const double gz = axis_gap(G, 2, z, q[2]), gz2 = gz * gz;
                 if (gz2 > lim) continue;
                 const bool zface = (z == c[2] - R) || (z == c[2] + R);
@@ -593,38 +579,9 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
                                            const uint32_t* __restrict__ start, const GridGeom& G,
                                            const P4<T>* __restrict__ rd, int64_t j, const Mat4<T>& Tm, int k,
                                            T maxR2, int oct, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                           T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa,
-                                           int32_t* __restrict__ next = nullptr, bool seed = false) {
+                                           T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa) {
     T qx, qy, qz;
     gxform(Tm, gld(rd, j), qx, qy, qz);
-    // The seed (a query whose certificate failed, previous match at this
-    // level): its k previous neighbours and the (k+1)-th point of its last
-    // full search are k + 1 distinct reference points, so the farthest of
-    // them from q bounds the (k+1)-th distance — the walk skips every row
-    // and cell beyond it.  The list it finds is the exact one either way.
-    double seed_lim = 1e300;
-    if (seed && next && k < KT) {
-        int32_t sid[KT];
-        bool ok = true;
-        const int32_t nx = next[j];
-#pragma unroll
-        for (int s = 0; s < KT; ++s) {
-            sid[s] = s < k ? out_i[j * k + s] : (s == k ? nx : 0);
-            ok = ok && (s > k || sid[s] >= 0);
-        }
-#pragma unroll
-        for (int s = 0; s < KT; ++s) ok = ok && (s >= k || sid[s] != nx);
-        if (ok) {
-            P4<T> sp[KT];
-#pragma unroll
-            for (int s = 0; s < KT; ++s) sp[s] = gld32(gpts, s <= k ? (uint32_t)sid[s] : 0u);
-            T mx = (T)0;
-#pragma unroll
-            for (int s = 0; s < KT; ++s)
-                if (s <= k) mx = fmax(mx, gsqd(qx, qy, qz, sp[s]));
-            if (mx < (T)__builtin_huge_val()) seed_lim = (double)mx / (1.0 - 1e-5);
-        }
-    }
     T kd[KT];
     int32_t ki[KT];
 #pragma unroll
@@ -646,17 +603,10 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
                 kd[s] = (T)__builtin_huge_val();
                 ki[s] = kNoPos;
             }
-            lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit, seed_lim);
+            lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit);
         }
     }
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
-    if (next) {
-        int32_t nx = -1;
-#pragma unroll
-        for (int s = 0; s < KT; ++s)
-            if (s == k && ki[s] != kNoPos) nx = ki[s];
-        next[j] = nx;
-    }
     // (a certified octant block bounds the rest by its interior faces, as a
     // shell walk's exit does)
     if (safe) safe[j] = safe_radius<T, KT>(kd, ki, k, lb_exit);
@@ -725,7 +675,6 @@ struct LaneQ {
 // takes 133-220 VGPRs, 2-3 waves, no spills): C5 1.79 -> 1.62 ms/iteration.
 // The float KT = 8 form spills 26 at 128 but measured faster that way than
 // unspilled at 3 waves (C4 0.202 vs 0.217 ms/iteration).
-int g_seed = 1;  // (PMX_SEED=0: full searches without the previous match's bound)
 template <typename T, int KT>
 struct LaneWaves {
     static constexpr int value = sizeof(T) == 8 ? 2 : 4;
@@ -741,8 +690,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                                                         int reuse, T* __restrict__ safe, Mat4<T> Tprev,
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
-                                                        SpecSel* __restrict__ spec, const T* __restrict__ radii,
-                                                        int32_t* __restrict__ next) {
+                                                        SpecSel* __restrict__ spec, const T* __restrict__ radii) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -856,7 +804,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
     for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
         const int64_t j2 = base + miss[t];
         full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
-                          sa, safe ? next : nullptr, reuse == 2);
+                          sa);
         if (Q == 1) break;
     }
     add_visits(visits, visited);
@@ -877,18 +825,18 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
     if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
                            G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
-                           ctl, gd, spec, ru.safe, ru.safe && g_seed ? ru.next : nullptr);
+                           ctl, gd, spec, ru.safe);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
         hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
                            rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
-                           ctl, gd, spec, radii, g_seed ? ru.next : nullptr);
+                           ctl, gd, spec, radii);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
                            waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 0, (const LoopCtl*)nullptr,
-                           (const GridDesc<T>*)nullptr, (SpecSel*)nullptr, (T*)nullptr, (int32_t*)nullptr);
+                           (const GridDesc<T>*)nullptr, (SpecSel*)nullptr, (T*)nullptr);
     }
 }
 

@@ -104,7 +104,6 @@ struct SelectState {
     int pad;
 };
 
-extern int g_seed;  // pmx_grid.hip (PMX_SEED)
 // ---- match (pmx_match.hip) ----
 template <typename T>
 void launch_match(const P4<T>* ref, int64_t M_pad, const P4<T>* rd, int64_t N, const Mat4<T>& Tm,
@@ -166,7 +165,6 @@ template <typename T>
 struct GridReuse {
     int mode = 0;
     T* safe = nullptr;
-    int32_t* next = nullptr;  // per query: the (k+1)-th point of its last full search (-1: none), the seed's bound
     Mat4<T> Tprev{};
 };
 template <typename T>
