@@ -120,6 +120,7 @@ def main():
     res = {"launches": n, "all": {"avg_ns": sum(dur) / max(n, 1), "launches_averaged": n}}
     for ph, (a, b) in phases.items():
         res[ph] = summarize(dur, f, w, a, b)
+        res[ph]["launch_ns"] = dur[a:b] if a >= 0 else []  # (the averaged launches themselves)
     out["match"] = res
 
     for name, sub in KERNELS.items():
