@@ -8,10 +8,10 @@ one ICP object), with pass A = prepare + W warmup + K timed iterations (the
 timed region) and pass B = prepare + W + K iterations with HIP events around
 every match (the live roofline measurement); nothing is dispatched after
 pass B.  Every iteration runs one match: the tile kernel (cold form, a new
-reading's first iteration), the per-lane kernel, or the certify kernel
-followed by the search kernel over its misses (PMX_LANE_SPLIT, the default).
-A match's duration and bytes are the sum over its kernels, so the last
-2 (W + K) matches are the two passes.  This tool averages the kernel trace
+reading's first iteration) or the per-lane kernel (a match of several
+launches — the round-4 certify / search split, since removed — is summed),
+so the last 2 (W + K) matches are the two passes; each phase also lists the
+durations it averages ("launch_ns").  This tool averages the kernel trace
 durations and the PMC counters (separate rocprofv3 --pmc runs of the same
 command, dispatches aligned by their order from the end) over:
   timed      pass A, iterations W .. W+K-1 (what ms_per_step covers)
