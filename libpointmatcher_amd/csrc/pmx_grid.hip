@@ -874,6 +874,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
             PMX_KT(2);
         else if (kl <= 4)
             PMX_KT(4);
+        else if (kl <= 5)
+            PMX_KT(5);  // (k = 4 with the (k+1)-th entry: 5 fit the 128-VGPR budget, 8 spilled)
         else if (kl <= 8)
             PMX_KT(8);
         else
