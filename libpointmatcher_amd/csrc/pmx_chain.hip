@@ -360,7 +360,7 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
                                  c->stream));
         c->has_order = true;
         launch_transform<T>((const P4<T>*)d_sorted, (P4<T>*)c->d_rd, N, M0, c->stream);
-        if (morton && (c->grid_mode == 0 || std::getenv("PMX_COLD_WAVES"))) {  // the tile kernel's wave table (host, from the sorted keys)
+        if (morton && c->grid_mode == 0) {  // the tile kernel's wave table (host, from the sorted keys)
             std::vector<unsigned long long> keys((size_t)N);
             HIPCHK(c, hipMemcpyAsync(keys.data(), c->setup.keys64_out, sizeof(unsigned long long) * N,
                                      hipMemcpyDeviceToHost, c->stream));

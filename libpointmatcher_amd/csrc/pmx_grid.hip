@@ -823,9 +823,8 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                       const T* radii, bool cold, hipStream_t s) {
     if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
-        const int64_t W = waves ? n_waves : (N + 63) / 64;
-        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start,
-                           G, rd, N, waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
+        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
+                           G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
                            ctl, gd, spec, ru.safe);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
