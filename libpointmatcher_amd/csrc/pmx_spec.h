@@ -50,6 +50,7 @@ struct KeyOf<double> {
 };
 
 constexpr unsigned kSpecCap = 16384;  // appended keys per iteration
+constexpr unsigned kSpecMinKeys = 256;  // keys on each side of the limit the next window holds at least
 
 // radix-select digit layout (pmx_select.hip): 11-bit digits from the top,
 // the last one(s) 10-bit
@@ -158,6 +159,10 @@ __device__ __forceinline__ void spec_update(SpecSel* sp, typename KeyOf<T>::K kl
     sp->mv = mv;
     double hw = 3.0 * mv + 64.0;
     const double dens = density > 1e-30 ? density : 1e-30;
+    // at least ~kSpecMinKeys keys on each side of the limit (a window of a
+    // few key units holds a handful of keys in a dense distribution)
+    const double min_hw = (double)kSpecMinKeys / dens;
+    if (hw < min_hw) hw = min_hw;
     // expected appends <= cap / 8: every append is an atomic on one counter
     // inside the match kernel, so the window is kept small
     const double cap_hw = (double)(kSpecCap / 16) / dens;
