@@ -50,7 +50,6 @@ struct KeyOf<double> {
 };
 
 constexpr unsigned kSpecCap = 16384;  // appended keys per iteration
-constexpr unsigned kSpecMinKeys = 256;  // keys on each side of the limit the next window holds at least
 
 // radix-select digit layout (pmx_select.hip): 11-bit digits from the top,
 // the last one(s) 10-bit
@@ -80,7 +79,6 @@ struct SpecSel {
     int hit;                    // this iteration's limit came from the window
     unsigned long long n_hit, n_miss;  // statistics (host-readable)
     double dens;                // key density estimate of the last radix select (keys per key unit)
-    double mv;                  // recent limit moves (key units): the larger of the last and half the one before
 };
 
 // ---- match side: classify every distance the match writes ----
@@ -153,16 +151,8 @@ __device__ __forceinline__ void spec_update(SpecSel* sp, typename KeyOf<T>::K kl
     using KO = KeyOf<T>;
     using K = typename KO::K;
     const double move = sp->have_prev ? (double)(kl > (K)sp->prev ? kl - (K)sp->prev : (K)sp->prev - kl) : 0.0;
-    // (a decaying memory of the moves: one small step between two larger
-    // ones no longer shrinks the next window below the moves still to come)
-    const double mv = sp->have_prev ? fmax(move, 0.5 * sp->mv) : move;
-    sp->mv = mv;
-    double hw = 3.0 * mv + 64.0;
+    double hw = 3.0 * move + 64.0;
     const double dens = density > 1e-30 ? density : 1e-30;
-    // at least ~kSpecMinKeys keys on each side of the limit (a window of a
-    // few key units holds a handful of keys in a dense distribution)
-    const double min_hw = (double)kSpecMinKeys / dens;
-    if (hw < min_hw) hw = min_hw;
     // expected appends <= cap / 8: every append is an atomic on one counter
     // inside the match kernel, so the window is kept small
     const double cap_hw = (double)(kSpecCap / 16) / dens;
