@@ -409,8 +409,6 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
 }
 
 // ------------------------------------------------------------------- match --
-int fuse_buffers(pmx_ctx* c);  // (below)
-
 template <typename T>
 int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
     if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
@@ -512,24 +510,12 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         c->spec_exchanged = false;
         // (this rank's segment is its block of the gathered array: an in-place all-gather)
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx + (size_t)kSpecXStride * c->rank : nullptr;
-        // the point-to-plane accumulation fused into a certified lane match
-        // (FuseP2P; the loop enqueue decided fuse_on for this iteration)
-        const FuseP2P* fz = nullptr;
-        c->fuse_now = false;
-        if (c->fuse_on && loop_ctl(c) && spec && !xseg && knn == 1 && c->grid_mode >= 1 && c->N > 0 &&
-            c->reuse_on && !no_prev && c->has_normals && (c->dim == 2 || c->dim == 3)) {
-            const int rc = fuse_buffers(c);
-            if (rc) return rc;
-            fz = &c->fz;
-            c->fuse_now = true;
-        }
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->d_vpart, c->merge_counter ? nullptr : c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on, e1, c->stream,
-                             fz, c->dim);
+                             c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on, e1, c->stream);
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
@@ -609,8 +595,7 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
         // (merged: this launch also runs the match's counter phase)
         const bool merged = c->merge_counter && spec;
         launch_select_all<T>(d, n, c->d_selx, st, ratio, ratio_dev, c->d_iter_err, loop_ctl(c), spec,
-                             merged ? c->d_vpart : nullptr, merged ? c->d_visited : nullptr, c->stream,
-                             merged && c->fuse_now ? c->fz.ovf : nullptr);
+                             merged ? c->d_vpart : nullptr, merged ? c->d_visited : nullptr, c->stream);
         if (merged) c->vpart_dirty = true;
         c->merge_counter = false;
     } else {
@@ -623,34 +608,6 @@ int quantile_select(pmx_ctx* c, const T* d, int64_t n, double ratio, const doubl
         }
     }
     HIPCHK(c, hipGetLastError());
-    return PMX_OK;
-}
-
-// the fused match's buffers (FuseP2P) for this reading: partials, listed
-// slots and their list words per match wave, the overflow flag (zeroed whenever
-// the layout moves)
-int fuse_buffers(pmx_ctx* c) {
-    const int64_t nmb = (c->N + 255) / 256;  // (the lane kernel's grid: one slot per thread)
-    const int64_t nwb = kRedBlocks;  // (the point-to-plane launch's grid: one listed-slot row per block)
-    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t b_part = al(sizeof(double) * kFuseNV * nmb), b_wpart = al(sizeof(double) * kFuseNV * nwb);
-    const size_t b_list = al(sizeof(int32_t) * kFuseCap * 4 * nmb), b_cnt = al(sizeof(uint32_t) * 4 * nmb);
-    void* old = c->d_fz;
-    const int rc = ensure(c, &c->d_fz, &c->fz_bytes, b_part + b_wpart + b_list + b_cnt + 256);
-    if (rc) return rc;
-    c->fz.cap = c->fz_cap;
-    c->fz.dbg = c->fz_dbg;
-    if (c->d_fz == old && c->fz.nmb == nmb && c->fz.part) return PMX_OK;
-    char* p = (char*)c->d_fz;
-    c->fz.part = (double*)p;
-    c->fz.wpart = (double*)(p += b_part);
-    c->fz.list = (int32_t*)(p += b_wpart);
-    c->fz.cnt = (uint32_t*)(p += b_list);
-    c->fz.ovf = (unsigned int*)(p += b_cnt);
-    c->fz.hit = &c->d_spec->hit;
-    c->fz.nmb = (int)nmb;
-    c->fz.nwb = (int)nwb;
-    HIPCHK(c, hipMemsetAsync(c->fz.ovf, 0, sizeof(unsigned int), c->stream));
     return PMX_OK;
 }
 
@@ -1033,15 +990,12 @@ int p2plane_enqueue(pmx_ctx* c) {
     const WChain<T> chain = chain_of<T>(c);
     const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
-    // (a fused match of this iteration: FuseP2P)
-    const FuseP2P* fz = c->fuse_now && !chain.robust ? &c->fz : nullptr;
-    c->fuse_now = false;
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
                               match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
                               loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->vpart_dirty ? c->d_vpart : nullptr,
-                              c->stream, fz);
+                              c->stream);
     c->vpart_dirty = false;
-    launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream, fz);
+    launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result, NV);
 }

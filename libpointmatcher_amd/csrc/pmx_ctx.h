@@ -250,17 +250,6 @@ struct pmx_ctx {
     // iteration; the point-to-plane launch then zeroes the spread counters
     bool merge_counter = false;  // (set for the match being enqueued)
     bool vpart_dirty = false;    // (the merged counter phase read them: the next reduction zeroes them)
-    // the point-to-plane accumulation fused into the match (FuseP2P,
-    // pmx_internal.h): allowed for the loop being enqueued (fuse_on), taken by
-    // the match being enqueued (fuse_now: a certified, non-cold lane match)
-    bool fuse_allowed = true;
-    int fz_dbg = 0;
-    int fz_cap = kFuseCap;  // (PMX_FUSE_CAP: a smaller list per block, to test the overflow path)
-    bool fuse_on = false;
-    bool fuse_now = false;
-    void* d_fz = nullptr;
-    size_t fz_bytes = 0;
-    FuseP2P fz{};
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }
     bool loop_begun = false;

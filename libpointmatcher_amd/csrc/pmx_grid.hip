@@ -43,7 +43,6 @@
 // per-lane search from LDS (broadcast reads) and measures 0.187 ms at C3: a
 // candidate for QPT > 1 and for very dense references.
 #include "pmx_internal.h"
-#include "pmx_p2plane.h"
 #include "pmx_spec.h"
 
 namespace pmx {
@@ -430,106 +429,6 @@ __device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&k
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, none);
 }
 
-// ---- the point-to-plane accumulation fused into the match (FuseP2P) ----
-// the thread's certified query (k = 1): slot, transformed point, the written
-// pair and its gathered record (point, normal: loaded with the certificate)
-template <typename T>
-struct FuseRec {
-    int64_t j = -1;  // (-1: none)
-    T x, y, z, d;
-    P4<T> q, n;
-};
-// The wave's point-to-plane sums over its certified queries, classified by
-// the quantile window (pmx_internal.h FuseP2P): +inf: a rejected point (as
-// p2plane_body counts it); key < lo: kept (the point-to-plane terms); key <=
-// hi: to be listed for the point-to-plane launch (returned: the slot, or -1);
-// above (or NaN): a rejected match and point.  Runs before the block's full
-// searches (nothing of it stays live through them) and leaves the wave's sums
-// in red[wave][.] (block_store's transposed wave sum); the barrier of the
-// miss compaction publishes them to fuse_store.
-template <typename T, int DIM>
-__device__ __forceinline__ int32_t fuse_partials(const FuseRec<T>& rc, const SpecAcc<T>& sa, double* red) {
-    using KO = KeyOf<T>;
-    using K = typename KO::K;
-    constexpr int NF = DIM == 3 ? 6 : 3;
-    constexpr int NS = NF * (NF + 1) / 2;
-    constexpr int NV = NS + NF + 5;
-    constexpr int V = NV <= 16 ? 16 : 32;
-    double acc[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) acc[v] = 0.0;
-    int32_t listed = -1;
-    if (rc.j >= 0) {
-        const T dv = rc.d;
-        const K key = KO::key(dv);
-        if (dv == (T)__builtin_huge_val()) {
-            acc[NS + NF + 3] += 1.0;  // rejected point
-        } else if (key < sa.lo) {
-            acc[NS + NF + 0] += 1.0;  // kept
-            acc[NS + NF + 1] += 1.0;  // nonzero weight
-            acc[NS + NF + 4] += 1.0;  // sum of the weights
-            p2plane_add<T, DIM, V>(acc, rc.x, rc.y, rc.z, rc.q, rc.n);
-        } else if (key <= sa.hi) {
-            listed = (int32_t)rc.j;
-        } else {
-            acc[NS + NF + 2] += 1.0;  // rejected match
-            acc[NS + NF + 3] += 1.0;  // rejected point
-        }
-    }
-    int idx;
-    const double s = wave_transpose_sum<V>(acc, idx);
-    if (transpose_writer<V>()) red[(threadIdx.x >> 6) * 32 + idx] = s;
-    return listed;
-}
-// The block's partials from the four waves' sums (after the miss compaction's
-// barrier; the first NV threads, no further barrier): part[v * nmb + block].
-template <int DIM>
-__device__ __forceinline__ void fuse_store(const double* red, const FuseP2P& fz) {
-    constexpr int NV = DIM == 3 ? 32 : 14;
-    const int v = threadIdx.x;
-    if (v < NV)
-        fz.part[(int64_t)v * fz.nmb + blockIdx.x] = ((red[v] + red[32 + v]) + red[64 + v]) + red[96 + v];
-}
-// The wave's list (pmx_internal.h FuseP2P; no barrier): its certified slot
-// inside the window (l0) and its full search (jfull, distance dfull) unless
-// that was rejected outright (+inf: a rejected point; above hi or NaN: a
-// rejected match and point, counted in the list word), in (lane, entry)
-// order; lane 0 writes the word  n | rejected matches << 10 | rejected
-// points << 20  and raises the overflow flag past fz.cap.
-template <typename T>
-__device__ __forceinline__ void fuse_list(int32_t l0, int64_t jfull, T dfull, const SpecAcc<T>& sa,
-                                          const FuseP2P& fz) {
-    using KO = KeyOf<T>;
-    bool rm = false, rp = false, lf = false;
-    if (jfull >= 0) {
-        if (dfull == (T)__builtin_huge_val()) {
-            rp = true;
-        } else if (KO::key(dfull) <= sa.hi) {
-            lf = true;
-        } else {
-            rm = true;
-            rp = true;
-        }
-    }
-    const int nl = (l0 >= 0 ? 1 : 0) + (lf ? 1 : 0);
-    const int32_t e0 = l0 >= 0 ? l0 : (int32_t)jfull, e1 = (int32_t)jfull;
-    const int lane = threadIdx.x & 63;
-    const unsigned long long b1 = __ballot(nl >= 1), b2 = __ballot(nl >= 2);
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    const uint32_t off = (uint32_t)(__popcll(b1 & lt) + __popcll(b2 & lt));
-    const uint32_t tot = (uint32_t)(__popcll(b1) + __popcll(b2));
-    const uint32_t nrm = (uint32_t)__popcll(__ballot(rm)), nrp = (uint32_t)__popcll(__ballot(rp));
-    const int64_t lw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    int32_t* L = fz.list + lw * kFuseCap;
-    const uint32_t cap = (uint32_t)fz.cap;
-    if (nl >= 1 && off < cap) L[off] = e0;
-    if (nl >= 2 && off + 1 < cap) L[off + 1] = e1;
-    if (lane == 0) {
-        fz.cnt[lw] = tot | nrm << 10 | nrp << 20;
-        if (tot > cap) atomicOr(fz.ovf, 1u);
-    }
-}
-
 // Pair / fallback counters.  One device-scope atomic per wave on a single
 // address serialises (~110 us for 16K waves at C3), so every wave adds into
 // one of kVSlots counters, each on its own 128-byte line; counter_sum_kernel
@@ -680,8 +579,7 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
                                            const uint32_t* __restrict__ start, const GridGeom& G,
                                            const P4<T>* __restrict__ rd, int64_t j, const Mat4<T>& Tm, int k,
                                            T maxR2, int oct, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                           T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa,
-                                           T* d0 = nullptr) {
+                                           T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa) {
     T qx, qy, qz;
     gxform(Tm, gld(rd, j), qx, qy, qz);
     T kd[KT];
@@ -709,7 +607,6 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
         }
     }
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
-    if (d0) *d0 = ki[0] == kNoPos || !(kd[0] <= maxR2) ? (T)__builtin_huge_val() : kd[0];  // (entry 0 as written)
     // (a certified octant block bounds the rest by its interior faces, as a
     // shell walk's exit does)
     if (safe) safe[j] = safe_radius<T, KT>(kd, ki, k, lb_exit);
@@ -783,9 +680,7 @@ struct LaneWaves {
     static constexpr int value = sizeof(T) == 8 ? 2 : 4;
 };
 
-// P = 0, or the dimension (2 / 3) of a fused point-to-plane accumulation
-// (FuseP2P; k = 1, device loop)
-template <typename T, int KT, int Q, int P>
+template <typename T, int KT, int Q>
 __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kernel(const P4<T>* __restrict__ gpts,
                                                         const int32_t* __restrict__ gidx,
                                                         const uint32_t* __restrict__ start, GridGeom G,
@@ -795,15 +690,11 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                                                         int reuse, T* __restrict__ safe, Mat4<T> Tprev,
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
-                                                        SpecSel* __restrict__ spec, const T* __restrict__ radii,
-                                                        FuseP2P fz) {
-    static_assert(P == 0 || Q == 1, "the fused accumulation takes one slot per thread");
-    const P4<T>* gpn = nullptr;
+                                                        SpecSel* __restrict__ spec, const T* __restrict__ radii) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
         gpts = D.gpts;
-        gpn = D.gpn;
         gidx = D.gidx;
         start = D.start;
         G = D.G;
@@ -819,10 +710,6 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
     // quantile window (pmx_spec.h): every written distance is classified
     SpecAcc<T> sa;
     spec_acc_init<T>(sa, spec);
-    FuseRec<T> rec;        // (P != 0: the thread's certified slot)
-    int64_t jfull = -1;    // (P != 0: the slot of its full search, its distance)
-    T dfull = (T)0;
-    __shared__ double fred[P != 0 ? 4 * 32 : 1];  // (P != 0: the waves' sums, fuse_partials)
     constexpr int B = 256 * Q;  // slots of the block
     __shared__ int miss[B];
     __shared__ int wave_cnt[Q][4];
@@ -868,18 +755,10 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             ok[q] = o && av < bq[q];
         }
         P4<T> r[Q][KR];
-        P4<T> nq[Q];  // (P != 0, k = 1: the candidate's normal, from its interleaved record)
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if (P != 0 && gpn && !(fz.dbg & 2)) {  // (uniform; gpn is there whenever the host fuses)
-                const uint32_t g = ok[q] ? 2u * (uint32_t)id[q][0] : 0u;
-                r[q][0] = gld32(gpn, g);
-                nq[q] = gld32(gpn, g + 1u);
-            } else {
+        for (int q = 0; q < Q; ++q)
 #pragma unroll
-                for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < k ? (uint32_t)id[q][s] : 0u);
-            }
-        }
+            for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < k ? (uint32_t)id[q][s] : 0u);
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if (!ok[q]) continue;
@@ -897,25 +776,9 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                 if (s < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx[q], qy[q], qz[q], r[q][s]), id[q][s]);
             visits += (uint32_t)k;
             write_out<T, KT>(j, k, qr2(radii, j, maxR2), kd, ki, out_d, out_i, sa);
-            if constexpr (P != 0) {  // (k = 1: entry 0 is the candidate, or (inf, -1) beyond the radius)
-                rec.j = j;
-                rec.x = qx[q];
-                rec.y = qy[q];
-                rec.z = qz[q];
-                rec.d = ki[0] == kNoPos || !(kd[0] <= qr2(radii, j, maxR2)) ? (T)__builtin_huge_val() : kd[0];
-                rec.q = r[q][0];
-                rec.n = nq[q];
-            }
             safe[j] = (T)(bq[q] * (1.0 - 1e-6));
             missed[q] = false;
         }
-    }
-    // (P != 0, uniform: a window and a fused launch; without a window the
-    // pick misses and the point-to-plane launch makes its full pass)
-    const bool fuse = P != 0 && sa.on && fz.part && gpn;
-    int32_t listed = -1;
-    if constexpr (P != 0) {
-        if (fuse && !(fz.dbg & 1)) listed = fuse_partials<T, P>(rec, sa, fred);
     }
     // the block's misses, compacted in slot order
     unsigned long long mq[Q];
@@ -941,19 +804,13 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
     for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
         const int64_t j2 = base + miss[t];
         full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
-                          sa, P != 0 ? &dfull : nullptr);
-        if constexpr (P != 0) jfull = j2;
+                          sa);
         if (Q == 1) break;
     }
     add_visits(visits, visited);
     // queries that took the full search (the "fallback" counter the level choice reads)
     if (threadIdx.x == 0 && visited && total && reuse) atomicAdd(vslot(visited, 1), (unsigned long long)total);
     if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
-    if constexpr (P != 0) {
-        if (fuse && !(fz.dbg & 4)) fuse_list<T>(listed, jfull, dfull, sa, fz);
-        if (fuse && !(fz.dbg & 1)) fuse_store<P>(fred, fz);
-        if (fuse && fz.dbg && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(fz.ovf, 1u);  // (experiments: a miss)
-    }
 }
 
 // ------------------------------------------------------------ tile kernel --
@@ -964,7 +821,7 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                      const T* radii, bool cold, hipStream_t s, const FuseP2P* fz, int fuse_dim) {
+                      const T* radii, bool cold, hipStream_t s) {
     if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
                            G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
@@ -972,22 +829,9 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
-#define PMX_LANE(P, F)                                                                                               \
-    hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q, P>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G, \
-                       rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,    \
-                       ctl, gd, spec, radii, F)
-        if constexpr (KT <= 2 && Q == 1) {  // (k = 1, with or without the reuse entry)
-            if (fz && fz->part && knn == 1 && fuse_dim == 3) {
-                PMX_LANE(3, *fz);
-                return;
-            }
-            if (fz && fz->part && knn == 1 && fuse_dim == 2) {
-                PMX_LANE(2, *fz);
-                return;
-            }
-        }
-        PMX_LANE(0, FuseP2P{});
-#undef PMX_LANE
+        hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
+                           rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
+                           ctl, gd, spec, radii);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -1003,7 +847,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                        SelectState* spec_st, unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end,
-                       hipStream_t s, const FuseP2P* fz, int fuse_dim) {
+                       hipStream_t s) {
     if (N <= 0) return;
     cold = cold && mode >= 1;
     if (mode < 1 || !visited) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
@@ -1020,7 +864,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     } else {
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, radii, cold, s, fz, fuse_dim)
+                     ru, ctl, gd, spec, radii, cold, s)
         // with reuse the list keeps room for the (k+1)-th point (the safe radius;
         // the cold tile writes radius 0 and keeps k entries)
         const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
@@ -1049,15 +893,13 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, const float*, bool, hipEvent_t, hipStream_t,
-                                       const FuseP2P*, int);
+                                       unsigned long long*, const float*, bool, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, const double*, bool, hipEvent_t, hipStream_t,
-                                        const FuseP2P*, int);
+                                        unsigned long long*, const double*, bool, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,
@@ -1082,7 +924,7 @@ void launch_pos_to_index(const int32_t* pos, const int32_t* gidx, int32_t* out, 
 // first ICP iteration.
 void preload_grid() {
     hipFuncAttributes a;
-    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1, 1, 0>));
+    (void)hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&grid_lane_kernel<float, 1, 1>));
 }
 
 }  // namespace pmx

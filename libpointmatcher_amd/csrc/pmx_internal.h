@@ -184,36 +184,6 @@ void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* star
                      SpecSel* spec, hipStream_t s);
 
 
-// ---- the point-to-plane accumulation fused into the match (pmx_grid.hip) ----
-// Device loop, single rank, chain = one TrimmedDist (the quantile window on),
-// k = 1, point-to-plane, a certified (non-cold) match.  The window splits the
-// distances before the limit is known: below lo every pair is kept (the limit
-// is inside [lo, hi] whenever the window resolves it), above hi every pair is
-// rejected.  So the match kernel adds, for its certified queries, the
-// point-to-plane terms of the pairs below lo (their point and normal gathered
-// with the certificate's load) and the counters of the others into per-block
-// partials, and each wave lists its slots inside the window and its full
-// searches that may be kept (their record was never gathered), counting the
-// full searches rejected outright in its list word.  After the pick, the
-// point-to-plane launch judges only the listed slots (the same chain_keep on
-// the resolved limit) and the finalize sums both partial sets in a fixed
-// order (deterministic).  When the window misses (or a wave listed more than
-// its room: the pick then counts as a miss), the point-to-plane launch makes
-// its full pass and the finalize sums those partials, as without fusion.
-constexpr int kFuseCap = 32;     // listed slots per match wave
-constexpr int kFuseNV = 32;      // partial rows (p2plane_nv(3))
-struct FuseP2P {
-    double* part = nullptr;      // the match blocks' partials [NV][nmb]
-    int32_t* list = nullptr;     // per match wave: the listed slots [4 nmb][kFuseCap]
-    uint32_t* cnt = nullptr;     // per match wave: n | rejected matches << 10 | rejected points << 20 (n > cap: overflow)
-    double* wpart = nullptr;     // the listed slots' partials [NV][nwb]
-    unsigned int* ovf = nullptr; // a block overflowed (reset by the select launch's commit)
-    const int* hit = nullptr;    // the window's verdict (SpecSel::hit)
-    int nmb = 0, nwb = 0;        // match blocks; listed-slot rows (the point-to-plane launch's grid)
-    int cap = kFuseCap;          // listed slots a block may hold (<= kFuseCap; PMX_FUSE_CAP, tests)
-    int dbg = 0;                 // (timing experiments, PMX_FUSE_DBG: 1 no partials, 2 no normal gather, 4 no list)
-};
-
 // ---- grid match (pmx_grid.hip) ----
 // mode 0 = wave-cooperative LDS tiles, 1 = per-lane shell search (default),
 // 2 = octant block first.  ids written are positions in gpts;
@@ -228,8 +198,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end, hipStream_t s,
-                       const FuseP2P* fz = nullptr, int fuse_dim = 0);
+                       unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end, hipStream_t s);
 // several ranks: the quantile window's pick over the all-gathered segments
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum.
 // stall: a miss sets ctl->done = kCtlStalled (the host did not read the
@@ -459,13 +428,11 @@ int64_t select_all_blocks(int64_t n);
 constexpr int kSelTimeout = -30;  // iteration error: a select_all wait timed out
 // vpart / vout (may be null): the match's counter phase merged into this
 // launch (pmx_selectall.h counter_merged); the spread counters are then
-// zeroed by the next point-to-plane launch (launch_p2plane_partial's vzero).
-// fuse_ovf (may be null): the fused match's overflow flag (FuseP2P): set, the
-// window's verdict is a miss; the commit resets it
+// zeroed by the next point-to-plane launch (launch_p2plane_partial's vzero)
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
                        int* iter_err, const LoopCtl* ctl, SpecSel* spec, const unsigned long long* vpart,
-                       unsigned long long* vout, hipStream_t s, unsigned int* fuse_ovf = nullptr);
+                       unsigned long long* vout, hipStream_t s);
 int select_bins(int pass, int key_bits);
 
 // VarTrimmed pieces
@@ -500,10 +467,8 @@ template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
-                            hipStream_t s, const FuseP2P* fz = nullptr);
-// fz (may be null): a fused match's partials (FuseP2P), summed instead when the window hit
-void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s,
-                     const FuseP2P* fz = nullptr);
+                            hipStream_t s);
+void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
                           const int32_t* ids, const WChain<T>& chain, int k, int64_t N, double* partials,

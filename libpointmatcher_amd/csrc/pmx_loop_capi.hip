@@ -176,11 +176,6 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     c->merge_counter = c->spec_on && !sharded(c) && cfg.minimizer == 0 && c->grid_mode >= 1 && c->N > 0 &&
                        cfg.knn <= kLaneMaxK && (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
     c->vpart_dirty = false;
-    // the point-to-plane accumulation fused into the match (FuseP2P): one
-    // TrimmedDist, k = 1 (the match decides per iteration: certified lane matches)
-    c->fuse_on = c->merge_counter && c->fuse_allowed && cfg.n_filters == 1 && k0 == PMX_FILTER_TRIMMED &&
-                 cfg.knn == 1;
-    c->fuse_now = false;
     c->shard_async = c->spec_on && sharded(c) && !c->shard_replay && !c->spec_fresh &&
                      c->shard_hit_streak >= kAsyncAfterHits;
     int rc;
@@ -224,7 +219,6 @@ int loop_enqueue_iteration(pmx_ctx* c) {
                         (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, c->stream);
     HIPCHK(c, hipGetLastError());
     c->shard_replay = false;
-    c->fuse_on = false;
     return PMX_OK;
 }
 

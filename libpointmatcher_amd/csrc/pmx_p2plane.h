@@ -61,10 +61,8 @@ __device__ __forceinline__ bool transpose_writer() {
 // (value-major: the finalize reads each value's block partials contiguously)
 // kCoherent: agent-scope atomic stores (another block of the same launch sums
 // the partials: pmx_post.hip's last-block finalize)
-// (block_store_at: partials[v * nblk + blk] for an explicit partial grid)
 template <int NV, bool kCoherent = false>
-__device__ __forceinline__ void block_store_at(double (&acc)[NV], double* __restrict__ partials, int64_t nblk,
-                                               int64_t blk) {
+__device__ __forceinline__ void block_store(double (&acc)[NV], double* __restrict__ partials) {
     // (the power of two the transposed wave sum takes)
     constexpr int V = NV <= 8 ? 8 : NV <= 16 ? 16 : NV <= 32 ? 32 : 64;
     static_assert(NV <= 64, "block_store: at most 64 values");
@@ -79,16 +77,12 @@ __device__ __forceinline__ void block_store_at(double (&acc)[NV], double* __rest
     __syncthreads();
     for (int v = threadIdx.x; v < NV; v += blockDim.x) {
         const double r = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
-        double* dst = &partials[(int64_t)v * nblk + blk];
+        double* dst = &partials[(int64_t)v * gridDim.x + blockIdx.x];
         if (kCoherent)
             __hip_atomic_store(dst, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else
             *dst = r;
     }
-}
-template <int NV, bool kCoherent = false>
-__device__ __forceinline__ void block_store(double (&acc)[NV], double* __restrict__ partials) {
-    block_store_at<NV, kCoherent>(acc, partials, gridDim.x, blockIdx.x);
 }
 
 

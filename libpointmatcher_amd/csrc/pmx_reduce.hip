@@ -47,53 +47,6 @@ __device__ __forceinline__ T p2pl_distance(T px, T py, T pz, const P4<T>& q, con
     return dot * dot;  // (pow(dot, 2) rounds to the same T)
 }
 
-// A fused match (FuseP2P, pmx_internal.h) whose window resolved the limit:
-// the match waves' lists (window slots, full searches) judged on the resolved
-// limit as p2plane_body judges a k = 1 slot, plus the rejections counted in
-// the list words, into fz.wpart (one row per block of this launch).  Thread g
-// of the launch takes the lists g, g + threads, ... in list order: a fixed
-// assignment, so the sums are deterministic.
-template <typename T, int DIM>
-__device__ __forceinline__ void p2plane_listed(const P4<T>* __restrict__ rd, const Mat4<T>& Tm,
-                                               const P4<T>* __restrict__ ref, const P4<T>* __restrict__ nrm, int rs,
-                                               const T* __restrict__ d, const int32_t* __restrict__ ids,
-                                               const WChain<T>& chain, const FuseP2P& fz) {
-    constexpr int NF = DIM == 3 ? 6 : 3;
-    constexpr int NS = NF * (NF + 1) / 2;
-    constexpr int NV = NS + NF + 5;
-    double acc[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
-    const WRange<T> wr = chain_resolve(chain);
-    const T inf = (T)__builtin_huge_val();
-    const int64_t nlists = (int64_t)fz.nmb * 4, stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t lw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; lw < nlists; lw += stride) {
-        const uint32_t w = fz.cnt[lw];
-        acc[NS + NF + 2] += (double)((w >> 10) & 1023u);  // rejected matches
-        acc[NS + NF + 3] += (double)((w >> 20) & 1023u);  // rejected points
-        uint32_t n = w & 1023u;
-        if (n > (uint32_t)fz.cap) n = (uint32_t)fz.cap;  // (an overflow made the window miss: not reached)
-        for (uint32_t i = 0; i < n; ++i) {
-            const int32_t j = fz.list[lw * kFuseCap + i];
-            const T dv = d[j];
-            const bool keep = chain_keep(wr, dv);
-            if (keep) acc[NS + NF + 1] += 1.0;                 // (w != 0).count()
-            if (dv != inf && !keep) acc[NS + NF + 2] += 1.0;  // rejected match
-            if (dv == inf || !keep) {
-                acc[NS + NF + 3] += 1.0;  // rejected point
-                continue;
-            }
-            acc[NS + NF + 0] += 1.0;
-            acc[NS + NF + 4] += 1.0;
-            const int64_t g = (int64_t)ids[j] * rs;
-            T px, py, pz;
-            xform3(Tm, rd[j], px, py, pz);
-            p2plane_add<T, DIM, NV>(acc, px, py, pz, gld(ref, g), gld(nrm, g));
-        }
-    }
-    block_store_at<NV>(acc, fz.wpart, gridDim.x, blockIdx.x);
-}
-
 // result layout: [0, NS) upper triangle of A row-major (r <= c), [NS, NS+NF) b,
 // then kept, nonzero weights, rejected matches, rejected points
 template <typename T, int DIM>
@@ -105,8 +58,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                                                               int k, int64_t N, double* __restrict__ partials,
                                                               const LoopCtl* __restrict__ ctl,
                                                               const GridDesc<T>* __restrict__ gd,
-                                                              unsigned long long* __restrict__ vzero,
-                                                              FuseP2P fz) {
+                                                              unsigned long long* __restrict__ vzero) {
     if (ctl) {  // device loop
         if (ctl->done) return;
         ctl_transform(ctl, Tm);
@@ -116,10 +68,6 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
     }
     if (vzero && blockIdx.x == 0)  // (the spread counters the merged counter phase read, for the next match)
         for (int c = 0; c < 4; ++c) vzero[(size_t)(c * kVSlots + threadIdx.x) * kVStride] = 0ull;
-    if (fz.part && *fz.hit) {  // (uniform) a fused match, the window resolved the limit
-        p2plane_listed<T, DIM>(rd, Tm, ref, nrm, rs, d, ids, chain, fz);
-        return;
-    }
     p2plane_body<T, DIM>(rd, Tm, ref, nrm, rs, d, ids, chain, k, N, partials);
 }
 
@@ -218,8 +166,7 @@ template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
-                            hipStream_t s, const FuseP2P* fz) {
-    const FuseP2P f = fz ? *fz : FuseP2P{};
+                            hipStream_t s) {
     if (chain.robust) {  // real-valued weights: the full asymmetric A
         if (dim == 3)
             hipLaunchKernelGGL((p2plane_weighted_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
@@ -231,40 +178,30 @@ void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref
     }
     if (dim == 3)
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
-                           d, ids, chain, k, N, partials, ctl, gd, vzero, f);
+                           d, ids, chain, k, N, partials, ctl, gd, vzero);
     else
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
-                           d, ids, chain, k, N, partials, ctl, gd, vzero, f);
+                           d, ids, chain, k, N, partials, ctl, gd, vzero);
 }
 
 // Sum the per-block partials: one block per accumulator, each thread adds a
 // fixed strided subset in order, then a fixed-shape tree — the summation
 // order never changes, so results are bitwise reproducible.
-// With a fused match whose window hit (FuseP2P): the match blocks' partials,
-// then the listed slots' partials, in the same fixed order.
 __global__ __launch_bounds__(256) void finalize_kernel(const double* __restrict__ partials, int nblocks, int nv,
-                                                       double* __restrict__ out, const LoopCtl* __restrict__ ctl,
-                                                       FuseP2P fz) {
+                                                       double* __restrict__ out, const LoopCtl* __restrict__ ctl) {
     __shared__ double red[4];
     if (ctl && ctl->done) return;
     const int v = blockIdx.x;
     double s = 0.0;
-    if (fz.part && *fz.hit) {  // (uniform)
-        for (int64_t b = threadIdx.x; b < fz.nmb; b += 256) s += fz.part[(int64_t)v * fz.nmb + b];
-        for (int b = threadIdx.x; b < fz.nwb; b += 256) s += fz.wpart[(int64_t)v * fz.nwb + b];
-    } else {
-        for (int b = threadIdx.x; b < nblocks; b += 256) s += partials[(int64_t)v * nblocks + b];
-    }
+    for (int b = threadIdx.x; b < nblocks; b += 256) s += partials[(int64_t)v * nblocks + b];
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) out[v] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s,
-                     const FuseP2P* fz) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(nv), dim3(256), 0, s, partials, nblocks, nv, out, ctl,
-                       fz ? *fz : FuseP2P{});
+void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(nv), dim3(256), 0, s, partials, nblocks, nv, out, ctl);
 }
 
 // ------------------------------------------------------------ point-to-point --
@@ -445,8 +382,7 @@ void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, c
 #define PMX_INST(T)                                                                                                  \
     template void launch_p2plane_partial<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const P4<T>*, int, const T*, \
                                             const int32_t*, const WChain<T>&, int, int64_t, int, double*,           \
-                                            const LoopCtl*, const GridDesc<T>*, unsigned long long*, hipStream_t,     \
-                                            const FuseP2P*);                                                          \
+                                            const LoopCtl*, const GridDesc<T>*, unsigned long long*, hipStream_t);    \
     template void launch_p2point_pass1<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
                                           const WChain<T>&, int, int64_t, double*, const LoopCtl*,                   \
                                           const GridDesc<T>*, hipStream_t);                                          \

@@ -255,18 +255,17 @@ __global__ __launch_bounds__(256) void select_all_kernel(const T* __restrict__ d
                                                          int* __restrict__ iter_err, const LoopCtl* __restrict__ ctl,
                                                          SpecSel* __restrict__ spec,
                                                          const unsigned long long* __restrict__ vpart,
-                                                         unsigned long long* __restrict__ vout,
-                                                         unsigned int* __restrict__ fuse_ovf) {
+                                                         unsigned long long* __restrict__ vout) {
     if (ctl && ctl->done) return;  // (uniform: no block arrives anywhere)
-    select_all_body<T>(d, n, sx, st, ratio_host, ratio_dev, iter_err, spec, vpart, vout, fuse_ovf);
+    select_all_body<T>(d, n, sx, st, ratio_host, ratio_dev, iter_err, spec, vpart, vout);
 }
 
 template <typename T>
 void launch_select_all(const T* d, int64_t n, void* selx, SelectState* st, double ratio, const double* ratio_dev,
                        int* iter_err, const LoopCtl* ctl, SpecSel* spec, const unsigned long long* vpart,
-                       unsigned long long* vout, hipStream_t s, unsigned int* fuse_ovf) {
+                       unsigned long long* vout, hipStream_t s) {
     hipLaunchKernelGGL(select_all_kernel<T>, dim3((unsigned)select_blocks(n)), dim3(256), 0, s, d, n, (SelX*)selx, st,
-                       ratio, ratio_dev, iter_err, ctl, spec, vpart, vout, vpart ? fuse_ovf : nullptr);
+                       ratio, ratio_dev, iter_err, ctl, spec, vpart, vout);
 }
 
 template <typename T>
@@ -1354,10 +1353,10 @@ template void launch_select_pick<double>(uint32_t*, SelectState*, int, double, c
                                          SpecSel*, hipStream_t);
 template void launch_select_all<float>(const float*, int64_t, void*, SelectState*, double, const double*, int*,
                                        const LoopCtl*, SpecSel*, const unsigned long long*, unsigned long long*,
-                                       hipStream_t, unsigned int*);
+                                       hipStream_t);
 template void launch_select_all<double>(const double*, int64_t, void*, SelectState*, double, const double*, int*,
                                         const LoopCtl*, SpecSel*, const unsigned long long*, unsigned long long*,
-                                        hipStream_t, unsigned int*);
+                                        hipStream_t);
 template void launch_vartrim<float>(const float*, int64_t, int, float, float, const float*, void*, size_t, double*,
                                     int*, SelectState*, const LoopCtl*, hipStream_t);
 template void launch_vartrim<double>(const double*, int64_t, int, double, double, const double*, void*, size_t,

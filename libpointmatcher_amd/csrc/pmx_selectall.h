@@ -105,7 +105,7 @@ template <typename T>
 __device__ __forceinline__ bool counter_merged(const unsigned long long* __restrict__ vpart,
                                                unsigned long long* __restrict__ out, int* __restrict__ iter_err,
                                                SpecSel* __restrict__ spec, SelectState* __restrict__ st,
-                                               SelX* __restrict__ sx, unsigned int* __restrict__ fuse_ovf) {
+                                               SelX* __restrict__ sx) {
     using K = typename KeyOf<T>::K;
     constexpr unsigned kLds = 4096;
     __shared__ unsigned long long red[4][kVSlots / 64];
@@ -117,9 +117,6 @@ __device__ __forceinline__ bool counter_merged(const unsigned long long* __restr
     const unsigned nk_raw = spec->n_keys;
     const K lo = (K)spec->lo, hi = (K)spec->hi;
     const bool valid = spec->valid != 0;
-    // a fused match wave listed more slots than it holds: a miss
-    // (every block reads the flag before block 0 resets it, below)
-    const bool ovf = fuse_ovf && __hip_atomic_load(fuse_ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     unsigned long long v[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) v[c] = vpart[(size_t)(c * kVSlots + t) * kVStride];
@@ -144,8 +141,8 @@ __device__ __forceinline__ bool counter_merged(const unsigned long long* __restr
     for (int c = 0; c < 4; ++c)
         for (int w = 0; w < kVSlots / 64; ++w) sum[c] += red[c][w];
     unsigned long long kl = 0;
-    const bool hit = spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap || ovf, src,
-                                           lh, part, bc, false, &kl);
+    const bool hit = spec_pick<T, kVSlots>(spec, st, sum[2], sum[3], src.n_local, nk_raw > kSpecCap, src, lh, part,
+                                           bc, false, &kl);
     __syncthreads();  // (every thread of the block has read)
     if (t == 0) {
         const unsigned old = atomicAdd(&sx->cread, 1u);
@@ -165,7 +162,6 @@ __device__ __forceinline__ bool counter_merged(const unsigned long long* __restr
             __hip_atomic_store(&out[1], sum[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(iter_err, all ? 0 : kSelTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             spec_commit<T>(spec, st, hit, lo, hi, (K)kl, sum[2], nk_raw);
-            if (ovf) __hip_atomic_store(fuse_ovf, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     return hit;
@@ -179,8 +175,7 @@ __device__ __forceinline__ void select_all_body(const T* __restrict__ d, int64_t
                                                 const double* __restrict__ ratio_dev, int* __restrict__ iter_err,
                                                 SpecSel* __restrict__ spec,
                                                 const unsigned long long* __restrict__ vpart = nullptr,
-                                                unsigned long long* __restrict__ vout = nullptr,
-                                                unsigned int* __restrict__ fuse_ovf = nullptr) {
+                                                unsigned long long* __restrict__ vout = nullptr) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     __shared__ uint32_t lh[2048];
@@ -189,7 +184,7 @@ __device__ __forceinline__ void select_all_body(const T* __restrict__ d, int64_t
     __shared__ int s_last;
     __shared__ unsigned int s_old;
     if (vpart) {
-        if (counter_merged<T>(vpart, vout, iter_err, spec, st, sx, fuse_ovf)) return;  // (the window resolved it)
+        if (counter_merged<T>(vpart, vout, iter_err, spec, st, sx)) return;  // (the window resolved it)
     } else if (spec && spec->hit) {
         return;  // (the window resolved it in the counter kernel before this launch)
     }

@@ -189,9 +189,6 @@ def test_quantile_window_is_exact(monkeypatch, dtype, filt, knn, max_dist):
     test_loop_equals_modules / _filter_chains.)"""
     ref, nrm = reference_cloud(60000, dtype)
     rd = reading_cloud(50000, dtype)
-    # (the fused point-to-plane accumulation sums in another order: its own
-    # test below; here the window's limit alone is compared)
-    monkeypatch.setenv("PMX_FUSE_P2P", "0")
     out = {}
     for on in ("1", "0"):
         monkeypatch.setenv("PMX_SPEC_SELECT", on)
@@ -210,47 +207,3 @@ def test_quantile_window_is_exact(monkeypatch, dtype, filt, knn, max_dist):
     assert hits + misses == 30 and hits >= 15, (hits, misses)
     assert kept1 == kept0
     assert np.array_equal(tr1, tr0)
-
-
-def _fused_run(monkeypatch, env, dtype, ref, nrm, rd, max_dist, ratio, iters=30):
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    ctx = _capi.Context(0, dtype)
-    ctx.set_reference(ref, nrm)
-    ctx.set_reading(rd)
-    ctx.loop_begin(knn=1, max_dist=max_dist, filters=[("TrimmedDistOutlierFilter", ratio)],
-                   checkers=[("CounterTransformationChecker", iters)], keep_trace=True)
-    st = ctx.loop_run(iters)
-    out = (ctx.loop_trace(0, st.iterations), ctx.loop_select_stats(), st.last.kept, st.last.rejected_matches,
-           st.last.rejected_points, st.iterations)
-    ctx.close()
-    return out
-
-
-@pytest.mark.parametrize("max_dist", [np.inf, 0.05])
-@pytest.mark.parametrize("ratio", [0.85, 1.0])
-@pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_fused_point_to_plane(monkeypatch, dtype, ratio, max_dist):
-    """The point-to-plane terms accumulated inside the match (FuseP2P,
-    pmx_internal.h): the pairs below the quantile window in the match's block
-    partials, the listed window slots judged after the pick.  Bar: the same
-    counters and iteration count as the unfused loop, the trace within the
-    loop tolerance (the sums are grouped differently), bit-identical over two
-    runs (fixed summation order); with no room in the block lists
-    (PMX_FUSE_CAP=0) every window overflows into a miss and the loop is the
-    unfused one bit for bit."""
-    ref, nrm = reference_cloud(60000, dtype)
-    rd = reading_cloud(50000, dtype)
-    base = {"PMX_FUSE_CAP": "32"}
-    fa = _fused_run(monkeypatch, {**base, "PMX_FUSE_P2P": "1"}, dtype, ref, nrm, rd, max_dist, ratio)
-    fb = _fused_run(monkeypatch, {**base, "PMX_FUSE_P2P": "1"}, dtype, ref, nrm, rd, max_dist, ratio)
-    un = _fused_run(monkeypatch, {**base, "PMX_FUSE_P2P": "0"}, dtype, ref, nrm, rd, max_dist, ratio)
-    ov = _fused_run(monkeypatch, {"PMX_FUSE_P2P": "1", "PMX_FUSE_CAP": "0"}, dtype, ref, nrm, rd, max_dist, ratio)
-    assert np.array_equal(fa[0], fb[0])
-    hits, misses = fa[1]
-    assert hits >= 15, (hits, misses)
-    assert fa[2:] == un[2:]  # kept, rejected matches / points, iterations
-    assert np.abs(fa[0] - un[0]).max() <= 10 * TOL[dtype]
-    # every overflowing window is a miss: radix select + the full pass
-    assert ov[1][0] == 0, ov[1]
-    assert np.array_equal(ov[0], un[0]) and ov[2:] == un[2:]
