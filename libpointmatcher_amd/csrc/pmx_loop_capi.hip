@@ -3,14 +3,24 @@
 // stream, transform, level and stop flag kept on the device (pmx_loop.hip).
 #include "pmx_ctx.h"
 
+#include <cstdlib>
+
 namespace pmxc {
 
 // ------------------------------------------------------------ device loop --
 // pmx_loop_*: whole ICP iterations enqueued back to back (pmx_loop.hip).  The
-// host checks the stop flag once per batch of kLoopBatch iterations while the
-// next batch is already queued, so the GPU never waits for the host; after a
-// stop the queued iterations return at once (every kernel reads LoopCtl.done).
+// host checks the stop flag once per batch of iterations while the next batch
+// is already queued, so the GPU never waits for the host; after a stop the
+// queued iterations return at once (every kernel reads LoopCtl.done).  Batches
+// of kLoopBatch while an ICP is young (one that stops early runs few no-op
+// iterations), of kLoopBatchLong from iteration kLoopBatchAfter on: one status
+// copy per 8 iterations.  Same-box means of four runs at C3: driver 0.06728 vs
+// 0.06775 ms/iteration with 4 throughout (8 throughout 0.0673), whole ICP
+// 0.0932 vs 0.0939 — small; 2 throughout is slower (0.068-0.071).
+// PMX_LOOP_BATCH fixes one size (A/Bs).
 constexpr int kLoopBatch = 4;
+constexpr int kLoopBatchLong = 8;
+constexpr int kLoopBatchAfter = 8;
 // pinned status slot s (a copy of the device status block)
 const char* stat_slot(const pmx_ctx* c, int s) { return (const char*)c->h_loop + (size_t)s * kStatBytes; }
 // pinned staging of pmx_loop_begin's uploads, after the two status slots
@@ -236,7 +246,12 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
     c->loop_on = true;
     while (!stop && rc == PMX_OK) {
         while (c->loop_issued - start < n && nfly < 2 && rc == PMX_OK) {
-            const int b = (int)std::min<int64_t>(kLoopBatch, n - (c->loop_issued - start));
+            static const int fixed = [] {
+                const char* e = std::getenv("PMX_LOOP_BATCH");
+                return e ? std::max(1, std::atoi(e)) : 0;
+            }();
+            const int kb = fixed ? fixed : c->loop_issued >= kLoopBatchAfter ? kLoopBatchLong : kLoopBatch;
+            const int b = (int)std::min<int64_t>(kb, n - (c->loop_issued - start));
             if (c->loop_cfg.keep_trace && (rc = loop_trace_room<T>(c, c->loop_issued + b))) break;
             for (int i = 0; i < b && rc == PMX_OK; ++i) {
                 c->enq_iter = c->loop_issued + i;
