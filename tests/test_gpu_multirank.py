@@ -359,3 +359,66 @@ def test_sharded_stall_replay_bit_identical(two_ranks, two_ranks_forced_miss, dn
     for tag in ("trim", "med"):
         np.testing.assert_array_equal(f[0][f"{dn}_icp_{tag}"], r[0][f"{dn}_icp_{tag}"])
         np.testing.assert_array_equal(f[1][f"{dn}_icp_{tag}"], r[1][f"{dn}_icp_{tag}"])
+
+
+# ---- the BASELINE C3 size, sharded (1M -> 1M float, two ranks of 500 K) ----
+def _worker_c3(rank, world, port, outdir):
+    import torch  # noqa: F401
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from libpointmatcher_amd import _capi
+        from libpointmatcher_amd.icp import ICP
+        from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+
+        comm = _capi.gloo_host_comm()
+        ref, nrm = reference_cloud(1_000_000, np.float32)
+        rd = reading_cloud(1_000_000, np.float32)
+        lo, hi = shard_range(rd.shape[0], world, rank)
+        icp = ICP(np.float32)
+        icp.comm_init_host(comm)
+        icp.load_yaml(chain_yaml(maxit=40))
+        T = icp.compute(np.ascontiguousarray(rd[lo:hi]), ref, nrm)
+        s = icp.stats()
+        icp.close()
+        assert not comm.errors, comm.errors
+        np.savez(os.path.join(outdir, f"c3_rank{rank}.npz"), T=T.astype(np.float64), it=s.iterations, kept=s.kept)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_sharded_c3_size_vs_oracle(tmp_path, oracle):
+    """The BASELINE C3 workload (1M -> 1M float, TrimmedDist 0.85,
+    point-to-plane, Counter 40) through the host chain on two ranks of 500 K
+    reading points each: every rank's final T within 1e-5 of the
+    single-process oracle on the whole reading, the same iteration count and
+    kept pairs (the kept count is global: every rank reads the all-reduced
+    system)."""
+    from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_c3, args=(i, 2, port, str(tmp_path))) for i in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(600)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert codes == [0, 0], codes
+    r = [dict(np.load(tmp_path / f"c3_rank{i}.npz")) for i in range(2)]
+    np.testing.assert_array_equal(r[0]["T"], r[1]["T"])
+    ref, nrm = reference_cloud(1_000_000, np.float32)
+    rd = reading_cloud(1_000_000, np.float32)
+    cfg = oracle.make_cfg(counter_max=40, threads=8)
+    rc, To, so, _ = oracle.icp(cfg, rd, ref, normals=nrm)
+    assert rc == 0
+    assert np.linalg.norm(r[0]["T"] - To) <= TOL["float32"]
+    assert int(r[0]["it"]) == 40
+    assert int(r[0]["kept"]) == 850001
