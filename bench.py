@@ -389,6 +389,14 @@ def main():
     barrier()
     elapsed = max_over_ranks(t1 - t0)
     st = icp.stats()
+    # per-iteration evidence of the timed iterations (pmx_loop_diag): the grid
+    # level each match ran on, the quantile window verdict, the pairs
+    # evaluated and the full searches (the rest certified by temporal reuse)
+    dg = icp.loop_diag(0, args.warmup + args.steps)[args.warmup:]
+    diag = {"levels": [int(x) for x in dg[:, 0]], "window": [int(x) for x in dg[:, 1]],
+            "pairs_evaluated": [int(x) for x in dg[:, 2]], "full_searches": [int(x) for x in dg[:, 3]],
+            "note": "timed iterations only: grid level index of each match (0 = the finest; DESIGN.md §3), "
+                    "window 1 = quantile resolved in the match's key window, 0 = radix passes, -1 = no window"}
     # collectives and host synchronisations of the timed iterations (sharded
     # runs: stall-and-replay)
     comm = ({k: v - cs0[k] for k, v in icp.comm_stats().items()} if dist else None)
@@ -410,15 +418,18 @@ def main():
     # algorithmic bytes of one match launch: the reading shard (4 T per point),
     # the reference (4 T per point) and the k (dist, id) outputs per query
     alg_bytes = N * 4 * esz + M * 4 * esz + N * knn * (esz + 4)
+    alg_bytes_survey = alg_bytes  # N*16 + M*16 + N*k*8 (fp32; doubled for fp64 but the ids)
     # pair evaluations per match launch: N*M for brute force, the measured
     # PointCountTouched per iteration for the grid search
-    pairs_eval = N * M if args.matcher == "brute" else st.point_count_touched / max(st.iterations, 1)
+    # (the timed iterations' own pairs, from the per-iteration record)
+    pairs_eval = N * M if args.matcher == "brute" else float(dg[:, 2].mean())
     flops = 8.0 * pairs_eval  # 3 sub + 3 mul + 2 add per pair
     if args.matcher == "grid":
         # the grid adds the order / id / cell-range traffic: ids (4 B) of every
         # reference point and the visit order (4 B) of every query
         alg_bytes += N * 4 + M * 4
-    achieved_gbs = alg_bytes / avg_match_s / 1e9
+    achieved_gbs = alg_bytes_survey / avg_match_s / 1e9
+    achieved_grid_gbs = alg_bytes / avg_match_s / 1e9
     # HBM traffic of the match kernel from the committed PMC passes of this
     # exact command (tools/pmc_phases.py: FETCH_SIZE x2 (gfx950 correction) +
     # WRITE_SIZE per launch, averaged over the launches of the timed steps);
@@ -468,9 +479,12 @@ def main():
         "icp_iterations_per_s": args.steps / elapsed,
         "comm_timed": comm,
         "kept_pairs_last_iter": st.kept,
+        "timed_iterations": diag,
         "whole_icp": whole,
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "achieved_with_grid_bytes": achieved_grid_gbs, "frac_with_grid_bytes": achieved_grid_gbs / HBM_PEAK_GBS,
+                     "grid_bytes_per_launch": alg_bytes,
                      "traffic_unit": "bytes per launch past L2 (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,
                      "kernel": "match (k-NN + fused transform)", "avg_launch_ms": avg_match_s * 1e3,
@@ -478,7 +492,10 @@ def main():
                                   f"untimed, then {args.steps} iterations with HIP events on the context stream around "
                                   f"each match: grid_lane_kernel; "
                                   f"tools/pmc_phases.py 'roofline' phase = the same launches in the rocprof trace)"),
-                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "algorithmic_bytes_per_launch": alg_bytes_survey,
+                     "algorithmic_bytes_rule": "SURVEY.md §8(d): N*4T + M*4T + N*k*(T + 4 id) per launch; "
+                                               "grid_bytes_per_launch adds the grid's order (4 B / query) and "
+                                               "id (4 B / reference point) arrays",
                      "note": "steady-state launches certify most k-lists from the previous iteration (exact temporal "
                              "reuse, DESIGN.md §5); the ~70 MB C3 working set fits the 256 MB Infinity Cache, so "
                              "PMC FETCH_SIZE counts L2-miss bytes (MALL hits included) and 8 TB/s HBM is not the "

@@ -305,6 +305,14 @@ int pmx_loop_trace(pmx_ctx* ctx, int first, int count, void* out);
  * that ran the radix passes instead.  Both results are exact; counts
  * accumulate over the loops of this context since the last pmx_loop_begin. */
 int pmx_loop_select_stats(pmx_ctx* ctx, uint64_t* window_hits, uint64_t* window_misses);
+/* Per-iteration diagnostics of the device loop (no reference counterpart):
+ * for iterations [first, first + count) of the current loop (at most the
+ * last 1024), 4 int64 each: the grid level the match ran on, the quantile
+ * window verdict (1 resolved in the window, 0 radix passes, -1 no window),
+ * the pairs the match evaluated (MatchersImpl.cpp:98's visit count) and the
+ * queries that needed a full search (the rest were certified by temporal
+ * reuse).  Synchronises the context stream. */
+int pmx_loop_diag(pmx_ctx* ctx, int first, int count, int64_t* out);
 
 /* ------------------------------------------------------ data filters --- */
 /* SurfaceNormalDataPointsFilter::inPlaceFilter

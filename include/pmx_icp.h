@@ -109,6 +109,10 @@ int pmx_icp_timing_read(pmx_icp* icp, double* match_ms, int64_t* match_launches)
  * was resolved inside the match's key window, and iterations that ran the
  * radix passes.  Diagnostics only (no reference counterpart). */
 int pmx_icp_select_stats(pmx_icp* icp, uint64_t* window_hits, uint64_t* window_misses);
+/* per-iteration diagnostics of the device loop since the last prepare
+ * (pmx_loop_diag): 4 int64 per iteration for iterations [first, first +
+ * count).  Diagnostics only (no reference counterpart). */
+int pmx_icp_loop_diag(pmx_icp* icp, int first, int count, int64_t* out);
 /* multi-rank: the context's collectives and loop synchronisations since
  * creation (pmx_comm_stats, pmx_comm_loop_stats).  Diagnostics only. */
 int pmx_icp_comm_stats(pmx_icp* icp, uint64_t* allreduces, uint64_t* allgathers, uint64_t* verdict_syncs,

@@ -155,7 +155,7 @@ EXPORTS = [
     "pmx_robust_scale", "pmx_set_reading_radii",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights", "pmx_vartrim_partial_sums",
     "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
-    "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_surface_normals",
+    "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_loop_diag", "pmx_surface_normals",
     "pmx_sampling_surface_normals", "pmx_voxel_grid",
 ]
 
@@ -207,6 +207,7 @@ def lib():
         l.pmx_loop_run.argtypes = [C.c_void_p, C.c_int, C.POINTER(LoopStatus)]
         l.pmx_loop_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         l.pmx_loop_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        l.pmx_loop_diag.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         l.pmx_surface_normals.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_double,
                                           C.c_uint] + [C.c_void_p] * 6 + [C.POINTER(C.c_int64)]
         l.pmx_voxel_grid.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_int,
@@ -555,6 +556,13 @@ class Context:
         h, m = C.c_uint64(), C.c_uint64()
         self._chk(self._l.pmx_loop_select_stats(self.h, C.byref(h), C.byref(m)))
         return h.value, m.value
+
+    def loop_diag(self, first, count):
+        """Per-iteration diagnostics of the current loop (pmx_loop_diag): int64
+        rows (grid level, window verdict 1/0/-1, pairs evaluated, full searches)."""
+        out = np.zeros((count, 4), np.int64)
+        self._chk(self._l.pmx_loop_diag(self.h, int(first), int(count), _ptr(out)))
+        return out
 
     def loop_T(self, st):
         r = self.rows

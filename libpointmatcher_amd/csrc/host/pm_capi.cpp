@@ -406,6 +406,15 @@ int pmx_icp_select_stats(pmx_icp* icp, uint64_t* hits, uint64_t* misses) {
     });
 }
 
+int pmx_icp_loop_diag(pmx_icp* icp, int first, int count, int64_t* out) {
+    if (!icp || (!out && count > 0)) return PMX_ICP_INVALID_PARAMETER;
+    return guarded(icp, [&] {
+        Device& dev = icp->dtype == 1 ? icp->d->dev : icp->f->dev;
+        dev.ensure();
+        dev.check(pmx_loop_diag(dev.ctx, first, count, out));
+    });
+}
+
 int pmx_icp_comm_stats(pmx_icp* icp, uint64_t* allreduces, uint64_t* allgathers, uint64_t* verdict_syncs,
                        uint64_t* async_iterations, uint64_t* stalls) {
     if (!icp || !allreduces || !allgathers || !verdict_syncs || !async_iterations || !stalls)

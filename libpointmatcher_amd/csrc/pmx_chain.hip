@@ -89,7 +89,9 @@ int upload_raw(pmx_ctx* c, const void* src, size_t bytes) {
 template <typename T>
 int build_grid(pmx_ctx* c, int64_t M) {
     const P4<T>* pts = (const P4<T>*)c->d_ref;
-    const P4<T>* nrm = (const P4<T>*)c->d_nrm;
+    // (d_nrm is kept across references: a reference without normals must not
+    // gather the previous reference's, which may also be shorter than M)
+    const P4<T>* nrm = c->has_normals ? (const P4<T>*)c->d_nrm : nullptr;
     // bounding box of the finite points (inf / NaN points can never be a neighbour)
     double* sb = nullptr;  // bbox partials, then 8 doubles of result
     size_t sbc = 0;
@@ -115,7 +117,9 @@ int build_grid(pmx_ctx* c, int64_t M) {
     // distinct occupied cells at two trial sizes (device bitmaps; one host sync)
     auto occupied = [&](double ha, double hb, int64_t& oa, int64_t& ob) -> int {
         const SetupShape sa = grid_shape(lo, ext, ha), sb = grid_shape(lo, ext, hb);
-        // (the count, then the per-slice bitmaps: pmx_setup.hip; cells <= 129^3 at these sizes)
+        // (the count, then the per-slice bitmaps: pmx_setup.hip)
+        if (sa.cells > kOccMaxCells || sb.cells > kOccMaxCells)
+            return fail(c, PMX_E_BAD_PARAM, "grid sizing: trial grid beyond 129^3 cells");
         const size_t ba = (occupancy_bytes(sa.cells) + 255) & ~(size_t)255;
         int r = ensure(c, &c->d_occ, &c->occ_bytes, ba + occupancy_bytes(sb.cells));
         if (r) return r;
@@ -189,6 +193,11 @@ int build_grid(pmx_ctx* c, int64_t M) {
             for (auto& K : keep) K.release();
             return r;
         };
+        if (!nrm && L.gpn) {  // (no normals: no interleaved records, so nothing stale can be gathered)
+            (void)hipFree(L.gpn);
+            L.gpn = nullptr;
+            L.cap_gpn = 0;
+        }
         if (!room(&L.gpts, &L.cap_pts, sizeof(P4<T>) * np) || !room((void**)&L.gidx, &L.cap_idx, sizeof(int32_t) * np) ||
             !room((void**)&L.gstart, &L.cap_start, sizeof(uint32_t) * (size_t)(s.cells + 1)) ||
             (nrm && !room(&L.gpn, &L.cap_gpn, 2 * sizeof(P4<T>) * np)))
@@ -509,6 +518,10 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         SpecSel* spec = c->spec_now();
         c->spec_exchanged = false;
         // (this rank's segment is its block of the gathered array: an in-place all-gather)
+        // (d_specx is allocated by a loop_begin on a sharded context: a window
+        // switched on before the context became sharded has none)
+        if (spec && sharded(c) && !c->d_specx)
+            HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * c->nranks));
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx + (size_t)kSpecXStride * c->rank : nullptr;
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,

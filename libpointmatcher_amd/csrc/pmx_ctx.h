@@ -236,6 +236,7 @@ struct pmx_ctx {
     void* d_loop = nullptr;       // LoopState<T>
     void* d_loop_T0 = nullptr;    // initial T_iter (upload)
     void* d_trace = nullptr;      // T_iter per iteration (keep_trace)
+    long long* d_diag = nullptr;  // per-iteration diagnostics ring (kDiagCap x kDiagWords, pmx_loop_diag)
     int64_t trace_cap = 0;        // iterations
     bool loop_on = false;         // enqueueing loop iterations
     // quantile window fused into the grid match (pmx_spec.h): device loop,

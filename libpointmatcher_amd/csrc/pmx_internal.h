@@ -244,6 +244,9 @@ size_t bbox_scratch_bytes();
 template <typename T>
 void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, void* scratch, hipStream_t st);
 size_t occupancy_bytes(int64_t cells);  // the scratch of launch_occupancy (count first)
+// the largest trial grid launch_occupancy takes: build_grid's trial sizes are
+// maxe/64 and maxe/128, i.e. at most 129 cells per axis
+constexpr int64_t kOccMaxCells = (int64_t)129 * 129 * 129;
 template <typename T>
 int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const SetupShape& s, int64_t valid,
                        const SetupScratch& sc, P4<T>* gp, P4<T>* gpn, int32_t* gi, uint32_t* gstart, hipStream_t st);

@@ -9,6 +9,12 @@ namespace pmx {
 constexpr int kLoopHist = 64;      // Differential checker history ring (smoothLength < 64)
 constexpr int kMaxCheckers = 8;
 constexpr int kMaxLevels = 8;
+// per-iteration diagnostics (pmx_loop_diag): a ring of kDiagCap records of
+// kDiagWords 64-bit words, written by the step kernel at iteration % kDiagCap:
+// [grid level of the match, quantile window (1 hit, 0 radix passes, -1 no
+// window), pairs evaluated, full searches]
+constexpr int kDiagCap = 1024;
+constexpr int kDiagWords = 4;
 
 enum CheckKind { kCheckCounter = 0, kCheckDifferential = 1, kCheckBound = 2 };
 // why the loop stopped
@@ -70,6 +76,6 @@ void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
-                      hipStream_t s);
+                      const int* spec_hit, long long* diag, hipStream_t s);
 
 }  // namespace pmx

@@ -34,12 +34,21 @@ template <typename T, int ROWS, int MIN>
 __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S,
                                  const double* __restrict__ res, const int* __restrict__ iter_err,
                                  const unsigned long long* __restrict__ visited, const T* __restrict__ means,
-                                 LoopCfg cfg, T* __restrict__ trace) {
+                                 LoopCfg cfg, T* __restrict__ trace, const int* __restrict__ spec_hit,
+                                 long long* __restrict__ diag) {
     if (ctl->done) return;  // (uniform)
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     // (every global read of the step first, together: each is a memory round trip)
     const int e = *iter_err;
     const unsigned long long vis0 = visited[0], vis1 = visited[1];
+    const int hit = spec_hit ? *spec_hit : -1;
+    if (diag) {
+        long long* r = diag + (size_t)(S->iter % kDiagCap) * kDiagWords;
+        r[0] = ctl->level;
+        r[1] = hit;
+        r[2] = (long long)vis0;
+        r[3] = (long long)vis1;
+    }
     step_body<T, ROWS, MIN>(ctl, S, res, e, vis0, vis1, means, cfg, trace);
 }
 
@@ -89,10 +98,10 @@ void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,
-                      hipStream_t s) {
+                      const int* spec_hit, long long* diag, hipStream_t s) {
 #define PMX_STEP(R, M)                                                                                            \
     hipLaunchKernelGGL((loop_step_kernel<T, R, M>), dim3(1), dim3(64), 0, s, ctl, S, res, iter_err, visited, means, \
-                       cfg, trace)
+                       cfg, trace, spec_hit, diag)
     if (cfg.rows == 4) {
         if (cfg.minimizer == 0)
             PMX_STEP(4, 0);
@@ -111,9 +120,11 @@ template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg
 template void launch_loop_init<double>(LoopCtl*, LoopState<double>*, const LoopCfg&, const double*, int, int,
                                        const double*, hipStream_t);
 template void launch_loop_step<float>(LoopCtl*, LoopState<float>*, const double*, const int*,
-                                      const unsigned long long*, const float*, const LoopCfg&, float*, hipStream_t);
+                                      const unsigned long long*, const float*, const LoopCfg&, float*, const int*,
+                                      long long*, hipStream_t);
 template void launch_loop_step<double>(LoopCtl*, LoopState<double>*, const double*, const int*,
-                                       const unsigned long long*, const double*, const LoopCfg&, double*, hipStream_t);
+                                       const unsigned long long*, const double*, const LoopCfg&, double*,
+                                       const int*, long long*, hipStream_t);
 
 
 // Load this translation unit's code object now (pmx_ctx_create): HIP loads a

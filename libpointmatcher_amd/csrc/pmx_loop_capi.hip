@@ -95,6 +95,10 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     (void)cap;  // (LoopState lives in the status block)
     cap = 0;
     if (!c->d_loop_T0 && (rc = ensure(c, &c->d_loop_T0, &cap, 16 * sizeof(double)))) return rc;
+    if (!c->d_diag) {
+        HIPCHK(c, hipMalloc((void**)&c->d_diag, sizeof(long long) * kDiagCap * kDiagWords));
+        HIPCHK(c, hipMemsetAsync(c->d_diag, 0, sizeof(long long) * kDiagCap * kDiagWords, c->stream));
+    }
     // pinned: two status-block slots (the batches in flight), then the
     // staging of this call's uploads (T0, the window reset): the uploads are
     // asynchronous, so the caller's T0 may go away and no host sync is needed
@@ -226,7 +230,8 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     }
     if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c))) return rc;
     launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
-                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr, c->stream);
+                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr,
+                        c->spec_on && c->d_spec ? &c->d_spec->hit : nullptr, c->d_diag, c->stream);
     HIPCHK(c, hipGetLastError());
     c->shard_replay = false;
     return PMX_OK;
@@ -438,6 +443,22 @@ int pmx_loop_run(pmx_ctx* c, int n, pmx_loop_status* st) {
 int pmx_loop_trace(pmx_ctx* c, int first, int count, void* out) {
     if (!c || (!out && count > 0)) return fail(c, PMX_E_BAD_PARAM, "null argument");
     return DISPATCH(c, loop_trace_impl<float>(c, first, count, out), loop_trace_impl<double>(c, first, count, out));
+}
+
+int pmx_loop_diag(pmx_ctx* c, int first, int count, int64_t* out) {
+    if (!c || (!out && count > 0)) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    if (!c->loop_begun || !c->d_diag) return fail(c, PMX_E_STATE, "no device loop");
+    if (first < 0 || count < 0 || first + count > c->loop_iters || count > kDiagCap ||
+        (int64_t)c->loop_iters - first > kDiagCap)
+        return fail(c, PMX_E_BAD_PARAM, "diagnostics range beyond the completed iterations or the ring");
+    (void)hipSetDevice(c->device);
+    std::vector<long long> ring((size_t)kDiagCap * kDiagWords);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(ring.data(), c->d_diag, sizeof(long long) * ring.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < count; ++i)
+        for (int w = 0; w < kDiagWords; ++w)
+            out[(size_t)i * kDiagWords + w] = (int64_t)ring[(size_t)((first + i) % kDiagCap) * kDiagWords + w];
+    return PMX_OK;
 }
 
 int pmx_loop_select_stats(pmx_ctx* c, uint64_t* window_hits, uint64_t* window_misses) {

@@ -193,6 +193,10 @@ __device__ __forceinline__ int64_t dcell_of(const SetupShape& s, double x, doubl
 // returned bits counted, at 1M points.)
 constexpr int kOccWords = 32768;  // 128 KB of LDS
 constexpr int kOccSlices = 32;
+// gfx950 gives a workgroup up to 160 KB of LDS; the bitmap must fit it (a
+// 64 KB-LDS target would need kOccWords <= 16384)
+static_assert(kOccWords * sizeof(uint32_t) <= 160 * 1024, "occupancy bitmap exceeds the gfx950 LDS budget");
+
 size_t occupancy_bytes(int64_t cells) { return 256 + sizeof(uint32_t) * (size_t)kOccSlices * (size_t)((cells + 31) / 32); }
 
 template <typename T>
@@ -242,6 +246,8 @@ __global__ __launch_bounds__(256) void occupancy_count_kernel(const uint32_t* __
 // caller) in its first 8 bytes
 template <typename T>
 void launch_occupancy(const P4<T>* p, int64_t n, const SetupShape& s, void* scratch, hipStream_t st) {
+    // (the caller sized `scratch` with occupancy_bytes(s.cells) and checked
+    // s.cells <= kOccMaxCells)
     const int64_t words = (s.cells + 31) / 32;
     unsigned long long* count = (unsigned long long*)scratch;
     uint32_t* slices = (uint32_t*)((char*)scratch + 256);

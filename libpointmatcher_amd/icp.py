@@ -89,6 +89,7 @@ def lib():
         l.pmx_icp_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         l.pmx_icp_select_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         l.pmx_icp_comm_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 5
+        l.pmx_icp_loop_diag.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
         l.pmx_icp_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.POINTER(C.c_int)]
         l.pmx_icp_clear_map.argtypes = [C.c_void_p]
         l.pmx_icp_has_map.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
@@ -268,6 +269,14 @@ class ICP:
         h, m = C.c_uint64(), C.c_uint64()
         self._chk(self._l.pmx_icp_select_stats(self.h, C.byref(h), C.byref(m)))
         return h.value, m.value
+
+    def loop_diag(self, first, count):
+        """Per-iteration diagnostics of the device loop since the last prepare
+        (pmx_icp_loop_diag): int64 rows [grid level, window verdict (1 hit, 0
+        radix passes, -1 no window), pairs evaluated, full searches]."""
+        out = np.zeros((count, 4), np.int64)
+        self._chk(self._l.pmx_icp_loop_diag(self.h, int(first), int(count), out.ctypes.data_as(C.c_void_p)))
+        return out
 
     def comm_stats(self):
         """Multi-rank diagnostics since creation: {allreduces, allgathers, verdict_syncs,
