@@ -418,6 +418,13 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
 }
 
 // ------------------------------------------------------------------- match --
+// reuse candidates per query for a k-NN match (K > k: the certificate
+// re-ranks the K nearest of the last full search; K = k: the k-list itself)
+int reuse_k(const pmx_ctx* c, int knn) {
+    const int K = c->reuse_cand_req;
+    return K > knn && K < 16 && knn <= kLaneMaxK ? K : knn;
+}
+
 template <typename T>
 int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
     if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
@@ -507,11 +514,19 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // temporal reuse: the output buffers hold this reading's previous
         // match (same k, same level) with its safe radii
         GridReuse<T> ru;
-        const bool no_prev = !(c->safe_valid && c->have_match && c->ids_grid && c->knn == knn);
+        const int K = reuse_k(c, knn);
+        const bool cand_ok = K == knn || c->cand_K == K;  // (the candidates of the last match are K wide)
+        const bool no_prev = !(c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && cand_ok);
         if (c->reuse_on && c->grid_mode >= 1 && knn <= kLaneMaxK) {  // (the wide search keeps no safe radii)
-            ru.mode = c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && c->ids_level == c->level ? 2 : 1;
+            ru.mode = !no_prev && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
             for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
+            if (K > knn) {
+                int rc = ensure(c, (void**)&c->d_cand, &c->cand_bytes, sizeof(int32_t) * (size_t)K * std::max<int64_t>(c->N, 1));
+                if (rc) return rc;
+                ru.K = K;
+                ru.cand = c->d_cand;
+            }
         }
         // several ranks: the counter sum packs this rank's window segment,
         // the segments are all-gathered and every rank picks from the union
@@ -541,6 +556,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             c->spec_exchanged = true;
         }
         c->safe_valid = ru.mode != 0;
+        c->cand_K = ru.mode != 0 && ru.cand ? ru.K : 0;
         c->visited_host = 0;
         c->ids_grid = true;
         c->ids_level = c->level;
@@ -654,7 +670,7 @@ void choose_level(pmx_ctx* c, uint64_t visited, uint64_t full) {
     double q = (double)c->N, v = (double)visited;
     if (c->safe_valid) {
         if ((double)full * 16.0 < q) return;
-        v -= (double)c->knn * (q - (double)full);
+        v -= (double)reuse_k(c, c->knn) * (q - (double)full);
         q = (double)full;
     }
     const double cells = v / (q * c->lv(l).ppc);

@@ -109,6 +109,14 @@ struct pmx_ctx {
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
     void* d_safe = nullptr;       // T[N]: safe radius per query
     int64_t safe_cap = 0;
+    // reuse candidates: each full search keeps its K nearest (K > k) and the
+    // certificate re-ranks them (pmx_grid.hip).  reuse_cand_req: requested K
+    // (0: off = the k-list itself; PMX_REUSE_CAND), cand_K: the K the
+    // buffers hold (0: none valid)
+    int reuse_cand_req = 0;
+    int cand_K = 0;
+    int32_t* d_cand = nullptr;    // int32[N * cand_K]
+    size_t cand_bytes = 0;
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }
     std::vector<int32_t> slot_query;  // host copy of d_order (host mirrors only; filled on demand)
@@ -331,6 +339,7 @@ void setup_release(pmx_ctx* c);
 int upload_raw(pmx_ctx* c, const void* src, size_t bytes);
 int host_order(pmx_ctx* c);
 int select_reset(pmx_ctx* c);
+int reuse_k(const pmx_ctx* c, int knn);  // reuse candidates of a k-NN match (pmx_chain.hip)
 double host_limit(const pmx_ctx* c);
 void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double rm, double rp, double sw,
                 double limit);

@@ -192,6 +192,8 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
                                               const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy,
                                               T qz, const double q[3], const int c[3], T maxR2, int k, T (&kd)[KT],
                                               int32_t (&ki)[KT], uint32_t& visits, double& lb_exit) {
+    // (k: the rank the exit certifies — the query's k, or the candidate
+    // count K of the temporal reuse, below)
     int b0[3], b1[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -262,11 +264,15 @@ __device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, co
 // initialised.  Certified on the k-th entry of the list (entries past k, when
 // KT > k, are the next-nearest points visited).  lb_exit: the distance from
 // the query to the unvisited region at exit (1e300: the whole grid).
+// kp: the list entry (1-based) cells are pruned against — the one the safe
+// radius of the temporal reuse takes as a bound on every point not kept
+// (k + 1, or K + 1 with K reuse candidates); 0: k + 1 when the list has room.
 template <typename T, int KT>
 __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                             const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy, T qz,
                             const double q[3], const int c[3], T maxR2, int k, T (&kd)[KT], int32_t (&ki)[KT],
-                            uint32_t& visits, double& lb_exit) {
+                            uint32_t& visits, double& lb_exit, int kp = 0) {
+    if (kp <= 0) kp = k < KT ? k + 1 : k;
     const double margin = 1.0 - 1e-5;
     lb_exit = 1e300;
     {
@@ -336,7 +342,7 @@ __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, cons
                 // point closer than it may be skipped)
                 T dkT;
                 int32_t ikT;
-                kth(kd, ki, k < KT ? k + 1 : k, dkT, ikT);
+                kth(kd, ki, kp, dkT, ikT);
                 const double lim = ikT == kNoPos ? 1e300 : (double)dkT / margin;
                 const double gz = axis_gap(G, 2, z, q[2]), gz2 = gz * gz;
                 if (gz2 > lim) continue;
@@ -414,8 +420,8 @@ __device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&k
                 d = (T)__builtin_huge_val();
                 id = -1;
             }
-            out_d[j * k + s] = d;
-            out_i[j * k + s] = id;
+            st_out(&out_d[j * k + s], d);
+            st_out(&out_i[j * k + s], id);
             if (sa.on) spec_acc<T>(sa, d);
         }
     }
@@ -546,7 +552,8 @@ size_t grid_counter_bytes() { return sizeof(unsigned long long) * 4 * kVSlots * 
 constexpr double kReuseMargin = 1e-5;
 
 // safe radius of a full search: the unvisited region and the (k+1)-th
-// visited point (list entry k, when KT > k) bound every non-neighbour
+// visited point (list entry k, when KT > k) bound every non-neighbour (with
+// K reuse candidates, k = K: every point outside the candidate list)
 template <typename T, int KT>
 __device__ __forceinline__ T safe_radius(const T (&kd)[KT], const int32_t (&ki)[KT], int k, double lb_exit) {
     double r = lb_exit;
@@ -579,7 +586,12 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
                                            const uint32_t* __restrict__ start, const GridGeom& G,
                                            const P4<T>* __restrict__ rd, int64_t j, const Mat4<T>& Tm, int k,
                                            T maxR2, int oct, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                           T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa) {
+                                           T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa,
+                                           int K = 0, int32_t* __restrict__ cand = nullptr) {
+    // K > k (reuse candidates, cand != null): the search certifies the K
+    // nearest, its list keeps the (K+1)-th, and the K nearest are stored as
+    // the next match's candidates
+    const int ks = cand ? K : k;
     T qx, qy, qz;
     gxform(Tm, gld(rd, j), qx, qy, qz);
     T kd[KT];
@@ -596,20 +608,26 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
     double lb_exit = -1.0;
     if (!qnan) {
         bool done = false;
-        if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit);
+        if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, ks, kd, ki, visits, lb_exit);
         if (!done) {
 #pragma unroll
             for (int s = 0; s < KT; ++s) {  // (a k-list must not see the octant's points twice)
                 kd[s] = (T)__builtin_huge_val();
                 ki[s] = kNoPos;
             }
-            lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit);
+            lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, ks, kd, ki, visits, lb_exit,
+                               ks < KT ? ks + 1 : ks);
         }
     }
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
+    if (cand) {
+#pragma unroll
+        for (int s = 0; s < KT; ++s)
+            if (s < K) st_out(&cand[j * K + s], ki[s] == kNoPos ? (int32_t)-1 : ki[s]);
+    }
     // (a certified octant block bounds the rest by its interior faces, as a
     // shell walk's exit does)
-    if (safe) safe[j] = safe_radius<T, KT>(kd, ki, k, lb_exit);
+    if (safe) st_out(&safe[j], safe_radius<T, KT>(kd, ki, ks, lb_exit));
 }
 
 // the certificate for query j; true when the k-list was rewritten from the
@@ -690,7 +708,8 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                                                         int reuse, T* __restrict__ safe, Mat4<T> Tprev,
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
-                                                        SpecSel* __restrict__ spec, const T* __restrict__ radii) {
+                                                        SpecSel* __restrict__ spec, const T* __restrict__ radii,
+                                                        int K, int32_t* __restrict__ cand) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -705,7 +724,15 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             for (int i = 0; i < 16; ++i) Tprev.m[i] = (T)ctl->Tprev[i];
         }
     }
-    if (!reuse) safe = nullptr;
+    if (!reuse) {
+        safe = nullptr;
+        cand = nullptr;
+    }
+    // reuse candidates (K > k, cand != null): the certificate keeps the K
+    // nearest of the last full search and re-ranks them at the new position
+    // (see the temporal reuse notes above)
+    const bool cm = cand != nullptr;
+    const int nc = cm ? K : k;
     uint32_t visits = 0;
     // quantile window (pmx_spec.h): every written distance is classified
     SpecAcc<T> sa;
@@ -723,6 +750,9 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         // stages so that each stage's loads are in flight together.  A list
         // kept for reuse holds k <= KT - 1 entries (room for the (k+1)-th:
         // the safe radius); KT = 16 keeps no room and never certifies.
+        // With K candidates (cm) the k-th distance is re-ranked at the new
+        // position: a = that distance, exact; without, a is bounded from the
+        // previous k-th distance (no gather for a query that cannot pass).
         constexpr int KR = KT > 1 ? KT - 1 : 1;
         P4<T> p[Q];
         T rs[Q], dkp[Q];
@@ -732,9 +762,9 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             const int64_t j = missed[q] ? base + q * 256 + threadIdx.x : base;  // (base < N: an in-range slot)
             p[q] = gld(rd, j);
             rs[q] = safe[j];
-            dkp[q] = out_d[j * k + k - 1];
+            dkp[q] = cm ? (T)0 : out_d[j * k + k - 1];
 #pragma unroll
-            for (int s = 0; s < KR; ++s) id[q][s] = s < k ? out_i[j * k + s] : 0;
+            for (int s = 0; s < KR; ++s) id[q][s] = s < nc ? (cm ? cand[j * K + s] : out_i[j * k + s]) : 0;
         }
         bool ok[Q];
         double bq[Q];
@@ -742,7 +772,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             gxform(Tm, p[q], qx[q], qy[q], qz[q]);
-            bool o = missed[q] && k <= KR && rs[q] > (T)0 && dkp[q] < (T)__builtin_huge_val();
+            bool o = missed[q] && nc <= KR && rs[q] > (T)0 && dkp[q] < (T)__builtin_huge_val();
 #pragma unroll
             for (int s = 0; s < KR; ++s) o = o && id[q][s] >= 0;
             T ox, oy, oz;
@@ -752,17 +782,17 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             const double delta = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + kReuseMargin);
             const double av = sqrt((double)dkp[q]) * (1.0 + kReuseMargin) + delta;
             bq[q] = (double)rs[q] * (1.0 - kReuseMargin) - delta;
-            ok[q] = o && av < bq[q];
+            ok[q] = o && (cm ? bq[q] > 0.0 : av < bq[q]);
         }
         P4<T> r[Q][KR];
 #pragma unroll
         for (int q = 0; q < Q; ++q)
 #pragma unroll
-            for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < k ? (uint32_t)id[q][s] : 0u);
+            for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < nc ? (uint32_t)id[q][s] : 0u);
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if (!ok[q]) continue;
-            // the same k points: new distances, sorted as a full search sorts them
+            // the same points: new distances, sorted as a full search sorts them
             const int64_t j = base + q * 256 + threadIdx.x;
             T kd[KT];
             int32_t ki[KT];
@@ -773,10 +803,18 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             }
 #pragma unroll
             for (int s = 0; s < KR; ++s)
-                if (s < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx[q], qy[q], qz[q], r[q][s]), id[q][s]);
-            visits += (uint32_t)k;
+                if (s < nc) ginsert<T, KT>(gidx, kd, ki, gsqd(qx[q], qy[q], qz[q], r[q][s]), id[q][s]);
+            visits += (uint32_t)nc;
+            if (cm) {
+                // every point outside the candidates is beyond bq; the k-th
+                // candidate, re-ranked, must be nearer than that
+                T dk;
+                int32_t ik;
+                kth(kd, ki, k, dk, ik);
+                if (!(sqrt((double)dk) * (1.0 + kReuseMargin) < bq[q])) continue;  // (a full search below)
+            }
             write_out<T, KT>(j, k, qr2(radii, j, maxR2), kd, ki, out_d, out_i, sa);
-            safe[j] = (T)(bq[q] * (1.0 - 1e-6));
+            st_out(&safe[j], (T)(bq[q] * (1.0 - 1e-6)));
             missed[q] = false;
         }
     }
@@ -804,7 +842,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
     for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
         const int64_t j2 = base + miss[t];
         full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
-                          sa);
+                          sa, K, cand);
         if (Q == 1) break;
     }
     add_visits(visits, visited);
@@ -829,9 +867,10 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
+        const bool cm = ru.mode && ru.cand && ru.K > knn && ru.K <= KT - 1;  // (the list holds K + 1)
         hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
                            rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
-                           ctl, gd, spec, radii);
+                           ctl, gd, spec, radii, cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
@@ -866,8 +905,10 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
                      ru, ctl, gd, spec, radii, cold, s)
         // with reuse the list keeps room for the (k+1)-th point (the safe radius;
-        // the cold tile writes radius 0 and keeps k entries)
-        const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
+        // the cold tile writes radius 0 and keeps k entries); with K reuse
+        // candidates, for the (K+1)-th
+        const int kr = ru.cand && ru.K > knn ? ru.K : knn;
+        const int kl = ru.mode && mode >= 1 && kr < 16 && !cold ? kr + 1 : knn;
         if (kl == 1)
             PMX_KT(1);
         else if (kl <= 2)

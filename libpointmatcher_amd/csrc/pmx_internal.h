@@ -84,6 +84,23 @@ __device__ __forceinline__ int32_t gld(const int32_t* p, int64_t i) {
     return ((const __attribute__((address_space(1))) int32_t*)p)[i];
 }
 
+// Stores of per-query outputs the NEXT kernel reads (match distances, ids,
+// safe radii).  PMX_WT=1 (experiment): agent-scope relaxed stores, which
+// write through L2 (sc1), so the kernel ends with no dirty lines to write
+// back at the boundary (MI355X_MICROARCH.md "boundary": + B / 6 TB/s for B
+// dirty bytes).
+#ifndef PMX_WT
+#define PMX_WT 0
+#endif
+template <typename V>
+__device__ __forceinline__ void st_out(V* p, V v) {
+#if PMX_WT
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
+
 template <typename T>
 struct Mat4 {
     T m[16];  // row-major
@@ -166,6 +183,10 @@ struct GridReuse {
     int mode = 0;
     T* safe = nullptr;
     Mat4<T> Tprev{};
+    // reuse candidates (K > k): the K nearest of each query's last full
+    // search, int32[N * K] (null: the k-list itself is the candidate set)
+    int K = 0;
+    int32_t* cand = nullptr;
 };
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {

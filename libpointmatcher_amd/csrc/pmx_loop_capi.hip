@@ -86,7 +86,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     }
     d.adaptive = c->adaptive ? 1 : 0;
     d.reuse = c->reuse_on && c->grid_mode >= 1 ? 1 : 0;
-    d.knn = cfg->knn;
+    d.knn = reuse_k(c, cfg->knn);  // (pairs a certified query evaluates: its reuse candidates)
     d.n_levels = (int)c->levels.size();
     for (int l = 0; l < d.n_levels; ++l) d.level_ppc[l] = c->lv(l).ppc;
     d.n_local = c->N;
@@ -114,8 +114,11 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     std::memcpy(stage, T0, sizeof(T) * rr);
     HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, stage, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
     // the first loop match may reuse the last classic one
-    const int prev_level =
-        c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn ? c->ids_level : -1;
+    const int Kr = reuse_k(c, cfg->knn);
+    const int prev_level = c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn &&
+                                   (Kr == cfg->knn || c->cand_K == Kr)
+                               ? c->ids_level
+                               : -1;
     launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, prev_level,
                         c->Tstep, c->stream);
     // quantile window: a fresh window each loop (the first iteration runs the

@@ -422,3 +422,102 @@ def test_sharded_c3_size_vs_oracle(tmp_path, oracle):
     assert np.linalg.norm(r[0]["T"] - To) <= TOL["float32"]
     assert int(r[0]["it"]) == 40
     assert int(r[0]["kept"]) == 850001
+
+
+# ---- the BASELINE multi-GPU configurations at their own sizes, sharded ----
+# (the north_star's 8-GPU configs C4 and C5 on two ranks of one MI355X over
+# the host-staged transport; the same library path as RCCL)
+BIG_CASES = {
+    # tag: (reading N, reference M, dtype, knn, filters, minimizer, Counter max, Differential, traced)
+    "c4": (1_000_000, 1_000_000, "float32", 4, (("MaxDistOutlierFilter", {"maxDist": 0.05}),), P2PLANE, 20, DIFF,
+           False),
+    "c5": (10_000_000, 1_000_000, "float64", 1, (), P2POINT, 5, None, False),
+    "c5x40": (2_000_000, 1_000_000, "float64", 1, (), P2POINT, 40, None, True),
+}
+
+
+def _worker_big(rank, world, port, outdir, tag):
+    import torch  # noqa: F401
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from libpointmatcher_amd import _capi
+        from libpointmatcher_amd.icp import ICP
+        from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+
+        n, m, dn, knn, filters, minimizer, maxit, diff, traced = BIG_CASES[tag]
+        dtype = np.dtype(dn)
+        comm = _capi.gloo_host_comm()
+        ref, nrm = reference_cloud(m, dtype)
+        rd = reading_cloud(n, dtype)
+        lo, hi = shard_range(n, world, rank)
+        shard = np.ascontiguousarray(rd[lo:hi])
+        del rd
+        icp = ICP(dtype)
+        icp.comm_init_host(comm)
+        if traced:
+            icp.keep_trace(True)
+        icp.load_yaml(chain_yaml(knn=knn, filters=filters, minimizer=minimizer, maxit=maxit, differential=diff))
+        T = icp.compute(shard, ref, nrm if minimizer == P2PLANE else None)
+        s = icp.stats()
+        tr = np.asarray(icp.trace(), np.float64) if traced else np.zeros((0, 4, 4))
+        icp.close()
+        assert not comm.errors, comm.errors
+        np.savez(os.path.join(outdir, f"{tag}_rank{rank}.npz"), T=T.astype(np.float64), it=s.iterations, kept=s.kept,
+                 trace=tr)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("tag", ["c4", "c5", "c5x40"])
+def test_sharded_baseline_configs_vs_oracle(tmp_path, oracle, tag):
+    """BASELINE C4 (1M -> 1M float, k = 4, MaxDist 0.05, point-to-plane,
+    Counter 20 + Differential) and C5 (10M -> 1M double, empty chain,
+    point-to-point, 5 iterations; and its chain for 40 traced iterations on
+    2M -> 1M) through the host chain on two ranks, each with half of the
+    reading: every rank the same T, within 1e-5 (float) / 1e-12 (double) of
+    the single-process oracle on the whole reading (every T_iter of the
+    trace for c5x40), with equal iteration counts and kept pairs.
+    Reference: MatchersImpl.cpp:85-101, ErrorMinimizers/PointToPoint.cpp:61-101,
+    PointToPlane.cpp:171-243, ICP.cpp:317-449."""
+    from libpointmatcher_amd.synth import reading_cloud, reference_cloud
+    from test_gpu_configs import THREADS
+
+    n, m, dn, knn, filters, minimizer, maxit, diff, traced = BIG_CASES[tag]
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_big, args=(i, 2, port, str(tmp_path), tag)) for i in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(900)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert codes == [0, 0], codes
+    r = [dict(np.load(tmp_path / f"{tag}_rank{i}.npz")) for i in range(2)]
+    np.testing.assert_array_equal(r[0]["T"], r[1]["T"])
+    np.testing.assert_array_equal(r[0]["trace"], r[1]["trace"])
+    dtype = np.dtype(dn)
+    ref, nrm = reference_cloud(m, dtype)
+    rd = reading_cloud(n, dtype)
+    cfg = oracle.make_cfg(knn=knn, filters=filters, minimizer=minimizer, counter_max=maxit, differential=diff,
+                          threads=THREADS)
+    rc, To, so, to = oracle.icp(cfg, rd, ref, normals=nrm if minimizer == P2PLANE else None, trace=traced)
+    assert rc == 0
+    frob = np.linalg.norm(r[0]["T"] - To.astype(np.float64))
+    print(f"{tag} sharded x2: iterations {int(r[0]['it'])}/{so.iterations} kept {int(r[0]['kept'])}/{so.kept} "
+          f"|dT|_F = {frob:.3g}")
+    assert int(r[0]["it"]) == so.iterations
+    assert int(r[0]["kept"]) == so.kept
+    assert frob <= TOL[dn]
+    if traced:
+        assert len(r[0]["trace"]) == so.iterations == maxit
+        worst = max(np.linalg.norm(a - np.asarray(b, np.float64)) for a, b in zip(r[0]["trace"], to))
+        print(f"{tag}: worst iteration |dT|_F = {worst:.3g}")
+        assert worst <= TOL[dn]
