@@ -217,6 +217,10 @@ def main():
                     help="seconds of untimed whole ICPs before the measured regions (GPU clock ramp)")
     ap.add_argument("--dist", action="store_true",
                     help="use the torchrun/RCCL multi-rank path even at world size 1 (rehearsal on one GPU)")
+    ap.add_argument("--emulate-ranks", type=int, default=1,
+                    help="per-rank cost model on one process: run only shard 0 of the global reading split G ways "
+                         "(the work one rank of a G-GPU strong-scaling run does; with --dist its collectives are "
+                         "issued at world size 1).  A projection input, not a multi-GPU measurement")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -250,14 +254,17 @@ def main():
     reference, normals = reference_cloud(M, dtype)
     strong = args.scaling == "strong"
     N_global = N_cfg if strong else N_cfg * world
-    if dist:
+    if dist or args.emulate_ranks > 1:
         full = reading_cloud(N_global, dtype)
-        lo, hi = shard_range(N_global, world, rank)
+        G = world if world > 1 else max(1, args.emulate_ranks)
+        lo, hi = shard_range(N_global, G, rank)
         reading = np.ascontiguousarray(full[lo:hi])
         del full
     else:
         reading = reading_cloud(N_global, dtype)
     N = reading.shape[0]  # this rank's shard
+    # (the per-rank cost model counts the shard's own pairs)
+    N_work = N if (args.emulate_ranks > 1 and world == 1) else N_global
 
     search_type = 0 if args.matcher == "brute" else 1
     total_it = args.warmup + args.steps + 10
@@ -341,7 +348,7 @@ def main():
     icp.timing(False)
     whole = {"iterations": int(wst.iterations), "ms": 1e3 * whole_s,
              "ms_per_iteration": 1e3 * whole_s / max(int(wst.iterations), 1),
-             "matched_pairs_per_s": N_global * knn * int(wst.iterations) / whole_s,
+             "matched_pairs_per_s": N_work * knn * int(wst.iterations) / whole_s,
              "cold_match_ms": first_match_us[0] * 1e-3 if first_match_us else None,
              "first_matches_us": first_match_us,
              "window_hits": int(hits), "window_misses": int(misses),
@@ -412,7 +419,7 @@ def main():
     match_ms, launches = icp.timing_read()
     icp.timing(False)
 
-    pairs = N_global * knn * args.steps
+    pairs = N_work * knn * args.steps
     avg_match_s = match_ms * 1e-3 / max(launches, 1)
     esz = np.dtype(dtype).itemsize
     # algorithmic bytes of one match launch: the reading shard (4 T per point),
@@ -453,7 +460,11 @@ def main():
             metric = json.load(f)["metric"]
     except Exception:
         pass
-    if dist:
+    if args.emulate_ranks > 1 and world == 1:
+        par = (f"per-rank cost model: shard 0 of {args.emulate_ranks} of the {N_global} reading on one GPU "
+               f"({'RCCL collectives issued at world size 1' if dist else 'no communicator'}); value is this shard's "
+               f"rate, not a multi-GPU measurement")
+    elif dist:
         par = (f"reading sharded x{world} ({'strong: ' + str(N_global) + ' global' if strong else 'weak: ' + str(N_cfg) + ' per rank'}), "
                f"reference replicated; RCCL per iteration: quantile window all-gather (+ radix histogram all-reduces "
                f"on a window miss) and the normal-equation all-reduce")
@@ -519,7 +530,7 @@ def main():
                             "filters + mean + centring (host, T-sequential), Matcher::init (reference upload, grid "
                             "levels built on the device), reading upload + Morton slot order (device sort); "
                             "first_prepare_ms adds the context creation (HIP runtime, code objects)")
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and args.emulate_ranks == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or usable_cores()[0]
         # GPU side of the parity checks: whole ICPs from the initial pose
         # with the timing chain and with the parity chain (same inputs)

@@ -520,6 +520,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         if (c->reuse_on && c->grid_mode >= 1 && knn <= kLaneMaxK) {  // (the wide search keeps no safe radii)
             ru.mode = !no_prev && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
+            ru.coop_max = c->coop_max;
             for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
             if (K > knn) {
                 int rc = ensure(c, (void**)&c->d_cand, &c->cand_bytes, sizeof(int32_t) * (size_t)K * std::max<int64_t>(c->N, 1));

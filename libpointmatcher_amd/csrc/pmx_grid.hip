@@ -671,6 +671,225 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
     return true;
 }
 
+// ---------------------------------------------- wave-cooperative search --
+// One query searched by a whole wave: the rows of each cubic ring are split
+// over the lanes (one round trip for their bounds, one for their points),
+// every lane keeps a private (distance, original index) list of the points it
+// evaluated, and the wave merges the lists after each ring.  A per-lane
+// search walks the same rings as a chain of dependent row gathers (tens of
+// round trips for a query whose certificate failed); here a ring costs two.
+// Used for the few queries of a wave that miss the reuse certificate in a
+// converged match (the per-lane kernel's phase 2).  The result is the exact
+// k-list of the per-lane search: the same (distance, original index) order,
+// the same certificate on the interior faces of the visited box.
+template <typename T>
+struct CoopEnt {
+    T d;
+    int32_t g;    // original reference index (ties)
+    int32_t pos;  // grid position (the match id)
+};
+template <typename T>
+__device__ __forceinline__ bool coop_less(T da, int32_t ga, T db, int32_t gb) {
+    return da < db || (da == db && ga < gb);
+}
+template <typename T, int KT>
+__device__ __forceinline__ void coop_insert(T (&ld)[KT], int32_t (&lg)[KT], int32_t (&lp)[KT], T d, int32_t g,
+                                            int32_t pos) {
+    if (!coop_less(d, g, ld[KT - 1], lg[KT - 1])) return;
+    ld[KT - 1] = d;
+    lg[KT - 1] = g;
+    lp[KT - 1] = pos;
+#pragma unroll
+    for (int s = KT - 1; s > 0; --s) {
+        const bool sw = coop_less(ld[s], lg[s], ld[s - 1], lg[s - 1]);
+        const T td = sw ? ld[s - 1] : ld[s];
+        const int32_t tg = sw ? lg[s - 1] : lg[s], tp = sw ? lp[s - 1] : lp[s];
+        ld[s - 1] = sw ? ld[s] : ld[s - 1];
+        lg[s - 1] = sw ? lg[s] : lg[s - 1];
+        lp[s - 1] = sw ? lp[s] : lp[s - 1];
+        ld[s] = td;
+        lg[s] = tg;
+        lp[s] = tp;
+    }
+}
+__device__ __forceinline__ float shfl_x(float v, int m) { return __shfl_xor(v, m); }
+__device__ __forceinline__ double shfl_x(double v, int m) { return __shfl_xor(v, m); }
+
+// Merge the wave's private lists into the KT smallest (uniform in kd / kg /
+// kp); afterwards lane 0 holds the merged list and every other lane an empty
+// one (no point is counted twice by a later merge).
+template <typename T, int KT>
+__device__ __forceinline__ void coop_merge(T (&ld)[KT], int32_t (&lg)[KT], int32_t (&lp)[KT], T (&kd)[KT],
+                                           int32_t (&kg)[KT], int32_t (&kp)[KT]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+        T md = ld[0];
+        int32_t mg = lg[0], mp = lp[0];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const T od = shfl_x(md, off);
+            const int32_t og = __shfl_xor(mg, off), op = __shfl_xor(mp, off);
+            if (coop_less(od, og, md, mg)) {
+                md = od;
+                mg = og;
+                mp = op;
+            }
+        }
+        kd[s] = md;
+        kg[s] = mg;
+        kp[s] = mp;
+        // the owner pops its head (an empty head, +inf / kNoPos, pops nothing real)
+        if (ld[0] == md && lg[0] == mg && mp != kNoPos) {
+#pragma unroll
+            for (int u = 0; u < KT - 1; ++u) {
+                ld[u] = ld[u + 1];
+                lg[u] = lg[u + 1];
+                lp[u] = lp[u + 1];
+            }
+            ld[KT - 1] = (T)__builtin_huge_val();
+            lg[KT - 1] = kNoPos;
+            lp[KT - 1] = kNoPos;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+        ld[s] = lane == 0 ? kd[s] : (T)__builtin_huge_val();
+        lg[s] = lane == 0 ? kg[s] : kNoPos;
+        lp[s] = lane == 0 ? kp[s] : kNoPos;
+    }
+}
+
+// The search of one query (uniform arguments), every lane of the wave
+// calling.  ks: the rank the exit certifies (k, or K reuse candidates).
+// Returns the merged list (uniform, kd / kp as lane_search leaves them:
+// positions, kNoPos for an empty entry), lb_exit and the points evaluated
+// (lane 0 adds them to its visit count).
+template <typename T, int KT>
+__device__ __forceinline__ void coop_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
+                                         const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy, T qz,
+                                         int ks, T maxR2, T (&kd)[KT], int32_t (&kp)[KT], double& lb_exit,
+                                         uint32_t& visits) {
+    const int lane = threadIdx.x & 63;
+    const double q[3] = {(double)qx, (double)qy, (double)qz};
+    int c[3];
+    bool qnan;
+    cell_of_q(G, q, c, qnan);
+    T ld[KT];
+    int32_t lg[KT], lp[KT];
+    int32_t kg[KT];
+#pragma unroll
+    for (int s = 0; s < KT; ++s) {
+        ld[s] = kd[s] = (T)__builtin_huge_val();
+        lg[s] = lp[s] = kg[s] = kp[s] = kNoPos;
+    }
+    lb_exit = -1.0;
+    if (qnan) return;  // (uniform: no neighbour, radius 0)
+    const double margin = 1.0 - 1e-5;
+    uint32_t evals = 0;
+    for (int R = 1;; ++R) {
+        // ring R: rows (y, z) in [c - R, c + R]^2; R = 1 takes the whole
+        // 3x3x3 block, later rings the cells at Chebyshev distance R only
+        const int side = 2 * R + 1, nrows = side * side;
+        for (int rb = 0; rb < nrows; rb += 64) {
+            uint32_t a1 = 0, l1 = 0, a2 = 0, l2 = 0;
+            const int r = rb + lane;
+            if (r < nrows) {
+                const int y = c[1] - R + r % side, z = c[2] - R + r / side;
+                if (y >= 0 && y < G.g[1] && z >= 0 && z < G.g[2]) {
+                    const uint32_t row = ((uint32_t)z * (uint32_t)G.g[1] + (uint32_t)y) * (uint32_t)G.g[0];
+                    const bool face = R == 1 || y == c[1] - R || y == c[1] + R || z == c[2] - R || z == c[2] + R;
+                    if (face) {
+                        const int xa = max(c[0] - R, 0), xb = min(c[0] + R, G.g[0] - 1);
+                        a1 = gld32(start, row + xa);
+                        l1 = gld32(start, row + xb + 1) - a1;
+                    } else {
+                        if (c[0] - R >= 0) {
+                            a1 = gld32(start, row + c[0] - R);
+                            l1 = gld32(start, row + c[0] - R + 1) - a1;
+                        }
+                        if (c[0] + R <= G.g[0] - 1) {
+                            a2 = gld32(start, row + c[0] + R);
+                            l2 = gld32(start, row + c[0] + R + 1) - a2;
+                        }
+                    }
+                }
+            }
+            // the segments' prefix over the wave
+            uint32_t incl = l1 + l2;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t v = __shfl_up(incl, off);
+                if (lane >= off) incl += v;
+            }
+            const uint32_t total = __shfl(incl, 63);
+            const uint32_t excl = incl - (l1 + l2);
+            evals += total;
+            // point t of the ring: the lane whose [excl, incl) holds it
+            for (uint32_t b0 = 0; b0 < total; b0 += 64 * 4) {
+                int32_t pos[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t t = b0 + (uint32_t)(u * 64 + lane);
+                    // binary search over the lanes' exclusive prefixes (uniform steps)
+                    int lo = 0;
+#pragma unroll
+                    for (int st = 32; st > 0; st >>= 1) {
+                        const uint32_t e = __shfl(excl, lo + st);
+                        if (lo + st < 64 && e <= t) lo += st;
+                    }
+                    const uint32_t e0 = __shfl(excl, lo), s1 = __shfl(a1, lo), n1 = __shfl(l1, lo),
+                                   s2 = __shfl(a2, lo);
+                    const uint32_t loc = t - e0;
+                    pos[u] = t < total ? (int32_t)(loc < n1 ? s1 + loc : s2 + (loc - n1)) : kNoPos;
+                }
+                P4<T> p[4];
+                int32_t g[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t pa = pos[u] == kNoPos ? 0u : (uint32_t)pos[u];  // (in-range dummy)
+                    p[u] = gld32(gpts, pa);
+                    g[u] = gld32(gidx, pa);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (pos[u] != kNoPos) coop_insert<T, KT>(ld, lg, lp, gsqd(qx, qy, qz, p[u]), g[u], pos[u]);
+            }
+        }
+        coop_merge<T, KT>(ld, lg, lp, kd, kg, kp);
+        // lower bound on the distance to any unvisited cell (lane_search's rule)
+        double lb = 1e300;
+        bool any = false;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (c[a] - R - 1 >= 0) {
+                lb = fmin(lb, q[a] - (G.lo[a] + (double)(c[a] - R) * G.h));
+                any = true;
+            }
+            if (c[a] + R + 1 <= G.g[a] - 1) {
+                lb = fmin(lb, (G.lo[a] + (double)(c[a] + R + 1) * G.h) - q[a]);
+                any = true;
+            }
+        }
+        lb_exit = any ? lb : 1e300;
+        if (!any) break;
+        if (lb > 0.0) {
+            const double lb2 = lb * lb * margin;
+            T dk = kd[0];
+            int32_t pk = kp[0];
+#pragma unroll
+            for (int s = 1; s < KT; ++s)
+                if (s == ks - 1) {
+                    dk = kd[s];
+                    pk = kp[s];
+                }
+            if ((double)dk < lb2 && pk != kNoPos) break;
+            if (lb2 > (double)maxR2) break;
+        }
+    }
+    if (lane == 0) visits += evals;
+}
+
 // ------------------------------------------------------- per-lane kernel --
 // Phase 1 (the reuse certificate) takes LaneQ slots per thread, its loads
 // staged so that a thread keeps every slot's chain in flight; phase 2 (full
@@ -709,7 +928,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
                                                         SpecSel* __restrict__ spec, const T* __restrict__ radii,
-                                                        int K, int32_t* __restrict__ cand) {
+                                                        int K, int32_t* __restrict__ cand, int coop_max) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         const GridDesc<T>& D = gd[ctl->level];
@@ -839,11 +1058,37 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         if (missed[q]) miss[off + __popcll(mq[q] & ((1ull << lane) - 1))] = q * 256 + threadIdx.x;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
-        const int64_t j2 = base + miss[t];
-        full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe, visits,
-                          sa, K, cand);
-        if (Q == 1) break;
+    if (total <= coop_max) {
+        // few misses (a converged match): each is searched by a whole wave
+        // (wave w takes misses w, w + 4, ...), two round trips per ring
+        // instead of a lane's chain of dependent row gathers
+        const int ks = cand ? K : k;
+        for (int t = wave; t < total; t += 4) {  // (wave-uniform)
+            const int64_t j2 = base + miss[t];
+            T qx, qy, qz;
+            gxform(Tm, gld(rd, j2), qx, qy, qz);
+            const T r2 = qr2(radii, j2, maxR2);
+            T kd[KT];
+            int32_t kp[KT];
+            double lbx;
+            coop_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, ks, r2, kd, kp, lbx, visits);
+            if (lane == 0) {
+                write_out<T, KT>(j2, k, r2, kd, kp, out_d, out_i, sa);
+                if (cand) {
+#pragma unroll
+                    for (int s = 0; s < KT; ++s)
+                        if (s < K) st_out(&cand[j2 * K + s], kp[s] == kNoPos ? (int32_t)-1 : kp[s]);
+                }
+                if (safe) st_out(&safe[j2], safe_radius<T, KT>(kd, kp, ks, lbx));
+            }
+        }
+    } else {
+        for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
+            const int64_t j2 = base + miss[t];
+            full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe,
+                              visits, sa, K, cand);
+            if (Q == 1) break;
+        }
     }
     add_visits(visits, visited);
     // queries that took the full search (the "fallback" counter the level choice reads)
@@ -870,7 +1115,7 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
         const bool cm = ru.mode && ru.cand && ru.K > knn && ru.K <= KT - 1;  // (the list holds K + 1)
         hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
                            rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
-                           ctl, gd, spec, radii, cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr);
+                           ctl, gd, spec, radii, cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr, ru.coop_max);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,

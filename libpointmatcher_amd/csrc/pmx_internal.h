@@ -187,6 +187,9 @@ struct GridReuse {
     // search, int32[N * K] (null: the k-list itself is the candidate set)
     int K = 0;
     int32_t* cand = nullptr;
+    // a block whose misses are at most this many searches each with a whole
+    // wave (pmx_grid.hip coop_search); more take the per-lane search
+    int coop_max = 0;
 };
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
