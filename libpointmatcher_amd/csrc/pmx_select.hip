@@ -335,6 +335,14 @@ __global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, i
         if (zt) atomicAdd(count + 2, zt);
     }
 }
+// the header's counters zeroed for this call — a kernel rather than a fill so
+// that an iteration queued after the device loop stopped leaves the last
+// call's header (count, error, zeros) for pmx_vartrim_partial_sums
+__global__ void vt_hdr_reset_kernel(int* __restrict__ hdr, const LoopCtl* __restrict__ ctl) {
+    if (ctl && ctl->done) return;
+    if (threadIdx.x < 64) hdr[threadIdx.x] = 0;
+}
+
 template <typename K>
 static size_t vt_sort_temp_bytes(int64_t n) {
     size_t t = 0;
@@ -1315,7 +1323,7 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
         p += al256(F * (4 * sizeof(long long) + 5 * sizeof(int)));
     }
 
-    (void)hipMemsetAsync(hdr, 0, 256, s);
+    hipLaunchKernelGGL(vt_hdr_reset_kernel, dim3(1), dim3(64), 0, s, hdr, ctl);
     K* src = keysB;  // (the sorted keys: the kept ones first)
     if (n > 0) {
         hipLaunchKernelGGL(vt_keys_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl);

@@ -228,3 +228,41 @@ def test_robust_device_loop_equals_modules(monkeypatch, oracle, dtype, case):
     assert sl.iterations == sm.iterations == so.iterations
     assert sl.kept == sm.kept
     assert fl <= tol and fm <= tol
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("params", [
+    {"robustFct": "huber", "scaleEstimator": "berg", "tuning": 0.05},
+    {"robustFct": "cauchy", "scaleEstimator": "mad", "tuning": 1, "nbIterationForScale": 3},
+])
+def test_robust_second_compute_loop_equals_modules(monkeypatch, dtype, params):
+    """RobustOutlierFilter keeps its iteration count across compute() calls
+    (OutlierFiltersImpl.cpp:509-540: berg's first-call scale, the
+    nbIterationForScale schedule).  A second compute on the same ICP object
+    starts past the first call's iterations; the device loop (scale mode per
+    loop iteration from the host module's count) must equal the per-module
+    path on both calls: same iterations, kept pairs, T within 1e-5 / 1e-12."""
+    from helpers import chain_yaml
+
+    ref, _ = reference_cloud(40_000, dtype)
+    rd = reading_cloud(20_000, dtype)
+    rd2 = reading_cloud(15_000, dtype)
+    yaml = chain_yaml(knn=2, filters=(("RobustOutlierFilter", params),), minimizer="PointToPointErrorMinimizer",
+                      maxit=12)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PMX_DEVICE_LOOP", mode)
+        icp = ICP(dtype)
+        icp.load_yaml(yaml)
+        res = []
+        for r in (rd, rd2):
+            T = icp.compute(r, ref, None)
+            s = icp.stats()
+            res.append((T.astype(np.float64), s.iterations, s.kept))
+        icp.close()
+        out[mode] = res
+    tol = 1e-5 if dtype == np.float32 else 1e-12
+    for (Tl, il, kl), (Tm, im, km) in zip(out["1"], out["0"]):
+        print(f"{params['scaleEstimator']}: iterations {il}/{im} kept {kl}/{km} |dT| {np.linalg.norm(Tl - Tm):.3g}")
+        assert il == im and kl == km
+        assert np.linalg.norm(Tl - Tm) <= tol
