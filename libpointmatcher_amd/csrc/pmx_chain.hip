@@ -19,6 +19,9 @@ namespace pmxc {
 // contiguous range.  The sizing runs on the host from three device counts;
 // the build itself is pmx_setup.hip.
 constexpr int64_t kMaxCells = (int64_t)1 << 26;
+int cold_level(const pmx_ctx* c);
+template <typename T>
+int build_levels(pmx_ctx* c, int upto);
 
 SetupShape grid_shape(const double lo[3], const double ext[3], double h) {
     SetupShape s;
@@ -174,6 +177,39 @@ int build_grid(pmx_ctx* c, int64_t M) {
         max_cells = std::max(max_cells, s.cells);
     }
     if ((rc = setup_room(c, M, max_cells))) return rc;
+    c->level_shapes = shapes;
+    c->grid_valid = valid;
+    c->levels_built = 0;
+    // every level entry exists (kept buffers reused); the finest ones up to
+    // the cold level are built now, the coarser ones on demand
+    for (size_t l = 0; l < shapes.size(); ++l) {
+        GridLevel L = keep[l];
+        keep[l] = GridLevel{};
+        L.ppc = c->level_ppc[l];
+        c->levels.push_back(L);
+    }
+    return build_levels<T>(c, c->adaptive ? cold_level(c) : 0);
+}
+
+// the level a new reading's first match runs on: the ppc nearest first_ppc
+int cold_level(const pmx_ctx* c) {
+    int best = 0;
+    for (int l = 0; l < (int)c->level_ppc.size(); ++l)
+        if (std::fabs(std::log(c->level_ppc[(size_t)l] / c->first_ppc)) <
+            std::fabs(std::log(c->level_ppc[(size_t)best] / c->first_ppc)))
+            best = l;
+    return best;
+}
+
+// build levels [levels_built, upto] of the current reference (stream order:
+// after whatever was enqueued before) and publish the device level table
+template <typename T>
+int build_levels(pmx_ctx* c, int upto) {
+    upto = std::min(upto, (int)c->levels.size() - 1);
+    if (upto < c->levels_built) return PMX_OK;
+    const P4<T>* pts = (const P4<T>*)c->d_ref;
+    const P4<T>* nrm = c->has_normals ? (const P4<T>*)c->d_nrm : nullptr;
+    const int64_t M = c->M, valid = c->grid_valid;
     const int64_t np = std::max<int64_t>(valid, 1);
     auto room = [](void** p, size_t* cap, size_t bytes) -> bool {
         if (*p && *cap >= bytes) return true;
@@ -184,15 +220,9 @@ int build_grid(pmx_ctx* c, int64_t M) {
         *cap = bytes;
         return true;
     };
-    for (size_t l = 0; l < shapes.size(); ++l) {
-        const SetupShape& s = shapes[l];
-        GridLevel L = keep[l];
-        keep[l] = GridLevel{};
-        auto bad = [&](int r) {
-            L.release();
-            for (auto& K : keep) K.release();
-            return r;
-        };
+    for (int l = c->levels_built; l <= upto; ++l) {
+        const SetupShape& s = c->level_shapes[(size_t)l];
+        GridLevel& L = c->levels[(size_t)l];
         if (!nrm && L.gpn) {  // (no normals: no interleaved records, so nothing stale can be gathered)
             (void)hipFree(L.gpn);
             L.gpn = nullptr;
@@ -200,22 +230,27 @@ int build_grid(pmx_ctx* c, int64_t M) {
         }
         if (!room(&L.gpts, &L.cap_pts, sizeof(P4<T>) * np) || !room((void**)&L.gidx, &L.cap_idx, sizeof(int32_t) * np) ||
             !room((void**)&L.gstart, &L.cap_start, sizeof(uint32_t) * (size_t)(s.cells + 1)) ||
-            (nrm && !room(&L.gpn, &L.cap_gpn, 2 * sizeof(P4<T>) * np)))
-            return bad(fail(c, PMX_E_HIP, "grid level allocation failed"));
+            (nrm && !room(&L.gpn, &L.cap_gpn, 2 * sizeof(P4<T>) * np))) {
+            c->grid_ready = false;
+            return fail(c, PMX_E_HIP, "grid level allocation failed");
+        }
         const int r = build_level_device<T>(pts, M, nrm, s, valid, c->setup, (P4<T>*)L.gpts, (P4<T>*)L.gpn, L.gidx,
                                             L.gstart, c->stream);
-        if (r) return bad(fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")"));
+        if (r) {
+            c->grid_ready = false;
+            return fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")");
+        }
         for (int a = 0; a < 3; ++a) {
             L.lo[a] = s.lo[a];
             L.dim[a] = s.g[a];
         }
         L.h = s.h;
-        L.ppc = c->level_ppc[l];
-        c->levels.push_back(L);
+        c->levels_built = l + 1;
     }
-    // the device table of levels (the device loop picks the level on the GPU)
-    std::vector<GridDesc<T>> tab(c->levels.size());
-    for (size_t l = 0; l < c->levels.size(); ++l) {
+    // the device table of the built levels (the device loop picks the level
+    // on the GPU, among the built ones)
+    std::vector<GridDesc<T>> tab((size_t)c->levels_built);
+    for (size_t l = 0; l < tab.size(); ++l) {
         const GridLevel& L = c->levels[l];
         GridDesc<T>& D = tab[l];
         D.gpts = (const P4<T>*)L.gpts;
@@ -394,11 +429,7 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     // walks few shells where the finest walks dozens (measured on MI355X, C3).
     // Any level answers exactly.
     if (c->adaptive && !c->levels.empty()) {
-        int best = 0;
-        for (int l = 0; l < (int)c->levels.size(); ++l)
-            if (std::fabs(std::log(c->lv(l).ppc / c->first_ppc)) < std::fabs(std::log(c->lv(best).ppc / c->first_ppc)))
-                best = l;
-        c->level = best;
+        c->level = std::min(cold_level(c), c->levels_built - 1);  // (built with the reference)
     }
     if (sharded(c)) {
         // global reading size and the largest shard (padding of all-gathers)
@@ -679,7 +710,7 @@ void choose_level(pmx_ctx* c, uint64_t visited, uint64_t full) {
     c->level_cells[(size_t)l] = cells;
     c->level_seen[(size_t)l] = c->match_count;
     int next = l;
-    if (cells > 32.0 && l + 1 < (int)c->levels.size()) {
+    if (cells > 32.0 && l + 1 < (int)c->levels.size() && ensure_level(c, l + 1) == PMX_OK) {
         next = l + 1;  // outer shells dominate: larger cells
     } else if (cells < 16.0 && l > 0) {
         // the 3x3x3 block sufficed: smaller cells evaluate fewer pairs, unless
@@ -688,6 +719,12 @@ void choose_level(pmx_ctx* c, uint64_t visited, uint64_t full) {
         if (!(recent && c->level_cells[(size_t)l - 1] > 32.0)) next = l - 1;
     }
     c->level = next;
+}
+
+// level l built (a coarser level on its first use)
+int ensure_level(pmx_ctx* c, int l) {
+    if (l < c->levels_built) return PMX_OK;
+    return c->dtype == PMX_F64 ? build_levels<double>(c, l) : build_levels<float>(c, l);
 }
 
 // slot-major device array -> query-major host array (the reference's order)

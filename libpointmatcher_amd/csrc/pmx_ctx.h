@@ -98,6 +98,12 @@ struct pmx_ctx {
     // large cells, see choose_level).
     std::vector<GridLevel> levels;
     std::vector<double> level_ppc{2.0, 4.0, 8.0, 16.0, 32.0, 64.0};
+    // Levels are built lazily: Matcher::init builds the finest ones up to
+    // the cold level (first_ppc), the coarser ones on the first match that
+    // wants one (ensure_level).  levels[0, levels_built) are built.
+    int levels_built = 0;
+    std::vector<SetupShape> level_shapes;
+    int64_t grid_valid = 0;   // finite reference points (the levels' size)
     int level = 0;      // level of the next grid match
     double first_ppc = 8.0;   // level of a new reading's first (cold) match (PMX_GRID_FIRST_PPC)
     int ids_level = 0;  // level whose positions the current match ids are
@@ -341,6 +347,7 @@ int upload_raw(pmx_ctx* c, const void* src, size_t bytes);
 int host_order(pmx_ctx* c);
 int select_reset(pmx_ctx* c);
 int reuse_k(const pmx_ctx* c, int knn);  // reuse candidates of a k-NN match (pmx_chain.hip)
+int ensure_level(pmx_ctx* c, int l);     // grid level l built (pmx_chain.hip)
 double host_limit(const pmx_ctx* c);
 void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double rm, double rp, double sw,
                 double limit);

@@ -41,7 +41,8 @@ struct LoopCfg {
     double checker_p[kMaxCheckers][3];
     // grid level adaptation (choose_level)
     int adaptive;
-    int n_levels;
+    int n_levels;       // levels built (the loop picks among them)
+    int n_levels_all;   // levels of the grid (a coarser unbuilt one is requested: LoopState.want_level)
     double level_ppc[kMaxLevels];
     int64_t n_local;
     int reuse;  // the grid match's temporal reuse is on (level choice on full searches only)
@@ -63,7 +64,7 @@ struct LoopState {
     double kept, nz, rejM, rejP, sw;  // last minimised iteration's ErrorElements statistics
     unsigned long long last_visited, touched;
     int last_level;
-    int pad;
+    int want_level;  // a coarser level the level rule wanted but was not built (the host builds it)
     long long match_count;
     double level_cells[kMaxLevels];
     long long level_seen[kMaxLevels];

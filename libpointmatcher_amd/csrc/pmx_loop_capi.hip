@@ -87,8 +87,9 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     d.adaptive = c->adaptive ? 1 : 0;
     d.reuse = c->reuse_on && c->grid_mode >= 1 ? 1 : 0;
     d.knn = reuse_k(c, cfg->knn);  // (pairs a certified query evaluates: its reuse candidates)
-    d.n_levels = (int)c->levels.size();
-    for (int l = 0; l < d.n_levels; ++l) d.level_ppc[l] = c->lv(l).ppc;
+    d.n_levels = c->levels_built;
+    d.n_levels_all = (int)c->levels.size();
+    for (int l = 0; l < d.n_levels_all; ++l) d.level_ppc[l] = c->lv(l).ppc;
     d.n_local = c->N;
     int rc;
     size_t cap = 0;
@@ -297,6 +298,12 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
             break;
         }
         const LoopState<T>* Sb = (const LoopState<T>*)(stat_slot(c, s) + kStatLoop);
+        if (!Sb->done && Sb->want_level >= c->levels_built) {
+            // a coarser grid level wanted: built now (enqueued after the
+            // batch in flight), offered to the step kernels enqueued next
+            if ((rc = ensure_level(c, Sb->want_level)) != PMX_OK) break;
+            c->loop_dev.n_levels = c->levels_built;
+        }
         if (Sb->done) {
             stop = true;
         } else if (((const LoopCtl*)(stat_slot(c, s) + kStatCtl))->done == kCtlStalled) {

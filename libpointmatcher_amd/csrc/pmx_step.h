@@ -330,7 +330,7 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
     // (with reuse: judged on the full searches only, kept while fewer than
     // 1/16 of the queries needed one — the rule of choose_level)
     double q = (double)cfg.n_local, v = (double)vis0;
-    bool adapt = cfg.adaptive && cfg.n_levels > 1 && cfg.n_local > 0;
+    bool adapt = cfg.adaptive && cfg.n_levels_all > 1 && cfg.n_local > 0;
     if (adapt && cfg.reuse) {
         const double full = (double)vis1;
         adapt = full * 16.0 >= q;
@@ -346,6 +346,8 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
         int next = l;
         if (cells > 32.0 && l + 1 < cfg.n_levels) {
             next = l + 1;
+        } else if (cells > 32.0 && l + 1 < cfg.n_levels_all) {
+            S->want_level = l + 1;  // (built by the host at its next batch check; this level meanwhile)
         } else if (cells < 16.0 && l > 0) {
             const bool recent = S->level_seen[l - 1] > 0 && S->match_count - S->level_seen[l - 1] <= 3;
             if (!(recent && S->level_cells[l - 1] > 32.0)) next = l - 1;
