@@ -682,6 +682,10 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
 // converged match (the per-lane kernel's phase 2).  The result is the exact
 // k-list of the per-lane search: the same (distance, original index) order,
 // the same certificate on the interior faces of the visited box.
+#ifndef PMX_COOP_U
+#define PMX_COOP_U 4
+#endif
+constexpr int kCoopU = PMX_COOP_U;  // ring points each lane has in flight
 template <typename T>
 struct CoopEnt {
     T d;
@@ -826,10 +830,10 @@ __device__ __forceinline__ void coop_search(const P4<T>* __restrict__ gpts, cons
             const uint32_t excl = incl - (l1 + l2);
             evals += total;
             // point t of the ring: the lane whose [excl, incl) holds it
-            for (uint32_t b0 = 0; b0 < total; b0 += 64 * 4) {
-                int32_t pos[4];
+            for (uint32_t b0 = 0; b0 < total; b0 += 64 * kCoopU) {
+                int32_t pos[kCoopU];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < kCoopU; ++u) {
                     const uint32_t t = b0 + (uint32_t)(u * 64 + lane);
                     // binary search over the lanes' exclusive prefixes (uniform steps)
                     int lo = 0;
@@ -843,16 +847,16 @@ __device__ __forceinline__ void coop_search(const P4<T>* __restrict__ gpts, cons
                     const uint32_t loc = t - e0;
                     pos[u] = t < total ? (int32_t)(loc < n1 ? s1 + loc : s2 + (loc - n1)) : kNoPos;
                 }
-                P4<T> p[4];
-                int32_t g[4];
+                P4<T> p[kCoopU];
+                int32_t g[kCoopU];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < kCoopU; ++u) {
                     const uint32_t pa = pos[u] == kNoPos ? 0u : (uint32_t)pos[u];  // (in-range dummy)
                     p[u] = gld32(gpts, pa);
                     g[u] = gld32(gidx, pa);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+                for (int u = 0; u < kCoopU; ++u)
                     if (pos[u] != kNoPos) coop_insert<T, KT>(ld, lg, lp, gsqd(qx, qy, qz, p[u]), g[u], pos[u]);
             }
         }
@@ -912,9 +916,19 @@ struct LaneQ {
 // takes 133-220 VGPRs, 2-3 waves, no spills): C5 1.79 -> 1.62 ms/iteration.
 // The float KT = 8 form spills 26 at 128 but measured faster that way than
 // unspilled at 3 waves (C4 0.202 vs 0.217 ms/iteration).
+#ifndef PMX_LIGHT
+#define PMX_LIGHT 0  // (experiment: every miss through the wave-cooperative search, PMX_LIGHT waves per SIMD)
+#endif
 template <typename T, int KT>
 struct LaneWaves {
-    static constexpr int value = sizeof(T) == 8 ? 2 : 4;
+    static constexpr int value = PMX_LIGHT ? PMX_LIGHT : (sizeof(T) == 8 ? 2 : 4);
+};
+#ifndef PMX_TILE_WAVES
+#define PMX_TILE_WAVES 0  // (experiment: the tile kernel's waves per SIMD; 0 = the per-lane kernel's default)
+#endif
+template <typename T, int KT>
+struct TileWaves {
+    static constexpr int value = PMX_TILE_WAVES ? PMX_TILE_WAVES : (sizeof(T) == 8 ? 2 : 4);
 };
 
 template <typename T, int KT, int Q>
@@ -1058,7 +1072,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         if (missed[q]) miss[off + __popcll(mq[q] & ((1ull << lane) - 1))] = q * 256 + threadIdx.x;
     }
     __syncthreads();
-    if (total <= coop_max) {
+    if (PMX_LIGHT || total <= coop_max) {
         // few misses (a converged match): each is searched by a whole wave
         // (wave w takes misses w, w + 4, ...), two round trips per ring
         // instead of a lane's chain of dependent row gathers
