@@ -171,6 +171,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_REUSE_CAND")) c->reuse_cand_req = std::max(0, std::min(15, std::atoi(e)));
+    if (const char* e = std::getenv("PMX_TILE_DISPATCH")) c->tile_dispatch_req = std::atoi(e);
     if (const char* e = std::getenv("PMX_COOP_MAX")) c->coop_max = std::max(0, std::min(256, std::atoi(e)));
     if (const char* e = std::getenv("PMX_VT_TRACE")) g_vt_trace = std::atoi(e);
     if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));

@@ -575,7 +575,8 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (T*)c->d_dists, c->d_ids, c->d_vpart, c->merge_counter ? nullptr : c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on, e1, c->stream);
+                             c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on,
+                             c->loop_on && c->loop_dev.tile_dispatch, e1, c->stream);
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));

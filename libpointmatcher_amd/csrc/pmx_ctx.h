@@ -120,6 +120,7 @@ struct pmx_ctx {
     // (0: off = the k-list itself; PMX_REUSE_CAND), cand_K: the K the
     // buffers hold (0: none valid)
     int reuse_cand_req = 0;
+    int tile_dispatch_req = -1;   // tile dispatch in the device loop: -1 auto (reading >= 4x the reference), 0 off, 1 on (PMX_TILE_DISPATCH)
     int coop_max = 4;             // wave-cooperative full searches for blocks with <= this many misses (PMX_COOP_MAX)
     int cand_K = 0;
     int32_t* d_cand = nullptr;    // int32[N * cand_K]

@@ -945,6 +945,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                                                         int K, int32_t* __restrict__ cand, int coop_max) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
+        if (ctl->use_tile) return;  // (tile dispatch: the tile kernel's warm form runs this match)
         const GridDesc<T>& D = gd[ctl->level];
         gpts = D.gpts;
         gidx = D.gidx;
@@ -1118,12 +1119,16 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                      const T* radii, bool cold, hipStream_t s) {
+                      const T* radii, bool cold, bool tile_disp, hipStream_t s) {
     if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
         hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
                            G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
                            ctl, gd, spec, ru.safe);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
+        if (tile_disp && ctl && ru.mode && !ru.cand)  // (device loop: the step picks one of the two forms)
+            hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx,
+                               start, G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited,
+                               radii, 2, ctl, gd, spec, ru.safe);
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
         const bool cm = ru.mode && ru.cand && ru.K > knn && ru.K <= KT - 1;  // (the list holds K + 1)
@@ -1144,8 +1149,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                       SelectState* spec_st, unsigned long long* xseg, const T* radii, bool cold, hipEvent_t ev_end,
-                       hipStream_t s) {
+                       SelectState* spec_st, unsigned long long* xseg, const T* radii, bool cold, bool tile_disp,
+                       hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     cold = cold && mode >= 1;
     if (mode < 1 || !visited) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
@@ -1162,7 +1167,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     } else {
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, radii, cold, s)
+                     ru, ctl, gd, spec, radii, cold, tile_disp, s)
         // with reuse the list keeps room for the (k+1)-th point (the safe radius;
         // the cold tile writes radius 0 and keeps k entries); with K reuse
         // candidates, for the (K+1)-th
@@ -1193,13 +1198,13 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, const float*, bool, hipEvent_t, hipStream_t);
+                                       unsigned long long*, const float*, bool, bool, hipEvent_t, hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, const double*, bool, hipEvent_t, hipStream_t);
+                                        unsigned long long*, const double*, bool, bool, hipEvent_t, hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

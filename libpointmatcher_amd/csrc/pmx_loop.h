@@ -47,6 +47,7 @@ struct LoopCfg {
     int64_t n_local;
     int reuse;  // the grid match's temporal reuse is on (level choice on full searches only)
     int knn;
+    int tile_dispatch;  // both match forms enqueued; the step picks the next (pmx_step.h)
 };
 
 template <typename T>
@@ -65,6 +66,8 @@ struct LoopState {
     unsigned long long last_visited, touched;
     int last_level;
     int want_level;  // a coarser level the level rule wanted but was not built (the host builds it)
+    int tile_run;    // tile dispatch: consecutive iterations on the tile kernel's warm form
+    int pad2;
     long long match_count;
     double level_cells[kMaxLevels];
     long long level_seen[kMaxLevels];

@@ -82,6 +82,7 @@ __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __rest
         }
     }
     ctl->done = 0;
+    ctl->use_tile = 0;
     ctl->level = level;
     ctl->prev_level = prev_level;
     for (int i = 0; i < 16; ++i) ctl->Tprev[i] = Tprev.m[i];

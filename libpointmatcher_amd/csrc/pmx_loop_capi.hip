@@ -87,6 +87,15 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     d.adaptive = c->adaptive ? 1 : 0;
     d.reuse = c->reuse_on && c->grid_mode >= 1 ? 1 : 0;
     d.knn = reuse_k(c, cfg->knn);  // (pairs a certified query evaluates: its reuse candidates)
+    // tile dispatch: a reading much denser than the reference (the tile
+    // kernel's wave-shared boxes serve 64 nearby queries with one load);
+    // the per-lane kernel's temporal reuse must be on (the step judges its
+    // certificate failures), no reuse candidates, k within the lane lists
+    {
+        const bool dense = c->N >= 4 * std::max<int64_t>(c->grid_valid, 1);
+        const bool want = c->tile_dispatch_req > 0 || (c->tile_dispatch_req < 0 && dense);
+        d.tile_dispatch = want && d.reuse && cfg->knn < kLaneMaxK && reuse_k(c, cfg->knn) == cfg->knn ? 1 : 0;
+    }
     d.n_levels = c->levels_built;
     d.n_levels_all = (int)c->levels.size();
     for (int l = 0; l < d.n_levels_all; ++l) d.level_ppc[l] = c->lv(l).ppc;

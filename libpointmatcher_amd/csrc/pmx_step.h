@@ -354,6 +354,23 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
         }
         ctl->level = next;
     }
+    // Tile dispatch (dense readings, LoopCfg.tile_dispatch): while almost
+    // every query fails the reuse certificate, the tile kernel's warm form
+    // (LDS boxes shared by a wave's 64 queries) is cheaper than 64 per-lane
+    // full searches.  A per-lane iteration measures the failure rate; two
+    // tile iterations follow a rate >= 98.5 %, then another per-lane probe.
+    if (cfg.tile_dispatch) {
+        const bool was_tile = ctl->use_tile != 0;
+        int next_tile = 0;
+        if (was_tile) {
+            S->tile_run += 1;
+            next_tile = S->tile_run < 2 ? 1 : 0;
+        } else {
+            S->tile_run = 0;
+            next_tile = (double)vis1 >= 0.985 * (double)cfg.n_local && cfg.n_local > 0 ? 1 : 0;
+        }
+        ctl->use_tile = next_tile;
+    }
     loop_publish(ctl, Tit, rows);
 }
 

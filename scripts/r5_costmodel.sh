@@ -17,7 +17,7 @@ for cfg in ${CFGS:-c3 c4 c5}; do
       fi
       timeout -k 10 300 $launch --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --emulate-ranks $G \
           > gpurun_out/cm_tmp.json 2>> gpurun_out/cm.err || exit 1
-      python -c "import json,sys; d=json.load(open('gpurun_out/cm_tmp.json')); print(json.dumps({'cfg': sys.argv[1], 'G': int(sys.argv[2]), 'mode': sys.argv[3], 'reading_per_rank': d['config']['reading_per_gpu'], 'ms_per_step': round(d['ms_per_step'],5), 'whole_ms_it': round(d['whole_icp']['ms_per_iteration'],5), 'match_ms': round(d['roofline']['avg_launch_ms'],5), 'comm_timed': d['comm_timed']}))" $cfg $G $mode | tee -a gpurun_out/costmodel.jsonl
+      python -c "import json,sys; d=json.loads([l for l in open('gpurun_out/cm_tmp.json') if l.startswith('{')][-1]); print(json.dumps({'cfg': sys.argv[1], 'G': int(sys.argv[2]), 'mode': sys.argv[3], 'reading_per_rank': d['config']['reading_per_gpu'], 'ms_per_step': round(d['ms_per_step'],5), 'whole_ms_it': round(d['whole_icp']['ms_per_iteration'],5), 'match_ms': round(d['roofline']['avg_launch_ms'],5), 'comm_timed': d['comm_timed']}))" $cfg $G $mode | tee -a gpurun_out/costmodel.jsonl
     done
   done
 done
