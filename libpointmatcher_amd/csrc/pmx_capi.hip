@@ -250,7 +250,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     void* bufs[] = {c->d_safe, c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
-                    c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace, c->d_diag, c->d_cand,
+                    c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace, c->d_diag, c->d_cand, c->d_ticket,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
                     c->d_rob, c->d_rdev, c->d_radii, c->d_rd_p4, c->d_rd_sorted};
     for (void* b : bufs)

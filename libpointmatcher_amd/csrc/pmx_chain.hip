@@ -1063,6 +1063,12 @@ int p2plane_enqueue(pmx_ctx* c) {
                               loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->vpart_dirty ? c->d_vpart : nullptr,
                               c->stream);
     c->vpart_dirty = false;
+    if (c->fuse_final) {  // (summed by the fused finalize + step launch)
+        c->final_out = c->d_result;
+        c->final_nv = NV;
+        HIPCHK(c, hipGetLastError());
+        return PMX_OK;
+    }
     launch_finalize(c->d_partials, kRedBlocks, NV, c->d_result, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result, NV);
@@ -1087,6 +1093,12 @@ int p2point_enqueue(pmx_ctx* c) {
     launch_p2point_means<T>(c->d_result, (T*)c->d_means, c->dim, loop_ctl(c), c->stream);
     launch_p2point_pass2<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
                             chain, c->knn, c->N, (const T*)c->d_means, c->d_partials, loop_ctl(c), gd, c->stream);
+    if (c->fuse_final) {  // (summed by the fused finalize + step launch)
+        c->final_out = c->d_result + 16;
+        c->final_nv = 9;
+        HIPCHK(c, hipGetLastError());
+        return PMX_OK;
+    }
     launch_finalize(c->d_partials, kRedBlocks, 9, c->d_result + 16, loop_ctl(c), c->stream);
     HIPCHK(c, hipGetLastError());
     return allreduce_f64(c, c->d_result + 16, 9);

@@ -253,6 +253,12 @@ struct pmx_ctx {
     void* d_loop_T0 = nullptr;    // initial T_iter (upload)
     void* d_trace = nullptr;      // T_iter per iteration (keep_trace)
     long long* d_diag = nullptr;  // per-iteration diagnostics ring (kDiagCap x kDiagWords, pmx_loop_diag)
+    unsigned int* d_ticket = nullptr;  // finalize_step_kernel's arrival ticket (0 between launches)
+    // device loop, one rank: the minimiser's last finalize is left to the
+    // fused finalize + step launch (final_out / final_nv: its accumulators)
+    bool fuse_final = false;
+    double* final_out = nullptr;
+    int final_nv = 0;
     int64_t trace_cap = 0;        // iterations
     bool loop_on = false;         // enqueueing loop iterations
     // quantile window fused into the grid match (pmx_spec.h): device loop,

@@ -15,6 +15,9 @@ constexpr int kMaxLevels = 8;
 // window), pairs evaluated, full searches]
 constexpr int kDiagCap = 1024;
 constexpr int kDiagWords = 4;
+// doubles of the iteration block the step reads (point-to-plane: <= 36 + 6 +
+// 5 in the full layout; point-to-point: the second pass at 16..24)
+constexpr int kStepRes = 48;
 
 enum CheckKind { kCheckCounter = 0, kCheckDifferential = 1, kCheckBound = 2 };
 // why the loop stopped
@@ -66,14 +69,18 @@ struct LoopState {
     unsigned long long last_visited, touched;
     int last_level;
     int want_level;  // a coarser level the level rule wanted but was not built (the host builds it)
-    int tile_run;    // tile dispatch: consecutive iterations on the tile kernel's warm form
-    int pad2;
+    int pad2[2];
     long long match_count;
     double level_cells[kMaxLevels];
     long long level_seen[kMaxLevels];
     T xsolve[6];  // the rank-deficient solve's result (loop_solve_rank_deficient)
 };
 
+template <typename T>
+void launch_finalize_step(const double* partials, int nblocks, int nv, double* out, double* res, unsigned int* ticket,
+                          LoopCtl* ctl, LoopState<T>* S, const int* iter_err, const unsigned long long* visited,
+                          const T* means, const LoopCfg& cfg, T* trace, const int* spec_hit, long long* diag,
+                          hipStream_t s);
 template <typename T>
 void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int prev_level,
                       const double* Tprev, hipStream_t s);

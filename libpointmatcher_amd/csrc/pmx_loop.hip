@@ -22,6 +22,7 @@
 // same dense code (common/pmx_dense.h) runs on the host in classic mode.
 #include "pmx_internal.h"
 
+#include "pmx_p2plane.h"
 #include "pmx_step.h"
 
 namespace pmx {
@@ -51,6 +52,90 @@ __global__ __launch_bounds__(64) void loop_step_kernel(LoopCtl* __restrict__ ctl
     }
     step_body<T, ROWS, MIN>(ctl, S, res, e, vis0, vis1, means, cfg, trace);
 }
+
+// The minimiser's last finalize and the step in one launch (device loop, one
+// rank): block v sums accumulator v exactly as finalize_kernel does
+// (pmx_reduce.hip) and publishes it write-through; the last block to take a
+// ticket reads the whole result block back coherently and runs the step.  It
+// saves the step's own launch (a dependent kernel boundary costs ~4.6 us in
+// the kernel trace here, an empty launch included: profiles/r05/anatomy).
+template <typename T, int ROWS, int MIN>
+__global__ __launch_bounds__(256) void finalize_step_kernel(const double* __restrict__ partials, int nblocks, int nv,
+                                                            double* __restrict__ out, double* __restrict__ res,
+                                                            unsigned int* __restrict__ ticket, LoopCtl* __restrict__ ctl,
+                                                            LoopState<T>* __restrict__ S,
+                                                            const int* __restrict__ iter_err,
+                                                            const unsigned long long* __restrict__ visited,
+                                                            const T* __restrict__ means, LoopCfg cfg,
+                                                            T* __restrict__ trace, const int* __restrict__ spec_hit,
+                                                            long long* __restrict__ diag) {
+    __shared__ double red[4];
+    __shared__ int s_last;
+    __shared__ double sres[kStepRes];
+    if (ctl->done) return;  // (uniform)
+    const int v = blockIdx.x;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < nblocks; b += 256) s += partials[(int64_t)v * nblocks + b];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // publish (write-through), then the ticket behind a release
+        __hip_atomic_store(&out[v], (red[0] + red[1]) + (red[2] + red[3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __atomic_thread_fence(__ATOMIC_RELEASE);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (unsigned)(nv - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_last) return;  // (block-uniform)
+    if (threadIdx.x < kStepRes) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        sres[threadIdx.x] = __hip_atomic_load(&res[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (the next launch starts at 0)
+    const int e = *iter_err;
+    const unsigned long long vis0 = visited[0], vis1 = visited[1];
+    const int hit = spec_hit ? *spec_hit : -1;
+    if (diag) {
+        long long* r = diag + (size_t)(S->iter % kDiagCap) * kDiagWords;
+        r[0] = ctl->level;
+        r[1] = hit;
+        r[2] = (long long)vis0;
+        r[3] = (long long)vis1;
+    }
+    step_body<T, ROWS, MIN>(ctl, S, sres, e, vis0, vis1, means, cfg, trace);
+}
+
+template <typename T>
+void launch_finalize_step(const double* partials, int nblocks, int nv, double* out, double* res, unsigned int* ticket,
+                          LoopCtl* ctl, LoopState<T>* S, const int* iter_err, const unsigned long long* visited,
+                          const T* means, const LoopCfg& cfg, T* trace, const int* spec_hit, long long* diag,
+                          hipStream_t s) {
+#define PMX_FSTEP(R, M)                                                                                          \
+    hipLaunchKernelGGL((finalize_step_kernel<T, R, M>), dim3(nv), dim3(256), 0, s, partials, nblocks, nv, out, res, \
+                       ticket, ctl, S, iter_err, visited, means, cfg, trace, spec_hit, diag)
+    if (cfg.rows == 4) {
+        if (cfg.minimizer == 0)
+            PMX_FSTEP(4, 0);
+        else
+            PMX_FSTEP(4, 1);
+    } else {
+        if (cfg.minimizer == 0)
+            PMX_FSTEP(3, 0);
+        else
+            PMX_FSTEP(3, 1);
+    }
+#undef PMX_FSTEP
+}
+template void launch_finalize_step<float>(const double*, int, int, double*, double*, unsigned int*, LoopCtl*,
+                                          LoopState<float>*, const int*, const unsigned long long*, const float*,
+                                          const LoopCfg&, float*, const int*, long long*, hipStream_t);
+template void launch_finalize_step<double>(const double*, int, int, double*, double*, unsigned int*, LoopCtl*,
+                                           LoopState<double>*, const int*, const unsigned long long*, const double*,
+                                           const LoopCfg&, double*, const int*, long long*, hipStream_t);
 
 // reset the loop state for a new ICP (checkers' init, ICP.cpp:368-369)
 template <typename T>

@@ -105,6 +105,10 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     (void)cap;  // (LoopState lives in the status block)
     cap = 0;
     if (!c->d_loop_T0 && (rc = ensure(c, &c->d_loop_T0, &cap, 16 * sizeof(double)))) return rc;
+    if (!c->d_ticket) {
+        HIPCHK(c, hipMalloc((void**)&c->d_ticket, 64));
+        HIPCHK(c, hipMemsetAsync(c->d_ticket, 0, 64, c->stream));
+    }
     if (!c->d_diag) {
         HIPCHK(c, hipMalloc((void**)&c->d_diag, sizeof(long long) * kDiagCap * kDiagWords));
         HIPCHK(c, hipMemsetAsync(c->d_diag, 0, sizeof(long long) * kDiagCap * kDiagWords, c->stream));
@@ -241,10 +245,26 @@ int loop_enqueue_iteration(pmx_ctx* c) {
         }
         if ((rc = outlier_impl<T>(c, cfg.filter_kind[i], i, p[0], p[1], p[2]))) return rc;
     }
-    if ((rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c))) return rc;
-    launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
-                        (const T*)c->d_means, c->loop_dev, cfg.keep_trace ? (T*)c->d_trace : nullptr,
-                        c->spec_on && c->d_spec ? &c->d_spec->hit : nullptr, c->d_diag, c->stream);
+    // one rank: the minimiser's last finalize and the step in one launch
+    static const bool fuse_env = [] {
+        const char* e = std::getenv("PMX_FUSE_STEP");
+        return !e || std::atoi(e) != 0;
+    }();
+    c->fuse_final = fuse_env && !sharded(c);
+    c->final_out = nullptr;
+    rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c);
+    const bool fused = c->fuse_final && c->final_out;
+    c->fuse_final = false;
+    if (rc) return rc;
+    const int* hitp = c->spec_on && c->d_spec ? &c->d_spec->hit : nullptr;
+    T* trace = cfg.keep_trace ? (T*)c->d_trace : nullptr;
+    if (fused)
+        launch_finalize_step<T>(c->d_partials, kRedBlocks, c->final_nv, c->final_out, c->d_result, c->d_ticket,
+                                c->d_ctl, (LoopState<T>*)c->d_loop, c->d_iter_err, c->d_visited, (const T*)c->d_means,
+                                c->loop_dev, trace, hitp, c->d_diag, c->stream);
+    else
+        launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
+                            (const T*)c->d_means, c->loop_dev, trace, hitp, c->d_diag, c->stream);
     HIPCHK(c, hipGetLastError());
     c->shard_replay = false;
     return PMX_OK;
