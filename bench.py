@@ -276,7 +276,17 @@ def main():
         uid = bytearray(_capi.Context.unique_id() if rank == 0 else bytes(128))
         t = torch.tensor(list(uid), dtype=torch.uint8)
         tdist.broadcast(t, src=0)
-        icp.comm_init(bytes(t.tolist()), world, rank)
+        # (RCCL prints its version banner on fd 1 at communicator creation:
+        # stdout stays the one JSON line)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            icp.comm_init(bytes(t.tolist()), world, rank)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     def barrier():
         if dist:

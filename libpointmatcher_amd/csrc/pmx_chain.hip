@@ -870,7 +870,10 @@ int outlier_impl(pmx_ctx* c, int kind, int chain_pos, double p0, double p1, doub
             c->deno_lambda = (double)lam;
         }
         const size_t need = vartrim_scratch_bytes<T>(nsrc);
+        const bool vt_new = !c->d_vt || c->vt_bytes < need;
         if ((rc = ensure(c, &c->d_vt, &c->vt_bytes, need))) return rc;
+        if (vt_new)  // (a new allocation: the radix sort's counters start at zero)
+            HIPCHK(c, hipMemsetAsync(c->d_vt, 0, vartrim_scratch_head(), c->stream));
         c->vt_n = nsrc;
         // (the quantile at the optimised ratio from the sorted keys: no radix
         // passes, and on several ranks no histogram all-reduces — the sort
@@ -1315,8 +1318,9 @@ int pmx_robust_scale(pmx_ctx* c, int pos, double* scale) {
 int pmx_vartrim_partial_sums(pmx_ctx* c, void* out, int64_t capacity, int64_t* count) {
     if (!c || !count) return fail(c, PMX_E_BAD_PARAM, "null argument");
     if (c->vt_n < 0 || !c->d_vt) return fail(c, PMX_E_STATE, "no VarTrimmedDist filter has run");
-    // scratch layout of launch_vartrim: the 256-byte header (count), two key
-    // arrays, then the partial sums
+    // scratch layout of launch_vartrim: the 256-byte header (count), the
+    // radix sort's counters (vartrim_scratch_head), two key arrays, then the
+    // partial sums
     const size_t ksz = c->dtype == PMX_F64 ? 8 : 4;
     const auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     int cnt = 0;
@@ -1325,7 +1329,7 @@ int pmx_vartrim_partial_sums(pmx_ctx* c, void* out, int64_t capacity, int64_t* c
     *count = cnt;
     if (!out) return PMX_OK;
     if (capacity < cnt) return fail(c, PMX_E_BAD_PARAM, "capacity below the partial-sum count");
-    const char* cum = (const char*)c->d_vt + 256 + 2 * al(ksz * (size_t)c->vt_n);
+    const char* cum = (const char*)c->d_vt + vartrim_scratch_head() + 2 * al(ksz * (size_t)c->vt_n);
     HIPCHK(c, hipMemcpyAsync(out, cum, ksz * (size_t)cnt, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (g_vt_trace) {  // (development trace of the last walk, PMX_VT_TRACE)

@@ -476,6 +476,7 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
                     const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 size_t vartrim_scratch_bytes(int64_t n);
+size_t vartrim_scratch_head();  // leading bytes of that scratch that must be zero at allocation
 
 // ---- reductions (pmx_reduce.hip) ----
 constexpr int kRedBlocks = 512;  // fixed reduction grid (deterministic sums)

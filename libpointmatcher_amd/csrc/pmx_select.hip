@@ -19,6 +19,7 @@
 // in T (one wave, bit-identical to the CPU), the FRMS curve and a first-index
 // argmin, then the same radix select with the optimised ratio.
 #include "pmx_internal.h"
+#include "pmx_radix.h"
 #include "pmx_sort.h"
 #include "pmx_spec.h"
 #include "pmx_selectall.h"
@@ -400,7 +401,11 @@ __device__ __forceinline__ long long sat_add(long long a, long long b, long long
     const long long v = a + b;
     return v < lim ? v : lim;
 }
-// exclusive saturating scan over the block (values and result <= lim)
+// exclusive saturating scan over the block (values and result <= lim; a
+// saturating add is associative, so every unsaturated prefix is exact).  The
+// exclusive value is the previous lane's inclusive one, not incl - v: a
+// thread whose own total saturates (its keys reach the crossing) still needs
+// the exact prefix before it for its keys ahead of the crossing.
 __device__ __forceinline__ long long cum_block_scan(long long v, long long lim, long long* wsum, long long& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     long long incl = v;
@@ -409,6 +414,8 @@ __device__ __forceinline__ long long cum_block_scan(long long v, long long lim, 
         const long long u = __shfl_up(incl, off);
         if (lane >= off) incl = sat_add(incl, u, lim);
     }
+    long long ex = __shfl_up(incl, 1);
+    if (lane == 0) ex = 0;
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     long long before = 0;
@@ -418,71 +425,87 @@ __device__ __forceinline__ long long cum_block_scan(long long v, long long lim, 
         total = sat_add(total, wsum[w], lim);
     }
     __syncthreads();
-    // exclusive = before + (incl - v), saturated (incl - v is exact: incl < lim, or the chunk has crossed anyway)
-    return sat_add(before, incl - v, lim);
+    return sat_add(before, ex, lim);
 }
 
 // The head (the first kCumHead keys, where the running sum leaves its binade
 // every few keys) is summed sequentially; the rest is cut into chunks of
 // kCumChunk keys.  vt_chunk_prep_kernel prepares every chunk in parallel
 // under the binade e GUESSED from a double prefix of the chunk sums, and under
-// e + 1: the integer prefixes P_e[j], P_e+1[j] of rnd(x / u) (stored), the
-// ties of both binades, and for binade e the ties' rounding already resolved
-// for an even and for an odd start: the parity of S0 / u decides every tie of
-// the chunk (the units before tie k are S0 + pb_k + up_k-1, so their parity
-// is that of S0 plus integers known beforehand).  vt_cumsum_kernel then walks
-// the chunks in order with the exact running sum S:
-//   fast   S in binade e, S / u + P_e + C_e[parity] < 2^P: the chunk's end
-//          sum in O(1) from the chunk table (preloaded in LDS);
+// e + 1: per key the integer prefix of rnd(x / u), with binade e's ties
+// already resolved for an even and for an odd start (Q_even, Q_odd) and binade
+// e + 1's ties counted as m (P1) beside a word locating the e + 1 ties (W1).
+// The ties resolve in parallel: tie k rounds up iff the units before it plus
+// m_k are odd, and with d_k = parity(pb_k + m_k) (pb_k: the prefix before the
+// tie, ties counted as m) the first tie after a start of parity B rounds up
+// iff B ^ d_k, every later one iff d_k ^ d_(k-1) — independent of the start,
+// so a prefix count D_k of those changes gives every tie's rounding for either
+// start parity.  vt_cumsum_kernel then walks the chunks in order with the
+// exact running sum S, wave 0 alone:
+//   fast   S in binade e, S / u + Q[end] < 2^P: the chunk's end sum in O(1)
+//          from the chunk table (preloaded in LDS), 64 chunks per step;
 //   cross  the sum leaves binade e inside the chunk: the crossing step (the
-//          first j whose units reach 2^P, found by the whole block over the
-//          stored P_e) is a plain T addition, and when it lands in binade
-//          e + 1 and the rest of the chunk stays there, the rest's sums are
-//          the e + 1 prefix from there (its few ties resolved in order);
+//          first j with S / u + Q[j] >= 2^P, a two-level search of the stored
+//          Q, 64 keys per level) is a plain T addition, and when it lands in
+//          binade e + 1 and the rest of the chunk stays there, the rest's sums
+//          are the e + 1 prefix from there (its ties by the D_k rule);
 //   slow   anything else (a wrong guess, many ties, two crossings, a
-//          subnormal sum): the passes below, which write the chunk's sums.
+//          subnormal sum): the block's passes below, which write the chunk.
 // vt_chunk_write_kernel writes the fast and crossing chunks' sums in
 // parallel.  Every path computes the sequential loop's bits.
 constexpr int kCumChunk = kCumThreads * kCumPer;
-constexpr int kCumHead = 4096;
+// (the head is summed by the preparation launch's extra block while the
+// other blocks prepare their chunks; 8 K measured slower: the serial sum of
+// the head, ~10 ns per key, outlasts the passes it saves)
+#ifndef PMX_VT_HEAD
+#define PMX_VT_HEAD 4096
+#endif
+constexpr int kCumHead = PMX_VT_HEAD;
 constexpr int kFastTies = 256;
 constexpr int kChunkLds = 512;  // chunk-table entries the walk preloads into LDS
 
+// the prefixes saturate here (a chunk far above its guessed binade would
+// overflow 64 bits; any value this large only says "past 2^P")
+constexpr long long kCumCap = 1ll << 61;
+
 struct VtChunk {
     double sum;       // double sum of the chunk's keys (the guess)
-    long long P[2];   // integer totals under binades e and e + 1
+    long long P[2];   // integer totals under binades e and e + 1 (ties as m; saturated at kCumCap)
     long long C[2];   // binade e: ties rounded up over the chunk, for an even / odd start
     double S0;        // exact start sum (T value): fast and crossing chunks
     double S1;        // crossing: the sum after the crossing step
     int e;            // guessed binade
     int nt[2];        // ties under e, e + 1 (kFastTies + 1: too many)
+    int D1;           // binade e + 1: D_k of the chunk's last tie
     int ok;           // 0: the passes wrote it; 1 fast; 2 crossing
     int par;          // parity of S0 / u
     int jc;           // crossing: chunk-local index of the crossing step
+    int k0, r0, Dk0;  // crossing: the first e + 1 tie after jc, its rounding, D_k0
 };
 
-// the per-chunk arrays of the prepared chunks (launch_vartrim lays them out)
+// the per-key arrays of the prepared chunks, index j - kCumHead
+// (launch_vartrim lays them out)
 struct VtPrep {
-    long long* P[2];  // inclusive prefixes, index j - kCumHead
-    int* t_idx[2];    // ties: chunk-local index, by chunk (kFastTies each)
-    long long* t_m[2];
-    long long* t_pb[2];  // prefix before the tie (ties counted as m)
-    int* t_c0[2];        // binade e: rounded-up ties up to and including tie k, even / odd start
-    int* t_c1;           // binade e + 1: the same after a crossing (written by the walk)
+    long long* Q[2];  // binade e: units added by keys up to j, ties resolved, even / odd start
+    long long* P1;    // binade e + 1: inclusive prefix, ties counted as m
+    int* W1;          // binade e + 1 ties up to j: count | d_next << 9 | d_last << 10 | D_last << 11
 };
 
 constexpr int kVtTraceMax = 2048;  // (development trace of the walk: marks, then the count)
 
 static int64_t vt_chunks(int64_t n) { return n > kCumHead ? (n - kCumHead + kCumChunk - 1) / kCumChunk : 0; }
 
+// the part of the VarTrimmed scratch that must be zero when it is allocated
+// (the radix sort's persistent counters); bytes from the scratch's start
+size_t vartrim_scratch_head() { return 256 + al256(sizeof(RsHead)); }
+
 template <typename T>
 size_t vartrim_scratch_bytes(int64_t n) {
     using K = typename KeyOf<T>::K;
     const int64_t nch = vt_chunks(n);
-    return 256 + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(8 * 256) +
-           al256(vt_sort_temp_bytes<K>(n)) + al256(sizeof(VtChunk) * (nch + 1)) + 2 * al256(8 * (size_t)n) +
-           al256((size_t)kFastTies * nch * (4 * sizeof(long long) + 5 * sizeof(int))) +
-           al256(8 * (2 * (size_t)kVtTraceMax + 1));
+    return 256 + al256(sizeof(RsHead)) + 2 * al256(sizeof(K) * n) + al256(sizeof(T) * n) + 2 * al256(8 * 256) +
+           al256(rs_state_bytes(n)) + al256(sizeof(VtChunk) * (nch + 1)) + 3 * al256(8 * (size_t)n) +
+           al256(4 * (size_t)n) + al256(8 * (2 * (size_t)kVtTraceMax + 1));
 }
 
 // this thread's kCumPer keys from j0 (16-byte loads when in range)
@@ -598,27 +621,101 @@ __device__ __forceinline__ long long block_excl_scan_ll(long long v, long long* 
 
 // per chunk: the guessed binade e; under e and e + 1 the inclusive prefixes,
 // the totals and the ties; binade e's ties resolved for both start parities
+// The head's sums (std::partial_sum's first kCumHead steps, sequentially in
+// T): keys staged in LDS by the block, one thread sums into LDS (no global
+// store in the serial loop), the block writes them out coalesced.  head_out
+// = the running sum after the head, for the walk.
+template <typename T>
+__device__ __forceinline__ void vt_cum_head(const typename KeyOf<T>::K* __restrict__ keys, int64_t c,
+                                            T* __restrict__ cum, T* __restrict__ head_out) {
+    using KO = KeyOf<T>;
+    __shared__ __attribute__((aligned(16))) T s_h[kCumHead];
+    const int ph = c < kCumHead ? (int)c : kCumHead;
+    for (int j = threadIdx.x; j < ph; j += kCumThreads) s_h[j] = KO::val(keys[j]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // Batches of 16 keys in 16-byte LDS vectors, software-pipelined: the
+        // next batch's loads are issued before this batch's dependent adds
+        // and its stores (LDS operations complete in order, so a store queued
+        // ahead of a load would make the load's wait cover it too); the adds
+        // then hide the load latency.  acc starts at -0: -0 + x0 = x0 exactly,
+        // partial_sum's first output.
+        using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+        constexpr int E = 16 / sizeof(T), NV = 16 / E;
+        V* hv = reinterpret_cast<V*>(s_h);
+        T acc = (T)-0.0;
+        const int nb = ph / 16;
+        V cur[NV], nxt[NV];
+        if (nb > 0) {
+#pragma unroll
+            for (int w = 0; w < NV; ++w) cur[w] = hv[w];
+        }
+        for (int bt = 0; bt < nb; ++bt) {
+            if (bt + 1 < nb) {
+#pragma unroll
+                for (int w = 0; w < NV; ++w) nxt[w] = hv[(bt + 1) * NV + w];
+            }
+#pragma unroll
+            for (int w = 0; w < NV; ++w) {
+                T* x = reinterpret_cast<T*>(&cur[w]);
+#pragma unroll
+                for (int q = 0; q < E; ++q) {
+                    acc = acc + x[q];
+                    x[q] = acc;
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < NV; ++w) hv[bt * NV + w] = cur[w];
+#pragma unroll
+            for (int w = 0; w < NV; ++w) cur[w] = nxt[w];
+        }
+        for (int j = nb * 16; j < ph; ++j) {
+            acc = acc + s_h[j];
+            s_h[j] = acc;
+        }
+        *head_out = acc;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < ph; j += kCumThreads) cum[j] = s_h[j];
+}
+
 template <typename T>
 __global__ __launch_bounds__(kCumThreads) void vt_chunk_prep_kernel(const typename KeyOf<T>::K* __restrict__ keys,
                                                                     const int* __restrict__ count,
                                                                     VtChunk* __restrict__ ch, VtPrep pr,
-                                                                    const LoopCtl* __restrict__ ctl) {
+                                                                    const LoopCtl* __restrict__ ctl,
+                                                                    T* __restrict__ cum, T* __restrict__ head_out) {
     using K = typename KeyOf<T>::K;
     constexpr int P = CumBits<T>::P;
     __shared__ long long wsum[kCumThreads / 64];
     __shared__ double s_approx;
-    __shared__ int l_idx[kFastTies];
-    __shared__ long long l_pb[kFastTies], l_m[kFastTies];
+    __shared__ double wsd[kCumThreads / 64];
+    __shared__ int l_d[kFastTies], l_D[kFastTies];
+    static_assert(kFastTies <= kCumThreads, "one tie per thread");
     if (ctl && ctl->done) return;
     const int64_t c = *count;
     const int b = blockIdx.x, t = threadIdx.x;
+    if (b == (int)gridDim.x - 1 && cum) {  // (the extra block: the head, vt_cum_head)
+        vt_cum_head<T>(keys, c, cum, head_out);
+        return;
+    }
     const int64_t lo = kCumHead + (int64_t)b * kCumChunk;
     if (lo >= c) return;
     const int64_t hi = lo + kCumChunk < c ? lo + kCumChunk : c;
-    if (t == 0) {
-        double a = 0.0;  // the head and every earlier chunk (an estimate of the running sum)
-        for (int i = 0; i <= b; ++i) a += ch[i].sum;
-        s_approx = a;
+    {
+        // the head and every earlier chunk: an estimate of the running sum
+        // (its binade is only a guess the walk verifies: any order will do;
+        // a fixed one keeps it deterministic), the block's threads in parallel
+        double a = 0.0;
+        for (int i = t; i <= b; i += kCumThreads) a += ch[i].sum;
+        for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+        if ((t & 63) == 0) wsd[t >> 6] = a;
+        __syncthreads();
+        if (t == 0) {
+            double s2 = 0.0;
+            for (int w = 0; w < kCumThreads / 64; ++w) s2 += wsd[w];
+            s_approx = s2;
+        }
     }
     __syncthreads();
     const int e = CumBits<T>::binade((T)s_approx);
@@ -631,45 +728,62 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_prep_kernel(const typena
         bool tie[kCumPer];
         int ntie;
         (void)vt_round<T>(kv, j0, lo, hi, inv_u, r, tie, ntie);
-        long long loc = 0;  // (exact: each r <= 2^P)
+        long long loc = 0;
 #pragma unroll
-        for (int i = 0; i < kCumPer; ++i) loc += r[i];
+        for (int i = 0; i < kCumPer; ++i) loc = sat_add(loc, r[i], kCumCap);
         long long tot, tt;
-        long long run = block_excl_scan_ll(loc, wsum, tot);
+        long long run = cum_block_scan(loc, kCumCap, wsum, tot);
         const long long tbase = block_excl_scan_ll((long long)ntie, wsum, tt);
-        int k = (int)tbase;
+        const int nt = tt <= kFastTies ? (int)tt : kFastTies + 1;
+        if (nt <= kFastTies) {  // each tie's d = parity of (the prefix before it + m)
+            int k = (int)tbase;
+            long long pb = run;
 #pragma unroll
-        for (int i = 0; i < kCumPer; ++i) {
-            if (tie[i] && tt <= kFastTies) {
-                l_idx[k] = t * kCumPer + i;
-                l_pb[k] = run;
-                l_m[k] = r[i];
-                ++k;
+            for (int i = 0; i < kCumPer; ++i) {
+                if (tie[i]) l_d[k++] = (int)((pb + r[i]) & 1ll);
+                pb = sat_add(pb, r[i], kCumCap);
             }
-            run += r[i];
-            const int64_t j = j0 + i;
-            if (j < hi) pr.P[v][j - kCumHead] = run;
         }
         __syncthreads();
-        const int nt = tt <= kFastTies ? (int)tt : kFastTies + 1;
+        {  // D_k: the changes of d over ties 1..k, one tie per thread
+            const long long x = t > 0 && t < nt && nt <= kFastTies ? (long long)(l_d[t] ^ l_d[t - 1]) : 0ll;
+            long long xt;
+            const long long ex = block_excl_scan_ll(x, wsum, xt);
+            if (t < nt && nt <= kFastTies) l_D[t] = (int)(ex + x);
+        }
+        __syncthreads();
         if (nt <= kFastTies) {
-            for (int q = t; q < nt; q += kCumThreads) {
-                pr.t_idx[v][b * kFastTies + q] = l_idx[q];
-                pr.t_pb[v][b * kFastTies + q] = l_pb[q];
-                pr.t_m[v][b * kFastTies + q] = l_m[q];
-            }
-            if (v == 0 && t < 2) {  // binade e: every tie's rounding for an even (t = 0) / odd (t = 1) start
-                int up = 0;
-                for (int q = 0; q < nt; ++q) {
-                    up += ((t + l_pb[q] + up + l_m[q]) & 1ll) ? 1 : 0;
-                    pr.t_c0[t][b * kFastTies + q] = up;
+            const int d0 = nt > 0 ? l_d[0] : 0;
+            int kt = (int)tbase;  // ties at or before the key
+#pragma unroll
+            for (int i = 0; i < kCumPer; ++i) {
+                run = sat_add(run, r[i], kCumCap);
+                kt += tie[i] ? 1 : 0;
+                const int64_t j = j0 + i;
+                if (j >= hi) continue;
+                if (v == 0) {  // the rounded-up ties so far, for an even / odd start
+                    const long long D = kt > 0 ? (long long)l_D[kt - 1] : 0ll;
+                    pr.Q[0][j - kCumHead] = run + (kt > 0 ? (long long)d0 + D : 0ll);
+                    pr.Q[1][j - kCumHead] = run + (kt > 0 ? (long long)(1 ^ d0) + D : 0ll);
+                } else {
+                    pr.P1[j - kCumHead] = run;
+                    const int dn = kt < nt ? l_d[kt] : 0, dl = kt > 0 ? l_d[kt - 1] : 0;
+                    const int Dl = kt > 0 ? l_D[kt - 1] : 0;
+                    pr.W1[j - kCumHead] = kt | (dn << 9) | (dl << 10) | (Dl << 11);
                 }
-                ch[b + 1].C[t] = up;
             }
         }
         if (t == 0) {
             ch[b + 1].P[v] = tot;
             ch[b + 1].nt[v] = nt;
+            const int Dt = nt > 0 && nt <= kFastTies ? l_D[nt - 1] : 0;
+            if (v == 0) {
+                const int d0 = nt > 0 && nt <= kFastTies ? l_d[0] : 0;
+                ch[b + 1].C[0] = nt > 0 ? d0 + Dt : 0;
+                ch[b + 1].C[1] = nt > 0 ? (1 ^ d0) + Dt : 0;
+            } else {
+                ch[b + 1].D1 = Dt;
+            }
         }
         __syncthreads();  // (the LDS tie list is rewritten for e + 1)
     }
@@ -679,8 +793,9 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_prep_kernel(const typena
     }
 }
 
-// the fast and crossing chunks' sums: S0 + P_j + C_j in units of binade e,
-// then after a crossing S1 + (P'_j - P'_jc) + C'_j in units of binade e + 1
+// the fast and crossing chunks' sums: S0 + Q_par[j] in units of binade e,
+// then after a crossing S1 + (P1[j] - P1[jc]) + the rest's rounded-up ties in
+// units of binade e + 1
 template <typename T>
 __global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typename KeyOf<T>::K* __restrict__ keys,
                                                                      const int* __restrict__ count,
@@ -688,8 +803,7 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typen
                                                                      T* __restrict__ cum,
                                                                      const LoopCtl* __restrict__ ctl) {
     constexpr int P = CumBits<T>::P;
-    __shared__ int l_idx[kFastTies], l_c[kFastTies];
-    __shared__ int l1_idx[kFastTies], l1_c[kFastTies];
+    (void)keys;
     if (ctl && ctl->done) return;
     const int64_t c = *count;
     const int b = blockIdx.x, t = threadIdx.x;
@@ -698,46 +812,27 @@ __global__ __launch_bounds__(kCumThreads) void vt_chunk_write_kernel(const typen
     const VtChunk q = ch[b + 1];
     if (!q.ok) return;  // (uniform: the passes wrote this chunk)
     const int64_t hi = lo + kCumChunk < c ? lo + kCumChunk : c;
-    const int nt0 = q.nt[0], nt1 = q.ok == 2 ? q.nt[1] : 0, jc = q.ok == 2 ? q.jc : 0x7fffffff;
-    for (int k = t; k < nt0; k += kCumThreads) {
-        l_idx[k] = pr.t_idx[0][b * kFastTies + k];
-        l_c[k] = pr.t_c0[q.par][b * kFastTies + k];
-    }
-    for (int k = t; k < nt1; k += kCumThreads) {
-        l1_idx[k] = pr.t_idx[1][b * kFastTies + k];
-        l1_c[k] = l1_idx[k] > jc ? pr.t_c1[b * kFastTies + k] : 0;
-    }
-    __syncthreads();
+    const int jc = q.ok == 2 ? q.jc : 0x7fffffff;
     const double u0 = ldexp(1.0, q.e - (P - 1)), u1 = ldexp(1.0, q.e + 1 - (P - 1));
     const long long U0 = CumBits<T>::units((T)q.S0);
     const long long U1 = q.ok == 2 ? CumBits<T>::units((T)q.S1) : 0;
-    const long long P1jc = q.ok == 2 ? pr.P[1][lo + jc - kCumHead] : 0;
-    // the ties at local indices below this thread's first key
-    auto first_at = [&](const int* idx, int n) {
-        int lo2 = 0, hi2 = n;
-        while (lo2 < hi2) {
-            const int mid = (lo2 + hi2) >> 1;
-            if (idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
-        }
-        return lo2;
-    };
-    int kt0 = first_at(l_idx, nt0), kt1 = first_at(l1_idx, nt1);
+    const long long P1jc = q.ok == 2 ? pr.P1[lo + jc - kCumHead] : 0;
+    const long long* __restrict__ Q = pr.Q[q.par];
 #pragma unroll
     for (int i = 0; i < kCumPer; ++i) {
         const int li = t * kCumPer + i;
         const int64_t j = lo + li;
-        if (kt0 < nt0 && l_idx[kt0] == li) ++kt0;
-        if (kt1 < nt1 && l1_idx[kt1] == li) ++kt1;
         if (j >= hi) continue;
         T v;
         if (li < jc) {
-            const long long C = kt0 > 0 ? (long long)l_c[kt0 - 1] : 0ll;
-            v = (T)((double)(U0 + pr.P[0][j - kCumHead] + C) * u0);
+            v = (T)((double)(U0 + Q[j - kCumHead]) * u0);
         } else if (li == jc) {
             v = (T)q.S1;
         } else {
-            const long long C = kt1 > 0 ? (long long)l1_c[kt1 - 1] : 0ll;  // (0 for ties at or before jc)
-            v = (T)((double)(U1 + (pr.P[1][j - kCumHead] - P1jc) + C) * u1);
+            const int w = pr.W1[j - kCumHead];
+            const int kt = w & 0x1ff;
+            const long long ups = kt > q.k0 ? (long long)(q.r0 + (w >> 11) - q.Dk0) : 0ll;
+            v = (T)((double)(U1 + (pr.P1[j - kCumHead] - P1jc) + ups) * u1);
         }
         cum[j] = v;
     }
@@ -749,7 +844,8 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
                                                                 const int* __restrict__ count, T* __restrict__ cum,
                                                                 VtChunk* __restrict__ ch, VtPrep pr, int nch,
                                                                 const LoopCtl* __restrict__ ctl,
-                                                                unsigned long long* __restrict__ trace) {
+                                                                unsigned long long* __restrict__ trace,
+                                                                const T* __restrict__ head_in) {
     using KO = KeyOf<T>;
     // (development trace, PMX_VT_TRACE: thread 0 stamps each step of the walk
     // with the 100 MHz real-time counter; pmx_vartrim_partial_sums prints it)
@@ -770,18 +866,13 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
     __shared__ long long tie_m[kCumMaxTies];
     __shared__ int tie_c[kCumMaxTies];          // rounded-up ties up to and including this one
     __shared__ int s_cross;
-    __shared__ int s_mode;
-    __shared__ long long s_U0;
-    __shared__ int s_par;
     __shared__ long long s_lo;                  // the walk's position (chunk start, chunk)
     __shared__ int s_b;
     __shared__ T s_run;                         // the running sum after the chunk
     // the chunk table of the fast test (the walk's per-chunk decision then
     // reads no global memory)
-    __shared__ long long c_P0[kChunkLds], c_C[2][kChunkLds];
-    __shared__ int c_e[kChunkLds], c_nt0[kChunkLds];
-    __shared__ int t1_idx[kFastTies];  // a crossing chunk's binade e + 1 ties
-    __shared__ long long t1_pb[kFastTies], t1_m[kFastTies];
+    __shared__ long long c_P0[kChunkLds], c_C[2][kChunkLds], c_P1[kChunkLds];
+    __shared__ int c_e[kChunkLds], c_nt0[kChunkLds], c_nt1[kChunkLds], c_D1[kChunkLds];
     if (ctl && ctl->done) return;
     const int t = threadIdx.x;
     const int64_t c = *count;
@@ -794,91 +885,207 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         c_C[1][i] = q.C[1];
         c_e[i] = q.e;
         c_nt0[i] = q.nt[0];
+        c_P1[i] = q.P[1];
+        c_nt1[i] = q.nt[1];
+        c_D1[i] = q.D1;
     }
-    // the head sequentially (keys staged in LDS by the whole block: the one
-    // summing thread then waits on no global load)
-    __shared__ typename KO::K s_head[kCumHead];
+    // the head: summed (and written) by the preparation launch's extra block
+    // when there are chunks (head_in), else here, the same way
     const int ph = c < kCumHead ? (int)c : kCumHead;
-    for (int j = t; j < ph; j += kCumThreads) s_head[j] = keys[j];
-    __syncthreads();
-    if (t == 0) {
-        T acc = KO::val(s_head[0]);  // partial_sum's first output is the first element
-        cum[0] = acc;
-#pragma unroll 8
-        for (int j = 1; j < ph; ++j) {
-            acc = acc + KO::val(s_head[j]);
-            cum[j] = acc;
-        }
-        s_run = acc;
+    if (head_in) {
+        if (t == 0) s_run = *head_in;
+    } else {
+        vt_cum_head<T>(keys, c, cum, &s_run);
     }
     VT_MARK(1, 0, ph);
     __syncthreads();
     T s = s_run;
     __syncthreads();
-    // The walk.  Thread 0 settles a run of fast chunks in one go (no block
-    // barrier between them: one per chunk made the ~50 fast chunks of a 1M
-    // sum most of the walk); the block then takes the first chunk that is
-    // not fast, as a crossing or through the passes.
+    // The walk.  Wave 0 settles runs of fast chunks and the crossings
+    // between them (no block barrier: one per chunk made the ~250 fast
+    // chunks of a 1M sum most of the walk); the block then takes the first
+    // chunk that is neither, through the passes.
     int64_t lo = ph;
     int b = 0;
     while (lo < c) {  // (uniform)
-        if (t == 0) {
-            // 1 fast: the guessed binade is the running sum's, few ties, and
-            // the chunk's last sum stays below the next binade (O(1): the
-            // ties were resolved for both parities of the start);
-            // 2 a crossing to examine; 0 the passes
-            // (integer units along a run: the run stays in S's binade es,
-            // so each chunk's end units are the next chunk's start units —
-            // no float round trips between chunks; the table reads of a
-            // chunk do not wait on the running units)
+        if (t < 64) {
+            // Fast chunks, 64 per step: the guessed binade is the running
+            // sum's, few ties, and the chunk's last sum stays below the next
+            // binade.  The run stays in S's binade es, so chunk i's start
+            // units are U + the increments of the chunks before it, an
+            // integer prefix sum, and each increment Q_par[end] = P0 +
+            // C[parity] depends on the parity of its start only: the
+            // parities are a prefix composition of 1-bit maps (p -> p ^
+            // parity(P0 + C_p)).  Bit-identical to the chunk-by-chunk walk.
+            const int lane = t;
             T sr = s;
-            int mode = 0;
             if (sr >= CumBits<T>::min_normal()) {
-                const int es = CumBits<T>::binade(sr);
-                const double u = ldexp(1.0, es - (P - 1));
+                int es = CumBits<T>::binade(sr);
+                double u = ldexp(1.0, es - (P - 1));
                 long long U = CumBits<T>::units(sr);
-                for (; lo < c; lo += kCumChunk, ++b) {
-                    int e, nt0;
-                    long long P0, C0, C1;
+                for (;;) {  // (wave-uniform)
+                    const int bi = b + lane;
+                    const int64_t loi = lo + (int64_t)lane * kCumChunk;
+                    int e = 0, nt0 = kFastTies + 1;
+                    long long P0 = 0, C0 = 0, C1 = 0;
+                    if (loi < c) {
+                        if (bi < kChunkLds) {
+                            e = c_e[bi];
+                            nt0 = c_nt0[bi];
+                            P0 = c_P0[bi];
+                            C0 = c_C[0][bi];
+                            C1 = c_C[1][bi];
+                        } else {
+                            const VtChunk& g = ch[bi + 1];
+                            e = g.e;
+                            nt0 = g.nt[0];
+                            P0 = g.P[0];
+                            C0 = g.C[0];
+                            C1 = g.C[1];
+                        }
+                    }
+                    const bool valid = loi < c && nt0 <= kFastTies && e == es;
+                    // this chunk's parity map as (image of 0, image of 1)
+                    int f0 = (int)((P0 + C0) & 1ll), f1 = 1 ^ (int)((P0 + C1) & 1ll);
+                    // exclusive prefix composition (lane i: the map from the
+                    // window's start parity to chunk i's start parity)
+                    int g0 = 0, g1 = 1;  // identity
+                    {
+                        int a0 = f0, a1 = f1;  // inclusive composition, scanned
+#pragma unroll
+                        for (int off = 1; off < 64; off <<= 1) {
+                            const int b0 = __shfl_up(a0, off), b1 = __shfl_up(a1, off);
+                            if (lane >= off) {  // a = a o b (b first)
+                                const int n0 = b0 ? a1 : a0, n1 = b1 ? a1 : a0;
+                                a0 = n0;
+                                a1 = n1;
+                            }
+                        }
+                        const int p0 = __shfl_up(a0, 1), p1 = __shfl_up(a1, 1);
+                        if (lane > 0) {
+                            g0 = p0;
+                            g1 = p1;
+                        }
+                    }
+                    const int par0 = (int)(U & 1ll);
+                    const int par = par0 ? g1 : g0;
+                    // (clamped: an increment of 2^P ends the run anyway; 64 of
+                    // them stay far from overflow)
+                    long long inc = P0 + (par ? C1 : C0);
+                    inc = inc < LIM ? inc : LIM;
+                    long long incl = inc;
+#pragma unroll
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const long long v2 = __shfl_up(incl, off);
+                        if (lane >= off) incl += v2;
+                    }
+                    const long long Ui = U + (incl - inc), fin = U + incl;
+                    const bool stop = !valid || fin >= LIM;
+                    const unsigned long long sm = __ballot(stop);
+                    const int first = sm ? __builtin_ctzll(sm) : 64;
+                    if (lane < first) {
+                        VtChunk& q = ch[bi + 1];
+                        q.S0 = (double)Ui * u;  // (the T value of the start sum, exactly)
+                        q.par = par;
+                        q.ok = 1;
+                    }
+                    if (first == 64) {
+                        U = __shfl(fin, 63);
+                        lo += (int64_t)64 * kCumChunk;
+                        b += 64;
+                        if (lo >= c) break;
+                        continue;
+                    }
+                    const long long Uf = __shfl(Ui, first);
+                    const int parf = __shfl(par, first);
+                    const int vf = __shfl(valid ? 1 : 0, first);
+                    U = Uf;
+                    lo += (int64_t)first * kCumChunk;
+                    b += first;
+                    if (!vf) break;  // (the passes)
+                    // A valid chunk whose end leaves the binade: the crossing.
+                    int nt1, D1;
+                    long long P1t;
                     if (b < kChunkLds) {
-                        e = c_e[b];
-                        nt0 = c_nt0[b];
-                        P0 = c_P0[b];
-                        C0 = c_C[0][b];
-                        C1 = c_C[1][b];
+                        nt1 = c_nt1[b];
+                        D1 = c_D1[b];
+                        P1t = c_P1[b];
                     } else {
                         const VtChunk& g = ch[b + 1];
-                        e = g.e;
-                        nt0 = g.nt[0];
-                        P0 = g.P[0];
-                        C0 = g.C[0];
-                        C1 = g.C[1];
+                        nt1 = g.nt[1];
+                        D1 = g.D1;
+                        P1t = g.P[1];
                     }
-                    if (!(nt0 <= kFastTies && e == es)) break;
-                    const int par = (int)(U & 1ll);
-                    const long long fin = U + P0 + (par ? C1 : C0);
-                    VtChunk& q = ch[b + 1];
-                    if (fin >= LIM) {
-                        if (q.nt[1] <= kFastTies) {
-                            s_U0 = U;
-                            s_par = par;
-                            mode = 2;
-                        }
-                        break;
+                    if (nt1 > kFastTies || P1t >= kCumCap) break;
+                    const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
+                    const int nl = (int)(cend - lo);
+                    const long long* __restrict__ Q = pr.Q[parf] + (lo - kCumHead);
+                    const long long need = LIM - Uf;  // the crossing: the first key with Q >= need
+                    // the 64-key segment holding it (Q is non-decreasing; the
+                    // chunk's last Q reaches need), then the key in it
+                    long long v1 = 0;
+                    if (64 * lane < nl) v1 = Q[64 * lane + 63 < nl ? 64 * lane + 63 : nl - 1];
+                    const unsigned long long m1 = __ballot(64 * lane < nl && v1 >= need);
+                    const int sg = m1 ? __builtin_ctzll(m1) : 0;
+                    const int pos = 64 * sg + lane;
+                    long long q2 = 0, p1 = 0;
+                    int w1 = 0;
+                    typename KO::K kx = 0;
+                    if (pos < nl) {
+                        q2 = Q[pos];
+                        p1 = pr.P1[lo - kCumHead + pos];
+                        w1 = pr.W1[lo - kCumHead + pos];
+                        kx = keys[lo + pos];
                     }
-                    q.S0 = (double)U * u;  // (the T value of the start sum, exactly)
-                    q.par = par;
-                    q.ok = 1;
-                    U = fin;
+                    const unsigned long long m2 = __ballot(pos < nl && q2 >= need);
+                    if (!m1 || !m2) break;  // (not reached: Q's last value reaches need)
+                    const int li = __builtin_ctzll(m2);
+                    const int jc = 64 * sg + li;
+                    const long long qin = __shfl(q2, li > 0 ? li - 1 : 0);
+                    const long long qseg = __shfl(v1, sg > 0 ? sg - 1 : 0);
+                    const long long qb = li > 0 ? qin : qseg;  // Q before the crossing (jc > 0)
+                    const T before = (T)((double)(Uf + (jc > 0 ? qb : 0ll)) * u);
+                    const T S1 = before + KO::val(__shfl(kx, li));  // the crossing step, in T
+                    if (!(S1 >= CumBits<T>::min_normal()) || CumBits<T>::binade(S1) != es + 1) break;
+                    // the rest of the chunk in binade e + 1: its ties from k0,
+                    // the first after jc (r0 its rounding, then the D_k rule)
+                    const long long U1 = CumBits<T>::units(S1);
+                    const long long P1jc = __shfl(p1, li);
+                    const int w = __shfl(w1, li);
+                    const int k0 = w & 0x1ff, dn = (w >> 9) & 1, dl = (w >> 10) & 1, Dl = w >> 11;
+                    const int Dk0 = k0 > 0 ? Dl + (dn ^ dl) : 0;
+                    const int r0 = (int)((U1 - P1jc) & 1ll) ^ dn;
+                    const long long ups = k0 < nt1 ? (long long)(r0 + D1 - Dk0) : 0ll;
+                    const long long fin1 = U1 + (P1t - P1jc) + ups;
+                    if (fin1 >= LIM) break;  // (a second crossing: the passes)
+                    if (lane == 0) {
+                        VtChunk& q = ch[b + 1];
+                        q.S0 = (double)Uf * u;
+                        q.par = parf;
+                        q.jc = jc;
+                        q.S1 = (double)S1;
+                        q.k0 = k0;
+                        q.r0 = r0;
+                        q.Dk0 = Dk0;
+                        q.ok = 2;
+                    }
+                    VT_MARK(3, b, jc);
+                    es += 1;
+                    u = ldexp(1.0, es - (P - 1));
+                    U = fin1;
+                    lo += kCumChunk;
+                    b += 1;
+                    if (lo >= c) break;
                 }
                 sr = (T)((double)U * u);
             }
-            s_run = sr;
-            VT_MARK(2, b, mode);
-            s_lo = lo;
-            s_b = b;
-            s_mode = mode;
-            s_cross = 0x7fffffff;
+            if (lane == 0) {
+                s_run = sr;
+                s_lo = lo;
+                s_b = b;
+                s_cross = 0x7fffffff;
+            }
+            VT_MARK(2, b, 0);
         }
         __syncthreads();
         s = s_run;
@@ -887,106 +1094,6 @@ __global__ __launch_bounds__(kCumThreads) void vt_cumsum_kernel(const typename K
         __syncthreads();  // (read before thread 0 rewrites them)
         if (lo >= c) break;
         const int64_t cend = lo + kCumChunk < c ? lo + kCumChunk : c;
-        if (s_mode == 2) {
-            // the first step whose units reach 2^P: every thread over its
-            // keys' stored prefix, with the ties' rounding for this start
-            const long long U0 = s_U0;
-            const int par = s_par;
-            const int nt0 = ch[b + 1].nt[0], nt1 = ch[b + 1].nt[1];
-            // this thread's 16 stored prefixes, all loads issued before any
-            // is used (a use-then-load loop made them 16 dependent round
-            // trips: 12-18 us per crossing chunk)
-            const int64_t jt = lo + (int64_t)t * kCumPer;
-            long long pv[kCumPer];
-            if (jt + kCumPer <= cend) {
-#pragma unroll
-                for (int i = 0; i < kCumPer; ++i) pv[i] = pr.P[0][jt + i - kCumHead];
-            } else {
-#pragma unroll
-                for (int i = 0; i < kCumPer; ++i) pv[i] = jt + i < cend ? pr.P[0][jt + i - kCumHead] : 0ll;
-            }
-            // the ties of binades e and e + 1 into LDS by the whole block (the
-            // serial resolution below then waits on no global load)
-            for (int k = t; k < nt0; k += kCumThreads) {
-                tie_idx[k] = pr.t_idx[0][b * kFastTies + k];
-                tie_c[k] = pr.t_c0[par][b * kFastTies + k];
-            }
-            for (int k = t; k < nt1; k += kCumThreads) {
-                t1_idx[k] = pr.t_idx[1][b * kFastTies + k];
-                t1_pb[k] = pr.t_pb[1][b * kFastTies + k];
-                t1_m[k] = pr.t_m[1][b * kFastTies + k];
-            }
-            __syncthreads();
-            int kt = 0;
-            {
-                int lo2 = 0, hi2 = nt0;  // first tie at a local index >= t * kCumPer
-                while (lo2 < hi2) {
-                    const int mid = (lo2 + hi2) >> 1;
-                    if (tie_idx[mid] < t * kCumPer) lo2 = mid + 1; else hi2 = mid;
-                }
-                kt = lo2;
-            }
-            int first = 0x7fffffff;
-#pragma unroll
-            for (int i = 0; i < kCumPer; ++i) {
-                const int li = t * kCumPer + i;
-                if (kt < nt0 && tie_idx[kt] == li) ++kt;
-                const long long C = kt > 0 ? (long long)tie_c[kt - 1] : 0ll;
-                if (jt + i < cend && first == 0x7fffffff && U0 + pv[i] + C >= LIM) first = li;
-            }
-            if (first != 0x7fffffff) atomicMin(&s_cross, first);
-            __syncthreads();
-            if (t == 0) {
-                VtChunk& q = ch[b + 1];
-                const int jc = s_cross;  // (exists: the chunk's last sum reaches 2^P)
-                const int e = q.e;
-                // (the three independent loads first, together)
-                const long long P0b = jc > 0 ? pr.P[0][lo + jc - 1 - kCumHead] : 0ll;
-                const T xc = KO::val(keys[lo + jc]);
-                const long long P1jc = pr.P[1][lo + jc - kCumHead];
-                const long long P1t = q.P[1];
-                T before = s;
-                if (jc > 0) {
-                    int n0 = 0;  // ties at local indices <= jc - 1
-                    while (n0 < nt0 && tie_idx[n0] <= jc - 1) ++n0;
-                    const long long C = n0 > 0 ? (long long)tie_c[n0 - 1] : 0ll;
-                    before = (T)((double)(U0 + P0b + C) * ldexp(1.0, e - (P - 1)));
-                }
-                const T S1 = before + xc;  // the crossing step, in T
-                int mode = 0;
-                if (S1 >= CumBits<T>::min_normal() && CumBits<T>::binade(S1) == e + 1) {
-                    // the rest of the chunk in binade e + 1: its ties in order
-                    const long long U1 = CumBits<T>::units(S1);
-                    int up = 0;
-                    for (int k = 0; k < nt1; ++k) {
-                        if (t1_idx[k] <= jc) continue;
-                        const long long bf = U1 + (t1_pb[k] - P1jc) + up;
-                        up += ((bf + t1_m[k]) & 1ll) ? 1 : 0;
-                        pr.t_c1[b * kFastTies + k] = up;
-                    }
-                    const long long fin = U1 + (P1t - P1jc) + up;
-                    if (fin < LIM) {
-                        q.S0 = (double)s;
-                        q.par = par;
-                        q.jc = jc;
-                        q.S1 = (double)S1;
-                        q.ok = 2;
-                        s_run = (T)((double)fin * ldexp(1.0, e + 1 - (P - 1)));
-                        mode = 3;
-                    }
-                }
-                s_mode = mode;
-            }
-            __syncthreads();
-            VT_MARK(3, b, s_mode);
-            if (s_mode == 3) {
-                s = s_run;
-                __syncthreads();
-                lo += kCumChunk;
-                ++b;
-                continue;
-            }
-        }
         int64_t p = lo;
         while (p < cend) {  // (uniform) passes over [p, cend)
             VT_MARK(4, b, p - lo);
@@ -1286,6 +1393,8 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     char* p = static_cast<char*>(scratch);
     int* hdr = reinterpret_cast<int*>(p);
     p += 256;
+    RsHead* rsh = reinterpret_cast<RsHead*>(p);  // (zeroed when the scratch is allocated: vartrim_scratch_head)
+    p += al256(sizeof(RsHead));
     K* keysA = reinterpret_cast<K*>(p);
     p += al256(sizeof(K) * n);
     K* keysB = reinterpret_cast<K*>(p);
@@ -1296,48 +1405,37 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     p += al256(8 * 256);
     int* part_i = reinterpret_cast<int*>(p);
     p += al256(8 * 256);
-    void* sort_temp = p;  // hipcub's radix sort scratch
-    const size_t sort_tb = vt_sort_temp_bytes<K>(n);
-    p += al256(sort_tb);
+    void* rs_state = p;  // the radix sort's look-back state (pmx_radix.h)
+    p += al256(rs_state_bytes(n));
     const int64_t nch = vt_chunks(n);
     VtChunk* ch = reinterpret_cast<VtChunk*>(p);
     p += al256(sizeof(VtChunk) * (nch + 1));
     VtPrep pr;
     for (int v = 0; v < 2; ++v) {
-        pr.P[v] = reinterpret_cast<long long*>(p);
+        pr.Q[v] = reinterpret_cast<long long*>(p);
         p += al256(8 * (size_t)n);
     }
-    {
-        const size_t F = (size_t)kFastTies * (size_t)nch;
-        long long* ll = reinterpret_cast<long long*>(p);
-        pr.t_m[0] = ll;
-        pr.t_m[1] = ll + F;
-        pr.t_pb[0] = ll + 2 * F;
-        pr.t_pb[1] = ll + 3 * F;
-        int* ii = reinterpret_cast<int*>(ll + 4 * F);
-        pr.t_idx[0] = ii;
-        pr.t_idx[1] = ii + F;
-        pr.t_c0[0] = ii + 2 * F;
-        pr.t_c0[1] = ii + 3 * F;
-        pr.t_c1 = ii + 4 * F;
-        p += al256(F * (4 * sizeof(long long) + 5 * sizeof(int)));
-    }
+    pr.P1 = reinterpret_cast<long long*>(p);
+    p += al256(8 * (size_t)n);
+    pr.W1 = reinterpret_cast<int*>(p);
+    p += al256(4 * (size_t)n);
 
     hipLaunchKernelGGL(vt_hdr_reset_kernel, dim3(1), dim3(64), 0, s, hdr, ctl);
     K* src = keysB;  // (the sorted keys: the kept ones first)
     if (n > 0) {
         hipLaunchKernelGGL(vt_keys_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl);
-        size_t tb = sort_tb;
-        (void)pmx_sort_keys(sort_temp, tb, keysA, keysB, (int)n, 0, KeyOf<T>::bits, s);
+        src = launch_radix_sort_keys<K>(keysA, keysB, n, 0, KeyOf<T>::bits, rsh, rs_state, ctl, s);
     }
+    // the head's running sum (written by the preparation launch's extra block)
+    T* head = reinterpret_cast<T*>(hdr + 8);
     if (nch > 0) {
         hipLaunchKernelGGL(vt_chunk_sum_kernel<T>, dim3((unsigned)(nch + 1)), dim3(kCumThreads), 0, s, src, hdr, ch, ctl);
-        hipLaunchKernelGGL(vt_chunk_prep_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
-                           ctl);
+        hipLaunchKernelGGL(vt_chunk_prep_kernel<T>, dim3((unsigned)(nch + 1)), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
+                           ctl, cum, head);
     }
     unsigned long long* trace = g_vt_trace ? reinterpret_cast<unsigned long long*>(p) : nullptr;
     hipLaunchKernelGGL(vt_cumsum_kernel<T>, dim3(1), dim3(kCumThreads), 0, s, src, hdr, cum, ch, pr, (int)nch, ctl,
-                       trace);
+                       trace, nch > 0 ? (const T*)head : (const T*)nullptr);
     if (nch > 0)
         hipLaunchKernelGGL(vt_chunk_write_kernel<T>, dim3((unsigned)nch), dim3(kCumThreads), 0, s, src, hdr, ch, pr,
                            cum, ctl);

@@ -254,8 +254,26 @@ def _subnormal_clouds(n_side, dtype, rng):
     return ref, rd
 
 
+def _spread_clouds(n_side, dtype, rng, jump):
+    """Twin points on a unit grid, the reading moved by offsets whose size
+    spans decades (jump=False: log-uniform over 1e-4..1e-1, the running sum
+    crosses a binade every few chunks) or jumps (jump=True: 90 % at 1e-4, the
+    rest at 0.3 — past the jump every key is ~40x the running sum, so the
+    chunks' integer prefixes under the guessed binade saturate)."""
+    g = np.stack(np.meshgrid(*[np.arange(n_side)] * 3, indexing="ij"), -1).reshape(-1, 3).astype(np.float64)
+    v = rng.normal(size=g.shape)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    if jump:
+        mag = np.where(rng.random(len(g)) < 0.9, 1e-4, 0.3)
+    else:
+        mag = 10.0 ** rng.uniform(-4, -1, size=len(g))
+    ref = np.hstack([g, np.ones((len(g), 1))]).astype(dtype)
+    rd = np.hstack([g + v * mag[:, None], np.ones((len(g), 1))]).astype(dtype)
+    return ref, rd
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-@pytest.mark.parametrize("data", ["surface", "surface1m", "dyadic", "subnormal"])
+@pytest.mark.parametrize("data", ["surface", "surface1m", "dyadic", "subnormal", "decades", "jump"])
 def test_vartrimmed_parallel_partial_sum(oracle, dtype, data):
     """VarTrimmed's std::partial_sum in T runs as a binade-segmented integer
     scan over chunks (pmx_select.hip vt_chunk_prep / vt_cumsum /
@@ -271,6 +289,8 @@ def test_vartrimmed_parallel_partial_sum(oracle, dtype, data):
         rd = reading_cloud(size, dtype)
     elif data == "subnormal":
         ref, rd = _subnormal_clouds(58, dtype, rng)
+    elif data in ("decades", "jump"):
+        ref, rd = _spread_clouds(64, dtype, rng, data == "jump")
     else:
         ref, rd = _grid_clouds(48, dtype, rng)
     filters = [("VarTrimmedDistOutlierFilter", {"minRatio": 0.05, "maxRatio": 0.99, "lambda": 2.35})]
