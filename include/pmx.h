@@ -146,6 +146,14 @@ int pmx_set_reference(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const
  * needs no centred host copy of the reference. */
 int pmx_set_reference_centred(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const void* normals,
                               const void* offset);
+/* pmx_set_reference_centred by the cloud's own mean: the mean in T, each
+ * coordinate summed sequentially in point order and divided by M
+ * (ICP.cpp:291-292), is computed on a host thread while the cloud and its
+ * normals upload, written to mean_out (rows - 1 T values) and subtracted on
+ * the device.  Replaces ICP::compute's host mean + centring (ICP.cpp:291-299)
+ * followed by Matcher::init (:302). */
+int pmx_set_reference_mean_centred(pmx_ctx* ctx, const void* feat, int rows, int64_t M, const void* normals,
+                                   void* mean_out);
 /* reading shard: rows x N.  T0 (rows x rows, row-major T) is applied once on
  * the device (T_refMean_dataIn, ICP.cpp:345-347). */
 int pmx_set_reading(pmx_ctx* ctx, const void* feat, int rows, int64_t N, const void* T0);

@@ -149,7 +149,7 @@ _lib = None
 
 EXPORTS = [
     "pmx_ctx_create", "pmx_ctx_destroy", "pmx_last_error", "pmx_device_count", "pmx_version",
-    "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_comm_stats", "pmx_comm_loop_stats", "pmx_set_reference", "pmx_set_reference_centred", "pmx_set_reading", "pmx_set_search", "pmx_match",
+    "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_comm_stats", "pmx_comm_loop_stats", "pmx_set_reference", "pmx_set_reference_centred", "pmx_set_reference_mean_centred", "pmx_set_reading", "pmx_set_search", "pmx_match",
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed", "pmx_outlier_robust",
     "pmx_robust_scale", "pmx_set_reading_radii",
@@ -179,6 +179,8 @@ def lib():
         l.pmx_comm_loop_stats.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 3
         l.pmx_set_reference.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
         l.pmx_set_reference_centred.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p]
+        l.pmx_set_reference_mean_centred.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p,
+                                                     C.c_void_p]
         l.pmx_set_reading.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_void_p]
         l.pmx_set_search.argtypes = [C.c_void_p, C.c_int]
         l.pmx_match.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double,

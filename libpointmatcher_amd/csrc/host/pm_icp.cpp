@@ -102,7 +102,7 @@ using PM = PointMatcher<T>;
 // Matcher::init of both kd-tree matchers: the reference (and its normals,
 // for the point-to-plane minimiser) to HBM, the search structure built there
 template <typename T>
-void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType, const T* centre) {
+void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType, const T* centre, T* mean_out) {
     dev.ensure();
     std::vector<T> nrm;
     const T* np = nullptr;
@@ -122,7 +122,9 @@ void matcher_init(Device& dev, const DataPoints<T>& ref, int searchType, const T
         np = nrm.data();
     }
     dev.check(pmx_set_search(dev.ctx, searchType));  // 0: brute force, 1/2: exact grid search
-    if (centre)
+    if (mean_out)
+        dev.check(pmx_set_reference_mean_centred(dev.ctx, ref.feat(), ref.rows, ref.n, np, mean_out));
+    else if (centre)
         dev.check(pmx_set_reference_centred(dev.ctx, ref.feat(), ref.rows, ref.n, np, centre));
     else
         dev.check(pmx_set_reference(dev.ctx, ref.feat(), ref.rows, ref.n, np));
@@ -162,8 +164,8 @@ struct KDTreeMatcherGPU : PM<T>::Matcher {
           searchType(this->template get<int>("searchType")),
           maxDist(this->template get<T>("maxDist")) {}
 
-    void init(Device& dev, const DataPoints<T>& ref, const T* centre) override {
-        matcher_init<T>(dev, ref, searchType, centre);
+    void init(Device& dev, const DataPoints<T>& ref, const T* centre, T* mean_out) override {
+        matcher_init<T>(dev, ref, searchType, centre, mean_out);
     }
     Matches findClosests(Device& dev, const std::vector<T>& T_iter) override {
         // PointCountTouched is added from the minimiser's pmx_stats.visited
@@ -204,8 +206,8 @@ struct KDTreeVarDistMatcherGPU : PM<T>::Matcher {
           epsilon(this->template get<T>("epsilon")),
           searchType(this->template get<int>("searchType")),
           maxDistField(this->template get<std::string>("maxDistField")) {}
-    void init(Device& dev, const DataPoints<T>& ref, const T* centre) override {
-        matcher_init<T>(dev, ref, searchType, centre);
+    void init(Device& dev, const DataPoints<T>& ref, const T* centre, T* mean_out) override {
+        matcher_init<T>(dev, ref, searchType, centre, mean_out);
     }
     void initReading(Device& dev, const DataPoints<T>& reading) override {
         // getDescriptorViewByName(maxDistField).transpose(): one radius per point
@@ -1368,31 +1370,16 @@ void PointMatcher<T>::ICP::prepare(const DataPoints& readingIn, const DataPoints
     const DataPoints& reference = filtered ? refCopy : referenceIn;
     const int64_t M = reference.n;
     if (M <= 0) throw ConvergenceError("empty reference");
-    // mean of the reference columns in T, ICP.cpp:291-292: each coordinate's
-    // sum sequential in point order (the three sums in one pass)
+    // mean of the reference columns in T, ICP.cpp:291-292 (each coordinate's
+    // sum sequential in point order), computed by the matcher's init on a
+    // host thread while the cloud uploads (pmx_set_reference_mean_centred)
     T_refIn_refMean_.assign((size_t)dim * dim, (T)0);
     for (int i = 0; i < dim; ++i) T_refIn_refMean_[i * dim + i] = 1;
-    T sum[3] = {0, 0, 0}, mean[3] = {0, 0, 0};
-    const T* f = reference.feat();
-    if (dim == 4) {
-        for (int64_t j = 0; j < M; ++j) {
-            sum[0] = sum[0] + f[j * 4];
-            sum[1] = sum[1] + f[j * 4 + 1];
-            sum[2] = sum[2] + f[j * 4 + 2];
-        }
-    } else {
-        for (int64_t j = 0; j < M; ++j) {
-            sum[0] = sum[0] + f[j * 3];
-            sum[1] = sum[1] + f[j * 3 + 1];
-        }
-    }
-    for (int r = 0; r < dim - 1; ++r) {
-        mean[r] = sum[r] / (T)M;
-        T_refIn_refMean_[r * dim + dim - 1] = mean[r];
-    }
+    T mean[3] = {0, 0, 0};
     dev.ensure();
-    mapIndexed_ = false;                  // (an ICPSequence map is no longer the device's reference, even if init throws)
-    matcher->init(dev, reference, mean);  // ICP.cpp:302 (features - mean, ICP.cpp:299, on the device)
+    mapIndexed_ = false;  // (an ICPSequence map is no longer the device's reference, even if init throws)
+    matcher->init(dev, reference, nullptr, mean);  // ICP.cpp:302 (features - mean, ICP.cpp:299, on the device)
+    for (int r = 0; r < dim - 1; ++r) T_refIn_refMean_[r * dim + dim - 1] = mean[r];
     referencePreprocessingDuration = since<T>(t);
     prefilteredReferencePtsCount = M;
     prepareReading(readingIn, T_init);

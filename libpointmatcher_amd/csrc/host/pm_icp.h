@@ -71,8 +71,12 @@ struct PointMatcher {
         void resetVisitCount() { visitCounter = 0; }
         uint64_t getVisitCount() const { return visitCounter; }
         // centre (may be null): rows - 1 values the matcher subtracts per axis
-        // in T (ICP.cpp:299's centring done with the upload, on the device)
-        virtual void init(Device& dev, const DataPoints& filteredReference, const T* centre = nullptr) = 0;
+        // in T (ICP.cpp:299's centring done with the upload, on the device);
+        // mean_out (may be null, then centre is ignored): the matcher
+        // computes the reference mean itself (ICP.cpp:291-292, on a host
+        // thread while the cloud uploads), centres by it and writes it here
+        virtual void init(Device& dev, const DataPoints& filteredReference, const T* centre = nullptr,
+                          T* mean_out = nullptr) = 0;
         // the reading's inputs of the match, once per compute after the
         // reading upload (KDTreeVarDistMatcher: its per-point radii)
         virtual void initReading(Device&, const DataPoints&) {}

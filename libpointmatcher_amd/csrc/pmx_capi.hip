@@ -253,6 +253,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
                     c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace, c->d_diag, c->d_cand, c->d_ticket,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
                     c->d_rob, c->d_rdev, c->d_radii, c->d_rd_p4, c->d_rd_sorted};
+    side_finish(c);  // (the side stream may still be building levels)
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& L : c->levels) L.release();
@@ -271,6 +272,14 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->h_flags) (void)hipHostFree(c->h_flags);
     if (c->d_specx) (void)hipFree(c->d_specx);
+    if (c->side_ev) (void)hipEventDestroy(c->side_ev);
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
+    if (c->d_raw2) (void)hipFree(c->d_raw2);
+    for (hipEvent_t e : {c->table_ev, c->raw_ev, c->copy_ev, c->nrm_ev})
+        if (e) (void)hipEventDestroy(e);
+    if (c->copy) (void)hipStreamDestroy(c->copy);
+    if (c->h_table) (void)hipHostFree(c->h_table);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PMX_OK;

@@ -8,6 +8,10 @@
 // solve (PointToPlane.cpp:108-161).
 #include "pmx_ctx.h"
 
+#include <chrono>
+#include <functional>
+#include <thread>
+
 namespace pmxc {
 
 // -------------------------------------------------------------------- grid --
@@ -22,6 +26,8 @@ constexpr int64_t kMaxCells = (int64_t)1 << 26;
 int cold_level(const pmx_ctx* c);
 template <typename T>
 int build_levels(pmx_ctx* c, int upto);
+template <typename T>
+int build_levels_cold(pmx_ctx* c, int cold);
 
 SetupShape grid_shape(const double lo[3], const double ext[3], double h) {
     SetupShape s;
@@ -35,32 +41,35 @@ SetupShape grid_shape(const double lo[3], const double ext[3], double h) {
     return s;
 }
 
-// setup scratch for n points and grids of up to max_cells cells
-int setup_room(pmx_ctx* c, int64_t n, int64_t max_cells) {
+// setup scratch for n points and grids of up to max_cells cells (the
+// context's, or the side stream's)
+int setup_room(pmx_ctx* c, int64_t n, int64_t max_cells, bool side = false) {
     n = std::max<int64_t>(n, 1);
-    SetupScratch& sc = c->setup;
-    if (c->setup_n < n) {
+    SetupScratch& sc = side ? c->setup_side : c->setup;
+    int64_t& setup_n = side ? c->setup_side_n : c->setup_n;
+    int64_t& setup_cells = side ? c->setup_side_cells : c->setup_cells;
+    if (setup_n < n) {
         for (void* p : {(void*)sc.keys64, (void*)sc.keys64_out, (void*)sc.idx, (void*)sc.idx_out})
             if (p) (void)hipFree(p);
         sc.keys64 = sc.keys64_out = nullptr;
         sc.idx = sc.idx_out = nullptr;
-        c->setup_n = 0;
+        setup_n = 0;
         HIPCHK(c, hipMalloc((void**)&sc.keys64, sizeof(unsigned long long) * n));
         HIPCHK(c, hipMalloc((void**)&sc.keys64_out, sizeof(unsigned long long) * n));
         HIPCHK(c, hipMalloc((void**)&sc.idx, sizeof(int32_t) * n));
         HIPCHK(c, hipMalloc((void**)&sc.idx_out, sizeof(int32_t) * n));
         sc.keys32 = (uint32_t*)sc.keys64;
         sc.keys32_out = (uint32_t*)sc.keys64_out;
-        c->setup_n = n;
+        setup_n = n;
     }
-    if (c->setup_cells < max_cells) {
+    if (setup_cells < max_cells) {
         if (sc.counts) (void)hipFree(sc.counts);
         sc.counts = nullptr;
-        c->setup_cells = 0;
+        setup_cells = 0;
         HIPCHK(c, hipMalloc((void**)&sc.counts, sizeof(uint32_t) * (size_t)(max_cells + 1)));
-        c->setup_cells = max_cells;
+        setup_cells = max_cells;
     }
-    const size_t tb = setup_temp_bytes(c->setup_n, c->setup_cells);
+    const size_t tb = setup_temp_bytes(setup_n, setup_cells);
     if (sc.temp_bytes < tb) {
         if (sc.temp) (void)hipFree(sc.temp);
         sc.temp = nullptr;
@@ -72,13 +81,45 @@ int setup_room(pmx_ctx* c, int64_t n, int64_t max_cells) {
 }
 
 void setup_release(pmx_ctx* c) {
-    SetupScratch& sc = c->setup;
-    for (void* p : {(void*)sc.keys64, (void*)sc.keys64_out, (void*)sc.idx, (void*)sc.idx_out, (void*)sc.counts,
-                    sc.temp})
-        if (p) (void)hipFree(p);
+    side_finish(c);
+    for (SetupScratch* sc : {&c->setup, &c->setup_side})
+        for (void* p : {(void*)sc->keys64, (void*)sc->keys64_out, (void*)sc->idx, (void*)sc->idx_out,
+                        (void*)sc->counts, sc->temp})
+            if (p) (void)hipFree(p);
     c->setup = SetupScratch{};
+    c->setup_side = SetupScratch{};
     c->setup_n = c->setup_cells = 0;
+    c->setup_side_n = c->setup_side_cells = 0;
 }
+
+// the side stream's level builds, ordered before everything enqueued next on
+// the context stream (a device-side wait: no host synchronisation)
+void side_join(pmx_ctx* c) {
+    if (!c->side_pending) return;
+    (void)hipStreamWaitEvent(c->stream, c->side_ev, 0);
+    c->side_pending = false;
+}
+// ... and finished on the host (before the level buffers are freed or reused)
+void side_finish(pmx_ctx* c) {
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    c->side_pending = false;
+}
+
+// Setup timeline (development trace, PMX_SETUP_TRACE=1): each mark waits for
+// the stream and prints the wall time since the previous mark to stderr.
+struct SetupTrace {
+    pmx_ctx* c;
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    explicit SetupTrace(pmx_ctx* cc) : c(cc), on(std::getenv("PMX_SETUP_TRACE") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(c->stream);
+        const auto n = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "setup_trace %-22s %8.3f ms\n", what, std::chrono::duration<double>(n - t).count() * 1e3);
+        t = n;
+    }
+};
 
 // host staging of one upload (the caller's cloud, pageable) into the raw buffer
 int upload_raw(pmx_ctx* c, const void* src, size_t bytes) {
@@ -88,13 +129,40 @@ int upload_raw(pmx_ctx* c, const void* src, size_t bytes) {
     return PMX_OK;
 }
 
+// upload_raw on the copy stream: after the last pack that read d_raw, but
+// not after the rest of the context stream (the level builds), which then
+// waits for the copy on the device
+int copy_stream(pmx_ctx* c) {
+    if (!c->copy) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->raw_ev, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->nrm_ev, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->raw_ev, c->stream));
+        HIPCHK(c, hipEventRecord(c->nrm_ev, c->stream));
+    }
+    return PMX_OK;
+}
+
+int upload_raw_async(pmx_ctx* c, const void* src, size_t bytes) {
+    if (int r = copy_stream(c)) return r;
+    // (ensure may free and reallocate d_raw: hipFree waits for the device)
+    int rc = ensure(c, &c->d_raw, &c->raw_bytes, std::max<size_t>(bytes, 16));
+    if (rc) return rc;
+    if (bytes) {
+        HIPCHK(c, hipStreamWaitEvent(c->copy, c->raw_ev, 0));
+        HIPCHK(c, hipMemcpyAsync(c->d_raw, src, bytes, hipMemcpyHostToDevice, c->copy));
+        HIPCHK(c, hipEventRecord(c->copy_ev, c->copy));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->copy_ev, 0));
+    }
+    return PMX_OK;
+}
+
 // the grid levels over the resident reference d_ref (M points) and d_nrm
 template <typename T>
-int build_grid(pmx_ctx* c, int64_t M) {
+int build_grid(pmx_ctx* c, int64_t M, const std::function<int()>& before_levels = {}) {
+    side_finish(c);  // (a previous reference's side builds write level buffers kept below)
     const P4<T>* pts = (const P4<T>*)c->d_ref;
-    // (d_nrm is kept across references: a reference without normals must not
-    // gather the previous reference's, which may also be shorter than M)
-    const P4<T>* nrm = c->has_normals ? (const P4<T>*)c->d_nrm : nullptr;
     // bounding box of the finite points (inf / NaN points can never be a neighbour)
     double* sb = nullptr;  // bbox partials, then 8 doubles of result
     size_t sbc = 0;
@@ -188,7 +256,9 @@ int build_grid(pmx_ctx* c, int64_t M) {
         L.ppc = c->level_ppc[l];
         c->levels.push_back(L);
     }
-    return build_levels<T>(c, c->adaptive ? cold_level(c) : 0);
+    SetupTrace(c).mark("bbox+sizing (from pack)");
+    if (before_levels && (rc = before_levels())) return rc;
+    return build_levels_cold<T>(c, c->adaptive ? cold_level(c) : 0);
 }
 
 // the level a new reading's first match runs on: the ppc nearest first_ppc
@@ -201,12 +271,10 @@ int cold_level(const pmx_ctx* c) {
     return best;
 }
 
-// build levels [levels_built, upto] of the current reference (stream order:
-// after whatever was enqueued before) and publish the device level table
+// one level of the current reference: buffers, the build enqueued on `st`
+// with scratch `sc`, the host's copy of its geometry
 template <typename T>
-int build_levels(pmx_ctx* c, int upto) {
-    upto = std::min(upto, (int)c->levels.size() - 1);
-    if (upto < c->levels_built) return PMX_OK;
+int build_one_level(pmx_ctx* c, int l, const SetupScratch& sc, hipStream_t st) {
     const P4<T>* pts = (const P4<T>*)c->d_ref;
     const P4<T>* nrm = c->has_normals ? (const P4<T>*)c->d_nrm : nullptr;
     const int64_t M = c->M, valid = c->grid_valid;
@@ -220,37 +288,45 @@ int build_levels(pmx_ctx* c, int upto) {
         *cap = bytes;
         return true;
     };
-    for (int l = c->levels_built; l <= upto; ++l) {
-        const SetupShape& s = c->level_shapes[(size_t)l];
-        GridLevel& L = c->levels[(size_t)l];
-        if (!nrm && L.gpn) {  // (no normals: no interleaved records, so nothing stale can be gathered)
-            (void)hipFree(L.gpn);
-            L.gpn = nullptr;
-            L.cap_gpn = 0;
-        }
-        if (!room(&L.gpts, &L.cap_pts, sizeof(P4<T>) * np) || !room((void**)&L.gidx, &L.cap_idx, sizeof(int32_t) * np) ||
-            !room((void**)&L.gstart, &L.cap_start, sizeof(uint32_t) * (size_t)(s.cells + 1)) ||
-            (nrm && !room(&L.gpn, &L.cap_gpn, 2 * sizeof(P4<T>) * np))) {
-            c->grid_ready = false;
-            return fail(c, PMX_E_HIP, "grid level allocation failed");
-        }
-        const int r = build_level_device<T>(pts, M, nrm, s, valid, c->setup, (P4<T>*)L.gpts, (P4<T>*)L.gpn, L.gidx,
-                                            L.gstart, c->stream);
-        if (r) {
-            c->grid_ready = false;
-            return fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")");
-        }
-        for (int a = 0; a < 3; ++a) {
-            L.lo[a] = s.lo[a];
-            L.dim[a] = s.g[a];
-        }
-        L.h = s.h;
-        c->levels_built = l + 1;
+    const SetupShape& s = c->level_shapes[(size_t)l];
+    GridLevel& L = c->levels[(size_t)l];
+    if (!nrm && L.gpn) {  // (no normals: no interleaved records, so nothing stale can be gathered)
+        (void)hipFree(L.gpn);
+        L.gpn = nullptr;
+        L.cap_gpn = 0;
     }
-    // the device table of the built levels (the device loop picks the level
-    // on the GPU, among the built ones)
-    std::vector<GridDesc<T>> tab((size_t)c->levels_built);
-    for (size_t l = 0; l < tab.size(); ++l) {
+    if (!room(&L.gpts, &L.cap_pts, sizeof(P4<T>) * np) || !room((void**)&L.gidx, &L.cap_idx, sizeof(int32_t) * np) ||
+        !room((void**)&L.gstart, &L.cap_start, sizeof(uint32_t) * (size_t)(s.cells + 1)) ||
+        (nrm && !room(&L.gpn, &L.cap_gpn, 2 * sizeof(P4<T>) * np))) {
+        c->grid_ready = false;
+        return fail(c, PMX_E_HIP, "grid level allocation failed");
+    }
+    const int r = build_level_device<T>(pts, M, nrm, s, valid, sc, (P4<T>*)L.gpts, (P4<T>*)L.gpn, L.gidx, L.gstart, st);
+    if (r) {
+        c->grid_ready = false;
+        return fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")");
+    }
+    for (int a = 0; a < 3; ++a) {
+        L.lo[a] = s.lo[a];
+        L.dim[a] = s.g[a];
+    }
+    L.h = s.h;
+    return PMX_OK;
+}
+
+// the device table of levels [0, levels_built) (the device loop picks the
+// level on the GPU, among the built ones)
+template <typename T>
+int publish_levels(pmx_ctx* c) {
+    if (c->levels_built > kMaxLevels) return fail(c, PMX_E_BAD_PARAM, "at most 8 grid levels");
+    if (!c->h_table) {
+        HIPCHK(c, hipHostMalloc(&c->h_table, sizeof(GridDesc<double>) * kMaxLevels, hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->table_ev, hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->table_ev, c->stream));
+    }
+    HIPCHK(c, hipEventSynchronize(c->table_ev));  // (the previous table's copy has read the staging)
+    GridDesc<T>* tab = (GridDesc<T>*)c->h_table;
+    for (size_t l = 0; l < (size_t)c->levels_built; ++l) {
         const GridLevel& L = c->levels[l];
         GridDesc<T>& D = tab[l];
         D.gpts = (const P4<T>*)L.gpts;
@@ -265,12 +341,63 @@ int build_levels(pmx_ctx* c, int upto) {
         D.G.inv_h = 1.0 / L.h;
     }
     if (!c->d_gdesc) HIPCHK(c, hipMalloc(&c->d_gdesc, sizeof(GridDesc<T>) * kMaxLevels));
-    if (tab.size() > (size_t)kMaxLevels) return fail(c, PMX_E_BAD_PARAM, "at most 8 grid levels");
-    HIPCHK(c, hipMemcpyAsync(c->d_gdesc, tab.data(), sizeof(GridDesc<T>) * tab.size(), hipMemcpyHostToDevice,
+    // (stream-ordered and asynchronous: the host goes on — the reading's
+    // upload overlaps the level builds still running)
+    HIPCHK(c, hipMemcpyAsync(c->d_gdesc, tab, sizeof(GridDesc<T>) * (size_t)c->levels_built, hipMemcpyHostToDevice,
                              c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventRecord(c->table_ev, c->stream));
     c->grid_ready = true;
     return PMX_OK;
+}
+
+// build levels [levels_built, upto] of the current reference (stream order:
+// after whatever was enqueued before) and publish the device level table
+template <typename T>
+int build_levels(pmx_ctx* c, int upto) {
+    upto = std::min(upto, (int)c->levels.size() - 1);
+    if (upto < c->levels_built) return PMX_OK;
+    SetupTrace tr(c);
+    for (int l = c->levels_built; l <= upto; ++l) {
+        int rc = build_one_level<T>(c, l, c->setup, c->stream);
+        if (rc) return rc;
+        c->levels_built = l + 1;
+        tr.mark(l == 0 ? "level 0" : l == 1 ? "level 1" : l == 2 ? "level 2" : l == 3 ? "level 3" : "level 4+");
+    }
+    return publish_levels<T>(c);
+}
+
+// Matcher::init's levels: the cold one (a new reading's first match) on the
+// context stream; the finer ones, which the matches after it move to, on the
+// side stream with their own scratch, overlapping the reading's setup and the
+// cold match (every match after a reading's first waits for them on the
+// device, side_join).  PMX_SIDE_LEVELS=0: all on the context stream.
+template <typename T>
+int build_levels_cold(pmx_ctx* c, int cold) {
+    static const bool side_env = [] {
+        const char* e = std::getenv("PMX_SIDE_LEVELS");
+        return !e || std::atoi(e) != 0;
+    }();
+    cold = std::min(cold, (int)c->levels.size() - 1);
+    if (cold <= 0 || !side_env || c->levels_built > 0) return build_levels<T>(c, cold);
+    if (!c->side) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming));
+    }
+    int64_t cells = 1;
+    for (int l = 0; l < cold; ++l) cells = std::max(cells, c->level_shapes[(size_t)l].cells);
+    int rc = setup_room(c, c->M, cells, true);
+    if (rc) return rc;
+    // (the reference's pack and the sizing counts completed: build_grid read
+    // them back, so the side stream needs no event to start)
+    for (int l = 0; l < cold; ++l)
+        if ((rc = build_one_level<T>(c, l, c->setup_side, c->side))) return rc;
+    HIPCHK(c, hipEventRecord(c->side_ev, c->side));
+    c->side_pending = true;
+    SetupTrace tr(c);
+    if ((rc = build_one_level<T>(c, cold, c->setup, c->stream))) return rc;
+    tr.mark("cold level");
+    c->levels_built = cold + 1;
+    return publish_levels<T>(c);
 }
 
 // Slot order of the reading: Morton order of the cell of the initially
@@ -322,8 +449,29 @@ int host_order(pmx_ctx* c) {
 }
 
 // ------------------------------------------------------------------ clouds --
+// the reference mean in T, ICP.cpp:291-292: each coordinate's sum sequential
+// in point order (the sums in one pass), divided by M
 template <typename T>
-int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals, const T* offset) {
+void reference_mean(const T* f, int rows, int64_t M, T* mean) {
+    T sum[3] = {0, 0, 0};
+    if (rows == 4) {
+        for (int64_t j = 0; j < M; ++j) {
+            sum[0] = sum[0] + f[j * 4];
+            sum[1] = sum[1] + f[j * 4 + 1];
+            sum[2] = sum[2] + f[j * 4 + 2];
+        }
+    } else {
+        for (int64_t j = 0; j < M; ++j) {
+            sum[0] = sum[0] + f[j * 3];
+            sum[1] = sum[1] + f[j * 3 + 1];
+        }
+    }
+    for (int r = 0; r < rows - 1; ++r) mean[r] = sum[r] / (T)M;
+}
+
+template <typename T>
+int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals, const T* offset,
+                       T* mean_out) {
     if (rows != 3 && rows != 4) return fail(c, PMX_E_BAD_PARAM, "reference must have 3 (2-D) or 4 (3-D) rows");
     if (M <= 0) return fail(c, PMX_E_BAD_PARAM, "empty reference");
     if (M > (int64_t)0x7fffffff - kTile) return fail(c, PMX_E_BAD_PARAM, "reference larger than int32 ids");
@@ -333,17 +481,64 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     const int D = rows - 1;
     const int64_t M_pad = ((M + kTile - 1) / kTile) * kTile;
     int rc;
+    SetupTrace tr(c);
+    // mean_out: the mean on a host thread while the normals, then the points
+    // upload (a sequential sum, ~0.4 ms per 1M points: it hides behind the
+    // ~0.5 ms of PCIe copies instead of preceding them)
+    std::thread mean_thread;
+    if (mean_out) {
+        mean_thread = std::thread([=] { reference_mean<T>(feat, rows, M, mean_out); });
+        offset = mean_out;
+    }
+    struct Join {
+        std::thread& t;
+        ~Join() {
+            if (t.joinable()) t.join();
+        }
+    } join{mean_thread};
+    // The normals cross PCIe on the copy stream, uploaded by a host thread
+    // (a pageable copy blocks its caller) while this one uploads the points,
+    // packs them and sizes the grid; they are packed just before the level
+    // builds, which interleave them (before_levels).
+    c->has_normals = normals != nullptr;
+    std::thread nrm_thread;
+    int nrm_rc = PMX_OK;
+    const size_t nrm_bytes = sizeof(T) * (size_t)D * M;
+    if (normals) {
+        if ((rc = ensure(c, &c->d_nrm, &c->nrm_bytes, sizeof(P4<T>) * M))) return rc;
+        if ((rc = ensure(c, &c->d_raw2, &c->raw2_bytes, std::max<size_t>(nrm_bytes, 16)))) return rc;
+        if ((rc = copy_stream(c))) return rc;
+        // (after the previous normals' pack, which read d_raw2)
+        HIPCHK(c, hipStreamWaitEvent(c->copy, c->nrm_ev, 0));
+        nrm_thread = std::thread([c, normals, nrm_bytes, &nrm_rc] {
+            (void)hipSetDevice(c->device);
+            hipError_t e = hipMemcpyAsync(c->d_raw2, normals, nrm_bytes, hipMemcpyHostToDevice, c->copy);
+            if (e == hipSuccess) e = hipEventRecord(c->nrm_ev, c->copy);
+            if (e != hipSuccess) nrm_rc = PMX_E_HIP;
+        });
+    }
+    struct JoinN {
+        std::thread& t;
+        ~JoinN() {
+            if (t.joinable()) t.join();
+        }
+    } join_n{nrm_thread};
     // (buffers kept across references; the stream orders a previous user's reads first)
     if ((rc = ensure(c, &c->d_ref, &c->ref_bytes, sizeof(P4<T>) * M_pad))) return rc;
     if ((rc = upload_raw(c, feat, sizeof(T) * (size_t)rows * M))) return rc;
+    if (mean_thread.joinable()) mean_thread.join();  // (the pack reads the offset on the host)
     launch_pack_p4<T>((const T*)c->d_raw, rows, M, M_pad, (P4<T>*)c->d_ref, c->stream, offset);
-    c->has_normals = normals != nullptr;
-    if (normals) {
-        if ((rc = ensure(c, &c->d_nrm, &c->nrm_bytes, sizeof(P4<T>) * M))) return rc;
-        // (the raw buffer is reused: the copy is ordered after the pack on the stream)
-        if ((rc = upload_raw(c, normals, sizeof(T) * (size_t)D * M))) return rc;
-        launch_pack_nrm<T>((const T*)c->d_raw, D, M, (P4<T>*)c->d_nrm, c->stream);
-    }
+    tr.mark("reference upload+pack");
+    auto pack_normals = [&]() -> int {
+        if (!normals) return PMX_OK;
+        nrm_thread.join();
+        if (nrm_rc) return fail(c, PMX_E_HIP, "normals upload failed");
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->nrm_ev, 0));
+        launch_pack_nrm<T>((const T*)c->d_raw2, D, M, (P4<T>*)c->d_nrm, c->stream);
+        HIPCHK(c, hipEventRecord(c->nrm_ev, c->stream));  // (d_raw2 free again after this pack)
+        tr.mark("normals upload+pack");
+        return PMX_OK;
+    };
     HIPCHK(c, hipGetLastError());
     c->rows = rows;
     c->dim = D;
@@ -353,7 +548,7 @@ int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* 
     c->grid_ready = false;
     // a resident reading keeps its slot order (any permutation is correct;
     // it was only chosen for the previous grid's locality)
-    return build_grid<T>(c, M);
+    return build_grid<T>(c, M, pack_normals);
 }
 
 template <typename T>
@@ -365,14 +560,16 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     const Mat4<T> M0 = embed<T>(T0, rows);
     int rc;
     const int64_t n1 = std::max<int64_t>(N, 1);
+    SetupTrace tr(c);
     c->has_radii = false;  // (a new reading: its radii, if any, follow)
     // raw P4 reading (pack), then the slot order, then T_refMean_dataIn
     // (scratch and the resident reading kept across readings: ICPSequence
     // scans pay no allocation)
     if ((rc = ensure(c, &c->d_rd_p4, &c->rd_p4_bytes, sizeof(P4<T>) * n1))) return rc;
     void* d_p4 = c->d_rd_p4;
-    if ((rc = upload_raw(c, feat, sizeof(T) * (size_t)rows * N))) return rc;
+    if ((rc = upload_raw_async(c, feat, sizeof(T) * (size_t)rows * N))) return rc;
     launch_pack_p4<T>((const T*)c->d_raw, rows, N, N, (P4<T>*)d_p4, c->stream);
+    HIPCHK(c, hipEventRecord(c->raw_ev, c->stream));
     if ((rc = ensure(c, &c->d_rd, &c->rd_bytes, sizeof(P4<T>) * n1))) return rc;
     if (c->d_waves) (void)hipFree(c->d_waves);
     c->d_waves = nullptr;
@@ -394,9 +591,11 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
         if ((rc = setup_room(c, N, std::max<int64_t>(c->setup_cells, 1)))) return rc;
         if ((rc = ensure(c, &c->d_rd_sorted, &c->rd_sorted_bytes, sizeof(P4<T>) * n1))) return rc;
         void* d_sorted = c->d_rd_sorted;
+        tr.mark("reading upload+pack");
         const int r = reading_order_device<T>((const P4<T>*)d_p4, N, M0, s, morton, c->setup, (P4<T>*)d_sorted,
                                               c->stream);
         if (r) return fail(c, PMX_E_HIP, "reading order failed (" + std::to_string(r) + ")");
+        tr.mark("reading order");
         size_t cap = c->order_bytes;
         if ((rc = ensure(c, (void**)&c->d_order, &cap, sizeof(int32_t) * n1))) return rc;
         c->order_bytes = cap;
@@ -414,6 +613,7 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
             HIPCHK(c, hipMemcpyAsync(c->d_waves, waves.data(), sizeof(uint32_t) * waves.size(),
                                      hipMemcpyHostToDevice, c->stream));
             c->n_waves = (int64_t)waves.size() - 1;
+            tr.mark("tile wave table");
         }
         HIPCHK(c, hipGetLastError());
     } else if (N > 0) {
@@ -537,6 +737,9 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         c->ids_grid = false;
         c->safe_valid = false;
     } else {
+        // a reading's first match runs on the cold level; any other match
+        // may use the finer levels the side stream builds
+        if (c->side_pending && (c->have_match || c->level != cold_level(c))) side_join(c);
         if (e0) (void)hipEventRecord(e0, c->stream);
         const GridLevel& L = c->lv(c->level);
         // warm start from the previous match of the same reading (same k):
@@ -1219,7 +1422,7 @@ int get_weights_impl(pmx_ctx* c, void* w) {
 
 // ---- instantiations used by the other translation units (pmx_ctx.h) ----
 #define PMX_INST(T)                                                                          \
-    template int set_reference_impl<T>(pmx_ctx*, const T*, int, int64_t, const T*, const T*); \
+    template int set_reference_impl<T>(pmx_ctx*, const T*, int, int64_t, const T*, const T*, T*); \
     template int set_reading_impl<T>(pmx_ctx*, const T*, int, int64_t, const T*);            \
     template int match_impl<T>(pmx_ctx*, const T*, int, double, uint64_t*);                  \
     template int outlier_impl<T>(pmx_ctx*, int, int, double, double, double);               \
@@ -1256,6 +1459,17 @@ int pmx_set_reference_centred(pmx_ctx* c, const void* feat, int rows, int64_t M,
                                               (const float*)offset),
                     set_reference_impl<double>(c, (const double*)feat, rows, M, (const double*)normals,
                                                (const double*)offset));
+}
+
+int pmx_set_reference_mean_centred(pmx_ctx* c, const void* feat, int rows, int64_t M, const void* normals,
+                                   void* mean_out) {
+    if (!c || !feat || !mean_out) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    (void)hipSetDevice(c->device);
+    return DISPATCH(c,
+                    set_reference_impl<float>(c, (const float*)feat, rows, M, (const float*)normals, nullptr,
+                                              (float*)mean_out),
+                    set_reference_impl<double>(c, (const double*)feat, rows, M, (const double*)normals, nullptr,
+                                               (double*)mean_out));
 }
 
 int pmx_set_reading(pmx_ctx* c, const void* feat, int rows, int64_t N, const void* T0) {

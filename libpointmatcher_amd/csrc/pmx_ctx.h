@@ -134,6 +134,25 @@ struct pmx_ctx {
     // once-per-compute setup on the device (pmx_setup.hip)
     SetupScratch setup;
     int64_t setup_n = 0, setup_cells = 0;
+    // the levels finer than the cold one, built on a side stream while the
+    // reading is set and the cold match runs (own scratch); every later match
+    // waits for side_ev on the context stream (side_join)
+    hipStream_t side = nullptr;
+    hipEvent_t side_ev = nullptr;
+    bool side_pending = false;
+    SetupScratch setup_side;
+    int64_t setup_side_n = 0, setup_side_cells = 0;
+    // the level table's pinned staging (its copy is asynchronous: table_ev
+    // guards the rewrite), and the reading's upload stream: the caller's
+    // cloud crosses PCIe while the context stream builds the cold level
+    // (raw_ev: the last pack that read d_raw; copy_ev: the upload done)
+    void* h_table = nullptr;
+    hipEvent_t table_ev = nullptr;
+    hipStream_t copy = nullptr;
+    hipEvent_t raw_ev = nullptr, copy_ev = nullptr;
+    void* d_raw2 = nullptr;  // the reference normals' upload staging (copy stream, beside d_raw's points)
+    size_t raw2_bytes = 0;
+    hipEvent_t nrm_ev = nullptr;
     void* d_raw = nullptr;            // upload staging of a caller's cloud
     size_t raw_bytes = 0;
     void* d_bbox = nullptr;
@@ -358,8 +377,11 @@ int ensure_level(pmx_ctx* c, int l);     // grid level l built (pmx_chain.hip)
 double host_limit(const pmx_ctx* c);
 void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double rm, double rp, double sw,
                 double limit);
+void side_join(pmx_ctx* c);
+void side_finish(pmx_ctx* c);
 template <typename T>
-int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals, const T* offset = nullptr);
+int set_reference_impl(pmx_ctx* c, const T* feat, int rows, int64_t M, const T* normals, const T* offset = nullptr,
+                       T* mean_out = nullptr);
 template <typename T>
 int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0);
 template <typename T>

@@ -10,7 +10,9 @@ every match (the live roofline measurement); nothing is dispatched after
 pass B.  Every iteration runs one match: the tile kernel (cold form, a new
 reading's first iteration) or the per-lane kernel (a match of several
 launches — the round-4 certify / search split, since removed — is summed),
-so the last 2 (W + K) matches are the two passes; each phase also lists the
+so the last 2 (W + K) matches are the two passes (with tile dispatch, C5,
+the tile kernel's warm form and the per-lane kernel it leaves the match to
+are launched back to back every iteration: the adjacent pair is one match); each phase also lists the
 durations it averages ("launch_ns").  This tool averages the kernel trace
 durations and the PMC counters (separate rocprofv3 --pmc runs of the same
 command, dispatches aligned by their order from the end) over:
@@ -36,6 +38,7 @@ import sys
 MATCH_OPEN = ("grid_lane_kernel", "grid_tile_kernel", "grid_certify_kernel")
 MATCH_MORE = ("grid_search_kernel",)
 KERNELS = {"p2plane": "p2plane_partial_kernel", "tail": "loop_tail_kernel", "step": "loop_step_kernel",
+           "finalize_step": "finalize_step_kernel", "p2point": "p2point_pass1_kernel",
            "counter_sum": "counter_sum_kernel", "select": "select_all_kernel", "finalize": "finalize_kernel"}
 
 
@@ -64,11 +67,18 @@ def match_series(rs, key):
     v = sorted(((int(x["Dispatch_Id"]), x) for x in rs if has(x["Kernel_Name"], MATCH_OPEN + MATCH_MORE)),
                key=lambda t: t[0])
     out = []
+    last = None  # (dispatch id, kernel name) of the previous match kernel
     for d, x in v:
-        if has(x["Kernel_Name"], MATCH_OPEN) or not out:
+        name = x["Kernel_Name"]
+        # (tile dispatch, C5: every iteration launches the tile kernel's warm
+        # form and then the per-lane kernel, one of which returns at once —
+        # the adjacent pair is one match)
+        pair = last is not None and "grid_lane_kernel" in name and "grid_tile_kernel" in last[1] and d == last[0] + 1
+        if (has(name, MATCH_OPEN) and not pair) or not out:
             out.append([d, key(x)])
         else:
             out[-1][1] += key(x)
+        last = (d, name)
     return out
 
 
