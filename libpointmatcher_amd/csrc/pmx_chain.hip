@@ -740,7 +740,6 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // a reading's first match runs on the cold level; any other match
         // may use the finer levels the side stream builds
         if (c->side_pending && (c->have_match || c->level != cold_level(c))) side_join(c);
-        if (e0) (void)hipEventRecord(e0, c->stream);
         const GridLevel& L = c->lv(c->level);
         // warm start from the previous match of the same reading (same k):
         // its ids are positions in the level it ran on (in loop mode the
@@ -779,7 +778,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on,
-                             c->loop_on && c->loop_dev.tile_dispatch, e1, c->stream);
+                             c->loop_on && c->loop_dev.tile_dispatch, e0, e1, c->stream);
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));

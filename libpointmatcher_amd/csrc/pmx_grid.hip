@@ -43,6 +43,8 @@
 // per-lane search from LDS (broadcast reads) and measures 0.187 ms at C3: a
 // candidate for QPT > 1 and for very dense references.
 #include "pmx_internal.h"
+
+#include <hip/hip_ext.h>
 #include "pmx_spec.h"
 
 namespace pmx {
@@ -1119,27 +1121,33 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                      const T* radii, bool cold, bool tile_disp, hipStream_t s) {
+                      const T* radii, bool cold, bool tile_disp, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
+    // (timing: e0 / e1 are recorded by the dispatch itself — the first
+    // launch's start, the last launch's end — hipExtLaunchKernelGGL, the
+    // kernel's own execution as a rocprofv3 kernel trace counts it; null
+    // events record nothing)
     if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
-        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx, start,
-                           G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 1,
-                           ctl, gd, spec, ru.safe);
+        hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, e0, e1, 0,
+                              gpts, gidx, start, G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists,
+                              ids, visited, radii, 1, ctl, gd, spec, ru.safe);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
-        if (tile_disp && ctl && ru.mode && !ru.cand)  // (device loop: the step picks one of the two forms)
-            hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, gpts, gidx,
-                               start, G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists, ids, visited,
-                               radii, 2, ctl, gd, spec, ru.safe);
+        const bool both = tile_disp && ctl && ru.mode && !ru.cand;
+        if (both)  // (device loop: the step picks one of the two forms)
+            hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, e0,
+                                  (hipEvent_t) nullptr, 0, gpts, gidx, start, G, rd, N, (const uint32_t*)nullptr, Tm,
+                                  knn, maxR2, max_pts, dists, ids, visited, radii, 2, ctl, gd, spec, ru.safe);
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
         const bool cm = ru.mode && ru.cand && ru.K > knn && ru.K <= KT - 1;  // (the list holds K + 1)
-        hipLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s, gpts, gidx, start, G,
-                           rd, N, Tm, knn, maxR2, dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev,
-                           ctl, gd, spec, radii, cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr, ru.coop_max);
+        hipExtLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s,
+                              both ? (hipEvent_t) nullptr : e0, e1, 0, gpts, gidx, start, G, rd, N, Tm, knn, maxR2,
+                              dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev, ctl, gd, spec, radii,
+                              cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr, ru.coop_max);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
-        hipLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, gpts, gidx, start, G, rd, N,
-                           waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 0, (const LoopCtl*)nullptr,
-                           (const GridDesc<T>*)nullptr, (SpecSel*)nullptr, (T*)nullptr);
+        hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, e0, e1, 0, gpts, gidx,
+                              start, G, rd, N, waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 0,
+                              (const LoopCtl*)nullptr, (const GridDesc<T>*)nullptr, (SpecSel*)nullptr, (T*)nullptr);
     }
 }
 
@@ -1150,7 +1158,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                        SelectState* spec_st, unsigned long long* xseg, const T* radii, bool cold, bool tile_disp,
-                       hipEvent_t ev_end, hipStream_t s) {
+                       hipEvent_t ev_start, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     cold = cold && mode >= 1;
     if (mode < 1 || !visited) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
@@ -1162,12 +1170,14 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     G.h = h;
     G.inv_h = 1.0 / h;
     if (knn > kLaneMaxK) {  // a k-list spread over a wave per query (pmx_knn_wide.hip; no reuse)
+        if (ev_start) (void)hipEventRecord(ev_start, s);
         launch_knn_wide<T>(gpts, gidx, start, &G, 0, rd, N, Tm, knn, maxR2, radii, dists, ids, visited, ctl, gd, spec,
                            s);
+        if (ev_end) (void)hipEventRecord(ev_end, s);
     } else {
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, radii, cold, tile_disp, s)
+                     ru, ctl, gd, spec, radii, cold, tile_disp, ev_start, ev_end, s)
         // with reuse the list keeps room for the (k+1)-th point (the safe radius;
         // the cold tile writes radius 0 and keeps k entries); with K reuse
         // candidates, for the (K+1)-th
@@ -1187,7 +1197,6 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
             PMX_KT(16);
 #undef PMX_KT
     }
-    if (ev_end) (void)hipEventRecord(ev_end, s);  // (timing: the match kernel)
     if (visited && vout)
         hipLaunchKernelGGL(counter_sum_kernel<T>, dim3(1), dim3(kVSlots), 0, s, visited, vout, iter_err, ctl, spec,
                            spec_st, xseg);
@@ -1198,13 +1207,15 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, const float*, bool, bool, hipEvent_t, hipStream_t);
+                                       unsigned long long*, const float*, bool, bool, hipEvent_t, hipEvent_t,
+                                       hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, const double*, bool, bool, hipEvent_t, hipStream_t);
+                                        unsigned long long*, const double*, bool, bool, hipEvent_t, hipEvent_t,
+                                        hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices
 __global__ void pos_to_index_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ gidx,

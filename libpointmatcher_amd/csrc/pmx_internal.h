@@ -222,8 +222,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       unsigned long long* xseg, const T* radii, bool cold, bool tile_disp, hipEvent_t ev_end,
-                       hipStream_t s);
+                       unsigned long long* xseg, const T* radii, bool cold, bool tile_disp, hipEvent_t ev_start,
+                       hipEvent_t ev_end, hipStream_t s);
 // several ranks: the quantile window's pick over the all-gathered segments
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum.
 // stall: a miss sets ctl->done = kCtlStalled (the host did not read the
