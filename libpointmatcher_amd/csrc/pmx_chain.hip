@@ -106,15 +106,18 @@ void side_finish(pmx_ctx* c) {
 }
 
 // Setup timeline (development trace, PMX_SETUP_TRACE=1): each mark waits for
-// the stream and prints the wall time since the previous mark to stderr.
+// the stream and prints the wall time since the previous mark to stderr
+// (PMX_SETUP_TRACE=2: host wall time only, no stream synchronisation).
 struct SetupTrace {
     pmx_ctx* c;
-    bool on;
+    int on;
     std::chrono::steady_clock::time_point t;
-    explicit SetupTrace(pmx_ctx* cc) : c(cc), on(std::getenv("PMX_SETUP_TRACE") != nullptr), t(std::chrono::steady_clock::now()) {}
+    explicit SetupTrace(pmx_ctx* cc)
+        : c(cc), on(std::getenv("PMX_SETUP_TRACE") ? std::atoi(std::getenv("PMX_SETUP_TRACE")) : 0),
+          t(std::chrono::steady_clock::now()) {}
     void mark(const char* what) {
         if (!on) return;
-        (void)hipStreamSynchronize(c->stream);
+        if (on == 1) (void)hipStreamSynchronize(c->stream);
         const auto n = std::chrono::steady_clock::now();
         std::fprintf(stderr, "setup_trace %-22s %8.3f ms\n", what, std::chrono::duration<double>(n - t).count() * 1e3);
         t = n;
@@ -161,7 +164,9 @@ int upload_raw_async(pmx_ctx* c, const void* src, size_t bytes) {
 // the grid levels over the resident reference d_ref (M points) and d_nrm
 template <typename T>
 int build_grid(pmx_ctx* c, int64_t M, const std::function<int()>& before_levels = {}) {
+    SetupTrace gt(c);
     side_finish(c);  // (a previous reference's side builds write level buffers kept below)
+    gt.mark("side finish");
     const P4<T>* pts = (const P4<T>*)c->d_ref;
     // bounding box of the finite points (inf / NaN points can never be a neighbour)
     double* sb = nullptr;  // bbox partials, then 8 doubles of result
@@ -175,6 +180,7 @@ int build_grid(pmx_ctx* c, int64_t M, const std::function<int()>& before_levels 
     double bb[7];
     HIPCHK(c, hipMemcpyAsync(bb, bb_out, sizeof(bb), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    gt.mark("bbox");
     double lo[3] = {bb[0], bb[1], bb[2]}, hi[3] = {bb[3], bb[4], bb[5]};
     const int64_t valid = (int64_t)bb[6];
     if (valid == 0)
@@ -214,6 +220,7 @@ int build_grid(pmx_ctx* c, int64_t M, const std::function<int()>& before_levels 
         if ((rc = occupied(h0, h1, o0, o1))) return rc;
         o0 = std::max<int64_t>(1, o0);
         o1 = std::max<int64_t>(1, o1);
+        gt.mark("occupancy");
         dim = std::log2((double)o1 / (double)o0);
         dim = std::min(3.0, std::max(1.0, dim));
         ppc1 = (double)valid / (double)o1;
@@ -256,8 +263,9 @@ int build_grid(pmx_ctx* c, int64_t M, const std::function<int()>& before_levels 
         L.ppc = c->level_ppc[l];
         c->levels.push_back(L);
     }
-    SetupTrace(c).mark("bbox+sizing (from pack)");
+    gt.mark("sizing");
     if (before_levels && (rc = before_levels())) return rc;
+    gt.mark("normals join+pack");
     return build_levels_cold<T>(c, c->adaptive ? cold_level(c) : 0);
 }
 
@@ -380,7 +388,11 @@ int build_levels_cold(pmx_ctx* c, int cold) {
     cold = std::min(cold, (int)c->levels.size() - 1);
     if (cold <= 0 || !side_env || c->levels_built > 0) return build_levels<T>(c, cold);
     if (!c->side) {
-        HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        // (the lowest priority: the context stream's cold level, reading
+        // order and first match go first when both have work)
+        int least = 0, greatest = 0;
+        HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCHK(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
         HIPCHK(c, hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming));
     }
     int64_t cells = 1;
@@ -394,10 +406,13 @@ int build_levels_cold(pmx_ctx* c, int cold) {
     HIPCHK(c, hipEventRecord(c->side_ev, c->side));
     c->side_pending = true;
     SetupTrace tr(c);
+    tr.mark("side levels enqueued");
     if ((rc = build_one_level<T>(c, cold, c->setup, c->stream))) return rc;
     tr.mark("cold level");
     c->levels_built = cold + 1;
-    return publish_levels<T>(c);
+    rc = publish_levels<T>(c);
+    tr.mark("publish");
+    return rc;
 }
 
 // Slot order of the reading: Morton order of the cell of the initially
@@ -567,7 +582,13 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     // scans pay no allocation)
     if ((rc = ensure(c, &c->d_rd_p4, &c->rd_p4_bytes, sizeof(P4<T>) * n1))) return rc;
     void* d_p4 = c->d_rd_p4;
-    if ((rc = upload_raw_async(c, feat, sizeof(T) * (size_t)rows * N))) return rc;
+    static const bool copy_env = [] {  // (PMX_READING_COPY=0: the reading's upload on the context stream)
+        const char* e = std::getenv("PMX_READING_COPY");
+        return !e || std::atoi(e) != 0;
+    }();
+    if ((rc = copy_env ? upload_raw_async(c, feat, sizeof(T) * (size_t)rows * N)
+                       : upload_raw(c, feat, sizeof(T) * (size_t)rows * N)))
+        return rc;
     launch_pack_p4<T>((const T*)c->d_raw, rows, N, N, (P4<T>*)d_p4, c->stream);
     HIPCHK(c, hipEventRecord(c->raw_ev, c->stream));
     if ((rc = ensure(c, &c->d_rd, &c->rd_bytes, sizeof(P4<T>) * n1))) return rc;
