@@ -153,6 +153,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_MODE"))
         c->grid_mode = std::strcmp(e, "tile") == 0 ? 0 : std::strcmp(e, "octant") == 0 ? 2 : 1;
     if (const char* e = std::getenv("PMX_GRID_TILE_MAX")) c->tile_max = (uint32_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("PMX_NBR_CACHE")) c->nbr_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_SPEC_SELECT")) c->spec_allowed = std::atoi(e) != 0;
     // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
     // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
@@ -250,7 +251,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     void* bufs[] = {c->d_safe, c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
-                    c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace, c->d_diag, c->d_cand, c->d_ticket,
+                    c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace, c->d_diag, c->d_cand, c->d_ticket, c->d_nbr,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
                     c->d_rob, c->d_rdev, c->d_radii, c->d_rd_p4, c->d_rd_sorted};
     side_finish(c);  // (the side stream may still be building levels)

@@ -781,8 +781,22 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                 if (rc) return rc;
                 ru.K = K;
                 ru.cand = c->d_cand;
+            } else if (knn == 1 && c->nbr_on && (ru.mode != 2 || c->nbr_prev || c->loop_on) &&
+                       !(c->loop_on && c->loop_dev.tile_dispatch)) {
+                // (a reuse match reads the records only if the last match
+                // wrote them; a device-loop match decides reuse on the device,
+                // where every match of the loop writes them.  Not for dense
+                // readings, tile dispatch: most queries miss there, and the
+                // records' writes cost more than the certificate saves, C5
+                // 1.51 vs 1.47 ms/iteration)
+                int rc = ensure(c, &c->d_nbr, &c->nbr_bytes, 2 * sizeof(P4<T>) * (size_t)std::max<int64_t>(c->N, 1));
+                if (rc) return rc;
+                ru.nbr = (P4<T>*)c->d_nbr;
+                ru.gpn = (const P4<T>*)L.gpn;
             }
         }
+        c->nbr_prev = ru.nbr != nullptr;
+        c->nbr_normals = ru.gpn != nullptr;
         // several ranks: the counter sum packs this rank's window segment,
         // the segments are all-gathered and every rank picks from the union
         SpecSel* spec = c->spec_now();
@@ -793,13 +807,64 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         if (spec && sharded(c) && !c->d_specx)
             HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * c->nranks));
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx + (size_t)kSpecXStride * c->rank : nullptr;
+        const bool cold_now = no_prev && c->reuse_on;
+        // (development profile of the cold form's waves, PMX_TILE_PROF=1: per
+        // wave duration, rounds and points copied, summarised on stderr)
+        static const bool tile_prof = std::getenv("PMX_TILE_PROF") != nullptr;
+        unsigned long long* prof_buf = nullptr;
+        const int64_t nw = (c->N + 63) / 64;
+        if (tile_prof && cold_now) {
+            HIPCHK(c, hipMalloc((void**)&prof_buf, sizeof(unsigned long long) * 4 * std::max<int64_t>(nw, 1)));
+            set_tile_prof(prof_buf);
+        }
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
                              (T*)c->d_dists, c->d_ids, c->d_vpart, c->merge_counter ? nullptr : c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
-                             c->has_radii ? (const T*)c->d_radii : nullptr, no_prev && c->reuse_on,
+                             c->has_radii ? (const T*)c->d_radii : nullptr, cold_now,
                              c->loop_on && c->loop_dev.tile_dispatch, e0, e1, c->stream);
+        if (prof_buf) {
+            std::vector<unsigned long long> h((size_t)(4 * nw));
+            HIPCHK(c, hipMemcpyAsync(h.data(), prof_buf, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            set_tile_prof(nullptr);
+            (void)hipFree(prof_buf);
+            std::vector<double> dur((size_t)nw);
+            unsigned long long t0 = ~0ull, t1 = 0;
+            double rsum = 0, csum = 0, fb = 0;
+            for (int64_t w = 0; w < nw; ++w) {
+                dur[(size_t)w] = (double)(h[4 * w + 1] - h[4 * w]) * 0.01;  // (100 MHz: us)
+                t0 = std::min(t0, h[4 * w]);
+                t1 = std::max(t1, h[4 * w + 1]);
+                rsum += (double)(h[4 * w + 2] & 0xffffffffull);
+                fb += (double)(h[4 * w + 2] >> 32);
+                csum += (double)h[4 * w + 3];
+            }
+            std::vector<double> sd = dur;
+            std::sort(sd.begin(), sd.end());
+            auto q = [&](double f) { return sd[(size_t)std::min<double>((double)(nw - 1), f * (double)nw)]; };
+            double tot = 0;
+            for (double d : dur) tot += d;
+            // the last-started waves: how long after the kernel's start they began and ran
+            int64_t last = 0;
+            for (int64_t w = 0; w < nw; ++w)
+                if (h[4 * w] > h[4 * last]) last = w;
+            std::fprintf(stderr,
+                         "tile_prof waves %lld span %.1f us  wave us: mean %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f"
+                         "  sum %.0f us  rounds/wave %.2f  points copied/wave %.0f  fallback lanes %.0f"
+                         "  last-started wave at %.1f us ran %.1f us\n",
+                         (long long)nw, (double)(t1 - t0) * 0.01, tot / (double)nw, q(0.5), q(0.9), q(0.99),
+                         sd.back(), tot, rsum / (double)nw, csum / (double)nw, fb, (double)(h[4 * last] - t0) * 0.01,
+                         dur[(size_t)last]);
+            // duration by dispatch decile
+            for (int dcl = 0; dcl < 10; ++dcl) {
+                double s2 = 0;
+                int64_t a = nw * dcl / 10, b = nw * (dcl + 1) / 10;
+                for (int64_t w = a; w < b; ++w) s2 += dur[(size_t)w];
+                std::fprintf(stderr, "tile_prof decile %d mean %.1f us\n", dcl, s2 / (double)std::max<int64_t>(b - a, 1));
+            }
+        }
         if (xseg) {
             if (c->N <= 0)  // (no match kernel ran: an empty segment)
                 HIPCHK(c, hipMemsetAsync(xseg, 0, kSpecXHdr * sizeof(unsigned long long), c->stream));
@@ -1284,10 +1349,13 @@ int p2plane_enqueue(pmx_ctx* c) {
     const WChain<T> chain = chain_of<T>(c);
     const int NV = chain.robust ? p2plane_nv_full(c->dim) : p2plane_nv(c->dim);
     Mat4<T> Tm = step_mat<T>(c);
+    // (k = 1 after a match that left its neighbour records with normals:
+    // the reduction reads them in slot order instead of gathering by id)
+    const bool nbr = c->nbr_prev && c->nbr_normals && c->knn == 1 && c->ids_grid && !chain.robust;
     launch_p2plane_partial<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_pn(c), (const P4<T>*)match_nrm(c),
                               match_rs(c), (const T*)c->d_dists, c->d_ids, chain, c->knn, c->N, c->dim, c->d_partials,
                               loop_ctl(c), (const GridDesc<T>*)c->d_gdesc, c->vpart_dirty ? c->d_vpart : nullptr,
-                              c->stream);
+                              c->stream, nbr ? (const P4<T>*)c->d_nbr : nullptr);
     c->vpart_dirty = false;
     if (c->fuse_final) {  // (summed by the fused finalize + step launch)
         c->final_out = c->d_result;

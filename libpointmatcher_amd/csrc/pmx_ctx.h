@@ -124,6 +124,13 @@ struct pmx_ctx {
     int coop_max = 4;             // wave-cooperative full searches for blocks with <= this many misses (PMX_COOP_MAX)
     int cand_K = 0;
     int32_t* d_cand = nullptr;    // int32[N * cand_K]
+    // k = 1 neighbour records (GridReuse::nbr): P4<T>[N]; nbr_prev: the last
+    // match wrote them (PMX_NBR_CACHE=0: off)
+    void* d_nbr = nullptr;
+    size_t nbr_bytes = 0;
+    bool nbr_prev = false;
+    bool nbr_normals = false;  // (the last match's records carry the normals, at d_nbr + N)
+    bool nbr_on = true;
     size_t cand_bytes = 0;
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }

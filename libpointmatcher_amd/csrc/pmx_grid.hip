@@ -429,6 +429,24 @@ __device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&k
     }
 }
 
+// k = 1 neighbour record (GridReuse::nbr): the point the k-list holds, with
+// the id write_out stores (-1: none, or beyond the radius) in w
+// (gpn: the level's interleaved point / normal records — the normal then
+// goes to nbr[N + j], what the point-to-plane reduction reads)
+template <typename T, int KT>
+__device__ __forceinline__ void write_nbr(P4<T>* __restrict__ nbr, const P4<T>* __restrict__ gpts,
+                                          const P4<T>* __restrict__ gpn, int64_t N, int64_t j, T maxR2,
+                                          const T (&kd)[KT], const int32_t (&ki)[KT]) {
+    if (!nbr) return;
+    int32_t id = ki[0];
+    if (id == kNoPos || !(kd[0] <= maxR2)) id = -1;
+    const uint32_t g = id >= 0 ? (uint32_t)id : 0u;
+    P4<T> r = gpn ? gpn[2 * (size_t)g] : gld32(gpts, g);
+    if (gpn) nbr[N + j] = gpn[2 * (size_t)g + 1];
+    r.w = pos_w((uint32_t)id, T(0));
+    nbr[j] = r;
+}
+
 template <typename T, int KT>
 __device__ __forceinline__ void write_out(int64_t j, int k, T maxR2, const T (&kd)[KT], const int32_t (&ki)[KT],
                                           T* __restrict__ out_d, int32_t* __restrict__ out_i) {
@@ -589,7 +607,9 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
                                            const P4<T>* __restrict__ rd, int64_t j, const Mat4<T>& Tm, int k,
                                            T maxR2, int oct, T* __restrict__ out_d, int32_t* __restrict__ out_i,
                                            T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa,
-                                           int K = 0, int32_t* __restrict__ cand = nullptr) {
+                                           int K = 0, int32_t* __restrict__ cand = nullptr,
+                                           P4<T>* __restrict__ nbr = nullptr, const P4<T>* __restrict__ gpn = nullptr,
+                                           int64_t N = 0) {
     // K > k (reuse candidates, cand != null): the search certifies the K
     // nearest, its list keeps the (K+1)-th, and the K nearest are stored as
     // the next match's candidates
@@ -622,6 +642,7 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
         }
     }
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
+    write_nbr<T, KT>(nbr, gpts, gpn, N, j, maxR2, kd, ki);
     if (cand) {
 #pragma unroll
         for (int s = 0; s < KT; ++s)
@@ -944,7 +965,8 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
                                                         SpecSel* __restrict__ spec, const T* __restrict__ radii,
-                                                        int K, int32_t* __restrict__ cand, int coop_max) {
+                                                        int K, int32_t* __restrict__ cand, int coop_max,
+                                                        P4<T>* __restrict__ nbr, const P4<T>* __restrict__ nbr_gpn) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         if (ctl->use_tile) return;  // (tile dispatch: the tile kernel's warm form runs this match)
@@ -953,6 +975,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         gidx = D.gidx;
         start = D.start;
         G = D.G;
+        if (nbr_gpn) nbr_gpn = D.gpn;
         ctl_transform(ctl, Tm);
         if (reuse) {
             reuse = ctl->prev_level == ctl->level ? 2 : 1;
@@ -964,6 +987,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         safe = nullptr;
         cand = nullptr;
     }
+    if (!safe || cand || k != 1 || KT < 2) nbr = nullptr;  // (the record serves the k = 1 certificate)
     // reuse candidates (K > k, cand != null): the certificate keeps the K
     // nearest of the last full search and re-ranks them at the new position
     // (see the temporal reuse notes above)
@@ -993,14 +1017,20 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         P4<T> p[Q];
         T rs[Q], dkp[Q];
         int32_t id[Q][KR];
+        P4<T> r[Q][KR];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int64_t j = missed[q] ? base + q * 256 + threadIdx.x : base;  // (base < N: an in-range slot)
             p[q] = gld(rd, j);
             rs[q] = safe[j];
             dkp[q] = cm ? (T)0 : out_d[j * k + k - 1];
+            if (nbr) {  // (k = 1: the neighbour's record with the query, no dependent gather)
+                r[q][0] = nbr[j];
+                id[q][0] = (int32_t)w_pos(r[q][0].w);
+            } else {
 #pragma unroll
-            for (int s = 0; s < KR; ++s) id[q][s] = s < nc ? (cm ? cand[j * K + s] : out_i[j * k + s]) : 0;
+                for (int s = 0; s < KR; ++s) id[q][s] = s < nc ? (cm ? cand[j * K + s] : out_i[j * k + s]) : 0;
+            }
         }
         bool ok[Q];
         double bq[Q];
@@ -1020,11 +1050,12 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             bq[q] = (double)rs[q] * (1.0 - kReuseMargin) - delta;
             ok[q] = o && (cm ? bq[q] > 0.0 : av < bq[q]);
         }
-        P4<T> r[Q][KR];
+        if (!nbr) {
 #pragma unroll
-        for (int q = 0; q < Q; ++q)
+            for (int q = 0; q < Q; ++q)
 #pragma unroll
-            for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < nc ? (uint32_t)id[q][s] : 0u);
+                for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < nc ? (uint32_t)id[q][s] : 0u);
+        }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if (!ok[q]) continue;
@@ -1091,6 +1122,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             coop_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, ks, r2, kd, kp, lbx, visits);
             if (lane == 0) {
                 write_out<T, KT>(j2, k, r2, kd, kp, out_d, out_i, sa);
+                write_nbr<T, KT>(nbr, gpts, nbr_gpn, N, j2, r2, kd, kp);
                 if (cand) {
 #pragma unroll
                     for (int s = 0; s < KT; ++s)
@@ -1103,7 +1135,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
             const int64_t j2 = base + miss[t];
             full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe,
-                              visits, sa, K, cand);
+                              visits, sa, K, cand, nbr, nbr_gpn, N);
             if (Q == 1) break;
         }
     }
@@ -1129,27 +1161,33 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
     if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
         hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, e0, e1, 0,
                               gpts, gidx, start, G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists,
-                              ids, visited, radii, 1, ctl, gd, spec, ru.safe);
+                              ids, visited, radii, 1, ctl, gd, spec, ru.safe, ru.nbr, ru.gpn);
     } else if (mode >= 1) {  // 1: shell search, 2: octant block first
         const bool both = tile_disp && ctl && ru.mode && !ru.cand;
         if (both)  // (device loop: the step picks one of the two forms)
             hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, e0,
                                   (hipEvent_t) nullptr, 0, gpts, gidx, start, G, rd, N, (const uint32_t*)nullptr, Tm,
-                                  knn, maxR2, max_pts, dists, ids, visited, radii, 2, ctl, gd, spec, ru.safe);
+                                  knn, maxR2, max_pts, dists, ids, visited, radii, 2, ctl, gd, spec, ru.safe,
+                                  ru.nbr, ru.gpn);
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
         const bool cm = ru.mode && ru.cand && ru.K > knn && ru.K <= KT - 1;  // (the list holds K + 1)
         hipExtLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s,
                               both ? (hipEvent_t) nullptr : e0, e1, 0, gpts, gidx, start, G, rd, N, Tm, knn, maxR2,
                               dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev, ctl, gd, spec, radii,
-                              cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr, ru.coop_max);
+                              cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr, ru.coop_max,
+                              cm ? (P4<T>*)nullptr : ru.nbr, ru.gpn);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, e0, e1, 0, gpts, gidx,
                               start, G, rd, N, waves, Tm, knn, maxR2, max_pts, dists, ids, visited, radii, 0,
-                              (const LoopCtl*)nullptr, (const GridDesc<T>*)nullptr, (SpecSel*)nullptr, (T*)nullptr);
+                              (const LoopCtl*)nullptr, (const GridDesc<T>*)nullptr, (SpecSel*)nullptr, (T*)nullptr,
+                              (P4<T>*)nullptr, (const P4<T>*)nullptr);
     }
 }
+
+// PMX_TILE_PROF: the cold form's per-wave profile into buf (4 words per wave)
+void set_tile_prof(unsigned long long* buf) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile_prof), &buf, sizeof(buf)); }
 
 template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,

@@ -190,6 +190,13 @@ struct GridReuse {
     // a block whose misses are at most this many searches each with a whole
     // wave (pmx_grid.hip coop_search); more take the per-lane search
     int coop_max = 0;
+    // k = 1: each query's neighbour record (the grid point, its position in
+    // w), written by every search that leaves a safe radius, so that the
+    // certificate reads it with the query instead of gathering it by id
+    // (null: off).  With the level's interleaved point / normal records
+    // (gpn) the normals follow at nbr + N, for the point-to-plane reduction.
+    P4<T>* nbr = nullptr;
+    const P4<T>* gpn = nullptr;
 };
 template <typename T>
 __device__ __forceinline__ void ctl_transform(const LoopCtl* ctl, Mat4<T>& Tm) {
@@ -216,6 +223,7 @@ void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* star
 // match (no previous match to certify from) on the tile kernel's cold form.
 // vout null: no counter-sum launch after the match (its counter phase is
 // merged into the select launch that follows, launch_select_all).
+void set_tile_prof(unsigned long long* buf);
 template <typename T>
 void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const double* lo,
                        double h, const int* g, const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves,
@@ -496,7 +504,7 @@ template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
-                            hipStream_t s);
+                            hipStream_t s, const P4<T>* nbr = nullptr);
 void launch_finalize(const double* partials, int nblocks, int nv, double* out, const LoopCtl* ctl, hipStream_t s);
 template <typename T>
 void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,

@@ -129,8 +129,11 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, stage, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
     // the first loop match may reuse the last classic one
     const int Kr = reuse_k(c, cfg->knn);
+    // (k = 1: only if that match left its neighbour records, which the
+    // loop's reuse reads)
+    const bool nbr_ok = !(cfg->knn == 1 && Kr == 1 && c->nbr_on) || c->nbr_prev;
     const int prev_level = c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn &&
-                                   (Kr == cfg->knn || c->cand_K == Kr)
+                                   (Kr == cfg->knn || c->cand_K == Kr) && nbr_ok
                                ? c->ids_level
                                : -1;
     launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, prev_level,

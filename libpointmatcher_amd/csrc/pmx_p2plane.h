@@ -132,7 +132,7 @@ __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const
                                              const P4<T>* __restrict__ ref, const P4<T>* __restrict__ nrm, int rs,
                                              const T* __restrict__ d, const int32_t* __restrict__ ids,
                                              const WChain<T>& chain, int k, int64_t N,
-                                             double* __restrict__ partials) {
+                                             double* __restrict__ partials, const P4<T>* __restrict__ nbr = nullptr) {
     constexpr int NF = DIM == 3 ? 6 : 3;
     constexpr int NS = NF * (NF + 1) / 2;
     constexpr int NV = NS + NF + 5;  // (the fifth counter, sum of w, is the kept count with 0/1 weights)
@@ -152,28 +152,37 @@ __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const
 #endif
     if (k == 1) {
         // k = 1: U slots per round with every load issued up front (the
-        // reduction is latency-bound: slot -> id -> gathered point / normal)
+        // reduction is latency-bound: slot -> id -> gathered point / normal;
+        // with the match's neighbour records, nbr, the point and the normal
+        // come in slot order with the query, no dependent gather)
         constexpr int U = 4;
         for (; i0 < N; i0 += U * stride) {
             P4<T> r[U];
             T dv[U];
             int32_t id[U];
+            P4<T> q[U], n[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t ii = i0 + u * stride;
                 const int64_t jj = ii < N ? ii : i0;
                 r[u] = rd[jj];
                 dv[u] = d[jj];
-                id[u] = ids[jj];
+                if (nbr) {
+                    q[u] = nbr[jj];
+                    n[u] = nbr[N + jj];
+                } else {
+                    id[u] = ids[jj];
+                }
             }
             bool kp[U];
-            P4<T> q[U], n[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 kp[u] = i0 + u * stride < N && dv[u] != inf && chain_keep(wr, dv[u]);
-                const int64_t g = (int64_t)(kp[u] ? id[u] : 0) * rs;  // (position 0 always exists)
-                q[u] = gld(ref, g);
-                n[u] = gld(nrm, g);
+                if (!nbr) {
+                    const int64_t g = (int64_t)(kp[u] ? id[u] : 0) * rs;  // (position 0 always exists)
+                    q[u] = gld(ref, g);
+                    n[u] = gld(nrm, g);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {

@@ -58,7 +58,8 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
                                                               int k, int64_t N, double* __restrict__ partials,
                                                               const LoopCtl* __restrict__ ctl,
                                                               const GridDesc<T>* __restrict__ gd,
-                                                              unsigned long long* __restrict__ vzero) {
+                                                              unsigned long long* __restrict__ vzero,
+                                                              const P4<T>* __restrict__ nbr) {
     if (ctl) {  // device loop
         if (ctl->done) return;
         ctl_transform(ctl, Tm);
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(256) void p2plane_partial_kernel(const P4<T>* __res
     }
     if (vzero && blockIdx.x == 0)  // (the spread counters the merged counter phase read, for the next match)
         for (int c = 0; c < 4; ++c) vzero[(size_t)(c * kVSlots + threadIdx.x) * kVStride] = 0ull;
-    p2plane_body<T, DIM>(rd, Tm, ref, nrm, rs, d, ids, chain, k, N, partials);
+    p2plane_body<T, DIM>(rd, Tm, ref, nrm, rs, d, ids, chain, k, N, partials, nbr);
 }
 
 // Real-valued weights (a RobustOutlierFilter in the chain; per-module path):
@@ -166,7 +167,7 @@ template <typename T>
 void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const P4<T>* nrm, int rs,
                             const T* d, const int32_t* ids, const WChain<T>& chain, int k, int64_t N, int dim,
                             double* partials, const LoopCtl* ctl, const GridDesc<T>* gd, unsigned long long* vzero,
-                            hipStream_t s) {
+                            hipStream_t s, const P4<T>* nbr) {
     if (chain.robust) {  // real-valued weights: the full asymmetric A
         if (dim == 3)
             hipLaunchKernelGGL((p2plane_weighted_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm,
@@ -178,10 +179,10 @@ void launch_p2plane_partial(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref
     }
     if (dim == 3)
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 3>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
-                           d, ids, chain, k, N, partials, ctl, gd, vzero);
+                           d, ids, chain, k, N, partials, ctl, gd, vzero, nbr);
     else
         hipLaunchKernelGGL((p2plane_partial_kernel<T, 2>), dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, nrm, rs,
-                           d, ids, chain, k, N, partials, ctl, gd, vzero);
+                           d, ids, chain, k, N, partials, ctl, gd, vzero, nbr);
 }
 
 // Sum the per-block partials: one block per accumulator, each thread adds a
@@ -382,7 +383,8 @@ void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, c
 #define PMX_INST(T)                                                                                                  \
     template void launch_p2plane_partial<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const P4<T>*, int, const T*, \
                                             const int32_t*, const WChain<T>&, int, int64_t, int, double*,           \
-                                            const LoopCtl*, const GridDesc<T>*, unsigned long long*, hipStream_t);    \
+                                            const LoopCtl*, const GridDesc<T>*, unsigned long long*, hipStream_t,     \
+                                            const P4<T>*);                                                            \
     template void launch_p2point_pass1<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
                                           const WChain<T>&, int, int64_t, double*, const LoopCtl*,                   \
                                           const GridDesc<T>*, hipStream_t);                                          \
