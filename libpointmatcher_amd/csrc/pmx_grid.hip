@@ -45,6 +45,10 @@
 #include "pmx_internal.h"
 
 #include <hip/hip_ext.h>
+
+#ifndef PMX_NOMISS
+#define PMX_NOMISS 0
+#endif
 #include "pmx_spec.h"
 
 namespace pmx {
@@ -1085,6 +1089,13 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             missed[q] = false;
         }
     }
+#if PMX_NOMISS  // (timing experiment only: the certificate pass without the misses' searches — wrong results)
+    if (reuse == 2) {
+        if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
+        add_visits(visits, visited);
+        return;
+    }
+#endif
     // the block's misses, compacted in slot order
     unsigned long long mq[Q];
 #pragma unroll
