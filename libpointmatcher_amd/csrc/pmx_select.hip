@@ -24,7 +24,6 @@
 #include "pmx_spec.h"
 #include "pmx_selectall.h"
 
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -285,12 +284,15 @@ static unsigned grid_for(int64_t n) {
 }
 
 // ============================================================ VarTrimmed ==
-// scratch layout (bytes, 256-aligned pieces):
-//   [hdr: 64 B]   int count, int err
+// scratch layout (bytes, 256-aligned pieces; launch_vartrim):
+//   [hdr: 256 B]         int count, int err, ..., the head's running sum
+//   RsHead               the radix sort's histograms and tile counters
+//                        (zeroed once at allocation: vartrim_scratch_head)
 //   keysA[n], keysB[n]   the keys, then sorted (K)
 //   cum[n]               sequential partial sums (T)
 //   argmin partials      (kFrmsBlocks values + indices)
-//   hipcub's sort scratch, the partial sum's chunk tables
+//   the radix sort's look-back state, the chunk table, Q_even / Q_odd / P1
+//   (8 B per key) and W1 (4 B per key), the walk's trace
 // deno: host-computed table pow(id / points_nbr, lambda) in T (the same libm
 // call as the reference's Eigen pow, OutlierFiltersImpl.cpp:209)
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -299,10 +301,8 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // The finite positive distances (OutlierFiltersImpl.cpp:186-188) as sort
 // keys in place, every other distance as the all-ones key (sorted after every
-// finite positive float's bits); the count of the kept ones.  hipcub's radix
-// sort then orders all n keys — the kept ones first — in one call (it
-// replaced a four-pass LSD sort of the compacted keys: 4 x (count, scan,
-// scatter) launches).
+// finite positive float's bits); the count of the kept ones.  The LSD radix
+// sort of pmx_radix.h then orders all n keys — the kept ones first.
 template <typename T>
 __global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, int64_t n,
                                                       typename KeyOf<T>::K* __restrict__ keys, int* __restrict__ count,
