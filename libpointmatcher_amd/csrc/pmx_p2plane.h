@@ -124,6 +124,8 @@ __device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz,
 // result layout: [0, NS) upper triangle of A row-major (r <= c), [NS, NS+NF) b,
 // then kept, nonzero weights, rejected matches, rejected points, sum of weights;
 // one block's sums to partials[v * gridDim.x + blockIdx.x]
+// k up to this: the reduction issues a query's k gathers together
+constexpr int kGatherK = 4;
 #ifndef PMX_P2P_XCD
 #define PMX_P2P_XCD 1
 #endif
@@ -200,6 +202,50 @@ __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const
                 xform3(Tm, r[u], px, py, pz);
                 p2plane_add<T, DIM, NV>(acc, px, py, pz, q[u], n[u]);
             }
+        }
+    }
+    if (k > 1 && k <= kGatherK) {
+        // 1 < k <= kGatherK: the query's k distances and ids first, then every
+        // kept entry's point and normal gathers in flight together, then the
+        // sums in rank order (the loop below, one dependent gather at a time,
+        // took 45 us for C4's 4 M pairs)
+        for (; i0 < N; i0 += stride) {
+            const int64_t i = i0;
+            const P4<T> rp = rd[i];
+            T dv[kGatherK];
+            int32_t id[kGatherK];
+#pragma unroll
+            for (int s = 0; s < kGatherK; ++s) {
+                dv[s] = s < k ? d[i * k + s] : inf;
+                id[s] = s < k ? ids[i * k + s] : -1;
+            }
+            P4<T> q[kGatherK], n[kGatherK];
+#pragma unroll
+            for (int s = 0; s < kGatherK; ++s) {
+                const bool kp = s < k && dv[s] != inf && chain_keep(wr, dv[s]);
+                const int64_t g = (int64_t)(kp ? id[s] : 0) * rs;  // (position 0 always exists)
+                q[s] = gld(ref, g);
+                n[s] = gld(nrm, g);
+            }
+            T px, py, pz;
+            xform3(Tm, rp, px, py, pz);
+            bool exist = false;
+#pragma unroll
+            for (int s = 0; s < kGatherK; ++s) {
+                if (s >= k) continue;
+                const bool keep = chain_keep(wr, dv[s]);
+                if (keep) acc[NS + NF + 1] += 1.0;  // (w != 0).count()
+                if (dv[s] == inf) continue;
+                if (!keep) {
+                    acc[NS + NF + 2] += 1.0;  // rejected match
+                    continue;
+                }
+                exist = true;
+                acc[NS + NF + 0] += 1.0;  // kept
+                acc[NS + NF + 4] += 1.0;  // sum of the 0/1 weights
+                p2plane_add<T, DIM, NV>(acc, px, py, pz, q[s], n[s]);
+            }
+            if (!exist) acc[NS + NF + 3] += 1.0;  // rejected point
         }
     }
     for (int64_t i = i0; k != 1 && i < N; i += stride) {
