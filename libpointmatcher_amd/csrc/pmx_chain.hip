@@ -857,6 +857,32 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                          (long long)nw, (double)(t1 - t0) * 0.01, tot / (double)nw, q(0.5), q(0.9), q(0.99),
                          sd.back(), tot, rsum / (double)nw, csum / (double)nw, fb, (double)(h[4 * last] - t0) * 0.01,
                          dur[(size_t)last]);
+            // the waves that handed lanes to the per-lane fallback walk
+            {
+                double fsum = 0, fmax = 0, nmax = 0;
+                int64_t fcnt = 0;
+                for (int64_t w = 0; w < nw; ++w) {
+                    if ((h[4 * w + 2] >> 32) > 0) {
+                        ++fcnt;
+                        fsum += dur[(size_t)w];
+                        fmax = std::max(fmax, dur[(size_t)w]);
+                    } else {
+                        nmax = std::max(nmax, dur[(size_t)w]);
+                    }
+                }
+                int64_t over = 0;  // waves over 150 us, and how many of them fell back
+                int64_t over_fb = 0;
+                for (int64_t w = 0; w < nw; ++w)
+                    if (dur[(size_t)w] > 150.0) {
+                        ++over;
+                        over_fb += (h[4 * w + 2] >> 32) > 0 ? 1 : 0;
+                    }
+                std::fprintf(stderr,
+                             "tile_prof fallback waves %lld mean %.1f us max %.1f us; other waves max %.1f us; "
+                             "waves over 150 us %lld (%lld with fallback)\n",
+                             (long long)fcnt, fcnt ? fsum / (double)fcnt : 0.0, fmax, nmax, (long long)over,
+                             (long long)over_fb);
+            }
             // duration by dispatch decile
             for (int dcl = 0; dcl < 10; ++dcl) {
                 double s2 = 0;

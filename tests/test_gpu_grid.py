@@ -211,3 +211,65 @@ def test_temporal_reuse_stays_exact(oracle, grid_mode, k):
         kc = int(os.environ.get("PMX_REUSE_CAND", "0") or 0)
         kr = kc if k < kc < 16 else k
         assert min(visits[2:5]) <= 1.1 * 20_000 * kr < visits[0]
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_neighbour_records_equal_gathers(oracle, grid_mode, monkeypatch, k):
+    # the k = 1 neighbour records (pmx_grid.hip write_nbr: the certificate's
+    # neighbour and the point-to-plane reduction's point and normal read in
+    # slot order) give the same matches and the same normal equations, bit
+    # for bit, as the gathers by id (PMX_NBR_CACHE=0), through reuse,
+    # a jump, a radius and a new reading
+    from libpointmatcher_amd.synth import t_gt
+
+    ref, nrm = reference_cloud(100_000)
+    rd = reading_cloud(20_000)
+    Tg = t_gt().astype(np.float32)
+    Tj = Tg.copy()
+    Tj[:3, 3] += 0.02
+    steps = [(np.eye(4, dtype=np.float32), np.inf), (Tg, np.inf), (Tg, np.inf), (Tj, np.inf), (Tj, 0.05),
+             (Tg, np.inf)]
+    runs = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("PMX_NBR_CACHE", on)
+        ctx = P.Context(0, np.float32)
+        ctx.set_search(1)
+        ctx.set_reference(ref, nrm)
+        out = []
+        for r in (rd, reading_cloud(20_000)[::-1].copy()):
+            ctx.set_reading(r)
+            for T, md in steps:
+                ctx.match(T, knn=k, max_dist=md)
+                d, i = ctx.get_matches()
+                ctx.outlier("TrimmedDistOutlierFilter", 0, ratio=0.85)
+                A, b, st = ctx.p2plane_system()
+                out.append((d, i, A, b, st.kept))
+        ctx.close()
+        runs.append(out)
+    for (d1, i1, A1, b1, k1), (d0, i0, A0, b0, k0) in zip(*runs):
+        assert np.array_equal(d1, d0) and np.array_equal(i1, i0)
+        assert np.array_equal(A1, A0) and np.array_equal(b1, b0) and k1 == k0
+    od, oi, _ = oracle.knn(ref, oracle.transform(Tg, rd), k=k, method="kdtree")
+    assert np.array_equal(runs[0][len(steps) - 1][0], od) and np.array_equal(runs[0][len(steps) - 1][1], oi)
+
+
+def test_reference_without_normals_after_one_with(oracle, grid_mode):
+    # a context that held a reference with normals (kept buffers) then a
+    # larger one without: nothing stale is gathered
+    ref1, nrm1 = reference_cloud(30_000)
+    ref2, _ = reference_cloud(120_000)
+    rd = reading_cloud(20_000)
+    T = np.eye(4, dtype=np.float32)
+    ctx = P.Context(0, np.float32)
+    ctx.set_search(1)
+    ctx.set_reference(ref1, nrm1)
+    ctx.set_reading(rd)
+    ctx.match(T, knn=1)
+    ctx.set_reference(ref2)
+    ctx.set_reading(rd)
+    for _ in range(2):
+        ctx.match(T, knn=1)
+        d, i = ctx.get_matches()
+        od, oi, _ = oracle.knn(ref2, oracle.transform(T, rd), k=1, method="kdtree")
+        assert np.array_equal(d, od) and np.array_equal(i, oi)
+    ctx.close()
