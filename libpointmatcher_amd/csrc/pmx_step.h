@@ -209,7 +209,11 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
         for (int i = 0; i < NF; ++i) x[i] = b[i] * (T)0;
 #else
         llt(A, NF, L);
+#if PMX_STEP_NOWC  // (timing experiment only: the conditioning bound's cost)
+        bool full = true;
+#else
         bool full = well_conditioned<T, NF>(A, L);
+#endif
         if (!full) {
             FullPivQR<T> qr;
             qr.compute(A, NF);
