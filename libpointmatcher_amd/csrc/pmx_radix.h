@@ -78,6 +78,25 @@ __global__ __launch_bounds__(kRsThreads) void rs_hist_kernel(const K* __restrict
     if (blockIdx.x == 0 && t == 0) head->tile_ctr[0] = 0u;
 }
 
+// the histogram launch's grid (a grid-stride loop: ~16 keys per thread)
+inline int rs_hist_blocks(int64_t n) {
+    return (int)std::min<int64_t>(256, std::max<int64_t>(1, (n + kRsThreads - 1) / kRsThreads / 16));
+}
+// the histogram pass folded into a kernel that produces the keys (one block
+// of kRsThreads; h: its LDS bins, zeroed and synchronised by the caller,
+// counted by it): the block's bins into head->hist, the first pass's
+// look-back words zeroed (grid-stride), the first tile counter reset
+template <typename K>
+__device__ __forceinline__ void rs_hist_block(unsigned int (*h)[kRsDigits], int npass, RsHead* __restrict__ head,
+                                              unsigned long long* __restrict__ state0, int64_t state_words) {
+    const int t = threadIdx.x;
+    for (int p = 0; p < npass; ++p)
+        if (h[p][t]) atomicAdd(&head->hist[p][t], h[p][t]);
+    const int64_t stride = (int64_t)gridDim.x * kRsThreads;
+    for (int64_t i = (int64_t)blockIdx.x * kRsThreads + t; i < state_words; i += stride) state0[i] = 0ull;
+    if (blockIdx.x == 0 && t == 0) head->tile_ctr[0] = 0u;
+}
+
 // look-back words: value in the low 32 bits, flag in the high ones
 constexpr unsigned long long kRsAgg = 1ull << 32, kRsInc = 2ull << 32;
 
@@ -233,17 +252,21 @@ __global__ __launch_bounds__(kRsThreads) void rs_pass_kernel(const K* __restrict
 // alternating between a and b; returns the buffer holding the result (b after
 // an odd number of passes, else a).  head: an RsHead, zero when allocated;
 // state: rs_state_bytes(n).
+// hist_ready: the keys' producer already added every pass's histogram into
+// head->hist, zeroed the first pass's look-back words and tile counter
+// (rs_hist_block below) — no histogram launch here.
 template <typename K>
 K* launch_radix_sort_keys(K* a, K* b, int64_t n, int begin_bit, int end_bit, RsHead* head, void* state,
-                          const LoopCtl* ctl, hipStream_t s) {
+                          const LoopCtl* ctl, hipStream_t s, bool hist_ready = false) {
     if (n <= 0) return a;
     const int npass = (end_bit - begin_bit + kRsBits - 1) / kRsBits;
     const int64_t ntiles = rs_tiles(n);
     const int64_t words = ntiles * kRsDigits;
     unsigned long long* st[2] = {(unsigned long long*)state, (unsigned long long*)state + words};
-    const int hb = (int)std::min<int64_t>(256, std::max<int64_t>(1, (n + kRsThreads - 1) / kRsThreads / 16));
-    hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(hb), dim3(kRsThreads), 0, s, a, n, begin_bit, npass, head, st[0], words,
-                       ctl);
+    const int hb = rs_hist_blocks(n);
+    if (!hist_ready)
+        hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(hb), dim3(kRsThreads), 0, s, a, n, begin_bit, npass, head, st[0],
+                           words, ctl);
     K* src = a;
     K* dst = b;
     for (int p = 0; p < npass; ++p) {

@@ -303,20 +303,32 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // keys in place, every other distance as the all-ones key (sorted after every
 // finite positive float's bits); the count of the kept ones.  The LSD radix
 // sort of pmx_radix.h then orders all n keys — the kept ones first.
+// (with the radix sort's histogram pass folded in, pmx_radix.h rs_hist_block:
+// the sort then starts with its first scatter pass)
 template <typename T>
 __global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, int64_t n,
                                                       typename KeyOf<T>::K* __restrict__ keys, int* __restrict__ count,
-                                                      const LoopCtl* __restrict__ ctl) {
+                                                      const LoopCtl* __restrict__ ctl, RsHead* __restrict__ rsh,
+                                                      unsigned long long* __restrict__ rs_state0,
+                                                      int64_t rs_words) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
+    constexpr int npass = KO::bits / kRsBits;
+    static_assert(KO::bits % kRsBits == 0 && npass <= kRsMaxPasses, "whole digits");
     __shared__ int wtot[4], wz[4];
+    __shared__ unsigned int h[npass][kRsDigits];
     if (ctl && ctl->done) return;
+    for (int p = 0; p < npass; ++p) h[p][threadIdx.x] = 0;
+    __syncthreads();
     int c = 0, z = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const T v = d[i];
         const bool keep = v != (T)__builtin_huge_val() && v > (T)0;
-        keys[i] = keep ? KO::key(v) : ~(K)0;
+        const K key = keep ? KO::key(v) : ~(K)0;
+        keys[i] = key;
+#pragma unroll
+        for (int p = 0; p < npass; ++p) atomicAdd(&h[p][rs_digit<K>(key, p * kRsBits, kRsBits)], 1u);
         c += keep ? 1 : 0;
         z += v == (T)0 ? 1 : 0;  // (finite, not kept: the quantile's population has them)
     }
@@ -335,6 +347,7 @@ __global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, i
         if (tot) atomicAdd(count, tot);
         if (zt) atomicAdd(count + 2, zt);
     }
+    rs_hist_block<K>(h, npass, rsh, rs_state0, rs_words);  // (after the barrier above: every bin counted)
 }
 // the header's counters zeroed for this call — a kernel rather than a fill so
 // that an iteration queued after the device loop stopped leaves the last
@@ -1423,8 +1436,9 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     hipLaunchKernelGGL(vt_hdr_reset_kernel, dim3(1), dim3(64), 0, s, hdr, ctl);
     K* src = keysB;  // (the sorted keys: the kept ones first)
     if (n > 0) {
-        hipLaunchKernelGGL(vt_keys_kernel<T>, dim3(grid_for(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl);
-        src = launch_radix_sort_keys<K>(keysA, keysB, n, 0, KeyOf<T>::bits, rsh, rs_state, ctl, s);
+        hipLaunchKernelGGL(vt_keys_kernel<T>, dim3(rs_hist_blocks(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl, rsh,
+                           (unsigned long long*)rs_state, rs_tiles(n) * kRsDigits);
+        src = launch_radix_sort_keys<K>(keysA, keysB, n, 0, KeyOf<T>::bits, rsh, rs_state, ctl, s, true);
     }
     // the head's running sum (written by the preparation launch's extra block)
     T* head = reinterpret_cast<T*>(hdr + 8);
