@@ -1652,7 +1652,8 @@ int pmx_vartrim_partial_sums(pmx_ctx* c, void* out, int64_t capacity, int64_t* c
     const size_t ksz = c->dtype == PMX_F64 ? 8 : 4;
     const auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     int cnt = 0;
-    HIPCHK(c, hipMemcpyAsync(&cnt, c->d_vt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&cnt, (const int*)c->d_vt + vartrim_hdr_copy(), sizeof(int), hipMemcpyDeviceToHost,
+                             c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *count = cnt;
     if (!out) return PMX_OK;

@@ -485,6 +485,7 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
 template <typename T>
 size_t vartrim_scratch_bytes(int64_t n);
 size_t vartrim_scratch_head();  // leading bytes of that scratch that must be zero at allocation
+int vartrim_hdr_copy();     // int offset of the last call's counters in that scratch (pmx_vartrim_partial_sums)
 
 // ---- reductions (pmx_reduce.hip) ----
 constexpr int kRedBlocks = 512;  // fixed reduction grid (deterministic sums)

@@ -349,13 +349,6 @@ __global__ __launch_bounds__(256) void vt_keys_kernel(const T* __restrict__ d, i
     }
     rs_hist_block<K>(h, npass, rsh, rs_state0, rs_words);  // (after the barrier above: every bin counted)
 }
-// the header's counters zeroed for this call — a kernel rather than a fill so
-// that an iteration queued after the device loop stopped leaves the last
-// call's header (count, error, zeros) for pmx_vartrim_partial_sums
-__global__ void vt_hdr_reset_kernel(int* __restrict__ hdr, const LoopCtl* __restrict__ ctl) {
-    if (ctl && ctl->done) return;
-    if (threadIdx.x < 64) hdr[threadIdx.x] = 0;
-}
 
 template <typename K>
 static size_t vt_sort_temp_bytes(int64_t n) {
@@ -1360,15 +1353,30 @@ __global__ __launch_bounds__(256) void vt_frms_final_kernel(const T* __restrict_
 // partial sum takes the positive ones only) followed by the sorted positive
 // keys.  The rank rule and the final select state are select_all_kernel's
 // (pick_phase, pass 0); one thread, one load instead of the radix passes.
+// header words: [0] kept keys (atomic), [1] error, [2] zero distances
+// (atomic), [8, 10) the head's running sum; the last call's counters are
+// copied from kVtHdrCopy on (the counters themselves are zeroed after use)
+constexpr int kVtHdrCopy = 16;
+int vartrim_hdr_copy() { return kVtHdrCopy; }
+
 template <typename T>
-__global__ void vt_quantile_kernel(const typename KeyOf<T>::K* __restrict__ sorted, const int* __restrict__ hdr,
+__global__ void vt_quantile_kernel(const typename KeyOf<T>::K* __restrict__ sorted, int* __restrict__ hdr,
                                    const double* __restrict__ ratio_dev, SelectState* __restrict__ st,
                                    int* __restrict__ iter_err, const LoopCtl* __restrict__ ctl) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
     if (threadIdx.x != 0 || (ctl && ctl->done)) return;
-    const unsigned long long zeros = (unsigned)hdr[2];
-    const unsigned long long total = (unsigned long long)(unsigned)hdr[0] + zeros;
+    // the last reader of this call's counters: they are kept for
+    // pmx_vartrim_partial_sums at kVtHdrCopy and zeroed for the next call
+    // (no reset launch; an iteration queued after the loop stopped returns
+    // before this, leaving the last call's copy)
+    const int h0 = hdr[0], h2 = hdr[2];
+    hdr[kVtHdrCopy] = h0;
+    hdr[kVtHdrCopy + 2] = h2;
+    hdr[0] = 0;
+    hdr[2] = 0;
+    const unsigned long long zeros = (unsigned)h2;
+    const unsigned long long total = (unsigned long long)(unsigned)h0 + zeros;
     const T q = (T)(*ratio_dev);
     unsigned long long rank = 0;
     int err = 0;
@@ -1433,7 +1441,6 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     pr.W1 = reinterpret_cast<int*>(p);
     p += al256(4 * (size_t)n);
 
-    hipLaunchKernelGGL(vt_hdr_reset_kernel, dim3(1), dim3(64), 0, s, hdr, ctl);
     K* src = keysB;  // (the sorted keys: the kept ones first)
     if (n > 0) {
         hipLaunchKernelGGL(vt_keys_kernel<T>, dim3(rs_hist_blocks(n)), dim3(256), 0, s, d, n, keysA, hdr, ctl, rsh,
