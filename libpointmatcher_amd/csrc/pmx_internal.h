@@ -488,7 +488,10 @@ size_t vartrim_scratch_head();  // leading bytes of that scratch that must be ze
 int vartrim_hdr_copy();     // int offset of the last call's counters in that scratch (pmx_vartrim_partial_sums)
 
 // ---- reductions (pmx_reduce.hip) ----
-constexpr int kRedBlocks = 512;  // fixed reduction grid (deterministic sums)
+#ifndef PMX_RED_BLOCKS
+#define PMX_RED_BLOCKS 512
+#endif
+constexpr int kRedBlocks = PMX_RED_BLOCKS;  // fixed reduction grid (deterministic sums)
 constexpr int kNVMax = 48;
 // point-to-plane result layout: upper triangle of A (NS), b (NF), then kept,
 // nonzero weights, rejected matches, rejected points, sum of the weights
