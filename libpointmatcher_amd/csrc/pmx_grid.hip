@@ -946,9 +946,12 @@ struct LaneQ {
 #ifndef PMX_LIGHT
 #define PMX_LIGHT 0  // (experiment: every miss through the wave-cooperative search, PMX_LIGHT waves per SIMD)
 #endif
+#ifndef PMX_LANE_WAVES
+#define PMX_LANE_WAVES 0  // (experiment: the per-lane kernel's waves per SIMD; 0 = 4 float / 2 double)
+#endif
 template <typename T, int KT>
 struct LaneWaves {
-    static constexpr int value = PMX_LIGHT ? PMX_LIGHT : (sizeof(T) == 8 ? 2 : 4);
+    static constexpr int value = PMX_LIGHT ? PMX_LIGHT : PMX_LANE_WAVES ? PMX_LANE_WAVES : (sizeof(T) == 8 ? 2 : 4);
 };
 #ifndef PMX_TILE_WAVES
 #define PMX_TILE_WAVES 0  // (experiment: the tile kernel's waves per SIMD; 0 = the per-lane kernel's default)
