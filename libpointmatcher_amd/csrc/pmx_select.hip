@@ -1314,45 +1314,14 @@ __global__ __launch_bounds__(256) void vt_frms_part_kernel(const T* __restrict__
 }
 
 // the blocks' argmins combined; writes the optimised ratio (:214-217)
-template <typename T>
-__global__ __launch_bounds__(256) void vt_frms_final_kernel(const T* __restrict__ part_v,
-                                                            const int* __restrict__ part_i,
-                                                            const int* __restrict__ count, int minEl, int maxEl,
-                                                            int points_nbr, double* __restrict__ ratio_dev,
-                                                            int* __restrict__ err, int* __restrict__ iter_err,
-                                                            const LoopCtl* __restrict__ ctl) {
-    __shared__ T sv[256];
-    __shared__ int si[256];
-    if (ctl && ctl->done) return;
-    const int t = threadIdx.x;
-    const int c = *count;
-    const int hi = maxEl < c ? maxEl : c;
-    if (c == 0 || hi - minEl <= 0) {
-        if (t == 0) {
-            const int e = c == 0 ? -2 : -3;
-            *err = e;
-            *iter_err = e;
-            *ratio_dev = __builtin_nan("");
-        }
-        return;
-    }
-    T bv = (T)__builtin_huge_val();
-    int bi = 0x7fffffff;
-    for (int b = t; b < kFrmsBlocks; b += 256) argmin_merge(bv, bi, part_v[b], part_i[b]);
-    block_argmin256(bv, bi, sv, si);
-    if (t == 0) {
-        const int minIndex = bi == 0x7fffffff ? 0 : bi;
-        *ratio_dev = (double)(T)((float)(minIndex + minEl) / (float)points_nbr);
-    }
-}
-
 // VarTrimmed's quantile at the optimised ratio (OutlierFiltersImpl.cpp:
 // 221-223, Matches::getDistsQuantile) straight from the sort: the radix
 // select over the same distances finds the same order statistic, and its
 // population — the finite distances — is the zeros (not sort keys: the
 // partial sum takes the positive ones only) followed by the sorted positive
 // keys.  The rank rule and the final select state are select_all_kernel's
-// (pick_phase, pass 0); one thread, one load instead of the radix passes.
+// (pick_phase, pass 0); one thread, one load instead of the radix passes —
+// run by the FRMS argmin's final block once it has the ratio (one launch).
 // header words: [0] kept keys (atomic), [1] error, [2] zero distances
 // (atomic), [8, 10) the head's running sum; the last call's counters are
 // copied from kVtHdrCopy on (the counters themselves are zeroed after use)
@@ -1360,12 +1329,11 @@ constexpr int kVtHdrCopy = 16;
 int vartrim_hdr_copy() { return kVtHdrCopy; }
 
 template <typename T>
-__global__ void vt_quantile_kernel(const typename KeyOf<T>::K* __restrict__ sorted, int* __restrict__ hdr,
-                                   const double* __restrict__ ratio_dev, SelectState* __restrict__ st,
-                                   int* __restrict__ iter_err, const LoopCtl* __restrict__ ctl) {
+__device__ __forceinline__ void vt_quantile_body(const typename KeyOf<T>::K* __restrict__ sorted,
+                                                 int* __restrict__ hdr, const double* __restrict__ ratio_dev,
+                                                 SelectState* __restrict__ st, int* __restrict__ iter_err) {
     using KO = KeyOf<T>;
     using K = typename KO::K;
-    if (threadIdx.x != 0 || (ctl && ctl->done)) return;
     // the last reader of this call's counters: they are kept for
     // pmx_vartrim_partial_sums at kVtHdrCopy and zeroed for the next call
     // (no reset launch; an iteration queued after the loop stopped returns
@@ -1403,6 +1371,42 @@ __global__ void vt_quantile_kernel(const typename KeyOf<T>::K* __restrict__ sort
     const K key = rank < zeros ? KO::key((T)0) : sorted[rank - zeros];
     st->prefix = (unsigned long long)key;
     st->limit = (double)KO::val(key);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void vt_frms_final_kernel(const T* __restrict__ part_v,
+                                                            const int* __restrict__ part_i,
+                                                            int* __restrict__ count, int minEl, int maxEl,
+                                                            int points_nbr, double* __restrict__ ratio_dev,
+                                                            int* __restrict__ err, int* __restrict__ iter_err,
+                                                            const LoopCtl* __restrict__ ctl,
+                                                            const typename KeyOf<T>::K* __restrict__ sorted,
+                                                            SelectState* __restrict__ st) {
+    __shared__ T sv[256];
+    __shared__ int si[256];
+    if (ctl && ctl->done) return;
+    const int t = threadIdx.x;
+    const int c = *count;
+    const int hi = maxEl < c ? maxEl : c;
+    if (c == 0 || hi - minEl <= 0) {
+        if (t == 0) {
+            const int e = c == 0 ? -2 : -3;
+            *err = e;
+            *iter_err = e;
+            *ratio_dev = __builtin_nan("");
+            vt_quantile_body<T>(sorted, count, ratio_dev, st, iter_err);
+        }
+        return;
+    }
+    T bv = (T)__builtin_huge_val();
+    int bi = 0x7fffffff;
+    for (int b = t; b < kFrmsBlocks; b += 256) argmin_merge(bv, bi, part_v[b], part_i[b]);
+    block_argmin256(bv, bi, sv, si);  // (its barriers: every thread has read the count)
+    if (t == 0) {
+        const int minIndex = bi == 0x7fffffff ? 0 : bi;
+        *ratio_dev = (double)(T)((float)(minIndex + minEl) / (float)points_nbr);
+        vt_quantile_body<T>(sorted, count, ratio_dev, st, iter_err);
+    }
 }
 
 template <typename T>
@@ -1464,9 +1468,9 @@ void launch_vartrim(const T* d, int64_t n, int points_nbr, T minRatio, T maxRati
     const int maxEl = (int)std::floor(maxRatio * (T)points_nbr);
     hipLaunchKernelGGL(vt_frms_part_kernel<T>, dim3(kFrmsBlocks), dim3(256), 0, s, cum, hdr, deno, minEl, maxEl, part_v,
                        part_i, ctl);
+    // (with the quantile at the optimised ratio: vt_quantile_body)
     hipLaunchKernelGGL(vt_frms_final_kernel<T>, dim3(1), dim3(256), 0, s, part_v, part_i, hdr, minEl, maxEl,
-                       points_nbr, ratio_dev, hdr + 1, err_dev, ctl);
-    hipLaunchKernelGGL(vt_quantile_kernel<T>, dim3(1), dim3(64), 0, s, src, hdr, ratio_dev, st, err_dev, ctl);
+                       points_nbr, ratio_dev, hdr + 1, err_dev, ctl, (const K*)src, st);
 }
 
 // explicit instantiations
