@@ -819,7 +819,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         }
         launch_grid_match<T>(c->grid_mode, (const P4<T>*)L.gpts, L.gidx, L.gstart, L.lo, L.h, L.dim,
                              (const P4<T>*)c->d_rd, c->N, c->d_waves, c->n_waves, Tm, knn, maxR2, c->tile_max,
-                             (T*)c->d_dists, c->d_ids, c->d_vpart, c->merge_counter ? nullptr : c->d_visited,
+                             (T*)c->d_dists, c->d_ids, c->d_vpart, c->merge_counter || c->step_counter ? nullptr : c->d_visited,
                              c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              c->has_radii ? (const T*)c->d_radii : nullptr, cold_now,

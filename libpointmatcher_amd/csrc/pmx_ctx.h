@@ -298,6 +298,7 @@ struct pmx_ctx {
     // the counters, pmx_selectall.h counter_merged), one launch fewer per
     // iteration; the point-to-plane launch then zeroes the spread counters
     bool merge_counter = false;  // (set for the match being enqueued)
+    bool step_counter = false;   // (the match's counter phase runs in the fused finalize + step launch)
     bool vpart_dirty = false;    // (the merged counter phase read them: the next reduction zeroes them)
     SpecSel spec_init{};  // (host staging of the reset)
     SpecSel* spec_now() const { return spec_on && loop_on ? d_spec : nullptr; }

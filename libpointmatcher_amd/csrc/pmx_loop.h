@@ -78,12 +78,12 @@ struct LoopState {
 
 template <typename T>
 void launch_finalize_step(const double* partials, int nblocks, int nv, double* out, double* res, unsigned int* ticket,
-                          LoopCtl* ctl, LoopState<T>* S, const int* iter_err, const unsigned long long* visited,
+                          LoopCtl* ctl, LoopState<T>* S, int* iter_err, unsigned long long* visited,
                           const T* means, const LoopCfg& cfg, T* trace, const int* spec_hit, long long* diag,
-                          hipStream_t s);
+                          unsigned long long* vpart, hipStream_t s);
 template <typename T>
 void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int prev_level,
-                      const double* Tprev, hipStream_t s);
+                      const double* Tprev, int* iter_err, hipStream_t s);
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
                       const unsigned long long* visited, const T* means, const LoopCfg& cfg, T* trace,

@@ -23,6 +23,7 @@
 #include "pmx_internal.h"
 
 #include "pmx_p2plane.h"
+#include "pmx_spec.h"
 #include "pmx_step.h"
 
 namespace pmx {
@@ -64,12 +65,14 @@ __global__ __launch_bounds__(256) void finalize_step_kernel(const double* __rest
                                                             double* __restrict__ out, double* __restrict__ res,
                                                             unsigned int* __restrict__ ticket, LoopCtl* __restrict__ ctl,
                                                             LoopState<T>* __restrict__ S,
-                                                            const int* __restrict__ iter_err,
-                                                            const unsigned long long* __restrict__ visited,
+                                                            int* __restrict__ iter_err,
+                                                            unsigned long long* __restrict__ visited,
                                                             const T* __restrict__ means, LoopCfg cfg,
                                                             T* __restrict__ trace, const int* __restrict__ spec_hit,
-                                                            long long* __restrict__ diag) {
+                                                            long long* __restrict__ diag,
+                                                            unsigned long long* __restrict__ vpart) {
     __shared__ double red[4];
+    __shared__ unsigned long long vred[2][4];
     __shared__ int s_last;
     __shared__ double sres[kStepRes];
     if (ctl->done) return;  // (uniform)
@@ -93,11 +96,42 @@ __global__ __launch_bounds__(256) void finalize_step_kernel(const double* __rest
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
         sres[threadIdx.x] = __hip_atomic_load(&res[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (vpart) {
+        static_assert(kVSlots == 256, "one spread slot per thread");
+        // the match's counter phase (counter_phase, pmx_spec.h) folded in
+        // here, no window in the loop: the pair / fallback counters summed
+        // and zeroed for the next match
+        unsigned long long v[2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            unsigned long long* p = vpart + (size_t)(q * kVSlots + threadIdx.x) * kVStride;
+            if (q < 2) v[q] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            v[0] += __shfl_xor(v[0], off);
+            v[1] += __shfl_xor(v[1], off);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            vred[0][threadIdx.x >> 6] = v[0];
+            vred[1][threadIdx.x >> 6] = v[1];
+        }
+    }
     __syncthreads();
     if (threadIdx.x != 0) return;
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (the next launch starts at 0)
     const int e = *iter_err;
-    const unsigned long long vis0 = visited[0], vis1 = visited[1];
+    unsigned long long vis0, vis1;
+    if (vpart) {
+        vis0 = (vred[0][0] + vred[0][1]) + (vred[0][2] + vred[0][3]);
+        vis1 = (vred[1][0] + vred[1][1]) + (vred[1][2] + vred[1][3]);
+        visited[0] = vis0;
+        visited[1] = vis1;
+        *iter_err = 0;  // (the next iteration's filters start clean; counter_phase's reset)
+    } else {
+        vis0 = visited[0];
+        vis1 = visited[1];
+    }
     const int hit = spec_hit ? *spec_hit : -1;
     if (diag) {
         long long* r = diag + (size_t)(S->iter % kDiagCap) * kDiagWords;
@@ -111,12 +145,12 @@ __global__ __launch_bounds__(256) void finalize_step_kernel(const double* __rest
 
 template <typename T>
 void launch_finalize_step(const double* partials, int nblocks, int nv, double* out, double* res, unsigned int* ticket,
-                          LoopCtl* ctl, LoopState<T>* S, const int* iter_err, const unsigned long long* visited,
+                          LoopCtl* ctl, LoopState<T>* S, int* iter_err, unsigned long long* visited,
                           const T* means, const LoopCfg& cfg, T* trace, const int* spec_hit, long long* diag,
-                          hipStream_t s) {
+                          unsigned long long* vpart, hipStream_t s) {
 #define PMX_FSTEP(R, M)                                                                                          \
     hipLaunchKernelGGL((finalize_step_kernel<T, R, M>), dim3(nv), dim3(256), 0, s, partials, nblocks, nv, out, res, \
-                       ticket, ctl, S, iter_err, visited, means, cfg, trace, spec_hit, diag)
+                       ticket, ctl, S, iter_err, visited, means, cfg, trace, spec_hit, diag, vpart)
     if (cfg.rows == 4) {
         if (cfg.minimizer == 0)
             PMX_FSTEP(4, 0);
@@ -131,16 +165,19 @@ void launch_finalize_step(const double* partials, int nblocks, int nv, double* o
 #undef PMX_FSTEP
 }
 template void launch_finalize_step<float>(const double*, int, int, double*, double*, unsigned int*, LoopCtl*,
-                                          LoopState<float>*, const int*, const unsigned long long*, const float*,
-                                          const LoopCfg&, float*, const int*, long long*, hipStream_t);
+                                          LoopState<float>*, int*, unsigned long long*, const float*,
+                                          const LoopCfg&, float*, const int*, long long*, unsigned long long*,
+                                          hipStream_t);
 template void launch_finalize_step<double>(const double*, int, int, double*, double*, unsigned int*, LoopCtl*,
-                                           LoopState<double>*, const int*, const unsigned long long*, const double*,
-                                           const LoopCfg&, double*, const int*, long long*, hipStream_t);
+                                           LoopState<double>*, int*, unsigned long long*, const double*,
+                                           const LoopCfg&, double*, const int*, long long*, unsigned long long*,
+                                           hipStream_t);
 
 // reset the loop state for a new ICP (checkers' init, ICP.cpp:368-369)
 template <typename T>
 __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __restrict__ S, LoopCfg cfg,
-                                 const T* __restrict__ T0, int level, int prev_level, Mat4d Tprev) {
+                                 const T* __restrict__ T0, int level, int prev_level, Mat4d Tprev,
+                                 int* __restrict__ iter_err) {
     // (the state zeroed by the whole wave, word by word: a LoopState<T> z = {}
     // copied by one lane went through scratch, ~60 us)
     static_assert(sizeof(LoopState<T>) % 4 == 0, "LoopState: whole words");
@@ -148,6 +185,7 @@ __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __rest
     for (int i = threadIdx.x; i < (int)(sizeof(LoopState<T>) / 4); i += blockDim.x) sw[i] = 0u;
     __syncthreads();
     if (threadIdx.x != 0) return;
+    *iter_err = 0;  // (a loop whose counter phase runs in the step resets it after each step only)
     const int rows = cfg.rows, D = rows - 1;
     for (int i = 0; i < rows * rows; ++i) S->Titer[i] = T0[i];
     for (int ci = 0; ci < cfg.n_checkers; ++ci) {
@@ -176,10 +214,10 @@ __global__ void loop_init_kernel(LoopCtl* __restrict__ ctl, LoopState<T>* __rest
 
 template <typename T>
 void launch_loop_init(LoopCtl* ctl, LoopState<T>* S, const LoopCfg& cfg, const T* T0, int level, int prev_level,
-                      const double* Tprev, hipStream_t s) {
+                      const double* Tprev, int* iter_err, hipStream_t s) {
     Mat4d tp;
     for (int i = 0; i < 16; ++i) tp.m[i] = Tprev[i];
-    hipLaunchKernelGGL(loop_init_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, cfg, T0, level, prev_level, tp);
+    hipLaunchKernelGGL(loop_init_kernel<T>, dim3(1), dim3(64), 0, s, ctl, S, cfg, T0, level, prev_level, tp, iter_err);
 }
 template <typename T>
 void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const int* iter_err,
@@ -202,9 +240,9 @@ void launch_loop_step(LoopCtl* ctl, LoopState<T>* S, const double* res, const in
 #undef PMX_STEP
 }
 template void launch_loop_init<float>(LoopCtl*, LoopState<float>*, const LoopCfg&, const float*, int, int,
-                                      const double*, hipStream_t);
+                                      const double*, int*, hipStream_t);
 template void launch_loop_init<double>(LoopCtl*, LoopState<double>*, const LoopCfg&, const double*, int, int,
-                                       const double*, hipStream_t);
+                                       const double*, int*, hipStream_t);
 template void launch_loop_step<float>(LoopCtl*, LoopState<float>*, const double*, const int*,
                                       const unsigned long long*, const float*, const LoopCfg&, float*, const int*,
                                       long long*, hipStream_t);

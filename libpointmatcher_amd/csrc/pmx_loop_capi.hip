@@ -137,7 +137,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
                                ? c->ids_level
                                : -1;
     launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, prev_level,
-                        c->Tstep, c->stream);
+                        c->Tstep, c->d_iter_err, c->stream);
     // quantile window: a fresh window each loop (the first iteration runs the
     // radix passes, which centre the window for the next)
     const int k0 = cfg->n_filters > 0 ? cfg->filter_kind[0] : -1;
@@ -209,6 +209,22 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     const int k0 = cfg.n_filters > 0 ? cfg.filter_kind[0] : -1;
     c->merge_counter = c->spec_on && !sharded(c) && cfg.minimizer == 0 && c->grid_mode >= 1 && c->N > 0 &&
                        cfg.knn <= kLaneMaxK && (k0 == PMX_FILTER_TRIMMED || k0 == PMX_FILTER_MEDIANDIST);
+    // no quantile window (a MaxDist chain, or none): the counter phase runs
+    // in the fused finalize + step launch instead (one launch fewer; the
+    // step is the first reader of the counters).  Not with a robust filter:
+    // its replayed iterations return before the step.
+    static const bool fuse_env = [] {
+        const char* e = std::getenv("PMX_FUSE_STEP");
+        return !e || std::atoi(e) != 0;
+    }();
+    static const bool step_counter_env = [] {
+        const char* e = std::getenv("PMX_STEP_COUNTER");
+        return !e || std::atoi(e) != 0;
+    }();
+    bool robust = false;
+    for (int i = 0; i < cfg.n_filters; ++i) robust = robust || cfg.filter_kind[i] == PMX_FILTER_ROBUST;
+    c->step_counter = step_counter_env && fuse_env && !c->spec_on && !sharded(c) && !robust && c->grid_mode >= 1 &&
+                      c->N > 0;
     c->vpart_dirty = false;
     c->shard_async = c->spec_on && sharded(c) && !c->shard_replay && !c->spec_fresh &&
                      c->shard_hit_streak >= kAsyncAfterHits;
@@ -249,22 +265,21 @@ int loop_enqueue_iteration(pmx_ctx* c) {
         if ((rc = outlier_impl<T>(c, cfg.filter_kind[i], i, p[0], p[1], p[2]))) return rc;
     }
     // one rank: the minimiser's last finalize and the step in one launch
-    static const bool fuse_env = [] {
-        const char* e = std::getenv("PMX_FUSE_STEP");
-        return !e || std::atoi(e) != 0;
-    }();
     c->fuse_final = fuse_env && !sharded(c);
     c->final_out = nullptr;
     rc = cfg.minimizer == 0 ? p2plane_enqueue<T>(c) : p2point_enqueue<T>(c);
     const bool fused = c->fuse_final && c->final_out;
     c->fuse_final = false;
+    const bool step_counter = c->step_counter;
+    c->step_counter = false;
     if (rc) return rc;
+    if (step_counter && !fused) return fail(c, PMX_E_STATE, "device loop: counter phase left unfolded");
     const int* hitp = c->spec_on && c->d_spec ? &c->d_spec->hit : nullptr;
     T* trace = cfg.keep_trace ? (T*)c->d_trace : nullptr;
     if (fused)
         launch_finalize_step<T>(c->d_partials, kRedBlocks, c->final_nv, c->final_out, c->d_result, c->d_ticket,
                                 c->d_ctl, (LoopState<T>*)c->d_loop, c->d_iter_err, c->d_visited, (const T*)c->d_means,
-                                c->loop_dev, trace, hitp, c->d_diag, c->stream);
+                                c->loop_dev, trace, hitp, c->d_diag, step_counter ? c->d_vpart : nullptr, c->stream);
     else
         launch_loop_step<T>(c->d_ctl, (LoopState<T>*)c->d_loop, c->d_result, c->d_iter_err, c->d_visited,
                             (const T*)c->d_means, c->loop_dev, trace, hitp, c->d_diag, c->stream);
