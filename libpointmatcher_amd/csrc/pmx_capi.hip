@@ -171,6 +171,7 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PMX_COLD_TREE")) c->tree_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_REUSE_CAND")) c->reuse_cand_req = std::max(0, std::min(15, std::atoi(e)));
     if (const char* e = std::getenv("PMX_TILE_DISPATCH")) c->tile_dispatch_req = std::atoi(e);
     if (const char* e = std::getenv("PMX_COOP_MAX")) c->coop_max = std::max(0, std::min(256, std::atoi(e)));
@@ -274,6 +275,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     if (c->h_flags) (void)hipHostFree(c->h_flags);
     if (c->d_specx) (void)hipFree(c->d_specx);
     if (c->side_ev) (void)hipEventDestroy(c->side_ev);
+    if (c->side_start_ev) (void)hipEventDestroy(c->side_start_ev);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->d_raw2) (void)hipFree(c->d_raw2);
     for (hipEvent_t e : {c->table_ev, c->raw_ev, c->copy_ev, c->nrm_ev})

@@ -314,6 +314,25 @@ int build_one_level(pmx_ctx* c, int l, const SetupScratch& sc, hipStream_t st) {
         c->grid_ready = false;
         return fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")");
     }
+    // the cold level's box tree (a new reading's first match), from the
+    // level's sorted cell keys still in this scratch
+    L.has_tree = false;
+    if (c->tree_on && c->grid_mode >= 1 && l == cold_level(c)) {
+        int64_t nrec = 0;
+        if (tree_layout(valid, L.tree_off, &nrec) < 1) return fail(c, PMX_E_BAD_PARAM, "tree layout");
+        if (!room(&L.tree_rec, &L.cap_tree, sizeof(float4) * kTreeRecF4 * (size_t)nrec) ||
+            (!L.tree_hdr && hipMalloc((void**)&L.tree_hdr, 64) != hipSuccess)) {
+            c->grid_ready = false;
+            return fail(c, PMX_E_HIP, "grid tree allocation failed");
+        }
+        const int rt = build_tree_device<T>((const P4<T>*)L.gpts, L.gstart, s, valid, sc, (float4*)L.tree_rec,
+                                            L.tree_hdr, L.tree_off, st);
+        if (rt) {
+            c->grid_ready = false;
+            return fail(c, PMX_E_HIP, "grid tree build failed (" + std::to_string(rt) + ")");
+        }
+        L.has_tree = true;
+    }
     for (int a = 0; a < 3; ++a) {
         L.lo[a] = s.lo[a];
         L.dim[a] = s.g[a];
@@ -347,6 +366,9 @@ int publish_levels(pmx_ctx* c) {
         }
         D.G.h = L.h;
         D.G.inv_h = 1.0 / L.h;
+        D.tree.rec = L.has_tree ? (const float4*)L.tree_rec : nullptr;
+        D.tree.hdr = L.has_tree ? L.tree_hdr : nullptr;
+        for (int i = 0; i < kTreeMaxLevels; ++i) D.tree.off[i] = L.tree_off[i];
     }
     if (!c->d_gdesc) HIPCHK(c, hipMalloc(&c->d_gdesc, sizeof(GridDesc<T>) * kMaxLevels));
     // (stream-ordered and asynchronous: the host goes on — the reading's
@@ -394,13 +416,19 @@ int build_levels_cold(pmx_ctx* c, int cold) {
         HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIPCHK(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
         HIPCHK(c, hipEventCreateWithFlags(&c->side_ev, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->side_start_ev, hipEventDisableTiming));
     }
     int64_t cells = 1;
     for (int l = 0; l < cold; ++l) cells = std::max(cells, c->level_shapes[(size_t)l].cells);
     int rc = setup_room(c, c->M, cells, true);
     if (rc) return rc;
-    // (the reference's pack and the sizing counts completed: build_grid read
-    // them back, so the side stream needs no event to start)
+    // The side builds read d_ref and d_nrm: the points' pack completed before
+    // build_grid read the sizing counts back, but the normals' pack was
+    // enqueued on the context stream after that (before_levels) and may still
+    // be waiting for its upload.  A device-side wait on everything enqueued
+    // so far orders both (no host synchronisation).
+    HIPCHK(c, hipEventRecord(c->side_start_ev, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->side, c->side_start_ev, 0));
     for (int l = 0; l < cold; ++l)
         if ((rc = build_one_level<T>(c, l, c->setup_side, c->side))) return rc;
     HIPCHK(c, hipEventRecord(c->side_ev, c->side));
@@ -808,6 +836,9 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * c->nranks));
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx + (size_t)kSpecXStride * c->rank : nullptr;
         const bool cold_now = no_prev && c->reuse_on;
+        // (the box tree of the match's level; in loop mode the kernel reads the
+        // level from LoopCtl, which the loop starts at c->level)
+        const int tree_level = cold_now && c->grid_mode >= 1 && knn <= kLaneMaxK && L.has_tree ? c->level : -1;
         // (development profile of the cold form's waves, PMX_TILE_PROF=1: per
         // wave duration, rounds and points copied, summarised on stderr)
         static const bool tile_prof = std::getenv("PMX_TILE_PROF") != nullptr;
@@ -823,7 +854,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              c->has_radii ? (const T*)c->d_radii : nullptr, cold_now,
-                             c->loop_on && c->loop_dev.tile_dispatch, e0, e1, c->stream);
+                             c->loop_on && c->loop_dev.tile_dispatch, tree_level, e0, e1, c->stream);
         if (prof_buf) {
             std::vector<unsigned long long> h((size_t)(4 * nw));
             HIPCHK(c, hipMemcpyAsync(h.data(), prof_buf, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1037,9 +1068,23 @@ void choose_level(pmx_ctx* c, uint64_t visited, uint64_t full) {
 }
 
 // level l built (a coarser level on its first use)
+// A coarser level that fails to build (allocation) leaves the grid as it was:
+// the built levels stay valid and published (grid_ready kept, levels_built
+// unchanged), the failed level's buffers are released, and the error is
+// returned (choose_level then keeps the current level: exact, only slower).
 int ensure_level(pmx_ctx* c, int l) {
     if (l < c->levels_built) return PMX_OK;
-    return c->dtype == PMX_F64 ? build_levels<double>(c, l) : build_levels<float>(c, l);
+    const int built = c->levels_built;
+    const bool ready = c->grid_ready;
+    const int rc = c->dtype == PMX_F64 ? build_levels<double>(c, l) : build_levels<float>(c, l);
+    if (rc != PMX_OK && built > 0) {
+        (void)hipStreamSynchronize(c->stream);  // (the failed builds' kernels may read the buffers)
+        // (levels built before the failing one were not published either)
+        for (int i = built; i < (int)c->levels.size() && i <= l; ++i) c->levels[(size_t)i].release();
+        c->levels_built = built;
+        c->grid_ready = ready;
+    }
+    return rc;
 }
 
 // slot-major device array -> query-major host array (the reference's order)

@@ -55,7 +55,7 @@ __device__ __forceinline__ unsigned rs_digit(K k, int shift, int bits) {
 // every pass's digit histogram; zeroes pass 0's look-back state and tile counter
 template <typename K>
 __global__ __launch_bounds__(kRsThreads) void rs_hist_kernel(const K* __restrict__ keys, int64_t n, int begin_bit,
-                                                             int npass, RsHead* __restrict__ head,
+                                                             int end_bit, int npass, RsHead* __restrict__ head,
                                                              unsigned long long* __restrict__ state0,
                                                              int64_t state_words, const LoopCtl* __restrict__ ctl) {
     __shared__ unsigned int h[kRsMaxPasses][kRsDigits];
@@ -67,8 +67,10 @@ __global__ __launch_bounds__(kRsThreads) void rs_hist_kernel(const K* __restrict
     for (int64_t i = (int64_t)blockIdx.x * kRsThreads + t; i < n; i += stride) {
         const K k = keys[i];
         for (int p = 0; p < npass; ++p) {
+            // (the last pass's digit is narrower when the key range is not a
+            // whole number of digits: the same width rs_pass_kernel scatters by)
             const int sh = begin_bit + p * kRsBits;
-            atomicAdd(&h[p][rs_digit<K>(k, sh, kRsBits)], 1u);
+            atomicAdd(&h[p][rs_digit<K>(k, sh, min(kRsBits, end_bit - sh))], 1u);
         }
     }
     __syncthreads();
@@ -265,7 +267,7 @@ K* launch_radix_sort_keys(K* a, K* b, int64_t n, int begin_bit, int end_bit, RsH
     unsigned long long* st[2] = {(unsigned long long*)state, (unsigned long long*)state + words};
     const int hb = rs_hist_blocks(n);
     if (!hist_ready)
-        hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(hb), dim3(kRsThreads), 0, s, a, n, begin_bit, npass, head, st[0],
+        hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(hb), dim3(kRsThreads), 0, s, a, n, begin_bit, end_bit, npass, head, st[0],
                            words, ctl);
     K* src = a;
     K* dst = b;

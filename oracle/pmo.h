@@ -142,6 +142,11 @@ int pmo_p2point_f32(int rows, const float* reading_t, const float* ref, const fl
 int pmo_icp_f32(const pmo_cfg* cfg, const float* reading, int rows, int64_t N,
                 const float* ref, int64_t M, const float* ref_normals,
                 const float* T_init, float* T_out, pmo_stats* st, float* trace);
+/* the same, cfg->robust being a RobustOutlierFilter object kept across
+ * calls (its iteration count and scale updated, OutlierFiltersImpl.cpp:500-540) */
+int pmo_icp_keep_f32(pmo_cfg* cfg, const float* reading, int rows, int64_t N,
+                     const float* ref, int64_t M, const float* ref_normals,
+                     const float* T_init, float* T_out, pmo_stats* st, float* trace);
 /* SurfaceNormalDataPointsFilter (DataPointsFilters/SurfaceNormal.cpp:80-290):
  * outputs point-major, any may be NULL (see pmo_impl.inc for the eigen
  * convention); smooth = smoothNormals */
@@ -187,6 +192,11 @@ int pmo_p2point_f64(int rows, const double* reading_t, const double* ref, const 
 int pmo_icp_f64(const pmo_cfg* cfg, const double* reading, int rows, int64_t N,
                 const double* ref, int64_t M, const double* ref_normals,
                 const double* T_init, double* T_out, pmo_stats* st, double* trace);
+/* the same, cfg->robust being a RobustOutlierFilter object kept across
+ * calls (its iteration count and scale updated, OutlierFiltersImpl.cpp:500-540) */
+int pmo_icp_keep_f64(pmo_cfg* cfg, const double* reading, int rows, int64_t N,
+                     const double* ref, int64_t M, const double* ref_normals,
+                     const double* T_init, double* T_out, pmo_stats* st, double* trace);
 int pmo_surface_normals_f64(const double* pts, int rows, int64_t n, int k, double maxDist, int threads, int smooth,
                             double* normals, double* dens, double* evals, double* evecs, double* ids, double* mdist,
                             int64_t* degenerate);

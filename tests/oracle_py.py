@@ -227,8 +227,10 @@ def make_cfg(knn=1, max_dist=np.inf, method="kdtree", threads=1, filters=(("Trim
     return cfg
 
 
-def icp(cfg, reading, reference, normals=None, T_init=None, trace=False):
-    """reading, reference: (n, rows) arrays incl. homogeneous row.  Returns (rc, T, stats, trace)."""
+def icp(cfg, reading, reference, normals=None, T_init=None, trace=False, keep_robust=False):
+    """reading, reference: (n, rows) arrays incl. homogeneous row.  Returns (rc, T, stats, trace).
+    keep_robust: cfg.robust is one RobustOutlierFilter object kept across calls
+    (pmo_icp_keep: its iteration count and scale are updated in cfg)."""
     dt = reference.dtype
     reading = np.ascontiguousarray(reading, dtype=dt)
     reference = np.ascontiguousarray(reference)
@@ -241,7 +243,7 @@ def icp(cfg, reading, reference, normals=None, T_init=None, trace=False):
     maxit = max(cfg.counter_max, 1) if cfg.counter_max >= 0 else 4096
     tr = np.zeros((maxit, rows, rows), dt) if trace else None
     nrm = np.ascontiguousarray(normals, dtype=dt) if normals is not None else None
-    rc = getattr(lib(), "pmo_icp_" + _sfx(dt))(
+    rc = getattr(lib(), ("pmo_icp_keep_" if keep_robust else "pmo_icp_") + _sfx(dt))(
         C.byref(cfg), _p(reading), rows, C.c_int64(reading.shape[0]), _p(reference),
         C.c_int64(reference.shape[0]), _p(nrm), _p(T_init), _p(T_out), C.byref(st), _p(tr))
     if trace:

@@ -235,20 +235,22 @@ def test_robust_device_loop_equals_modules(monkeypatch, oracle, dtype, case):
     {"robustFct": "huber", "scaleEstimator": "berg", "tuning": 0.05},
     {"robustFct": "cauchy", "scaleEstimator": "mad", "tuning": 1, "nbIterationForScale": 3},
 ])
-def test_robust_second_compute_loop_equals_modules(monkeypatch, dtype, params):
+def test_robust_second_compute_vs_oracle(monkeypatch, oracle, dtype, params):
     """RobustOutlierFilter keeps its iteration count across compute() calls
-    (OutlierFiltersImpl.cpp:509-540: berg's first-call scale, the
+    (OutlierFiltersImpl.cpp:500-540: berg's first-call scale, the
     nbIterationForScale schedule).  A second compute on the same ICP object
-    starts past the first call's iterations; the device loop (scale mode per
-    loop iteration from the host module's count) must equal the per-module
-    path on both calls: same iterations, kept pairs, T within 1e-5 / 1e-12."""
+    starts past the first call's iterations.  Both calls of the device loop
+    (scale mode per loop iteration from the host module's count) and of the
+    per-module path against the oracle ICP with ONE filter object kept across
+    its two calls (pmo_icp_keep): same iterations, T within 1e-5 / 1e-12."""
     from helpers import chain_yaml
 
     ref, _ = reference_cloud(40_000, dtype)
     rd = reading_cloud(20_000, dtype)
     rd2 = reading_cloud(15_000, dtype)
-    yaml = chain_yaml(knn=2, filters=(("RobustOutlierFilter", params),), minimizer="PointToPointErrorMinimizer",
-                      maxit=12)
+    maxit = 12
+    filters = (("RobustOutlierFilter", params),)
+    yaml = chain_yaml(knn=2, filters=filters, minimizer="PointToPointErrorMinimizer", maxit=maxit)
     out = {}
     for mode in ("1", "0"):
         monkeypatch.setenv("PMX_DEVICE_LOOP", mode)
@@ -261,8 +263,26 @@ def test_robust_second_compute_loop_equals_modules(monkeypatch, dtype, params):
             res.append((T.astype(np.float64), s.iterations, s.kept))
         icp.close()
         out[mode] = res
+    cfg = oracle.make_cfg(knn=2, filters=filters, minimizer="PointToPointErrorMinimizer", counter_max=maxit,
+                          threads=8)
+    ores = []
+    for r in (rd, rd2):
+        rc, To, so, _ = oracle.icp(cfg, r, ref, keep_robust=True)
+        assert rc == 0
+        ores.append((To.astype(np.float64), so.iterations))
+    # the filter object saw both calls' iterations (its counter starts at 1)
+    assert cfg.robust.iteration == 1 + ores[0][1] + ores[1][1]
     tol = 1e-5 if dtype == np.float32 else 1e-12
-    for (Tl, il, kl), (Tm, im, km) in zip(out["1"], out["0"]):
-        print(f"{params['scaleEstimator']}: iterations {il}/{im} kept {kl}/{km} |dT| {np.linalg.norm(Tl - Tm):.3g}")
-        assert il == im and kl == km
-        assert np.linalg.norm(Tl - Tm) <= tol
+    for call in range(2):
+        (Tl, il, kl), (Tm, im, km), (To, io) = out["1"][call], out["0"][call], ores[call]
+        fl, fm = np.linalg.norm(Tl - To), np.linalg.norm(Tm - To)
+        print(f"{params['scaleEstimator']} call {call + 1}: iterations {il}/{im}/{io} kept {kl}/{km} "
+              f"|dT| loop {fl:.3g} modules {fm:.3g}")
+        assert il == im == io and kl == km
+        assert fl <= tol and fm <= tol
+    # the second call differs from a fresh filter's (the schedule carried over)
+    cfg2 = oracle.make_cfg(knn=2, filters=filters, minimizer="PointToPointErrorMinimizer", counter_max=maxit,
+                           threads=8)
+    rc, Tf, _, _ = oracle.icp(cfg2, rd2, ref)
+    assert rc == 0
+    print(f"fresh filter vs kept on call 2: |dT| {np.linalg.norm(Tf.astype(np.float64) - ores[1][0]):.3g}")

@@ -142,3 +142,33 @@ def test_oracle_icp_robust_config_matches_ref_trans(golden, oracle):
     err = rel_displacement(T, refT, g["vtk1"])
     print(f"oracle robust icp: rel err {err:.5f}, iterations {st.iterations}")
     assert err < kat["icp_data_rel_tol"]
+
+
+@pytest.mark.parametrize("scale,nb", [("berg", 0), ("mad", 3)])
+def test_oracle_icp_keeps_robust_state_across_calls(golden, oracle, scale, nb):
+    """pmo_icp_keep: the filter object outlives a compute() (the reference's ICP
+    owns its chain, OutlierFiltersImpl.cpp:500-540).  Its first call equals
+    pmo_icp's; the iteration counter advances by the iterations run (one
+    robustFiltering per iteration) on both calls, and the second call differs
+    from a fresh filter's compute."""
+    g, _ = golden
+    p = {"robustFct": "huber" if scale == "berg" else "cauchy", "scaleEstimator": scale, "tuning": 0.05 if
+         scale == "berg" else 1, "nbIterationForScale": nb}
+    filt = (("RobustOutlierFilter", p),)
+    rd, ref = hom(g["vtk1"], np.float32), hom(g["vtk0"], np.float32)
+    mk = lambda: oracle.make_cfg(knn=3, filters=filt, minimizer="PointToPointErrorMinimizer", counter_max=6,
+                                 threads=8)
+    c = mk()
+    rc, T1, s1, _ = oracle.icp(c, rd, ref, keep_robust=True)
+    rc0, T0, s0, _ = oracle.icp(mk(), rd, ref)
+    assert rc == rc0 == 0 and np.array_equal(T1, T0) and s1.iterations == s0.iterations
+    assert c.robust.iteration == 1 + s1.iterations
+    it1 = c.robust.iteration
+    rc, T2, s2, _ = oracle.icp(c, rd, ref, keep_robust=True)
+    assert rc == 0 and c.robust.iteration == it1 + s2.iterations
+    # the schedule carried over: past nbIterationForScale (mad) the scale is
+    # kept, and berg never re-runs its first-call estimate — so the second
+    # call is not a fresh filter's compute
+    rcf, Tf, _, _ = oracle.icp(mk(), rd, ref)
+    assert rcf == 0
+    assert not np.array_equal(T2, Tf)
