@@ -171,7 +171,6 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
     if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_COLD_TREE")) c->tree_on = std::atoi(e) != 0;
     if (const char* e = std::getenv("PMX_REUSE_CAND")) c->reuse_cand_req = std::max(0, std::min(15, std::atoi(e)));
     if (const char* e = std::getenv("PMX_TILE_DISPATCH")) c->tile_dispatch_req = std::atoi(e);
     if (const char* e = std::getenv("PMX_COOP_MAX")) c->coop_max = std::max(0, std::min(256, std::atoi(e)));

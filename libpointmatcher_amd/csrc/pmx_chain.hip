@@ -314,25 +314,7 @@ int build_one_level(pmx_ctx* c, int l, const SetupScratch& sc, hipStream_t st) {
         c->grid_ready = false;
         return fail(c, PMX_E_HIP, "grid level build failed (" + std::to_string(r) + ")");
     }
-    // the cold level's box tree (a new reading's first match), from the
-    // level's sorted cell keys still in this scratch
-    L.has_tree = false;
-    if (c->tree_on && c->grid_mode >= 1 && l == cold_level(c)) {
-        int64_t nrec = 0;
-        if (tree_layout(valid, L.tree_off, &nrec) < 1) return fail(c, PMX_E_BAD_PARAM, "tree layout");
-        if (!room(&L.tree_rec, &L.cap_tree, sizeof(float4) * kTreeRecF4 * (size_t)nrec) ||
-            (!L.tree_hdr && hipMalloc((void**)&L.tree_hdr, 64) != hipSuccess)) {
-            c->grid_ready = false;
-            return fail(c, PMX_E_HIP, "grid tree allocation failed");
-        }
-        const int rt = build_tree_device<T>((const P4<T>*)L.gpts, L.gstart, s, valid, sc, (float4*)L.tree_rec,
-                                            L.tree_hdr, L.tree_off, st);
-        if (rt) {
-            c->grid_ready = false;
-            return fail(c, PMX_E_HIP, "grid tree build failed (" + std::to_string(rt) + ")");
-        }
-        L.has_tree = true;
-    }
+
     for (int a = 0; a < 3; ++a) {
         L.lo[a] = s.lo[a];
         L.dim[a] = s.g[a];
@@ -366,9 +348,6 @@ int publish_levels(pmx_ctx* c) {
         }
         D.G.h = L.h;
         D.G.inv_h = 1.0 / L.h;
-        D.tree.rec = L.has_tree ? (const float4*)L.tree_rec : nullptr;
-        D.tree.hdr = L.has_tree ? L.tree_hdr : nullptr;
-        for (int i = 0; i < kTreeMaxLevels; ++i) D.tree.off[i] = L.tree_off[i];
     }
     if (!c->d_gdesc) HIPCHK(c, hipMalloc(&c->d_gdesc, sizeof(GridDesc<T>) * kMaxLevels));
     // (stream-ordered and asynchronous: the host goes on — the reading's
@@ -836,9 +815,6 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * c->nranks));
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx + (size_t)kSpecXStride * c->rank : nullptr;
         const bool cold_now = no_prev && c->reuse_on;
-        // (the box tree of the match's level; in loop mode the kernel reads the
-        // level from LoopCtl, which the loop starts at c->level)
-        const int tree_level = cold_now && c->grid_mode >= 1 && knn <= kLaneMaxK && L.has_tree ? c->level : -1;
         // (development profile of the cold form's waves, PMX_TILE_PROF=1: per
         // wave duration, rounds and points copied, summarised on stderr)
         static const bool tile_prof = std::getenv("PMX_TILE_PROF") != nullptr;
@@ -854,7 +830,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              c->d_iter_err, ru, loop_ctl(c),
                              (const GridDesc<T>*)c->d_gdesc, spec, c->d_sel, xseg,
                              c->has_radii ? (const T*)c->d_radii : nullptr, cold_now,
-                             c->loop_on && c->loop_dev.tile_dispatch, tree_level, e0, e1, c->stream);
+                             c->loop_on && c->loop_dev.tile_dispatch, e0, e1, c->stream);
         if (prof_buf) {
             std::vector<unsigned long long> h((size_t)(4 * nw));
             HIPCHK(c, hipMemcpyAsync(h.data(), prof_buf, h.size() * 8, hipMemcpyDeviceToHost, c->stream));

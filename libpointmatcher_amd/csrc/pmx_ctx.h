@@ -59,25 +59,16 @@ struct GridLevel {
     double h = 1.0;
     int dim[3] = {1, 1, 1};
     double ppc = 0.0;
-    // the box tree over the level's occupied cells (the cold match's,
-    // pmx_grid_tree.inc): records + header; null: none
-    void* tree_rec = nullptr;
-    uint32_t* tree_hdr = nullptr;
-    uint32_t tree_off[kTreeMaxLevels] = {};
-    bool has_tree = false;
     // allocated capacities (a new reference reuses the buffers when it fits:
     // hipMalloc / hipFree of 4 buffers x 6 levels was a large part of setup)
-    size_t cap_pts = 0, cap_gpn = 0, cap_idx = 0, cap_start = 0, cap_tree = 0;
+    size_t cap_pts = 0, cap_gpn = 0, cap_idx = 0, cap_start = 0;
     void release() {
-        for (void* b : {gpts, gpn, (void*)gidx, (void*)gstart, tree_rec, (void*)tree_hdr})
+        for (void* b : {gpts, gpn, (void*)gidx, (void*)gstart})
             if (b) (void)hipFree(b);
         gpts = gpn = nullptr;
         gidx = nullptr;
         gstart = nullptr;
-        tree_rec = nullptr;
-        tree_hdr = nullptr;
-        has_tree = false;
-        cap_pts = cap_gpn = cap_idx = cap_start = cap_tree = 0;
+        cap_pts = cap_gpn = cap_idx = cap_start = 0;
     }
 };
 
@@ -120,7 +111,6 @@ struct pmx_ctx {
     std::vector<int64_t> level_seen;   // match count when it was seen (0: never)
     int64_t match_count = 0;
     bool adaptive = true;
-    bool tree_on = true;          // the cold match over the cold level's box tree (PMX_COLD_TREE=0: the tile form)
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
     void* d_safe = nullptr;       // T[N]: safe radius per query

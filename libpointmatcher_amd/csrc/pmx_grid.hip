@@ -1161,25 +1161,18 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
 
 // ------------------------------------------------------------ tile kernel --
 #include "pmx_grid_tile.inc"
-// ------------------------------------------------------------ tree kernel --
-#include "pmx_grid_tree.inc"
 
 template <typename T, int KT>
 static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const uint32_t* start, const GridGeom& G,
                       const P4<T>* rd, int64_t N, const uint32_t* waves, int64_t n_waves, const Mat4<T>& Tm, int knn,
                       T maxR2, uint32_t max_pts, T* dists, int32_t* ids, unsigned long long* visited,
                       const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
-                      const T* radii, bool cold, bool tile_disp, int tree_level, hipEvent_t e0, hipEvent_t e1,
-                      hipStream_t s) {
+                      const T* radii, bool cold, bool tile_disp, hipEvent_t e0, hipEvent_t e1, hipStream_t s) {
     // (timing: e0 / e1 are recorded by the dispatch itself — the first
     // launch's start, the last launch's end — hipExtLaunchKernelGGL, the
     // kernel's own execution as a rocprofv3 kernel trace counts it; null
     // events record nothing)
-    if (cold && tree_level >= 0) {  // a new reading's first match over the level's box tree (pmx_grid_tree.inc)
-        hipExtLaunchKernelGGL((grid_tree_kernel<T, KT>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, e0, e1, 0,
-                              gd, tree_level, rd, N, Tm, knn, maxR2, dists, ids, visited, radii, ctl, spec, ru.safe,
-                              ru.nbr, ru.gpn ? 1 : 0);
-    } else if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
+    if (cold) {  // a new reading's first match: the tile kernel's cold form (pmx_grid_tile.inc)
         hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, e0, e1, 0,
                               gpts, gidx, start, G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists,
                               ids, visited, radii, 1, ctl, gd, spec, ru.safe, ru.nbr, ru.gpn);
@@ -1217,7 +1210,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        unsigned long long* visited, unsigned long long* vout, int* iter_err,
                        const GridReuse<T>& ru, const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec,
                        SelectState* spec_st, unsigned long long* xseg, const T* radii, bool cold, bool tile_disp,
-                       int tree_level, hipEvent_t ev_start, hipEvent_t ev_end, hipStream_t s) {
+                       hipEvent_t ev_start, hipEvent_t ev_end, hipStream_t s) {
     if (N <= 0) return;
     cold = cold && mode >= 1;
     if (mode < 1 || !visited) spec = nullptr;  // (the window needs the per-lane kernel and the counters)
@@ -1236,7 +1229,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     } else {
 #define PMX_KT(KT) \
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
-                     ru, ctl, gd, spec, radii, cold, tile_disp, tree_level, ev_start, ev_end, s)
+                     ru, ctl, gd, spec, radii, cold, tile_disp, ev_start, ev_end, s)
         // with reuse the list keeps room for the (k+1)-th point (the safe radius;
         // the cold tile writes radius 0 and keeps k entries); with K reuse
         // candidates, for the (K+1)-th
@@ -1266,14 +1259,14 @@ template void launch_grid_match<float>(int, const P4<float>*, const int32_t*, co
                                        const Mat4<float>&, int, float, uint32_t, float*, int32_t*,
                                        unsigned long long*, unsigned long long*, int*, const GridReuse<float>&,
                                        const LoopCtl*, const GridDesc<float>*, SpecSel*, SelectState*,
-                                       unsigned long long*, const float*, bool, bool, int, hipEvent_t, hipEvent_t,
+                                       unsigned long long*, const float*, bool, bool, hipEvent_t, hipEvent_t,
                                        hipStream_t);
 template void launch_grid_match<double>(int, const P4<double>*, const int32_t*, const uint32_t*, const double*, double,
                                         const int*, const P4<double>*, int64_t, const uint32_t*, int64_t,
                                         const Mat4<double>&, int, double, uint32_t, double*, int32_t*,
                                         unsigned long long*, unsigned long long*, int*, const GridReuse<double>&,
                                         const LoopCtl*, const GridDesc<double>*, SpecSel*, SelectState*,
-                                        unsigned long long*, const double*, bool, bool, int, hipEvent_t, hipEvent_t,
+                                        unsigned long long*, const double*, bool, bool, hipEvent_t, hipEvent_t,
                                         hipStream_t);
 
 // map match ids (grid positions, -1 = none) back to reference indices

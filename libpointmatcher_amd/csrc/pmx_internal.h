@@ -149,22 +149,6 @@ struct GridGeom {
     double h, inv_h;
     int g[3];
 };
-// Bounding-box tree over one grid level's occupied cells (pmx_setup.hip
-// build_tree_device, searched by the cold match, pmx_grid_tree.inc).  The
-// leaves are the level's occupied cells in Morton order (each a contiguous
-// position range of gpts, so the tree's results are that level's positions);
-// a record at level l >= 1 holds the boxes of its 4 children (level l - 1
-// records, or leaves at l = 1) in 128 bytes, SoA:
-//   [min x 4][min y 4][min z 4][max x 4][max y 4][max z 4] (float, rounded outward)
-//   level 1 only: [first, end) of its 4 leaves (uint32 pairs) in the last 32 bytes
-// Empty children: min +inf, max -inf (their box distance is +inf).
-constexpr int kTreeMaxLevels = 16;
-constexpr int kTreeRecF4 = 8;  // float4 per record
-struct TreeDesc {
-    const float4* rec;                // records, level l at rec + off[l] * kTreeRecF4
-    const uint32_t* hdr;              // [0] leaves, [1] the top level (one record)
-    uint32_t off[kTreeMaxLevels];     // first record of level l (l >= 1)
-};
 // one grid level as the kernels see it (device table, indexed by LoopCtl::level)
 template <typename T>
 struct GridDesc {
@@ -173,7 +157,6 @@ struct GridDesc {
     const int32_t* gidx;
     const uint32_t* start;
     GridGeom G;
-    TreeDesc tree;     // (rec null: no tree over this level)
 };
 // Per-context control word of the device-resident ICP loop (pmx_loop.hip):
 // every kernel of an enqueued iteration reads it first.  done != 0 makes the
@@ -237,9 +220,7 @@ void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* star
 // 2 = octant block first.  ids written are positions in gpts;
 // launch_pos_to_index maps them back.  ctl / gd (device loop, modes 1-2):
 // transform and level are read on the device.  cold: a new reading's first
-// match (no previous match to certify from): over the box tree of level
-// tree_level when >= 0 (the gd table's entry; device loop: ctl->level's),
-// else on the tile kernel's cold form.
+// match (no previous match to certify from) on the tile kernel's cold form.
 // vout null: no counter-sum launch after the match (its counter phase is
 // merged into the select launch that follows, launch_select_all).
 void set_tile_prof(unsigned long long* buf);
@@ -249,8 +230,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
                        const Mat4<T>& Tm, int knn, T maxR2, uint32_t max_pts, T* dists, int32_t* ids,
                        unsigned long long* vpart, unsigned long long* vout, int* iter_err, const GridReuse<T>& ru,
                        const LoopCtl* ctl, const GridDesc<T>* gd, SpecSel* spec, SelectState* spec_st,
-                       unsigned long long* xseg, const T* radii, bool cold, bool tile_disp, int tree_level,
-                       hipEvent_t ev_start, hipEvent_t ev_end, hipStream_t s);
+                       unsigned long long* xseg, const T* radii, bool cold, bool tile_disp, hipEvent_t ev_start,
+                       hipEvent_t ev_end, hipStream_t s);
 // several ranks: the quantile window's pick over the all-gathered segments
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum.
 // stall: a miss sets ctl->done = kCtlStalled (the host did not read the
@@ -302,16 +283,6 @@ constexpr int64_t kOccMaxCells = (int64_t)129 * 129 * 129;
 template <typename T>
 int build_level_device(const P4<T>* pts, int64_t M, const P4<T>* nrm, const SetupShape& s, int64_t valid,
                        const SetupScratch& sc, P4<T>* gp, P4<T>* gpn, int32_t* gi, uint32_t* gstart, hipStream_t st);
-// the record layout of a tree over `valid` points (an upper bound on the
-// occupied cells): off[l] for l = 1..top_max, the record count, top_max
-int tree_layout(int64_t valid, uint32_t off[kTreeMaxLevels], int64_t* records);
-// the tree over a grid level just built by build_level_device with the same
-// scratch (its sorted cell keys are still in sc.keys32_out): rec
-// (tree_layout's records * 128 bytes), hdr (2 words)
-template <typename T>
-int build_tree_device(const P4<T>* gp, const uint32_t* gstart, const SetupShape& s, int64_t valid,
-                      const SetupScratch& sc, float4* rec, uint32_t* hdr, const uint32_t off[kTreeMaxLevels],
-                      hipStream_t st);
 template <typename T>
 int reading_order_device(const P4<T>* raw, int64_t n, const Mat4<T>& M0, const SetupShape& s, bool morton,
                          const SetupScratch& sc, P4<T>* sorted, hipStream_t st);

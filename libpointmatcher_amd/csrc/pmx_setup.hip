@@ -344,206 +344,6 @@ size_t setup_temp_bytes(int64_t n, int64_t max_cells) {
     return std::max(a, std::max(b, c));
 }
 
-// ------------------------------------------------------------------ tree --
-// The cold match's bounding-box tree over one grid level (MatchersImpl.cpp:
-// 77-83: libnabo builds a kd-tree once per Matcher::init; here a 4-ary box
-// tree whose leaves are the level's occupied cells, so a leaf is a contiguous
-// position range and the search returns that level's positions).  Built from
-// the level's sorted cell keys in five steps, no host synchronisation:
-//   keys     the first position of every occupied cell gets the cell's
-//            Morton code, every other position a sentinel (sorted last); the
-//            occupied cells are counted into hdr[0]
-//   sort     (Morton code, cell) pairs, stable (pmx_sort_pairs): the leaves
-//            in Morton order come first
-//   leaves   a leaf's position range from the cell starts and its box from its
-//            points (float, rounded outward) into the level-1 records
-//   levels   level l's record c-th box = the union of record (l-1, 4r + c)'s
-//            four boxes, one launch per level up to the layout's top
-// The record count of a level and the top level follow from hdr[0] on the
-// device (the host sizes the layout from the point count, an upper bound).
-constexpr uint32_t kTreeSentinel = 0xffffffffu;
-
-__device__ __forceinline__ uint32_t spread3_10(uint32_t v) {
-    v &= 0x3ffu;
-    v = (v | (v << 16)) & 0x030000ffu;
-    v = (v | (v << 8)) & 0x0300f00fu;
-    v = (v | (v << 4)) & 0x030c30c3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-
-__global__ __launch_bounds__(256) void tree_keys_kernel(const uint32_t* __restrict__ ckey, int64_t valid, int g0,
-                                                        int g1, int shift, uint32_t* __restrict__ okey,
-                                                        int32_t* __restrict__ oval, uint32_t* __restrict__ hdr) {
-    __shared__ uint32_t cnt[4];
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    bool first = false;
-    if (i < valid) {
-        const uint32_t c = ckey[i];
-        first = i == 0 || ckey[i - 1] != c;
-        uint32_t k = kTreeSentinel;
-        if (first) {
-            const uint32_t x = c % (uint32_t)g0, y = (c / (uint32_t)g0) % (uint32_t)g1,
-                           z = c / ((uint32_t)g0 * (uint32_t)g1);
-            k = spread3_10(x >> shift) | (spread3_10(y >> shift) << 1) | (spread3_10(z >> shift) << 2);
-        }
-        okey[i] = k;
-        oval[i] = (int32_t)c;
-    }
-    const unsigned long long b = __ballot(first);
-    if ((threadIdx.x & 63) == 0) cnt[threadIdx.x >> 6] = (uint32_t)__popcll(b);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t n = cnt[0] + cnt[1] + cnt[2] + cnt[3];
-        if (n) atomicAdd(hdr, n);
-    }
-}
-
-// records at level l of a tree with n leaves (l = 0: the leaves)
-__device__ __forceinline__ uint32_t tree_records(uint32_t n, int l) {
-    for (int i = 0; i < l; ++i) n = (n + 3u) >> 2;
-    return n;
-}
-
-template <typename T>
-__device__ __forceinline__ float f_down(T v);
-template <>
-__device__ __forceinline__ float f_down<float>(float v) { return v; }
-template <>
-__device__ __forceinline__ float f_down<double>(double v) { return __double2float_rd(v); }
-template <typename T>
-__device__ __forceinline__ float f_up(T v);
-template <>
-__device__ __forceinline__ float f_up<float>(float v) { return v; }
-template <>
-__device__ __forceinline__ float f_up<double>(double v) { return __double2float_ru(v); }
-
-// one record slot: box (mn, mx) of child c of record r
-__device__ __forceinline__ void tree_put(float4* __restrict__ rec, uint32_t r, int c, const float (&mn)[3],
-                                         const float (&mx)[3]) {
-    float* R = reinterpret_cast<float*>(rec + (size_t)r * kTreeRecF4);
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        R[4 * a + c] = mn[a];
-        R[12 + 4 * a + c] = mx[a];
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void tree_leaf_kernel(const int32_t* __restrict__ cells,
-                                                        const uint32_t* __restrict__ gstart,
-                                                        const P4<T>* __restrict__ gp, int64_t slots,
-                                                        uint32_t* __restrict__ hdr, float4* __restrict__ rec) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= slots) return;
-    const uint32_t n = hdr[0];
-    float mn[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
-    float mx[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
-    uint32_t a = 0, b = 0;
-    if (i < (int64_t)n) {
-        const uint32_t cell = (uint32_t)cells[i];
-        a = gstart[cell];
-        b = gstart[cell + 1];
-        for (uint32_t p = a; p < b; ++p) {
-            const P4<T> q = gp[p];
-            mn[0] = fminf(mn[0], f_down<T>(q.x));
-            mn[1] = fminf(mn[1], f_down<T>(q.y));
-            mn[2] = fminf(mn[2], f_down<T>(q.z));
-            mx[0] = fmaxf(mx[0], f_up<T>(q.x));
-            mx[1] = fmaxf(mx[1], f_up<T>(q.y));
-            mx[2] = fmaxf(mx[2], f_up<T>(q.z));
-        }
-    }
-    const uint32_t r = (uint32_t)(i >> 2);
-    const int c = (int)(i & 3);
-    tree_put(rec, r, c, mn, mx);
-    uint32_t* U = reinterpret_cast<uint32_t*>(rec + (size_t)r * kTreeRecF4) + 24;
-    U[2 * c] = a;
-    U[2 * c + 1] = b;
-    if (i == 0) {
-        uint32_t R = (n + 3u) >> 2;
-        int l = 1;
-        while (R > 1u) {
-            R = (R + 3u) >> 2;
-            ++l;
-        }
-        hdr[1] = (uint32_t)l;
-    }
-}
-
-__global__ __launch_bounds__(256) void tree_level_kernel(float4* __restrict__ rec, uint32_t off_child,
-                                                         uint32_t off_cur, int lvl, int64_t slots,
-                                                         const uint32_t* __restrict__ hdr) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= slots) return;
-    const uint32_t n = hdr[0];
-    const uint32_t child = (uint32_t)i;  // (record 4r + c of level lvl - 1)
-    float mn[3] = {__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf()};
-    float mx[3] = {-__builtin_huge_valf(), -__builtin_huge_valf(), -__builtin_huge_valf()};
-    if (child < tree_records(n, lvl - 1)) {
-        const float4* C = rec + (size_t)(off_child + child) * kTreeRecF4;
-        const float4 v[6] = {C[0], C[1], C[2], C[3], C[4], C[5]};
-        mn[0] = fminf(fminf(v[0].x, v[0].y), fminf(v[0].z, v[0].w));
-        mn[1] = fminf(fminf(v[1].x, v[1].y), fminf(v[1].z, v[1].w));
-        mn[2] = fminf(fminf(v[2].x, v[2].y), fminf(v[2].z, v[2].w));
-        mx[0] = fmaxf(fmaxf(v[3].x, v[3].y), fmaxf(v[3].z, v[3].w));
-        mx[1] = fmaxf(fmaxf(v[4].x, v[4].y), fmaxf(v[4].z, v[4].w));
-        mx[2] = fmaxf(fmaxf(v[5].x, v[5].y), fmaxf(v[5].z, v[5].w));
-    }
-    tree_put(rec, off_cur + (uint32_t)(i >> 2), (int)(i & 3), mn, mx);
-}
-
-int tree_layout(int64_t valid, uint32_t off[kTreeMaxLevels], int64_t* records) {
-    for (int l = 0; l < kTreeMaxLevels; ++l) off[l] = 0;
-    int64_t R = (std::max<int64_t>(valid, 1) + 3) / 4, total = R;
-    int l = 1;
-    off[1] = 0;
-    while (R > 1) {
-        R = (R + 3) / 4;
-        ++l;
-        if (l >= kTreeMaxLevels) return -1;
-        off[l] = (uint32_t)total;
-        total += R;
-    }
-    if (records) *records = total;
-    return l;  // the layout's top level
-}
-
-template <typename T>
-int build_tree_device(const P4<T>* gp, const uint32_t* gstart, const SetupShape& s, int64_t valid,
-                      const SetupScratch& sc, float4* rec, uint32_t* hdr, const uint32_t off[kTreeMaxLevels],
-                      hipStream_t st) {
-    (void)off;  // (the caller's copy of the same layout)
-    uint32_t lay[kTreeMaxLevels];
-    int64_t nrec = 0;
-    const int top = tree_layout(valid, lay, &nrec);
-    if (top < 1) return -5;
-    hipError_t e = hipMemsetAsync(hdr, 0, 2 * sizeof(uint32_t), st);
-    if (e != hipSuccess) return -1;
-    if (valid > 0) {
-        int gm = std::max(s.g[0], std::max(s.g[1], s.g[2])), shift = 0;
-        while (((gm - 1) >> shift) >= 1024) ++shift;
-        hipLaunchKernelGGL(tree_keys_kernel, dim3(blocks_for(valid)), dim3(256), 0, st, sc.keys32_out, valid,
-                           s.g[0], s.g[1], shift, sc.keys32, sc.idx, hdr);
-        size_t tb = sc.temp_bytes;
-        e = pmx_sort_pairs(sc.temp, tb, sc.keys32, sc.keys32_out, sc.idx, sc.idx_out, (int)valid, 0, 32, st);
-        if (e != hipSuccess) return -2;
-    }
-    int64_t R = (std::max<int64_t>(valid, 1) + 3) / 4;
-    hipLaunchKernelGGL(tree_leaf_kernel<T>, dim3(blocks_for(4 * R)), dim3(256), 0, st, sc.idx_out, gstart, gp, 4 * R,
-                       hdr, rec);
-    for (int l = 2; l <= top; ++l) {
-        R = (R + 3) / 4;  // (every record of level l in the layout; the ones past the tree's get empty boxes)
-        hipLaunchKernelGGL(tree_level_kernel, dim3(blocks_for(4 * R)), dim3(256), 0, st, rec, lay[l - 1], lay[l], l,
-                           4 * R, (const uint32_t*)hdr);
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -4;
-}
-template int build_tree_device<float>(const P4<float>*, const uint32_t*, const SetupShape&, int64_t,
-                                      const SetupScratch&, float4*, uint32_t*, const uint32_t*, hipStream_t);
-template int build_tree_device<double>(const P4<double>*, const uint32_t*, const SetupShape&, int64_t,
-                                       const SetupScratch&, float4*, uint32_t*, const uint32_t*, hipStream_t);
-
 // ---------------------------------------------------------------- morton --
 __device__ __forceinline__ uint64_t dspread3(uint64_t v) {
     v &= 0x1fffffull;
