@@ -87,6 +87,13 @@ typedef struct pmx_stats {
 /* device: HIP device ordinal; dtype: PMX_F32 | PMX_F64. */
 int pmx_ctx_create(int device, int dtype, pmx_ctx** out);
 int pmx_ctx_destroy(pmx_ctx* ctx);
+/* One developer option of the context (README "Options": switches between
+ * measured alternatives and test hooks; the defaults are the tuned path).
+ * Also read at pmx_ctx_create from PMX_OPTS="name=value,...".  No reference
+ * counterpart: the reference's tuning is its YAML parameters, which the host
+ * chain (include/pmx_icp.h) maps as they are.  PMX_E_BAD_PARAM for an
+ * unknown name or a malformed value. */
+int pmx_ctx_set_option(pmx_ctx* ctx, const char* name, const char* value);
 const char* pmx_last_error(const pmx_ctx* ctx);
 /* number of visible HIP devices (0 when no GPU / driver) */
 int pmx_device_count(void);

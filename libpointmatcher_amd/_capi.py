@@ -148,7 +148,7 @@ def gloo_host_comm():
 _lib = None
 
 EXPORTS = [
-    "pmx_ctx_create", "pmx_ctx_destroy", "pmx_last_error", "pmx_device_count", "pmx_version",
+    "pmx_ctx_create", "pmx_ctx_destroy", "pmx_ctx_set_option", "pmx_last_error", "pmx_device_count", "pmx_version",
     "pmx_comm_unique_id", "pmx_comm_init", "pmx_comm_init_host", "pmx_comm_size", "pmx_comm_stats", "pmx_comm_loop_stats", "pmx_set_reference", "pmx_set_reference_centred", "pmx_set_reference_mean_centred", "pmx_set_reading", "pmx_set_search", "pmx_match",
     "pmx_outlier_default", "pmx_outlier_null", "pmx_outlier_maxdist", "pmx_outlier_mindist",
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed", "pmx_outlier_robust",
@@ -171,6 +171,7 @@ def lib():
         l.pmx_last_error.argtypes = [C.c_void_p]
         l.pmx_ctx_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
         l.pmx_ctx_destroy.argtypes = [C.c_void_p]
+        l.pmx_ctx_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p]
         l.pmx_comm_unique_id.argtypes = [C.c_void_p]
         l.pmx_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         l.pmx_comm_init_host.argtypes = [C.c_void_p, C.c_int, C.c_int, ALLREDUCE_FN, ALLGATHER_FN, C.c_void_p]
@@ -347,11 +348,16 @@ class Context:
         h = C.c_void_p()
         rc = self._l.pmx_ctx_create(device, PMX_F64 if self.dtype == np.float64 else PMX_F32, C.byref(h))
         if rc != PMX_OK:
-            raise PmxError(f"pmx_ctx_create failed ({rc}); visible HIP devices: {device_count()}")
+            raise PmxError(f"pmx_ctx_create failed ({rc}: {self._l.pmx_last_error(None).decode()}); "
+                           f"visible HIP devices: {device_count()}")
         self.h = h
         self.rows = None
         self.knn = None
         self.N = 0
+
+    def set_option(self, name, value):
+        """One developer option (README "Options"; pmx_ctx_set_option)."""
+        self._chk(self._l.pmx_ctx_set_option(self.h, str(name).encode(), str(value).encode()))
 
     def close(self):
         if self.h:

@@ -122,6 +122,92 @@ hipEvent_t get_event(pmx_ctx* c) {
     return e;
 }
 
+// ---------------------------------------------------------------- options --
+// The developer options of a context (README "Options"): switches between
+// measured alternatives and test hooks, set from PMX_OPTS="name=value,..." at
+// pmx_ctx_create or one at a time by pmx_ctx_set_option.  Lists (grid_levels,
+// force_miss) are ':'-separated.  An unknown name or a malformed value is an
+// error (PMX_E_BAD_PARAM), never silently ignored.
+int set_option(pmx_ctx* c, const std::string& key, const std::string& val) {
+    auto num = [&](double& out) -> bool {
+        if (val.empty()) return false;
+        char* end = nullptr;
+        out = std::strtod(val.c_str(), &end);
+        return end && *end == 0 && out == out;
+    };
+    auto list = [&](std::vector<double>& out) -> bool {
+        out.clear();
+        size_t p = 0;
+        while (p <= val.size()) {
+            const size_t q = std::min(val.find(':', p), val.size());
+            const std::string t = val.substr(p, q - p);
+            char* end = nullptr;
+            const double x = std::strtod(t.c_str(), &end);
+            if (t.empty() || !end || *end != 0 || x != x) return false;
+            out.push_back(x);
+            p = q + 1;
+        }
+        return !out.empty();
+    };
+    double v = 0;
+    std::vector<double> xs;
+    bool ok = true;
+    if (key == "grid_mode") {
+        ok = val == "tile" || val == "lane";
+        if (ok) c->grid_mode = val == "tile" ? 0 : 1;
+    } else if (key == "grid_levels") {  // points per occupied cell of each level, e.g. 2:8:32 (one value: one level)
+        ok = list(xs);
+        for (double x : xs) ok = ok && x >= 0.25;
+        if (ok) c->level_ppc = xs;
+    } else if (key == "first_ppc") {
+        ok = num(v) && v >= 0.25;
+        if (ok) c->first_ppc = v;
+    } else if (key == "force_miss") {  // test hook: device-loop iterations whose sharded window pick misses
+        ok = list(xs);
+        if (ok) {
+            c->debug_force_miss.clear();
+            for (double x : xs) c->debug_force_miss.push_back((int64_t)x);
+        }
+    } else if ((ok = num(v))) {
+        const bool b = v != 0;
+        if (key == "tile_max") c->tile_max = (uint32_t)std::max(0.0, v);
+        else if (key == "nbr_cache") c->nbr_on = b;
+        else if (key == "spec_select") c->spec_allowed = b;
+        else if (key == "grid_adapt") c->adaptive = b;
+        else if (key == "grid_reuse") c->reuse_on = b;
+        else if (key == "tile_dispatch") c->tile_dispatch_req = v < 0 ? -1 : (b ? 1 : 0);
+        else if (key == "coop_max") c->coop_max = (int)std::max(0.0, std::min(256.0, v));
+        else if (key == "fuse_step") c->fuse_step = b;
+        else if (key == "step_counter") c->step_counter_on = b;
+        else if (key == "side_levels") c->side_levels = b;
+        else if (key == "reading_copy") c->reading_copy = b;
+        else if (key == "reading_order") c->reading_order = b;
+        else if (key == "loop_batch") c->loop_batch = (int)std::max(0.0, v);
+        else if (key == "wave_fill") c->wave_fill = std::max(1.0, v);
+        else if (key == "setup_trace") c->setup_trace = (int)v;
+        else if (key == "tile_prof") c->tile_prof = b;
+        else if (key == "vt_trace") g_vt_trace = (int)v;
+        else ok = false;
+    }
+    if (!ok) return fail(c, PMX_E_BAD_PARAM, "unknown option or bad value: " + key + "=" + val);
+    return PMX_OK;
+}
+
+int set_options(pmx_ctx* c, const char* s) {
+    const std::string all(s);
+    size_t p = 0;
+    while (p < all.size()) {
+        const size_t q = std::min(all.find(',', p), all.size());
+        const std::string item = all.substr(p, q - p);
+        p = q + 1;
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos) return fail(c, PMX_E_BAD_PARAM, "option without a value: " + item);
+        if (int rc = set_option(c, item.substr(0, eq), item.substr(eq + 1))) return rc;
+    }
+    return PMX_OK;
+}
+
 }  // namespace pmxc
 
 using namespace pmxc;
@@ -149,53 +235,19 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     pmx_ctx* c = new pmx_ctx();
     c->device = device;
     c->dtype = dtype;
-    // tuning knobs (defaults are the measured optimum on MI355X)
-    if (const char* e = std::getenv("PMX_GRID_MODE"))
-        c->grid_mode = std::strcmp(e, "tile") == 0 ? 0 : std::strcmp(e, "octant") == 0 ? 2 : 1;
-    if (const char* e = std::getenv("PMX_GRID_TILE_MAX")) c->tile_max = (uint32_t)std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("PMX_NBR_CACHE")) c->nbr_on = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_SPEC_SELECT")) c->spec_allowed = std::atoi(e) != 0;
-    // grid levels: PMX_GRID_LEVELS="2,8,32" (points per occupied cell), or
-    // PMX_GRID_PPC=x for a single fixed level; PMX_GRID_ADAPT=0 pins level 0
-    if (const char* e = std::getenv("PMX_GRID_LEVELS")) {
-        std::vector<double> v;
-        for (const char* p = e; *p;) {
-            char* end = nullptr;
-            const double x = std::strtod(p, &end);
-            if (end == p) break;
-            if (x >= 0.25) v.push_back(x);
-            p = *end == ',' ? end + 1 : end;
+    // developer options (defaults are the measured optimum on MI355X)
+    if (const char* e = std::getenv("PMX_OPTS")) {
+        if (set_options(c, e) != PMX_OK) {
+            g_err = c->err;
+            delete c;
+            return PMX_E_BAD_PARAM;
         }
-        if (!v.empty()) c->level_ppc = v;
     }
-    if (const char* e = std::getenv("PMX_GRID_PPC")) c->level_ppc = {std::max(0.25, std::atof(e))};
-    if (const char* e = std::getenv("PMX_GRID_ADAPT")) c->adaptive = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_GRID_REUSE")) c->reuse_on = std::atoi(e) != 0;
-    if (const char* e = std::getenv("PMX_REUSE_CAND")) c->reuse_cand_req = std::max(0, std::min(15, std::atoi(e)));
-    if (const char* e = std::getenv("PMX_TILE_DISPATCH")) c->tile_dispatch_req = std::atoi(e);
-    if (const char* e = std::getenv("PMX_COOP_MAX")) c->coop_max = std::max(0, std::min(256, std::atoi(e)));
-    if (const char* e = std::getenv("PMX_VT_TRACE")) g_vt_trace = std::atoi(e);
-    if (const char* e = std::getenv("PMX_GRID_FIRST_PPC")) c->first_ppc = std::max(0.25, std::atof(e));
-    // test hook: device-loop iterations (0-based, comma separated) whose
-    // sharded window pick is forced to miss (the stall-and-replay path)
-    if (const char* e = std::getenv("PMX_DEBUG_FORCE_MISS"))
-        for (const char* p = e; *p;) {
-            char* end = nullptr;
-            const long long v = std::strtoll(p, &end, 10);
-            if (end == p) break;
-            c->debug_force_miss.push_back((int64_t)v);
-            p = *end == ',' ? end + 1 : end;
-        }
     auto bad = [&](int code) {
         pmx_ctx_destroy(c);
         return code;
     };
     if (hipSetDevice(device) != hipSuccess) return bad(PMX_E_HIP);
-    if (const char* e = std::getenv("PMX_SYNC")) {  // host wait policy for the per-iteration sync
-        if (std::strcmp(e, "spin") == 0) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
-        if (std::strcmp(e, "yield") == 0) (void)hipSetDeviceFlags(hipDeviceScheduleYield);
-        if (std::strcmp(e, "block") == 0) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
-    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
@@ -244,6 +296,11 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     return PMX_OK;
 }
 
+int pmx_ctx_set_option(pmx_ctx* c, const char* name, const char* value) {
+    if (!c || !name || !value) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    return set_option(c, name, value);
+}
+
 int pmx_ctx_destroy(pmx_ctx* c) {
     if (!c) return PMX_OK;
     (void)hipSetDevice(c->device);
@@ -251,7 +308,7 @@ int pmx_ctx_destroy(pmx_ctx* c) {
     void* bufs[] = {c->d_safe, c->d_ref,  c->d_nrm,      c->d_rd,     c->d_dists,  c->d_ids,   c->d_w,    c->d_part_d,
                     c->d_part_i, c->d_hist,   c->d_vt,     c->d_deno,  c->d_gather, c->d_partials,
                     c->d_result, c->d_waves, c->d_vpart,
-                    c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace, c->d_diag, c->d_cand, c->d_ticket, c->d_nbr,
+                    c->d_sel_more, c->d_gdesc, c->d_loop_T0, c->d_trace, c->d_diag, c->d_ticket, c->d_nbr,
                     c->d_spec, c->d_spec_keys, c->d_order, c->d_raw, c->d_bbox, c->d_occ, c->d_selx,
                     c->d_rob, c->d_rdev, c->d_radii, c->d_rd_p4, c->d_rd_sorted};
     side_finish(c);  // (the side stream may still be building levels)

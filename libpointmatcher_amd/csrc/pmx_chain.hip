@@ -105,16 +105,15 @@ void side_finish(pmx_ctx* c) {
     c->side_pending = false;
 }
 
-// Setup timeline (development trace, PMX_SETUP_TRACE=1): each mark waits for
-// the stream and prints the wall time since the previous mark to stderr
-// (PMX_SETUP_TRACE=2: host wall time only, no stream synchronisation).
+// Setup timeline (development trace, option setup_trace=1): each mark waits
+// for the stream and prints the wall time since the previous mark to stderr
+// (setup_trace=2: host wall time only, no stream synchronisation).
 struct SetupTrace {
     pmx_ctx* c;
     int on;
     std::chrono::steady_clock::time_point t;
     explicit SetupTrace(pmx_ctx* cc)
-        : c(cc), on(std::getenv("PMX_SETUP_TRACE") ? std::atoi(std::getenv("PMX_SETUP_TRACE")) : 0),
-          t(std::chrono::steady_clock::now()) {}
+        : c(cc), on(cc->setup_trace), t(std::chrono::steady_clock::now()) {}
     void mark(const char* what) {
         if (!on) return;
         if (on == 1) (void)hipStreamSynchronize(c->stream);
@@ -379,15 +378,11 @@ int build_levels(pmx_ctx* c, int upto) {
 // context stream; the finer ones, which the matches after it move to, on the
 // side stream with their own scratch, overlapping the reading's setup and the
 // cold match (every match after a reading's first waits for them on the
-// device, side_join).  PMX_SIDE_LEVELS=0: all on the context stream.
+// device, side_join).  Option side_levels=0: all on the context stream.
 template <typename T>
 int build_levels_cold(pmx_ctx* c, int cold) {
-    static const bool side_env = [] {
-        const char* e = std::getenv("PMX_SIDE_LEVELS");
-        return !e || std::atoi(e) != 0;
-    }();
     cold = std::min(cold, (int)c->levels.size() - 1);
-    if (cold <= 0 || !side_env || c->levels_built > 0) return build_levels<T>(c, cold);
+    if (cold <= 0 || !c->side_levels || c->levels_built > 0) return build_levels<T>(c, cold);
     if (!c->side) {
         // (the lowest priority: the context stream's cold level, reading
         // order and first match go first when both have work)
@@ -430,16 +425,14 @@ int build_levels_cold(pmx_ctx* c, int cold) {
 // (pmx_setup.hip): the slot -> query order stays there (d_order) and is
 // copied to the host only for a host mirror.
 //
-// Waves of the tile kernel (PMX_GRID_MODE=tile only): a wave takes up to 64
+// Waves of the tile kernel (option grid_mode=tile only): a wave takes up to 64
 // consecutive slots but never crosses the boundary of an aligned Morton
 // block of 2^L cells per side, so its queries never straddle two distant
 // regions (a straddling wave would share one huge LDS box).  L is the
-// smallest level whose wave count stays within `fill` (default 1.25,
-// PMX_GRID_WAVE_FILL) of ceil(N / 64).
-std::vector<uint32_t> tile_waves(const std::vector<unsigned long long>& key, int64_t N) {
+// smallest level whose wave count stays within `fill` (default 1.25, option
+// wave_fill) of ceil(N / 64).
+std::vector<uint32_t> tile_waves(const std::vector<unsigned long long>& key, int64_t N, double fill) {
     std::vector<uint32_t> waves;
-    double fill = 1.25;
-    if (const char* e = std::getenv("PMX_GRID_WAVE_FILL")) fill = std::max(1.0, std::atof(e));
     const int64_t full = (N + 63) / 64;
     auto cut = [&](int L, std::vector<uint32_t>* out) -> int64_t {
         int64_t W = 0;
@@ -589,11 +582,8 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     // scans pay no allocation)
     if ((rc = ensure(c, &c->d_rd_p4, &c->rd_p4_bytes, sizeof(P4<T>) * n1))) return rc;
     void* d_p4 = c->d_rd_p4;
-    static const bool copy_env = [] {  // (PMX_READING_COPY=0: the reading's upload on the context stream)
-        const char* e = std::getenv("PMX_READING_COPY");
-        return !e || std::atoi(e) != 0;
-    }();
-    if ((rc = copy_env ? upload_raw_async(c, feat, sizeof(T) * (size_t)rows * N)
+    // (option reading_copy=0: the reading's upload on the context stream)
+    if ((rc = c->reading_copy ? upload_raw_async(c, feat, sizeof(T) * (size_t)rows * N)
                        : upload_raw(c, feat, sizeof(T) * (size_t)rows * N)))
         return rc;
     launch_pack_p4<T>((const T*)c->d_raw, rows, N, N, (P4<T>*)d_p4, c->stream);
@@ -604,7 +594,7 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
     c->n_waves = 0;
     c->slot_query.clear();
     c->has_order = false;
-    const bool order = c->grid_ready && N > 0 && !std::getenv("PMX_GRID_NOORDER");  // (knob: identity slot order)
+    const bool order = c->grid_ready && N > 0 && c->reading_order;  // (option reading_order=0: identity slot order)
     if (order) {
         // Morton order over the finest level's cells
         const GridLevel& L0 = c->lv(0);
@@ -636,7 +626,7 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
             HIPCHK(c, hipMemcpyAsync(keys.data(), c->setup.keys64_out, sizeof(unsigned long long) * N,
                                      hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
-            const std::vector<uint32_t> waves = tile_waves(keys, N);
+            const std::vector<uint32_t> waves = tile_waves(keys, N, c->wave_fill);
             HIPCHK(c, hipMalloc((void**)&c->d_waves, sizeof(uint32_t) * waves.size()));
             HIPCHK(c, hipMemcpyAsync(c->d_waves, waves.data(), sizeof(uint32_t) * waves.size(),
                                      hipMemcpyHostToDevice, c->stream));
@@ -677,13 +667,6 @@ int set_reading_impl(pmx_ctx* c, const T* feat, int rows, int64_t N, const T* T0
 }
 
 // ------------------------------------------------------------------- match --
-// reuse candidates per query for a k-NN match (K > k: the certificate
-// re-ranks the K nearest of the last full search; K = k: the k-list itself)
-int reuse_k(const pmx_ctx* c, int knn) {
-    const int K = c->reuse_cand_req;
-    return K > knn && K < 16 && knn <= kLaneMaxK ? K : knn;
-}
-
 template <typename T>
 int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* visited) {
     if (!c->d_ref) return fail(c, PMX_E_STATE, "no reference (Matcher::init not called)");
@@ -775,20 +758,13 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
         // temporal reuse: the output buffers hold this reading's previous
         // match (same k, same level) with its safe radii
         GridReuse<T> ru;
-        const int K = reuse_k(c, knn);
-        const bool cand_ok = K == knn || c->cand_K == K;  // (the candidates of the last match are K wide)
-        const bool no_prev = !(c->safe_valid && c->have_match && c->ids_grid && c->knn == knn && cand_ok);
+        const bool no_prev = !(c->safe_valid && c->have_match && c->ids_grid && c->knn == knn);
         if (c->reuse_on && c->grid_mode >= 1 && knn <= kLaneMaxK) {  // (the wide search keeps no safe radii)
             ru.mode = !no_prev && c->ids_level == c->level ? 2 : 1;
             ru.safe = (T*)c->d_safe;
             ru.coop_max = c->coop_max;
             for (int i = 0; i < 16; ++i) ru.Tprev.m[i] = (T)c->Tprev[i];
-            if (K > knn) {
-                int rc = ensure(c, (void**)&c->d_cand, &c->cand_bytes, sizeof(int32_t) * (size_t)K * std::max<int64_t>(c->N, 1));
-                if (rc) return rc;
-                ru.K = K;
-                ru.cand = c->d_cand;
-            } else if (knn == 1 && c->nbr_on && (ru.mode != 2 || c->nbr_prev || c->loop_on) &&
+            if (knn == 1 && c->nbr_on && (ru.mode != 2 || c->nbr_prev || c->loop_on) &&
                        !(c->loop_on && c->loop_dev.tile_dispatch)) {
                 // (a reuse match reads the records only if the last match
                 // wrote them; a device-loop match decides reuse on the device,
@@ -815,9 +791,9 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             HIPCHK(c, hipMalloc((void**)&c->d_specx, sizeof(unsigned long long) * kSpecXStride * c->nranks));
         unsigned long long* xseg = spec && sharded(c) ? c->d_specx + (size_t)kSpecXStride * c->rank : nullptr;
         const bool cold_now = no_prev && c->reuse_on;
-        // (development profile of the cold form's waves, PMX_TILE_PROF=1: per
-        // wave duration, rounds and points copied, summarised on stderr)
-        static const bool tile_prof = std::getenv("PMX_TILE_PROF") != nullptr;
+        // (development profile of the cold form's waves, option tile_prof=1:
+        // per wave duration, rounds and points copied, summarised on stderr)
+        const bool tile_prof = c->tile_prof;
         unsigned long long* prof_buf = nullptr;
         const int64_t nw = (c->N + 63) / 64;
         if (tile_prof && cold_now) {
@@ -910,7 +886,6 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
             c->spec_exchanged = true;
         }
         c->safe_valid = ru.mode != 0;
-        c->cand_K = ru.mode != 0 && ru.cand ? ru.K : 0;
         c->visited_host = 0;
         c->ids_grid = true;
         c->ids_level = c->level;
@@ -1024,7 +999,7 @@ void choose_level(pmx_ctx* c, uint64_t visited, uint64_t full) {
     double q = (double)c->N, v = (double)visited;
     if (c->safe_valid) {
         if ((double)full * 16.0 < q) return;
-        v -= (double)reuse_k(c, c->knn) * (q - (double)full);
+        v -= (double)c->knn * (q - (double)full);
         q = (double)full;
     }
     const double cells = v / (q * c->lv(l).ppc);

@@ -89,10 +89,10 @@ struct pmx_ctx {
 
     // uniform grid over the reference (exact shell search, pmx_grid.hip)
     int search_type = 1;
-    int grid_mode = 1;            // 1 = per-lane shell search (default), 0 = LDS tiles (PMX_GRID_MODE=tile)
-    uint32_t tile_max = 4096;     // largest per-wave box scanned from LDS (PMX_GRID_TILE_MAX)
+    int grid_mode = 1;            // 1 = per-lane shell search (default), 0 = LDS tiles (option grid_mode=tile)
+    uint32_t tile_max = 4096;     // largest per-wave box scanned from LDS (option tile_max)
     // Grid levels of increasing cell size (points per occupied cell:
-    // level_ppc, PMX_GRID_LEVELS).  Every level answers exactly; the level of
+    // level_ppc, option grid_levels).  Every level answers exactly; the level of
     // the next match is chosen from the last match's pair count (adaptive:
     // converged iterations want small cells, misaligned ones or large k want
     // large cells, see choose_level).
@@ -105,33 +105,36 @@ struct pmx_ctx {
     std::vector<SetupShape> level_shapes;
     int64_t grid_valid = 0;   // finite reference points (the levels' size)
     int level = 0;      // level of the next grid match
-    double first_ppc = 8.0;   // level of a new reading's first (cold) match (PMX_GRID_FIRST_PPC)
+    double first_ppc = 8.0;   // level of a new reading's first (cold) match (option first_ppc)
     int ids_level = 0;  // level whose positions the current match ids are
     std::vector<double> level_cells;   // last cells-per-query seen at each level
     std::vector<int64_t> level_seen;   // match count when it was seen (0: never)
     int64_t match_count = 0;
     bool adaptive = true;
-    bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; PMX_GRID_REUSE=0: off)
+    // developer options (PMX_OPTS / pmx_ctx_set_option, README "Options"):
+    // A/B switches of measured alternatives and test hooks, per context
+    bool fuse_step = true;        // fuse_step: the last finalize and the step in one launch (device loop, one rank)
+    bool step_counter_on = true;  // step_counter: the match's counter phase folded into that launch (no window)
+    bool side_levels = true;      // side_levels: the levels finer than the cold one on a side stream
+    bool reading_copy = true;     // reading_copy: the reading's upload on the copy stream
+    bool reading_order = true;    // reading_order: the reading in slot (Morton) order
+    int loop_batch = 0;           // loop_batch: one status batch size for the device loop (0: 4, then 8)
+    double wave_fill = 1.25;      // wave_fill: the tile mode's wave table fill
+    int setup_trace = 0;          // setup_trace: setup timeline on stderr (1: stream-synchronised marks, 2: host)
+    bool tile_prof = false;       // tile_prof: the cold tile form's per-wave profile on stderr
+    bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; option grid_reuse=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
     void* d_safe = nullptr;       // T[N]: safe radius per query
     int64_t safe_cap = 0;
-    // reuse candidates: each full search keeps its K nearest (K > k) and the
-    // certificate re-ranks them (pmx_grid.hip).  reuse_cand_req: requested K
-    // (0: off = the k-list itself; PMX_REUSE_CAND), cand_K: the K the
-    // buffers hold (0: none valid)
-    int reuse_cand_req = 0;
-    int tile_dispatch_req = -1;   // tile dispatch in the device loop: -1 auto (reading >= 4x the reference), 0 off, 1 on (PMX_TILE_DISPATCH)
-    int coop_max = 4;             // wave-cooperative full searches for blocks with <= this many misses (PMX_COOP_MAX)
-    int cand_K = 0;
-    int32_t* d_cand = nullptr;    // int32[N * cand_K]
+    int tile_dispatch_req = -1;   // tile dispatch in the device loop: -1 auto (reading >= 4x the reference), 0 off, 1 on (option tile_dispatch)
+    int coop_max = 4;             // wave-cooperative full searches for blocks with <= this many misses (option coop_max)
     // k = 1 neighbour records (GridReuse::nbr): P4<T>[N]; nbr_prev: the last
-    // match wrote them (PMX_NBR_CACHE=0: off)
+    // match wrote them (option nbr_cache=0: off)
     void* d_nbr = nullptr;
     size_t nbr_bytes = 0;
     bool nbr_prev = false;
     bool nbr_normals = false;  // (the last match's records carry the normals, at d_nbr + N)
     bool nbr_on = true;
-    size_t cand_bytes = 0;
     bool grid_ready = false;
     const GridLevel& lv(int i) const { return levels[(size_t)i]; }
     std::vector<int32_t> slot_query;  // host copy of d_order (host mirrors only; filled on demand)
@@ -269,7 +272,7 @@ struct pmx_ctx {
     bool spec_fresh = false;      // the window is empty (a loop's first iteration): a known miss
     int64_t enq_iter = -1;        // loop iteration being enqueued (-1: not in a loop)
     uint64_t n_verdict_sync = 0, n_async = 0, n_stall = 0;  // pmx_comm_loop_stats
-    std::vector<int64_t> debug_force_miss;  // PMX_DEBUG_FORCE_MISS: loop iterations whose window pick misses
+    std::vector<int64_t> debug_force_miss;  // option force_miss: loop iterations whose window pick misses
     size_t h_stage_cap = 0;
     unsigned long long* d_specx = nullptr;  // quantile window exchange: own segment, then nranks gathered
 
@@ -289,7 +292,7 @@ struct pmx_ctx {
     int64_t trace_cap = 0;        // iterations
     bool loop_on = false;         // enqueueing loop iterations
     // quantile window fused into the grid match (pmx_spec.h): device loop,
-    // single rank, quantile filter at chain position 0 (PMX_SPEC_SELECT=0: off)
+    // single rank, quantile filter at chain position 0 (option spec_select=0: off)
     SpecSel* d_spec = nullptr;
     void* d_spec_keys = nullptr;
     bool spec_allowed = true;
@@ -381,7 +384,6 @@ void setup_release(pmx_ctx* c);
 int upload_raw(pmx_ctx* c, const void* src, size_t bytes);
 int host_order(pmx_ctx* c);
 int select_reset(pmx_ctx* c);
-int reuse_k(const pmx_ctx* c, int knn);  // reuse candidates of a k-NN match (pmx_chain.hip)
 int ensure_level(pmx_ctx* c, int l);     // grid level l built (pmx_chain.hip)
 double host_limit(const pmx_ctx* c);
 void fill_stats(const pmx_ctx* c, pmx_stats* st, double kept, double nz, double rm, double rp, double sw,

@@ -24,7 +24,7 @@
 // 0.106 ms per 1M queries); it is bound by the dependent gather latency of
 // the row scans, not by pair evaluation.
 //
-// Tile kernel (PMX_GRID_MODE=tile, pmx_grid_tile.inc).  One wave = up to 64
+// Tile kernel (option grid_mode=tile, pmx_grid_tile.inc).  One wave = up to 64
 // queries inside one aligned Morton block (the wave table of
 // pmx_set_reading).  The wave takes the bounding box of its queries' cells, grows it
 // by one cell, copies the box's reference points (ny * nz contiguous row
@@ -46,9 +46,6 @@
 
 #include <hip/hip_ext.h>
 
-#ifndef PMX_NOMISS
-#define PMX_NOMISS 0
-#endif
 #include "pmx_spec.h"
 
 namespace pmx {
@@ -135,19 +132,10 @@ __device__ __forceinline__ void kth(const T (&kd)[KT], const int32_t (&ki)[KT], 
 // points are fetched kScanU at a time with independent loads; a short row
 // (a few points at the default density) is one masked chunk — a scalar tail
 // loop would make every point its own dependent round trip.
-#ifndef PMX_SCAN_U
-#define PMX_SCAN_U 4
-#endif
-constexpr int kScanU = PMX_SCAN_U;
+constexpr int kScanU = 4;
 // phase-1 row grouping of the per-lane search (rows per group, points per row)
-#ifndef PMX_P1_G
-#define PMX_P1_G 3
-#endif
-#ifndef PMX_P1_U
-#define PMX_P1_U 4
-#endif
-constexpr int kP1G = PMX_P1_G;
-constexpr int kP1U = PMX_P1_U;
+constexpr int kP1G = 3;
+constexpr int kP1U = 4;
 static_assert(9 % kP1G == 0, "phase-1 groups must tile the nine rows");
 template <typename T, int KT>
 __device__ __forceinline__ void scan_range(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
@@ -188,91 +176,13 @@ __device__ __forceinline__ int cell_x(const GridGeom& G, double v) {
     return f < 0.0 ? 0 : (f >= (double)G.g[0] ? G.g[0] - 1 : (int)f);
 }
 
-// Octant search: the 2x2x2 cells nearest to the query (its cell and, per
-// axis, the neighbour on the query's side of the cell centre: 4 rows of 2
-// cells).  Every point outside the block is at least LB = the distance to
-// the block's interior faces (>= h/2) away, so the result is final when it
-// passes the same certification as the shell search; true then.
-template <typename T, int KT>
-__device__ __forceinline__ bool octant_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
-                                              const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy,
-                                              T qz, const double q[3], const int c[3], T maxR2, int k, T (&kd)[KT],
-                                              int32_t (&ki)[KT], uint32_t& visits, double& lb_exit) {
-    // (k: the rank the exit certifies — the query's k, or the candidate
-    // count K of the temporal reuse, below)
-    int b0[3], b1[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const double mid = G.lo[a] + ((double)c[a] + 0.5) * G.h;
-        const int o = q[a] >= mid ? c[a] + 1 : c[a] - 1;
-        b0[a] = o < c[a] ? max(o, 0) : c[a];
-        b1[a] = o > c[a] ? min(o, G.g[a] - 1) : c[a];
-    }
-    uint32_t ra[4], rb[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int y = (r & 1) ? b1[1] : b0[1], z = (r & 2) ? b1[2] : b0[2];
-        const bool ok = !((r & 1) && b1[1] == b0[1]) && !((r & 2) && b1[2] == b0[2]);  // no duplicate rows
-        const uint32_t row = ((uint32_t)z * (uint32_t)G.g[1] + (uint32_t)y) * (uint32_t)G.g[0];
-        const uint32_t va = gld32(start, row + b0[0]);
-        const uint32_t vb = gld32(start, row + b1[0] + 1);
-        ra[r] = ok ? va : 0u;
-        rb[r] = ok ? vb : 0u;
-    }
-    constexpr int U = kP1U;
-    P4<T> p[4][U];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = ra[r] + u;
-            p[r][u] = gld32(gpts, j < rb[r] ? j : 0u);  // masked: any in-range address
-        }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t j = ra[r] + u;
-            if (j < rb[r]) consider<T, KT>(gidx, (int32_t)j, gsqd(qx, qy, qz, p[r][u]), kd, ki);
-        }
-        visits += rb[r] - ra[r];
-        if (ra[r] + U < rb[r]) {
-            uint32_t v0 = 0;
-            scan_range<T, KT>(gpts, gidx, ra[r] + U, rb[r], qx, qy, qz, kd, ki, v0);
-        }
-    }
-    double lb = 1e300;
-    bool any = false;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        if (b0[a] > 0) {
-            lb = fmin(lb, q[a] - (G.lo[a] + (double)b0[a] * G.h));
-            any = true;
-        }
-        if (b1[a] < G.g[a] - 1) {
-            lb = fmin(lb, (G.lo[a] + (double)(b1[a] + 1) * G.h) - q[a]);
-            any = true;
-        }
-    }
-    lb_exit = any ? lb : 1e300;  // (every point outside the block is at least lb away)
-    if (!any) return true;  // the block is the whole grid
-    if (lb > 0.0) {
-        const double lb2 = lb * lb * (1.0 - 1e-5);
-        T dk;
-        int32_t ik;
-        kth(kd, ki, k, dk, ik);
-        if (((double)dk < lb2 && ik != kNoPos) || lb2 > (double)maxR2) return true;
-    }
-    return false;
-}
-
 // Exact shell search for one query (from scratch); kd/ki must be
 // initialised.  Certified on the k-th entry of the list (entries past k, when
 // KT > k, are the next-nearest points visited).  lb_exit: the distance from
 // the query to the unvisited region at exit (1e300: the whole grid).
 // kp: the list entry (1-based) cells are pruned against — the one the safe
-// radius of the temporal reuse takes as a bound on every point not kept
-// (k + 1, or K + 1 with K reuse candidates); 0: k + 1 when the list has room.
+// radius of the temporal reuse takes as a bound on every point not kept;
+// 0: k + 1 when the list has room.
 template <typename T, int KT>
 __device__ __forceinline__ void lane_search(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                             const uint32_t* __restrict__ start, const GridGeom& G, T qx, T qy, T qz,
@@ -576,8 +486,7 @@ size_t grid_counter_bytes() { return sizeof(unsigned long long) * 4 * kVSlots * 
 constexpr double kReuseMargin = 1e-5;
 
 // safe radius of a full search: the unvisited region and the (k+1)-th
-// visited point (list entry k, when KT > k) bound every non-neighbour (with
-// K reuse candidates, k = K: every point outside the candidate list)
+// visited point (list entry k, when KT > k) bound every non-neighbour
 template <typename T, int KT>
 __device__ __forceinline__ T safe_radius(const T (&kd)[KT], const int32_t (&ki)[KT], int k, double lb_exit) {
     double r = lb_exit;
@@ -604,20 +513,16 @@ __device__ __forceinline__ T qr2(const T* __restrict__ radii, int64_t j, T maxR2
     return r * r;
 }
 
-// one query from scratch: octant block (oct) or the shell search
+// one query from scratch: the shell search; its k-list, the neighbour record
+// (k = 1) and its safe radius
 template <typename T, int KT>
 __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
                                            const uint32_t* __restrict__ start, const GridGeom& G,
                                            const P4<T>* __restrict__ rd, int64_t j, const Mat4<T>& Tm, int k,
-                                           T maxR2, int oct, T* __restrict__ out_d, int32_t* __restrict__ out_i,
+                                           T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
                                            T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa,
-                                           int K = 0, int32_t* __restrict__ cand = nullptr,
                                            P4<T>* __restrict__ nbr = nullptr, const P4<T>* __restrict__ gpn = nullptr,
                                            int64_t N = 0) {
-    // K > k (reuse candidates, cand != null): the search certifies the K
-    // nearest, its list keeps the (K+1)-th, and the K nearest are stored as
-    // the next match's candidates
-    const int ks = cand ? K : k;
     T qx, qy, qz;
     gxform(Tm, gld(rd, j), qx, qy, qz);
     T kd[KT];
@@ -632,70 +537,10 @@ __device__ __forceinline__ void full_query(const P4<T>* __restrict__ gpts, const
     bool qnan;
     cell_of_q(G, q, c, qnan);
     double lb_exit = -1.0;
-    if (!qnan) {
-        bool done = false;
-        if (oct) done = octant_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, ks, kd, ki, visits, lb_exit);
-        if (!done) {
-#pragma unroll
-            for (int s = 0; s < KT; ++s) {  // (a k-list must not see the octant's points twice)
-                kd[s] = (T)__builtin_huge_val();
-                ki[s] = kNoPos;
-            }
-            lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, ks, kd, ki, visits, lb_exit,
-                               ks < KT ? ks + 1 : ks);
-        }
-    }
+    if (!qnan) lane_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, q, c, maxR2, k, kd, ki, visits, lb_exit);
     write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
     write_nbr<T, KT>(nbr, gpts, gpn, N, j, maxR2, kd, ki);
-    if (cand) {
-#pragma unroll
-        for (int s = 0; s < KT; ++s)
-            if (s < K) st_out(&cand[j * K + s], ki[s] == kNoPos ? (int32_t)-1 : ki[s]);
-    }
-    // (a certified octant block bounds the rest by its interior faces, as a
-    // shell walk's exit does)
-    if (safe) st_out(&safe[j], safe_radius<T, KT>(kd, ki, ks, lb_exit));
-}
-
-// the certificate for query j; true when the k-list was rewritten from the
-// previous one
-template <typename T, int KT>
-__device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, const int32_t* __restrict__ gidx,
-                                            const P4<T>& p, T qx, T qy, T qz, const Mat4<T>& Tprev, int64_t j,
-                                            int k, T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                            T* __restrict__ safe, uint32_t& visits, SpecAcc<T>& sa) {
-    const T rs = safe[j];
-    const T dkp = out_d[j * k + k - 1];
-    int32_t id[KT];
-    bool ok = rs > (T)0 && dkp < (T)__builtin_huge_val();
-#pragma unroll
-    for (int s = 0; s < KT; ++s) {
-        id[s] = s < k ? out_i[j * k + s] : 0;
-        ok = ok && id[s] >= 0;
-    }
-    if (!ok) return false;
-    T ox, oy, oz;
-    gxform(Tprev, p, ox, oy, oz);
-    const double ex = (double)qx - (double)ox, ey = (double)qy - (double)oy, ez = (double)qz - (double)oz;
-    const double delta = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + kReuseMargin);
-    const double a = sqrt((double)dkp) * (1.0 + kReuseMargin) + delta;
-    const double b = (double)rs * (1.0 - kReuseMargin) - delta;
-    if (!(a < b)) return false;
-    // the same k points: new distances, sorted as a full search sorts them
-    T kd[KT];
-    int32_t ki[KT];
-#pragma unroll
-    for (int s = 0; s < KT; ++s) {
-        kd[s] = (T)__builtin_huge_val();
-        ki[s] = kNoPos;
-    }
-#pragma unroll
-    for (int s = 0; s < KT; ++s)
-        if (s < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx, qy, qz, gld32(gpts, (uint32_t)id[s])), id[s]);
-    visits += (uint32_t)k;
-    write_out<T, KT>(j, k, maxR2, kd, ki, out_d, out_i, sa);
-    safe[j] = (T)(b * (1.0 - 1e-6));
-    return true;
+    if (safe) st_out(&safe[j], safe_radius<T, KT>(kd, ki, k, lb_exit));
 }
 
 // ---------------------------------------------- wave-cooperative search --
@@ -709,10 +554,7 @@ __device__ __forceinline__ bool reuse_query(const P4<T>* __restrict__ gpts, cons
 // converged match (the per-lane kernel's phase 2).  The result is the exact
 // k-list of the per-lane search: the same (distance, original index) order,
 // the same certificate on the interior faces of the visited box.
-#ifndef PMX_COOP_U
-#define PMX_COOP_U 4
-#endif
-constexpr int kCoopU = PMX_COOP_U;  // ring points each lane has in flight
+constexpr int kCoopU = 4;  // ring points each lane has in flight
 template <typename T>
 struct CoopEnt {
     T d;
@@ -792,7 +634,7 @@ __device__ __forceinline__ void coop_merge(T (&ld)[KT], int32_t (&lg)[KT], int32
 }
 
 // The search of one query (uniform arguments), every lane of the wave
-// calling.  ks: the rank the exit certifies (k, or K reuse candidates).
+// calling.  ks: the rank the exit certifies (k).
 // Returns the merged list (uniform, kd / kp as lane_search leaves them:
 // positions, kNoPos for an empty entry), lb_exit and the points evaluated
 // (lane 0 adds them to its visit count).
@@ -943,22 +785,13 @@ struct LaneQ {
 // takes 133-220 VGPRs, 2-3 waves, no spills): C5 1.79 -> 1.62 ms/iteration.
 // The float KT = 8 form spills 26 at 128 but measured faster that way than
 // unspilled at 3 waves (C4 0.202 vs 0.217 ms/iteration).
-#ifndef PMX_LIGHT
-#define PMX_LIGHT 0  // (experiment: every miss through the wave-cooperative search, PMX_LIGHT waves per SIMD)
-#endif
-#ifndef PMX_LANE_WAVES
-#define PMX_LANE_WAVES 0  // (experiment: the per-lane kernel's waves per SIMD; 0 = 4 float / 2 double)
-#endif
 template <typename T, int KT>
 struct LaneWaves {
-    static constexpr int value = PMX_LIGHT ? PMX_LIGHT : PMX_LANE_WAVES ? PMX_LANE_WAVES : (sizeof(T) == 8 ? 2 : 4);
+    static constexpr int value = sizeof(T) == 8 ? 2 : 4;
 };
-#ifndef PMX_TILE_WAVES
-#define PMX_TILE_WAVES 0  // (experiment: the tile kernel's waves per SIMD; 0 = the per-lane kernel's default)
-#endif
 template <typename T, int KT>
 struct TileWaves {
-    static constexpr int value = PMX_TILE_WAVES ? PMX_TILE_WAVES : (sizeof(T) == 8 ? 2 : 4);
+    static constexpr int value = sizeof(T) == 8 ? 2 : 4;
 };
 
 template <typename T, int KT, int Q>
@@ -967,13 +800,13 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
                                                         const uint32_t* __restrict__ start, GridGeom G,
                                                         const P4<T>* __restrict__ rd, int64_t N, Mat4<T> Tm, int k,
                                                         T maxR2, T* __restrict__ out_d, int32_t* __restrict__ out_i,
-                                                        unsigned long long* __restrict__ visited, int oct,
-                                                        int reuse, T* __restrict__ safe, Mat4<T> Tprev,
+                                                        unsigned long long* __restrict__ visited, int reuse,
+                                                        T* __restrict__ safe, Mat4<T> Tprev,
                                                         const LoopCtl* __restrict__ ctl,
                                                         const GridDesc<T>* __restrict__ gd,
                                                         SpecSel* __restrict__ spec, const T* __restrict__ radii,
-                                                        int K, int32_t* __restrict__ cand, int coop_max,
-                                                        P4<T>* __restrict__ nbr, const P4<T>* __restrict__ nbr_gpn) {
+                                                        int coop_max, P4<T>* __restrict__ nbr,
+                                                        const P4<T>* __restrict__ nbr_gpn) {
     if (ctl) {  // device loop: transform, level and reuse state from the device
         if (ctl->done) return;
         if (ctl->use_tile) return;  // (tile dispatch: the tile kernel's warm form runs this match)
@@ -990,16 +823,8 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             for (int i = 0; i < 16; ++i) Tprev.m[i] = (T)ctl->Tprev[i];
         }
     }
-    if (!reuse) {
-        safe = nullptr;
-        cand = nullptr;
-    }
-    if (!safe || cand || k != 1 || KT < 2) nbr = nullptr;  // (the record serves the k = 1 certificate)
-    // reuse candidates (K > k, cand != null): the certificate keeps the K
-    // nearest of the last full search and re-ranks them at the new position
-    // (see the temporal reuse notes above)
-    const bool cm = cand != nullptr;
-    const int nc = cm ? K : k;
+    if (!reuse) safe = nullptr;
+    if (!safe || k != 1 || KT < 2) nbr = nullptr;  // (the record serves the k = 1 certificate)
     uint32_t visits = 0;
     // quantile window (pmx_spec.h): every written distance is classified
     SpecAcc<T> sa;
@@ -1013,13 +838,12 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
 #pragma unroll
     for (int q = 0; q < Q; ++q) missed[q] = base + q * 256 + threadIdx.x < N;
     if (reuse == 2) {
-        // the certificate (reuse_query's rule) for the thread's Q slots, in
-        // stages so that each stage's loads are in flight together.  A list
-        // kept for reuse holds k <= KT - 1 entries (room for the (k+1)-th:
-        // the safe radius); KT = 16 keeps no room and never certifies.
-        // With K candidates (cm) the k-th distance is re-ranked at the new
-        // position: a = that distance, exact; without, a is bounded from the
-        // previous k-th distance (no gather for a query that cannot pass).
+        // the certificate (see the temporal reuse notes above) for the
+        // thread's Q slots, in stages so that each stage's loads are in flight
+        // together.  A list kept for reuse holds k <= KT - 1 entries (room for
+        // the (k+1)-th: the safe radius); KT = 16 keeps no room and never
+        // certifies.  The bound a uses the previous k-th distance, so a query
+        // that cannot pass costs no gather.
         constexpr int KR = KT > 1 ? KT - 1 : 1;
         P4<T> p[Q];
         T rs[Q], dkp[Q];
@@ -1030,13 +854,13 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             const int64_t j = missed[q] ? base + q * 256 + threadIdx.x : base;  // (base < N: an in-range slot)
             p[q] = gld(rd, j);
             rs[q] = safe[j];
-            dkp[q] = cm ? (T)0 : out_d[j * k + k - 1];
+            dkp[q] = out_d[j * k + k - 1];
             if (nbr) {  // (k = 1: the neighbour's record with the query, no dependent gather)
                 r[q][0] = nbr[j];
                 id[q][0] = (int32_t)w_pos(r[q][0].w);
             } else {
 #pragma unroll
-                for (int s = 0; s < KR; ++s) id[q][s] = s < nc ? (cm ? cand[j * K + s] : out_i[j * k + s]) : 0;
+                for (int s = 0; s < KR; ++s) id[q][s] = s < k ? out_i[j * k + s] : 0;
             }
         }
         bool ok[Q];
@@ -1045,7 +869,7 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             gxform(Tm, p[q], qx[q], qy[q], qz[q]);
-            bool o = missed[q] && nc <= KR && rs[q] > (T)0 && dkp[q] < (T)__builtin_huge_val();
+            bool o = missed[q] && k <= KR && rs[q] > (T)0 && dkp[q] < (T)__builtin_huge_val();
 #pragma unroll
             for (int s = 0; s < KR; ++s) o = o && id[q][s] >= 0;
             T ox, oy, oz;
@@ -1055,13 +879,13 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             const double delta = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + kReuseMargin);
             const double av = sqrt((double)dkp[q]) * (1.0 + kReuseMargin) + delta;
             bq[q] = (double)rs[q] * (1.0 - kReuseMargin) - delta;
-            ok[q] = o && (cm ? bq[q] > 0.0 : av < bq[q]);
+            ok[q] = o && av < bq[q];
         }
         if (!nbr) {
 #pragma unroll
             for (int q = 0; q < Q; ++q)
 #pragma unroll
-                for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < nc ? (uint32_t)id[q][s] : 0u);
+                for (int s = 0; s < KR; ++s) r[q][s] = gld32(gpts, ok[q] && s < k ? (uint32_t)id[q][s] : 0u);
         }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -1077,28 +901,13 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             }
 #pragma unroll
             for (int s = 0; s < KR; ++s)
-                if (s < nc) ginsert<T, KT>(gidx, kd, ki, gsqd(qx[q], qy[q], qz[q], r[q][s]), id[q][s]);
-            visits += (uint32_t)nc;
-            if (cm) {
-                // every point outside the candidates is beyond bq; the k-th
-                // candidate, re-ranked, must be nearer than that
-                T dk;
-                int32_t ik;
-                kth(kd, ki, k, dk, ik);
-                if (!(sqrt((double)dk) * (1.0 + kReuseMargin) < bq[q])) continue;  // (a full search below)
-            }
+                if (s < k) ginsert<T, KT>(gidx, kd, ki, gsqd(qx[q], qy[q], qz[q], r[q][s]), id[q][s]);
+            visits += (uint32_t)k;
             write_out<T, KT>(j, k, qr2(radii, j, maxR2), kd, ki, out_d, out_i, sa);
             st_out(&safe[j], (T)(bq[q] * (1.0 - 1e-6)));
             missed[q] = false;
         }
     }
-#if PMX_NOMISS  // (timing experiment only: the certificate pass without the misses' searches — wrong results)
-    if (reuse == 2) {
-        if (sa.on) spec_acc_flush<T>(sa, vslot(visited, 2), vslot(visited, 3));
-        add_visits(visits, visited);
-        return;
-    }
-#endif
     // the block's misses, compacted in slot order
     unsigned long long mq[Q];
 #pragma unroll
@@ -1120,11 +929,10 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
         if (missed[q]) miss[off + __popcll(mq[q] & ((1ull << lane) - 1))] = q * 256 + threadIdx.x;
     }
     __syncthreads();
-    if (PMX_LIGHT || total <= coop_max) {
+    if (total <= coop_max) {
         // few misses (a converged match): each is searched by a whole wave
         // (wave w takes misses w, w + 4, ...), two round trips per ring
         // instead of a lane's chain of dependent row gathers
-        const int ks = cand ? K : k;
         for (int t = wave; t < total; t += 4) {  // (wave-uniform)
             const int64_t j2 = base + miss[t];
             T qx, qy, qz;
@@ -1133,23 +941,18 @@ __global__ __launch_bounds__(256, (LaneWaves<T, KT>::value)) void grid_lane_kern
             T kd[KT];
             int32_t kp[KT];
             double lbx;
-            coop_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, ks, r2, kd, kp, lbx, visits);
+            coop_search<T, KT>(gpts, gidx, start, G, qx, qy, qz, k, r2, kd, kp, lbx, visits);
             if (lane == 0) {
                 write_out<T, KT>(j2, k, r2, kd, kp, out_d, out_i, sa);
                 write_nbr<T, KT>(nbr, gpts, nbr_gpn, N, j2, r2, kd, kp);
-                if (cand) {
-#pragma unroll
-                    for (int s = 0; s < KT; ++s)
-                        if (s < K) st_out(&cand[j2 * K + s], kp[s] == kNoPos ? (int32_t)-1 : kp[s]);
-                }
-                if (safe) st_out(&safe[j2], safe_radius<T, KT>(kd, kp, ks, lbx));
+                if (safe) st_out(&safe[j2], safe_radius<T, KT>(kd, kp, k, lbx));
             }
         }
     } else {
         for (int t = threadIdx.x; t < (Q == 1 ? min(total, 256) : total); t += 256) {  // (Q = 1: at most once)
             const int64_t j2 = base + miss[t];
-            full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), oct, out_d, out_i, safe,
-                              visits, sa, K, cand, nbr, nbr_gpn, N);
+            full_query<T, KT>(gpts, gidx, start, G, rd, j2, Tm, k, qr2(radii, j2, maxR2), out_d, out_i, safe, visits,
+                              sa, nbr, nbr_gpn, N);
             if (Q == 1) break;
         }
     }
@@ -1176,8 +979,8 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
         hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, e0, e1, 0,
                               gpts, gidx, start, G, rd, N, (const uint32_t*)nullptr, Tm, knn, maxR2, max_pts, dists,
                               ids, visited, radii, 1, ctl, gd, spec, ru.safe, ru.nbr, ru.gpn);
-    } else if (mode >= 1) {  // 1: shell search, 2: octant block first
-        const bool both = tile_disp && ctl && ru.mode && !ru.cand;
+    } else if (mode >= 1) {  // the per-lane shell search
+        const bool both = tile_disp && ctl && ru.mode;
         if (both)  // (device loop: the step picks one of the two forms)
             hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, e0,
                                   (hipEvent_t) nullptr, 0, gpts, gidx, start, G, rd, N, (const uint32_t*)nullptr, Tm,
@@ -1185,12 +988,10 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
                                   ru.nbr, ru.gpn);
         constexpr int Q = LaneQ<KT>::value;
         const int64_t grid = (N + 256 * Q - 1) / (256 * Q);
-        const bool cm = ru.mode && ru.cand && ru.K > knn && ru.K <= KT - 1;  // (the list holds K + 1)
         hipExtLaunchKernelGGL((grid_lane_kernel<T, KT, Q>), dim3((unsigned)grid), dim3(256), 0, s,
                               both ? (hipEvent_t) nullptr : e0, e1, 0, gpts, gidx, start, G, rd, N, Tm, knn, maxR2,
-                              dists, ids, visited, mode == 2 ? 1 : 0, ru.mode, ru.safe, ru.Tprev, ctl, gd, spec, radii,
-                              cm ? ru.K : knn, cm ? ru.cand : (int32_t*)nullptr, ru.coop_max,
-                              cm ? (P4<T>*)nullptr : ru.nbr, ru.gpn);
+                              dists, ids, visited, ru.mode, ru.safe, ru.Tprev, ctl, gd, spec, radii, ru.coop_max,
+                              ru.nbr, ru.gpn);
     } else {
         const int64_t W = waves ? n_waves : (N + 63) / 64;
         hipExtLaunchKernelGGL((grid_tile_kernel<T, KT>), dim3((unsigned)W), dim3(64), 0, s, e0, e1, 0, gpts, gidx,
@@ -1200,7 +1001,7 @@ static void launch_kt(int mode, const P4<T>* gpts, const int32_t* gidx, const ui
     }
 }
 
-// PMX_TILE_PROF: the cold form's per-wave profile into buf (4 words per wave)
+// option tile_prof: the cold form's per-wave profile into buf (4 words per wave)
 void set_tile_prof(unsigned long long* buf) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tile_prof), &buf, sizeof(buf)); }
 
 template <typename T>
@@ -1231,10 +1032,8 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
     launch_kt<T, KT>(mode, gpts, gidx, start, G, rd, N, waves, n_waves, Tm, knn, maxR2, max_pts, dists, ids, visited, \
                      ru, ctl, gd, spec, radii, cold, tile_disp, ev_start, ev_end, s)
         // with reuse the list keeps room for the (k+1)-th point (the safe radius;
-        // the cold tile writes radius 0 and keeps k entries); with K reuse
-        // candidates, for the (K+1)-th
-        const int kr = ru.cand && ru.K > knn ? ru.K : knn;
-        const int kl = ru.mode && mode >= 1 && kr < 16 && !cold ? kr + 1 : knn;
+        // the cold tile writes radius 0 and keeps k entries)
+        const int kl = ru.mode && mode >= 1 && knn < 16 && !cold ? knn + 1 : knn;
         if (kl == 1)
             PMX_KT(1);
         else if (kl <= 2)

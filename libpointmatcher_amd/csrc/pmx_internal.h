@@ -85,20 +85,11 @@ __device__ __forceinline__ int32_t gld(const int32_t* p, int64_t i) {
 }
 
 // Stores of per-query outputs the NEXT kernel reads (match distances, ids,
-// safe radii).  PMX_WT=1 (experiment): agent-scope relaxed stores, which
-// write through L2 (sc1), so the kernel ends with no dirty lines to write
-// back at the boundary (MI355X_MICROARCH.md "boundary": + B / 6 TB/s for B
-// dirty bytes).
-#ifndef PMX_WT
-#define PMX_WT 0
-#endif
+// safe radii): plain stores (write-through agent-scope stores measured the
+// same)
 template <typename V>
 __device__ __forceinline__ void st_out(V* p, V v) {
-#if PMX_WT
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
     *p = v;
-#endif
 }
 
 template <typename T>
@@ -183,10 +174,6 @@ struct GridReuse {
     int mode = 0;
     T* safe = nullptr;
     Mat4<T> Tprev{};
-    // reuse candidates (K > k): the K nearest of each query's last full
-    // search, int32[N * K] (null: the k-list itself is the candidate set)
-    int K = 0;
-    int32_t* cand = nullptr;
     // a block whose misses are at most this many searches each with a whole
     // wave (pmx_grid.hip coop_search); more take the per-lane search
     int coop_max = 0;
@@ -216,8 +203,8 @@ void launch_knn_wide(const P4<T>* pts, const int32_t* gidx, const uint32_t* star
 
 
 // ---- grid match (pmx_grid.hip) ----
-// mode 0 = wave-cooperative LDS tiles, 1 = per-lane shell search (default),
-// 2 = octant block first.  ids written are positions in gpts;
+// mode 0 = wave-cooperative LDS tiles, 1 = per-lane shell search (default).
+// ids written are positions in gpts;
 // launch_pos_to_index maps them back.  ctl / gd (device loop, modes 1-2):
 // transform and level are read on the device.  cold: a new reading's first
 // match (no previous match to certify from) on the tile kernel's cold form.
@@ -236,7 +223,7 @@ void launch_grid_match(int mode, const P4<T>* gpts, const int32_t* gidx, const u
 // (pmx_spec.h); xseg above is this rank's segment, packed by the counter sum.
 // stall: a miss sets ctl->done = kCtlStalled (the host did not read the
 // verdict; it replays the iteration).  force_miss: treat the window as
-// missed (test hook, PMX_DEBUG_FORCE_MISS).
+// missed (test hook, option force_miss).
 template <typename T>
 void launch_spec_pick(const unsigned long long* segs, int nseg, SpecSel* spec, SelectState* st, LoopCtl* ctl,
                       int stall, int force_miss, hipStream_t s);
@@ -488,10 +475,7 @@ size_t vartrim_scratch_head();  // leading bytes of that scratch that must be ze
 int vartrim_hdr_copy();     // int offset of the last call's counters in that scratch (pmx_vartrim_partial_sums)
 
 // ---- reductions (pmx_reduce.hip) ----
-#ifndef PMX_RED_BLOCKS
-#define PMX_RED_BLOCKS 512
-#endif
-constexpr int kRedBlocks = PMX_RED_BLOCKS;  // fixed reduction grid (deterministic sums)
+constexpr int kRedBlocks = 512;  // fixed reduction grid (deterministic sums; 256 / 1024 measured slower)
 constexpr int kNVMax = 48;
 // point-to-plane result layout: upper triangle of A (NS), b (NF), then kept,
 // nonzero weights, rejected matches, rejected points, sum of the weights

@@ -17,7 +17,7 @@ namespace pmxc {
 // copy per 8 iterations.  Same-box means of four runs at C3: driver 0.06728 vs
 // 0.06775 ms/iteration with 4 throughout (8 throughout 0.0673), whole ICP
 // 0.0932 vs 0.0939 — small; 2 throughout is slower (0.068-0.071).
-// PMX_LOOP_BATCH fixes one size (A/Bs).
+// Option loop_batch fixes one size (A/Bs).
 constexpr int kLoopBatch = 4;
 constexpr int kLoopBatchLong = 8;
 constexpr int kLoopBatchAfter = 8;
@@ -86,7 +86,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     }
     d.adaptive = c->adaptive ? 1 : 0;
     d.reuse = c->reuse_on && c->grid_mode >= 1 ? 1 : 0;
-    d.knn = reuse_k(c, cfg->knn);  // (pairs a certified query evaluates: its reuse candidates)
+    d.knn = cfg->knn;  // (pairs a certified query evaluates)
     // tile dispatch: a reading much denser than the reference (the tile
     // kernel's wave-shared boxes serve 64 nearby queries with one load);
     // the per-lane kernel's temporal reuse must be on (the step judges its
@@ -94,7 +94,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     {
         const bool dense = c->N >= 4 * std::max<int64_t>(c->grid_valid, 1);
         const bool want = c->tile_dispatch_req > 0 || (c->tile_dispatch_req < 0 && dense);
-        d.tile_dispatch = want && d.reuse && cfg->knn < kLaneMaxK && reuse_k(c, cfg->knn) == cfg->knn ? 1 : 0;
+        d.tile_dispatch = want && d.reuse && cfg->knn < kLaneMaxK ? 1 : 0;
     }
     d.n_levels = c->levels_built;
     d.n_levels_all = (int)c->levels.size();
@@ -128,12 +128,10 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     std::memcpy(stage, T0, sizeof(T) * rr);
     HIPCHK(c, hipMemcpyAsync(c->d_loop_T0, stage, sizeof(T) * rr, hipMemcpyHostToDevice, c->stream));
     // the first loop match may reuse the last classic one
-    const int Kr = reuse_k(c, cfg->knn);
     // (k = 1: only if that match left its neighbour records, which the
     // loop's reuse reads)
-    const bool nbr_ok = !(cfg->knn == 1 && Kr == 1 && c->nbr_on) || c->nbr_prev;
-    const int prev_level = c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn &&
-                                   (Kr == cfg->knn || c->cand_K == Kr) && nbr_ok
+    const bool nbr_ok = !(cfg->knn == 1 && c->nbr_on) || c->nbr_prev;
+    const int prev_level = c->reuse_on && c->safe_valid && c->have_match && c->ids_grid && c->knn == cfg->knn && nbr_ok
                                ? c->ids_level
                                : -1;
     launch_loop_init<T>(c->d_ctl, (LoopState<T>*)c->d_loop, d, (const T*)c->d_loop_T0, c->level, prev_level,
@@ -213,14 +211,7 @@ int loop_enqueue_iteration(pmx_ctx* c) {
     // in the fused finalize + step launch instead (one launch fewer; the
     // step is the first reader of the counters).  Not with a robust filter:
     // its replayed iterations return before the step.
-    static const bool fuse_env = [] {
-        const char* e = std::getenv("PMX_FUSE_STEP");
-        return !e || std::atoi(e) != 0;
-    }();
-    static const bool step_counter_env = [] {
-        const char* e = std::getenv("PMX_STEP_COUNTER");
-        return !e || std::atoi(e) != 0;
-    }();
+    const bool fuse_env = c->fuse_step, step_counter_env = c->step_counter_on;  // (options fuse_step, step_counter)
     bool robust = false;
     for (int i = 0; i < cfg.n_filters; ++i) robust = robust || cfg.filter_kind[i] == PMX_FILTER_ROBUST;
     c->step_counter = step_counter_env && fuse_env && !c->spec_on && !sharded(c) && !robust && c->grid_mode >= 1 &&
@@ -302,10 +293,7 @@ int loop_run_impl(pmx_ctx* c, int n, pmx_loop_status* st) {
     c->loop_on = true;
     while (!stop && rc == PMX_OK) {
         while (c->loop_issued - start < n && nfly < 2 && rc == PMX_OK) {
-            static const int fixed = [] {
-                const char* e = std::getenv("PMX_LOOP_BATCH");
-                return e ? std::max(1, std::atoi(e)) : 0;
-            }();
+            const int fixed = c->loop_batch;  // (option loop_batch)
             // (sharded loops keep batches of 4: a stall replays from the stalled
             // iteration, and the rest of its batch ran as no-ops; world size 1
             // over RCCL 0.0812 with 8 vs 0.077 ms/iteration)

@@ -126,9 +126,6 @@ __device__ __forceinline__ void p2plane_add(double (&acc)[NV], T px, T py, T pz,
 // one block's sums to partials[v * gridDim.x + blockIdx.x]
 // k up to this: the reduction issues a query's k gathers together
 constexpr int kGatherK = 4;
-#ifndef PMX_P2P_XCD
-#define PMX_P2P_XCD 1
-#endif
 template <typename T, int DIM, bool kCoherent = false>
 __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const Mat4<T>& Tm,
                                              const P4<T>* __restrict__ ref, const P4<T>* __restrict__ nrm, int rs,
@@ -144,14 +141,10 @@ __device__ __forceinline__ void p2plane_body(const P4<T>* __restrict__ rd, const
     const WRange<T> wr = chain_resolve(chain);
     const T inf = (T)__builtin_huge_val();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-#if PMX_P2P_XCD
     // XCD-aware block order (pmx_internal.h): the blocks of one XCD take
     // adjacent slot ranges, so the gathered point/normal records of
     // neighbouring queries meet in one L2 (the partial slot stays blockIdx.x)
     int64_t i0 = (int64_t)xcd_block() * blockDim.x + threadIdx.x;
-#else
-    int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#endif
     if (k == 1) {
         // k = 1: U slots per round with every load issued up front (the
         // reduction is latency-bound: slot -> id -> gathered point / normal;

@@ -463,10 +463,7 @@ constexpr int kCumChunk = kCumThreads * kCumPer;
 // (the head is summed by the preparation launch's extra block while the
 // other blocks prepare their chunks; 8 K measured slower: the serial sum of
 // the head, ~10 ns per key, outlasts the passes it saves)
-#ifndef PMX_VT_HEAD
-#define PMX_VT_HEAD 4096
-#endif
-constexpr int kCumHead = PMX_VT_HEAD;
+constexpr int kCumHead = 4096;
 constexpr int kFastTies = 256;
 constexpr int kChunkLds = 512;  // chunk-table entries the walk preloads into LDS
 

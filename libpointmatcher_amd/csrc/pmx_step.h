@@ -204,16 +204,8 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
         // solve_full_rank: FullPivQR(A).isInvertible() -> LLT solve.  The
         // QR's rank test is skipped when the LLT factor proves A far from
         // rank-deficient (well_conditioned below): its answer is then known.
-#if PMX_STEP_NOMATH  // (timing experiment only: the step's memory and launch cost without its arithmetic)
-        (void)L;
-        for (int i = 0; i < NF; ++i) x[i] = b[i] * (T)0;
-#else
         llt(A, NF, L);
-#if PMX_STEP_NOWC  // (timing experiment only: the conditioning bound's cost)
-        bool full = true;
-#else
         bool full = well_conditioned<T, NF>(A, L);
-#endif
         if (!full) {
             FullPivQR<T> qr;
             qr.compute(A, NF);
@@ -225,7 +217,6 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
             loop_solve_rank_deficient<T, NF>(res, cfg.full, S->xsolve);
             for (int i = 0; i < NF; ++i) x[i] = S->xsolve[i];
         }
-#endif
         p2plane_transform(rows, x, dT);
     } else {
         T m[9], mp[3], mq[3];

@@ -13,20 +13,16 @@ from libpointmatcher_amd.synth import random_cloud, reading_cloud, reference_clo
 pytestmark = pytest.mark.gpu
 
 # every test runs against each grid search form: the per-lane kernel (default),
-# the octant block first, coarse / fine levels, no temporal reuse, and the
-# wave-cooperative tile kernel (with a box budget that sends most lanes to the
-# per-lane fallback)
-MODES = {"lane": {}, "lane_coarse": {"PMX_GRID_PPC": "32"}, "octant": {"PMX_GRID_MODE": "octant"},
-         "lane_noreuse": {"PMX_GRID_REUSE": "0"}, "lane_fine": {"PMX_GRID_PPC": "1"},
-         "tile": {"PMX_GRID_MODE": "tile"}, "tile_fallback": {"PMX_GRID_MODE": "tile", "PMX_GRID_TILE_MAX": "16"}}
+# coarse / fine levels, no temporal reuse, and the wave-cooperative tile kernel
+# (with a box budget that sends most lanes to the per-lane fallback); the
+# forms are context options (PMX_OPTS, README "Options")
+MODES = {"lane": "", "lane_coarse": "grid_levels=32", "lane_noreuse": "grid_reuse=0", "lane_fine": "grid_levels=1",
+         "tile": "grid_mode=tile", "tile_fallback": "grid_mode=tile,tile_max=16"}
 
 
 @pytest.fixture(autouse=True, params=sorted(MODES))
 def grid_mode(request, monkeypatch):
-    for k in ("PMX_GRID_MODE", "PMX_GRID_TILE_MAX", "PMX_GRID_PPC", "PMX_GRID_LEVELS", "PMX_GRID_ADAPT", "PMX_GRID_REUSE"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in MODES[request.param].items():
-        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PMX_OPTS", MODES[request.param])
     return request.param
 
 
@@ -203,14 +199,9 @@ def test_temporal_reuse_stays_exact(oracle, grid_mode, k):
     ctx.close()
     if grid_mode in ("lane", "lane_coarse", "lane_fine"):
         # the repeated pose was certified from the previous match (k pairs per
-        # query; K with PMX_REUSE_CAND = K > k reuse candidates)
-        # (the adaptive level may move during the first repeats: a level change
-        # restarts the reuse chain)
-        import os
-
-        kc = int(os.environ.get("PMX_REUSE_CAND", "0") or 0)
-        kr = kc if k < kc < 16 else k
-        assert min(visits[2:5]) <= 1.1 * 20_000 * kr < visits[0]
+        # query) (the adaptive level may move during the first repeats: a
+        # level change restarts the reuse chain)
+        assert min(visits[2:5]) <= 1.1 * 20_000 * k < visits[0]
 
 
 @pytest.mark.parametrize("k", [1, 3])
@@ -218,7 +209,7 @@ def test_neighbour_records_equal_gathers(oracle, grid_mode, monkeypatch, k):
     # the k = 1 neighbour records (pmx_grid.hip write_nbr: the certificate's
     # neighbour and the point-to-plane reduction's point and normal read in
     # slot order) give the same matches and the same normal equations, bit
-    # for bit, as the gathers by id (PMX_NBR_CACHE=0), through reuse,
+    # for bit, as the gathers by id (option nbr_cache=0), through reuse,
     # a jump, a radius and a new reading
     from libpointmatcher_amd.synth import t_gt
 
@@ -231,7 +222,7 @@ def test_neighbour_records_equal_gathers(oracle, grid_mode, monkeypatch, k):
              (Tg, np.inf)]
     runs = []
     for on in ("1", "0"):
-        monkeypatch.setenv("PMX_NBR_CACHE", on)
+        monkeypatch.setenv("PMX_OPTS", ",".join(o for o in (MODES[grid_mode], "nbr_cache=" + on) if o))
         ctx = P.Context(0, np.float32)
         ctx.set_search(1)
         ctx.set_reference(ref, nrm)

@@ -37,7 +37,7 @@ def run_mode(monkeypatch, mode, yaml, rd, ref, nrm, dtype):
 def test_loop_equals_modules(monkeypatch, oracle, dtype, minimizer, reuse):
     # reuse=1: the grid match may certify the previous iteration's k-lists
     # (LoopCtl.Tprev in loop mode, the host's previous step in module mode)
-    monkeypatch.setenv("PMX_GRID_REUSE", reuse)
+    monkeypatch.setenv("PMX_OPTS", "grid_reuse=" + reuse)
     ref, nrm = reference_cloud(50000, dtype)
     rd = reading_cloud(40000, dtype)
     yaml = chain_yaml(minimizer=minimizer, maxit=25, differential=DIFF)
@@ -191,7 +191,7 @@ def test_quantile_window_is_exact(monkeypatch, dtype, filt, knn, max_dist):
     rd = reading_cloud(50000, dtype)
     out = {}
     for on in ("1", "0"):
-        monkeypatch.setenv("PMX_SPEC_SELECT", on)
+        monkeypatch.setenv("PMX_OPTS", "spec_select=" + on)
         ctx = _capi.Context(0, dtype)
         ctx.set_reference(ref, nrm)
         ctx.set_reading(rd)

@@ -17,7 +17,7 @@ Bars (against the single-process oracle on the WHOLE reading):
     as all-gathered segments): final T within 1e-5 (f32) / 1e-12 (f64) with
     equal iteration counts and kept pairs, every rank the same T;
   * the sharded window resolves quantiles (hits > 0) and equals the radix
-    path (PMX_SPEC_SELECT=0) bit for bit;
+    path (option spec_select=0) bit for bit;
   * a window hit costs an iteration two collectives (pmx_comm_stats).
 Reference semantics: OutlierFilter.cpp:63-103, Matches.cpp:60-87,
 OutlierFiltersImpl.cpp:132-223, PointToPlane.cpp:171-243, ICP.cpp:317-449.
@@ -185,7 +185,7 @@ def two_ranks(tmp_path_factory):
 def two_ranks_radix(tmp_path_factory):
     # the same runs with the quantile window off: every limit from the radix
     # passes with their histogram all-reduce
-    return _run_two_ranks(tmp_path_factory.mktemp("mr_gpu_radix"), {"PMX_SPEC_SELECT": "0"})
+    return _run_two_ranks(tmp_path_factory.mktemp("mr_gpu_radix"), {"PMX_OPTS": "spec_select=0"})
 
 
 @pytest.mark.timeout(900)
@@ -338,7 +338,7 @@ def test_rccl_one_rank_is_bit_identical(oracle, dn, monkeypatch):
 def two_ranks_forced_miss(tmp_path_factory):
     # misses forced at loop iterations 10 and 17 (past the settling
     # iterations: enqueued blind, so they stall the device loop and replay)
-    return _run_two_ranks(tmp_path_factory.mktemp("mr_gpu_miss"), {"PMX_DEBUG_FORCE_MISS": "10,17",
+    return _run_two_ranks(tmp_path_factory.mktemp("mr_gpu_miss"), {"PMX_OPTS": "force_miss=10:17",
                                                                    "MR_LOOP_ONLY": "1"})
 
 

@@ -42,8 +42,7 @@ def main():
     t1 = time.perf_counter()
     ms, n = ctx.timing_read()
     per = ms / n
-    print(f"N={N} M={M} k={k} {dt.__name__} search={search} ppc={os.environ.get('PMX_GRID_PPC', '8')} "
-          f"order={'off' if os.environ.get('PMX_GRID_NOORDER') else 'on'}: setup {t_setup:.2f}s, "
+    print(f"N={N} M={M} k={k} {dt.__name__} search={search} options={os.environ.get('PMX_OPTS', '')!r}: setup {t_setup:.2f}s, "
           f"iter {1e3 * (t1 - t0) / iters:.3f} ms wall, match {per:.3f} ms, visited/query {st.visited / N:.1f}, "
           f"{st.visited / (per * 1e-3) / 1e9:.1f} Gpair/s, kept={st.kept}, fallback={st.fallback_queries}")
 

@@ -1,8 +1,8 @@
 """Setup timeline of ICP::compute's prepare (development tool): prepares the
 bench configuration's clouds three times on one context with
-PMX_SETUP_TRACE=1 (the library prints each phase), and prints the host-side
+PMX_OPTS=setup_trace=1 (the library prints each phase), and prints the host-side
 prepare wall time and the stats' reference / reading parts.
-usage: PMX_SETUP_TRACE=1 python tools/setup_trace.py [c3|c5]"""
+usage: PMX_OPTS=setup_trace=1 python tools/setup_trace.py [c3|c5]"""
 import os
 import sys
 import time

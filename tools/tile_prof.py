@@ -1,7 +1,7 @@
 """Per-wave profile of the cold tile match (development tool): one ICP of
-the bench configuration with PMX_TILE_PROF=1 (the library prints the cold
+the bench configuration with PMX_OPTS=tile_prof=1 (the library prints the cold
 form's per-wave durations, rounds and copied points to stderr).
-usage: PMX_TILE_PROF=1 python tools/tile_prof.py [c3|c5|...] [reps]"""
+usage: PMX_OPTS=tile_prof=1 python tools/tile_prof.py [c3|c5|...] [reps]"""
 import os
 import sys
 

@@ -1,6 +1,6 @@
 """VarTrimmed partial sums on the spread/jump parity data, with the walk's
 trace (development tool): prints the first differing sums and the walk's
-steps.  usage: PMX_VT_TRACE=1 python tools/vt_debug.py [jump|decades] [f32|f64]"""
+steps.  usage: PMX_OPTS=vt_trace=1 python tools/vt_debug.py [jump|decades] [f32|f64]"""
 import os
 import sys
 

@@ -1,10 +1,10 @@
 """Timeline of the VarTrimmed partial-sum walk at C3 (development tool).
 
 Runs the C3 ICP for a few iterations (for a realistic pose), then one match +
-VarTrimmedDist at that pose through the context API with PMX_VT_TRACE=1: the
+VarTrimmedDist at that pose through the context API with PMX_OPTS=vt_trace=1: the
 library prints every step of vt_cumsum_kernel's walk (100 MHz real-time
 stamps) to stderr.
-usage: PMX_VT_TRACE=1 python tools/vt_trace.py [iterations]
+usage: PMX_OPTS=vt_trace=1 python tools/vt_trace.py [iterations]
 """
 import os
 import sys
