@@ -1,5 +1,5 @@
 """Steady-state anatomy of the device loop from a rocprofv3 kernel trace
-(development tool): the last N iterations (delimited by loop_step_kernel),
+(development tool): the last N iterations (delimited by the step launch),
 per-kernel average duration, the average gap in front of each kernel, and
 the iteration period.  Usage: python tools/trace_iter.py run_kernel_trace.csv [N]"""
 import csv
@@ -21,7 +21,7 @@ def main(path, n_last=20):
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
-    steps = [i for i, r in enumerate(rows) if r[2] == "loop_step_kernel"]
+    steps = [i for i, r in enumerate(rows) if r[2] in ("loop_step_kernel", "finalize_step_kernel")]
     if len(steps) < n_last + 1:
         print("not enough loop iterations", len(steps))
         return
@@ -29,7 +29,8 @@ def main(path, n_last=20):
     # steady ones: period below `cut` us
     loopk = {"grid_lane_kernel", "counter_sum_kernel", "select_all_kernel", "p2plane_partial_kernel",
              "finalize_kernel", "loop_step_kernel", "__amd_rocclr_copyBuffer", "p2point_pass1_kernel",
-             "p2point_pass2_kernel", "p2point_means_kernel", "grid_tile_kernel"}
+             "p2point_pass2_kernel", "p2point_means_kernel", "grid_tile_kernel", "finalize_step_kernel",
+             "p2plane_select_kernel"}
     cut = float(sys.argv[3]) if len(sys.argv) > 3 else 150.0
     its = []
     for a, b in zip(steps[:-1], steps[1:]):
