@@ -179,6 +179,7 @@ int set_option(pmx_ctx* c, const std::string& key, const std::string& val) {
         else if (key == "coop_max") c->coop_max = (int)std::max(0.0, std::min(256.0, v));
         else if (key == "fuse_step") c->fuse_step = b;
         else if (key == "step_counter") c->step_counter_on = b;
+        else if (key == "p2p_onepass") c->p2p_onepass = b;
         else if (key == "side_levels") c->side_levels = b;
         else if (key == "reading_copy") c->reading_copy = b;
         else if (key == "reading_order") c->reading_order = b;

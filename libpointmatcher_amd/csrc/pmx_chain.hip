@@ -1401,6 +1401,21 @@ int p2point_enqueue(pmx_ctx* c) {
         chain.w_arr = (const T*)c->d_w;
     }
     const GridDesc<T>* gd = (const GridDesc<T>*)c->d_gdesc;
+    if (c->loop_on && c->loop_dev.p2p_onepass) {
+        // device loop: both passes' sums in one read of the matches, the
+        // step centres the moments (LoopCfg.p2p_onepass)
+        launch_p2point_moments<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists,
+                                  c->d_ids, chain, c->knn, c->N, c->d_partials, loop_ctl(c), gd, c->stream);
+        if (c->fuse_final) {  // (summed by the fused finalize + step launch)
+            c->final_out = c->d_result;
+            c->final_nv = 20;
+            HIPCHK(c, hipGetLastError());
+            return PMX_OK;
+        }
+        launch_finalize(c->d_partials, kRedBlocks, 20, c->d_result, loop_ctl(c), c->stream);
+        HIPCHK(c, hipGetLastError());
+        return allreduce_f64(c, c->d_result, 20);
+    }
     launch_p2point_pass1<T>((const P4<T>*)c->d_rd, Tm, (const P4<T>*)match_ref(c), (const T*)c->d_dists, c->d_ids,
                             chain, c->knn, c->N, c->d_partials, loop_ctl(c), gd, c->stream);
     launch_finalize(c->d_partials, kRedBlocks, 11, c->d_result, loop_ctl(c), c->stream);

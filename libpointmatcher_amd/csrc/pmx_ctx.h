@@ -115,6 +115,7 @@ struct pmx_ctx {
     // A/B switches of measured alternatives and test hooks, per context
     bool fuse_step = true;        // fuse_step: the last finalize and the step in one launch (device loop, one rank)
     bool step_counter_on = true;  // step_counter: the match's counter phase folded into that launch (no window)
+    bool p2p_onepass = true;      // p2p_onepass: device-loop point-to-point in one moments pass (the step centres)
     bool side_levels = true;      // side_levels: the levels finer than the cold one on a side stream
     bool reading_copy = true;     // reading_copy: the reading's upload on the copy stream
     bool reading_order = true;    // reading_order: the reading in slot (Morton) order

@@ -500,6 +500,12 @@ void launch_p2point_pass1(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, 
                           const LoopCtl* ctl, const GridDesc<T>* gd, hipStream_t s);
 template <typename T>
 void launch_p2point_means(const double* sums, T* means_dev, int dim, const LoopCtl* ctl, hipStream_t s);
+// both passes' sums in one (device loop; the step centres the moments,
+// pmx_step.h): 20 values, layout in pmx_reduce.hip
+template <typename T>
+void launch_p2point_moments(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
+                            const WChain<T>& chain, int k, int64_t N, double* partials, const LoopCtl* ctl,
+                            const GridDesc<T>* gd, hipStream_t s);
 template <typename T>
 void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d,
                           const int32_t* ids, const WChain<T>& chain, int k, int64_t N, const T* means_dev,

@@ -51,6 +51,7 @@ struct LoopCfg {
     int reuse;  // the grid match's temporal reuse is on (level choice on full searches only)
     int knn;
     int tile_dispatch;  // both match forms enqueued; the step picks the next (pmx_step.h)
+    int p2p_onepass;    // point-to-point: one moments pass (launch_p2point_moments layout), the step centres
 };
 
 template <typename T>

@@ -100,6 +100,10 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
     d.n_levels_all = (int)c->levels.size();
     for (int l = 0; l < d.n_levels_all; ++l) d.level_ppc[l] = c->lv(l).ppc;
     d.n_local = c->N;
+    // (double only: in float the reference centres in T before its products,
+    // and the one-pass form drifted 1.05e-5 from the per-module path over 25
+    // iterations, past the 1e-5 bar; in double both are far inside 1e-12)
+    d.p2p_onepass = cfg->minimizer == 1 && c->p2p_onepass && c->dtype == PMX_F64 ? 1 : 0;
     int rc;
     size_t cap = 0;
     (void)cap;  // (LoopState lives in the status block)

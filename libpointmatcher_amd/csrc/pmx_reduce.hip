@@ -342,6 +342,77 @@ void launch_p2point_pass2(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, 
                        means_dev, partials, ctl, gd);
 }
 
+// Point-to-point in one pass (device loop): the sums both of the reference's
+// passes need — sum w, sum w p, sum w q, the ErrorElements counters and the
+// raw moments sum (w q) p^T — in one read of the matches.  The step forms the
+// weighted means in T as p2point_means_kernel does and centres the moments in
+// fp64: sum w (q - mq)(p - mp)^T = sum (w q) p^T - mq (sum w p)^T
+// - (sum w q) mp^T + (sum w) mq mp^T (PointToPoint.cpp:67-81 by the same
+// identity; the two-pass kernels above are the per-module path's).
+// Layout: [0] sum w, [1, 4) sum w p, [4, 7) sum w q, [7, 11) kept, nonzero
+// weights, rejected matches, rejected points, [11, 20) sum (w q_r) p_c.
+template <typename T>
+__global__ __launch_bounds__(256) void p2point_moments_kernel(const P4<T>* __restrict__ rd, Mat4<T> Tm,
+                                                              const P4<T>* __restrict__ ref, const T* __restrict__ d,
+                                                              const int32_t* __restrict__ ids, WChain<T> chain, int k,
+                                                              int64_t N, double* __restrict__ partials,
+                                                              const LoopCtl* __restrict__ ctl,
+                                                              const GridDesc<T>* __restrict__ gd) {
+    constexpr int NV = 20;
+    if (ctl) {  // device loop
+        if (ctl->done) return;
+        ctl_transform(ctl, Tm);
+        ref = gd[ctl->level].gpts;
+    }
+    double acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+    const WRange<T> wr = chain_resolve(chain);
+    const T inf = (T)__builtin_huge_val();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)xcd_block() * blockDim.x + threadIdx.x; i < N; i += stride) {
+        T px, py, pz;
+        xform3(Tm, rd[i], px, py, pz);
+        bool exist = false;
+        for (int s = 0; s < k; ++s) {
+            const int64_t e = i * k + s;
+            const T dv = d[e];
+            const T w = chain.robust ? robust_chain_weight(chain, wr, dv, e) : (chain_keep(wr, dv) ? (T)1 : (T)0);
+            if (w != (T)0) acc[8] += 1.0;
+            if (dv == inf) continue;
+            if (w == (T)0) {
+                acc[9] += 1.0;
+                continue;
+            }
+            exist = true;
+            acc[7] += 1.0;
+            const P4<T> q = gld(ref, ids[e]);
+            const T wq[3] = {q.x * w, q.y * w, q.z * w};
+            const double p[3] = {(double)px, (double)py, (double)pz};
+            acc[0] += (double)w;
+            acc[1] += (double)(px * w);
+            acc[2] += (double)(py * w);
+            acc[3] += (double)(pz * w);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                acc[4 + r] += (double)wq[r];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[11 + r * 3 + c] += (double)wq[r] * p[c];
+            }
+        }
+        if (!exist) acc[10] += 1.0;
+    }
+    block_store<NV>(acc, partials);
+}
+
+template <typename T>
+void launch_p2point_moments(const P4<T>* rd, const Mat4<T>& Tm, const P4<T>* ref, const T* d, const int32_t* ids,
+                            const WChain<T>& chain, int k, int64_t N, double* partials, const LoopCtl* ctl,
+                            const GridDesc<T>* gd, hipStream_t s) {
+    hipLaunchKernelGGL(p2point_moments_kernel<T>, dim3(kRedBlocks), dim3(256), 0, s, rd, Tm, ref, d, ids, chain, k,
+                       N, partials, ctl, gd);
+}
+
 // materialise the chain's weights (host mirror only); point-to-plane robust
 // distances need the step reading, the match ids and the reference records
 template <typename T>
@@ -389,6 +460,9 @@ void launch_weights_chain(const T* d, T* w, int64_t n, const WChain<T>& chain, c
                                           const WChain<T>&, int, int64_t, double*, const LoopCtl*,                   \
                                           const GridDesc<T>*, hipStream_t);                                          \
     template void launch_p2point_means<T>(const double*, T*, int, const LoopCtl*, hipStream_t);                      \
+    template void launch_p2point_moments<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,   \
+                                            const WChain<T>&, int, int64_t, double*, const LoopCtl*,              \
+                                            const GridDesc<T>*, hipStream_t);                                      \
     template void launch_p2point_pass2<T>(const P4<T>*, const Mat4<T>&, const P4<T>*, const T*, const int32_t*,     \
                                           const WChain<T>&, int, int64_t, const T*, double*, const LoopCtl*,         \
                                           const GridDesc<T>*, hipStream_t);                                          \

@@ -220,10 +220,25 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
         p2plane_transform(rows, x, dT);
     } else {
         T m[9], mp[3], mq[3];
-        for (int i = 0; i < D; ++i) {
-            mp[i] = means[i];
-            mq[i] = means[3 + i];
-            for (int j = 0; j < D; ++j) m[i * D + j] = (T)res[16 + i * 3 + j];
+        if (cfg.p2p_onepass) {
+            // one moments pass (launch_p2point_moments): the weighted means in
+            // T (p2point_means_kernel's arithmetic), the moments centred in fp64
+            const T winv = (T)1 / (T)res[0];
+            for (int i = 0; i < D; ++i) {
+                mp[i] = (T)res[1 + i] * winv;
+                mq[i] = (T)res[4 + i] * winv;
+            }
+            for (int i = 0; i < D; ++i)
+                for (int j = 0; j < D; ++j) {
+                    const double a = (double)mq[i], bb = (double)mp[j];
+                    m[i * D + j] = (T)(((res[11 + i * 3 + j] - a * res[1 + j]) - res[4 + i] * bb) + res[0] * a * bb);
+                }
+        } else {
+            for (int i = 0; i < D; ++i) {
+                mp[i] = means[i];
+                mq[i] = means[3 + i];
+                for (int j = 0; j < D; ++j) m[i * D + j] = (T)res[16 + i * 3 + j];
+            }
         }
         p2point_transform(rows, m, mp, mq, dT);
     }
