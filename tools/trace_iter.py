@@ -3,6 +3,7 @@
 per-kernel average duration, the average gap in front of each kernel, and
 the iteration period.  Usage: python tools/trace_iter.py run_kernel_trace.csv [N]"""
 import csv
+import os
 import re
 import sys
 from collections import defaultdict
@@ -36,7 +37,7 @@ def main(path, n_last=20):
     for a, b in zip(steps[:-1], steps[1:]):
         ks = {rows[i][2] for i in range(a + 1, b + 1)}
         per = (rows[b][1] - rows[a][1]) / 1e3
-        if ks <= loopk and per < cut:
+        if (ks <= loopk or os.environ.get("TRACE_ALL")) and per < cut:
             its.append((a, b, per))
     its = its[-n_last:]
     dur = defaultdict(list)
