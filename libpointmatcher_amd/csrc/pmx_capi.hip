@@ -186,7 +186,10 @@ int set_option(pmx_ctx* c, const std::string& key, const std::string& val) {
         else if (key == "loop_batch") c->loop_batch = (int)std::max(0.0, v);
         else if (key == "wave_fill") c->wave_fill = std::max(1.0, v);
         else if (key == "setup_trace") c->setup_trace = (int)v;
-        else if (key == "tile_prof") c->tile_prof = b;
+        else if (key == "tile_prof") {
+            c->tile_prof = b;
+            c->tile_prof_raw = v >= 2;
+        }
         else if (key == "vt_trace") g_vt_trace = (int)v;
         else ok = false;
     }

@@ -866,6 +866,13 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                              (long long)fcnt, fcnt ? fsum / (double)fcnt : 0.0, fmax, nmax, (long long)over,
                              (long long)over_fb);
             }
+            // (tile_prof=2: the raw per-wave words to tile_prof.bin in the working directory)
+            if (c->tile_prof_raw) {
+                if (FILE* f = std::fopen("tile_prof.bin", "wb")) {
+                    std::fwrite(h.data(), 8, h.size(), f);
+                    std::fclose(f);
+                }
+            }
             // duration by dispatch decile
             for (int dcl = 0; dcl < 10; ++dcl) {
                 double s2 = 0;

@@ -123,6 +123,7 @@ struct pmx_ctx {
     double wave_fill = 1.25;      // wave_fill: the tile mode's wave table fill
     int setup_trace = 0;          // setup_trace: setup timeline on stderr (1: stream-synchronised marks, 2: host)
     bool tile_prof = false;       // tile_prof: the cold tile form's per-wave profile on stderr
+    bool tile_prof_raw = false;   // (tile_prof=2: and the raw words to tile_prof.bin)
     bool reuse_on = true;         // temporal reuse of the grid match (pmx_grid.hip; option grid_reuse=0: off)
     bool safe_valid = false;      // d_safe holds the safe radii of the match in d_dists / d_ids
     void* d_safe = nullptr;       // T[N]: safe radius per query
