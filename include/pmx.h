@@ -243,6 +243,14 @@ int pmx_get_weights(pmx_ctx* ctx, void* w);
 int pmx_vartrim_partial_sums(pmx_ctx* ctx, void* out, int64_t capacity, int64_t* count);
 /* shape of the current match arrays */
 int pmx_get_shape(const pmx_ctx* ctx, int64_t* n_local, int* knn);
+/* Grid level `level` of the reference (the spatial index Matcher::init
+ * builds, MatchersImpl.cpp:77-83), once its build on any stream is complete
+ * (built on demand if it was not): *count records; ids (count int32) the
+ * original reference index of each record, points (count x 4 T) and normals
+ * (count x 4 T, only with normals on the reference) the records the matcher
+ * and the point-to-plane reduction read.  Any of the three may be NULL.
+ * Diagnostic (tests check the records against the input clouds). */
+int pmx_grid_level_records(pmx_ctx* ctx, int level, int64_t* count, int32_t* ids, void* points, void* normals);
 
 /* ------------------------------------------------------------- timing --- */
 /* HIP-event timing of the dominant kernel (the match kernel) on the context

@@ -154,7 +154,7 @@ EXPORTS = [
     "pmx_outlier_mediandist", "pmx_outlier_trimmed", "pmx_outlier_vartrimmed", "pmx_outlier_robust",
     "pmx_robust_scale", "pmx_set_reading_radii",
     "pmx_p2plane_system", "pmx_p2point_system", "pmx_get_matches", "pmx_get_weights", "pmx_vartrim_partial_sums",
-    "pmx_get_shape", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
+    "pmx_get_shape", "pmx_grid_level_records", "pmx_timing_enable", "pmx_timing_read", "pmx_sync",
     "pmx_loop_begin", "pmx_loop_run", "pmx_loop_trace", "pmx_loop_select_stats", "pmx_loop_diag", "pmx_surface_normals",
     "pmx_sampling_surface_normals", "pmx_voxel_grid",
 ]
@@ -202,6 +202,8 @@ def lib():
         l.pmx_get_weights.argtypes = [C.c_void_p, C.c_void_p]
         l.pmx_vartrim_partial_sums.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
         l.pmx_get_shape.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
+        l.pmx_grid_level_records.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int64), C.c_void_p, C.c_void_p,
+                                             C.c_void_p]
         l.pmx_timing_enable.argtypes = [C.c_void_p, C.c_int]
         l.pmx_timing_read.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                       C.POINTER(C.c_double)]
@@ -358,6 +360,18 @@ class Context:
     def set_option(self, name, value):
         """One developer option (README "Options"; pmx_ctx_set_option)."""
         self._chk(self._l.pmx_ctx_set_option(self.h, str(name).encode(), str(value).encode()))
+
+    def level_records(self, level, normals=True):
+        """Grid level `level`'s records (pmx_grid_level_records): original
+        reference ids, points (n, 4) and, with normals, normals (n, 4)."""
+        n = C.c_int64(0)
+        self._chk(self._l.pmx_grid_level_records(self.h, int(level), C.byref(n), None, None, None))
+        ids = np.zeros(n.value, np.int32)
+        pts = np.zeros((n.value, 4), self.dtype)
+        nrm = np.zeros((n.value, 4), self.dtype) if normals else None
+        self._chk(self._l.pmx_grid_level_records(self.h, int(level), C.byref(n), _ptr(ids), _ptr(pts),
+                                                 _ptr(nrm) if normals else None))
+        return ids, pts, nrm
 
     def close(self):
         if self.h:

@@ -412,6 +412,28 @@ int pmx_get_shape(const pmx_ctx* c, int64_t* n_local, int* knn) {
     return PMX_OK;
 }
 
+int pmx_grid_level_records(pmx_ctx* c, int level, int64_t* count, int32_t* ids, void* points, void* normals) {
+    if (!c || !count) return fail(c, PMX_E_BAD_PARAM, "null argument");
+    if (!c->grid_ready || level < 0 || level >= (int)c->levels.size())
+        return fail(c, PMX_E_BAD_PARAM, "pmx_grid_level_records: no such grid level");
+    HIPCHK(c, hipSetDevice(c->device));
+    side_join(c);  // (the finer levels build on the side stream)
+    int rc = ensure_level(c, level);
+    if (rc) return rc;
+    const GridLevel& L = c->lv(level);
+    const int64_t n = c->grid_valid;
+    *count = n;
+    if (normals && !L.gpn) return fail(c, PMX_E_STATE, "pmx_grid_level_records: the reference has no normals");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t rec = 4 * (c->dtype == PMX_F64 ? sizeof(double) : sizeof(float));
+    if (ids) HIPCHK(c, hipMemcpy(ids, L.gidx, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
+    if (points) HIPCHK(c, hipMemcpy(points, L.gpts, rec * (size_t)n, hipMemcpyDeviceToHost));
+    if (normals) {  // (the interleaved point / normal records: every second one)
+        HIPCHK(c, hipMemcpy2D(normals, rec, (const char*)L.gpn + rec, 2 * rec, rec, (size_t)n, hipMemcpyDeviceToHost));
+    }
+    return PMX_OK;
+}
+
 int pmx_set_search(pmx_ctx* c, int search_type) {
     if (!c) return PMX_E_BAD_PARAM;
     if (search_type < 0 || search_type > 2) return fail(c, PMX_E_BAD_PARAM, "searchType must be 0, 1 or 2");

@@ -95,3 +95,29 @@ def test_coarse_levels_on_demand():
     n3, tr3, _ = _loop({}, ref, nrm, rd, T0, *args, iters=12)
     assert n == n2 == n3 == 12
     assert np.array_equal(tr, tr2) and np.array_equal(tr, tr3)
+
+
+def test_level_records_follow_the_reference():
+    """Every grid level's records hold the reference's points and normals
+    (pmx_grid_level_records).  The levels finer than the cold one build on a
+    side stream from the packed normals, which the context stream packs after
+    their upload: the side stream waits for that (the side_start event,
+    pmx_chain.hip build_levels_cold).  A new reference on the same context
+    each time, so a level built from stale normals would hold the previous
+    cloud's."""
+    ctx = P.Context(0, np.float32)
+    for seed in (1, 2, 3):
+        ref, nrm = reference_cloud(300_000, seed=seed)
+        ctx.set_reference(ref, nrm)
+        n_levels = 0
+        while True:
+            try:
+                ids, pts, nn = ctx.level_records(n_levels)
+            except P.InvalidParameter:  # (past the last level)
+                break
+            assert np.array_equal(np.sort(ids), np.arange(len(ref)))
+            assert np.array_equal(pts[:, :3], ref[ids, :3]), f"level {n_levels}: points"
+            assert np.array_equal(nn[:, :3], nrm[ids]), f"level {n_levels}: normals"
+            n_levels += 1
+        assert n_levels >= 2
+    ctx.close()
