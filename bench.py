@@ -461,7 +461,8 @@ def main():
     # null for other configurations
     traffic, traffic_src = None, None
     if args.matcher == "grid" and world == 1:
-        for src in (os.path.join("profiles", "r05", f"pmc_{args.config}_driver.json"),
+        for src in (os.path.join("profiles", "r06", f"pmc_{args.config}_driver.json"),
+                    os.path.join("profiles", "r05", f"pmc_{args.config}_driver.json"),
                     os.path.join("profiles", "r04", f"pmc_{args.config}_driver.json"),
                     os.path.join("profiles", "r03", f"pmc_{args.config}_driver.json")):
             try:
