@@ -822,7 +822,7 @@ int match_impl(pmx_ctx* c, const T* Titer, int knn, double maxDist, uint64_t* vi
                 t1 = std::max(t1, h[4 * w + 1]);
                 rsum += (double)(h[4 * w + 2] & 0xffffffffull);
                 fb += (double)(h[4 * w + 2] >> 32);
-                csum += (double)h[4 * w + 3];
+                csum += (double)(h[4 * w + 3] & 0xffffffffull);
             }
             std::vector<double> sd = dur;
             std::sort(sd.begin(), sd.end());

@@ -31,8 +31,12 @@ def main(cfg="c3", out="."):
     os.remove("tile_prof.bin")
     np.save(os.path.join(out, f"tile_prof_{cfg}.npy"), w)
     d = (w[:, 1] - w[:, 0]) * 0.01
-    print(cfg, "waves", len(w), "span us", (w[:, 1].max() - w[:, 0].min()) * 0.01, "sum us", d.sum(),
-          "p50/p90/p99/max", np.percentile(d, [50, 90, 99, 100]))
+    fin = w[:, 0] + (w[:, 3] >> 32)  # (the wave's end after its fallback walks)
+    fb = (w[:, 2] >> 32) > 0
+    print(cfg, "waves", len(w), "span us", (w[:, 1].max() - w[:, 0].min()) * 0.01,
+          "span with fallback us", (fin.max() - w[:, 0].min()) * 0.01, "sum us", d.sum(),
+          "p50/p90/p99/max", np.percentile(d, [50, 90, 99, 100]), "fallback waves", int(fb.sum()),
+          "lanes", int((w[:, 2] >> 32).sum()), "their walk us max", ((fin - w[:, 1]) * 0.01)[fb].max() if fb.any() else 0)
 
 
 if __name__ == "__main__":
