@@ -5,6 +5,8 @@
 // filters in pmx_filters_capi.hip (pmx_ctx.h lists them).
 #include "pmx_ctx.h"
 
+#include <chrono>
+
 namespace pmxc {
 
 thread_local std::string g_err;  // message of a failed standalone call (pmx_last_error(NULL))
@@ -258,14 +260,22 @@ int pmx_ctx_create(int device, int dtype, pmx_ctx** out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bad(PMX_E_HIP);
     static bool preloaded = false;  // (once per process; modules are per process)
     if (!preloaded) {
-        preload_match();
-        preload_grid();
-        preload_select();
-        preload_reduce();
-        preload_loop();
-        preload_normals();
-        preload_setup();
-        preload_ssn();
+        // (option setup_trace: each module's load time on stderr)
+        auto timed = [&](const char* name, void (*f)()) {
+            const auto t0 = std::chrono::steady_clock::now();
+            f();
+            if (c->setup_trace)
+                std::fprintf(stderr, "preload %s %.2f ms\n", name,
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        };
+        timed("match", preload_match);
+        timed("grid", preload_grid);
+        timed("select", preload_select);
+        timed("reduce", preload_reduce);
+        timed("loop", preload_loop);
+        timed("normals", preload_normals);
+        timed("setup", preload_setup);
+        timed("ssn", preload_ssn);
         preloaded = true;
     }
     // One small "iteration block" holds everything the host reads back per
