@@ -195,9 +195,11 @@ int loop_trace_room(pmx_ctx* c, int64_t iters) {
 // iteration) while the quantile is still moving: after a miss, until this
 // many hits in a row.  Past that the iterations are enqueued blind (stall and
 // replay, loop_run_impl).
-// (1: C3 dist 0.0726 -> 0.0720 ms at world size 1, 0.0523 -> 0.0508 at G = 8
-// in the cost model, the same stalls; profiles/r06/scale/async_after_hits.txt)
-constexpr int kAsyncAfterHits = 1;
+// 0: every iteration after the loop's first is enqueued blind; a miss
+// costs its stall and replay only (C3 dist at world size 1: 0.0726 with 2,
+// 0.0711 with 1, 0.0694 ms with 0 — the same stalls;
+// profiles/r06/scale/async_after_hits.txt)
+constexpr int kAsyncAfterHits = 0;
 
 // one ICP iteration, device-driven (transform and level from LoopCtl)
 template <typename T>
