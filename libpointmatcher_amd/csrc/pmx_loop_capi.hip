@@ -155,6 +155,7 @@ int loop_begin_impl(pmx_ctx* c, const pmx_loop_cfg* cfg, const T* T0) {
         SpecSel init{};
         init.keys = c->d_spec_keys;
         init.ratio = (double)(T)(k0 == PMX_FILTER_TRIMMED ? cfg->filter_p[0][0] : 0.5);
+        init.wide = sharded(c) ? 1 : 0;
         c->spec_init = init;
         std::memcpy(stage + 256, &c->spec_init, sizeof(SpecSel));
         HIPCHK(c, hipMemcpyAsync(c->d_spec, stage + 256, sizeof(SpecSel), hipMemcpyHostToDevice, c->stream));

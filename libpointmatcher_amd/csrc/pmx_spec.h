@@ -79,6 +79,7 @@ struct SpecSel {
     int hit;                    // this iteration's limit came from the window
     unsigned long long n_hit, n_miss;  // statistics (host-readable)
     double dens;                // key density estimate of the last radix select (keys per key unit)
+    int wide;                   // several ranks: a miss costs a stall and a replay, so a wider window
 };
 
 // ---- match side: classify every distance the match writes ----
@@ -151,7 +152,11 @@ __device__ __forceinline__ void spec_update(SpecSel* sp, typename KeyOf<T>::K kl
     using KO = KeyOf<T>;
     using K = typename KO::K;
     const double move = sp->have_prev ? (double)(kl > (K)sp->prev ? kl - (K)sp->prev : (K)sp->prev - kl) : 0.0;
-    double hw = 3.0 * move + 64.0;
+    // (several ranks: a miss stalls the blind batch and replays it, so the
+    // window is wider — C3 sharded: no stall in 20 iterations instead of 1-2,
+    // profiles/r06/scale/wide_window.txt; one rank resolves a miss inside the
+    // select launch, and a wider window costs it appends)
+    double hw = sp->wide ? 6.0 * move + 256.0 : 3.0 * move + 64.0;
     const double dens = density > 1e-30 ? density : 1e-30;
     // expected appends <= cap / 8: every append is an atomic on one counter
     // inside the match kernel, so the window is kept small
