@@ -369,11 +369,13 @@ __device__ __forceinline__ void step_body(LoopCtl* __restrict__ ctl, LoopState<T
     // (LDS boxes shared by a wave's 64 queries) is cheaper than 64 per-lane
     // full searches.  Both forms report the queries that fail the per-lane
     // certificate (the tile form evaluates its bound without using it); the
-    // tile form runs the next match while that is >= 94 % of the queries
-    // (MI355X, C5: the per-lane match at 93.6 % failures costs about what
-    // the warm tile form costs, profiles/r05/exp).
+    // tile form runs the next match while that is >= 85 % of the queries
+    // (MI355X, C5: round 5 set 94 %, where the per-lane match costs about
+    // what the warm tile form costs; round 6 A/B of 80 / 85 / 90 / 94 / 97 %:
+    // 1.274 / 1.270 / 1.272 / 1.279 / 1.315 ms per timed iteration,
+    // profiles/r06/c5/tile_dispatch_threshold.txt).
     if (cfg.tile_dispatch)
-        ctl->use_tile = cfg.n_local > 0 && (double)vis1 >= 0.94 * (double)cfg.n_local ? 1 : 0;
+        ctl->use_tile = cfg.n_local > 0 && (double)vis1 >= 0.85 * (double)cfg.n_local ? 1 : 0;
     loop_publish(ctl, Tit, rows);
 }
 
